@@ -1,0 +1,399 @@
+"""Benchmark: TAS software TCP/IP checksum path on MI355X (BASELINE.json metric
+"TCP/IP checksum GiB/s (device-resident), 1500B MTU batch, 1/2/4/8 GPU").
+
+One step = one launch of the TCP4 checksum kernel (tcp_checksums() flag-off
+branch: rte_ipv4_cksum + rte_ipv4_udptcp_cksum per frame) over one batch of
+65,536 TAS TX data segments (1514 B frames, ip.len 1500, one per 2048 B mbuf
+data room: BASELINE.json configs[1] / BASELINE.md).  Inputs are resident in HBM
+before the timed region; steps rotate over R distinct batches (R x 134 MB >>
+the 256 MiB Infinity Cache) so every step reads HBM, not MALL.
+
+Algorithmic bytes per frame = ip.total_length (1500, the bytes summed) + 4
+(results written) -- SURVEY.md section 8d.  GiB/s = bytes / s / 2^30.
+
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+One process per GPU, each with its own batches and stream (weak scaling, no
+data-path collective); the timed region is barrier + synchronize on both sides
+and the MAX over ranks is taken.  Rank 0 prints one JSON line.
+
+Extra legs (rank 0, N == 1): the RAW payload fold (rte_raw_cksum over 64K x
+1500 B), the end-to-end host-memory rate through pinned hipMemcpyAsync, the
+CPU oracle baseline, and (--pmc) HBM traffic from rocprofv3 counters.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from tas_amd import pktgen, xsum  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+METRIC = "TCP/IP checksum GiB/s (device-resident), 1500B MTU batch, 1/2/4/8 GPU"
+
+N_FRAMES = 65536
+STRIDE = pktgen.MBUF_ROOM      # 2048
+IP_TOTAL = 1500
+RAW_LEN = 1500
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rotate", type=int, default=16, help="distinct device batches cycled through")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-raw", action="store_true")
+    ap.add_argument("--pmc", action="store_true", help="collect HBM traffic via rocprofv3 child runs")
+    ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# distributed plumbing (one process per GPU)
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, ws: int) -> float:
+    if ws == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, ws: int) -> float:
+    if ws == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ---------------------------------------------------------------------------
+# workloads
+
+class Tcp4Workload:
+    name = "tcp4"
+    desc = (f"{N_FRAMES} TAS TX segments (1514 B frames, ip.len {IP_TOTAL}, {STRIDE} B mbuf stride), "
+            "tcp_checksums() flag-off per frame")
+
+    def __init__(self, rotate: int, seed: int):
+        self.n = N_FRAMES
+        self.host = pktgen.tcp4_frames(self.n, payload=IP_TOTAL - 52, stride=STRIDE, seed=seed)
+        first = torch.from_numpy(self.host).cuda()
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.outs = [torch.empty(2 * self.n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
+        self.bytes_per_step = self.n * (IP_TOTAL + 4)
+
+    def launcher(self):
+        L = xsum.lib()
+        fn = L.tasx_tcp4_cksum_batch_dev
+        stream = torch.cuda.current_stream().cuda_stream
+        args = [(b.data_ptr(), None, STRIDE, self.n, pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN,
+                 o.data_ptr(), 0, stream) for b, o in zip(self.bufs, self.outs)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev")
+        return launch
+
+
+class RawWorkload:
+    name = "raw"
+    desc = f"{N_FRAMES} x {RAW_LEN} B packed payloads, rte_raw_cksum per packet"
+
+    def __init__(self, rotate: int, seed: int):
+        self.n = N_FRAMES
+        self.host, _ = pktgen.raw_uniform(self.n, RAW_LEN, seed=seed)
+        first = torch.from_numpy(self.host).cuda()
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.outs = [torch.empty(self.n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
+        self.bytes_per_step = self.n * (RAW_LEN + 2)
+
+    def launcher(self):
+        L = xsum.lib()
+        fn = L.tasx_raw_cksum_batch_dev
+        stream = torch.cuda.current_stream().cuda_stream
+        args = [(b.data_ptr(), None, RAW_LEN, None, RAW_LEN, self.n, o.data_ptr(), stream)
+                for b, o in zip(self.bufs, self.outs)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_raw_cksum_batch_dev")
+        return launch
+
+
+def timed_run(wl, steps: int, warmup: int, ws: int):
+    """W untimed steps, then exactly K timed steps between barrier+sync pairs.
+    Per-launch HIP events on the launch stream give the kernel duration."""
+    launch = wl.launcher()
+    for k in range(warmup):
+        launch(k)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier(ws)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record()
+        launch(warmup + k)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    barrier(ws)
+    t1 = time.perf_counter()
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return t1 - t0, kern_ms
+
+
+# ---------------------------------------------------------------------------
+# extra legs
+
+def e2e_leg(reps: int = 5) -> dict:
+    """Host-memory frames -> pinned H2D -> kernel -> D2H results (tasx_*_host)."""
+    n = N_FRAMES
+    frames = pktgen.tcp4_frames(n, payload=IP_TOTAL - 52, stride=STRIDE, seed=41)
+    pin = xsum.PinnedBuffer(frames.size)
+    pin.array[:] = frames
+    out = np.empty(2 * n, np.uint16)
+    xsum.ctx_init(0, torch.cuda.current_device(), 32 << 20)
+    try:
+        xsum.tcp4_cksum_batch_host(0, pin.addr, STRIDE, n, out.ctypes.data)  # warm
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            xsum.tcp4_cksum_batch_host(0, pin.addr, STRIDE, n, out.ctypes.data)
+            ts.append(time.perf_counter() - t0)
+        # deferred per-frame surface with TAS's own batch size (TXBUF_SIZE 32)
+        frames32 = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
+        base = frames32.ctypes.data
+        fl = []
+        for r in range(50):
+            t0 = time.perf_counter()
+            for i in range(32):
+                xsum.defer_tcp4(0, base + i * STRIDE)
+            xsum.tx_flush(0)
+            fl.append(time.perf_counter() - t0)
+    finally:
+        xsum.ctx_destroy(0)
+        pin.free()
+    t = float(np.median(ts))
+    alg = n * (IP_TOTAL + 4)
+    return {
+        "value": alg / t / GIB, "unit": "GiB/s",
+        "pcie_h2d_bytes": n * STRIDE, "pcie_d2h_bytes": n * 4,
+        "ms_per_batch": t * 1e3,
+        "desc": "64K TAS frames in pinned host memory: chunked hipMemcpyAsync H2D (whole 2048 B mbuf rooms) "
+                "-> kernel -> D2H of results, 3 slots pipelined; median of 5",
+        "defer_flush_32_us": float(np.median(fl)) * 1e6,
+    }
+
+
+def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> dict:
+    """The oracle (C restatement of the reference path, per-frame calls) timed on
+    this box's host cores, on a bounded sample of the same workload."""
+    from oracle import oracle_lib
+    lib_path = None
+    try:  # the reference's own flags: -O3 -march=native, built for THIS host
+        tmp = Path(tempfile.mkdtemp(prefix="tasx_oracle_"))
+        lib_path = oracle_lib.build(out_dir=tmp, march="native")
+        kind_note = "-O3 -march=native (built on this host)"
+    except Exception:
+        lib_path = None
+        kind_note = "-O3 -march=x86-64-v3 (prebuilt)"
+    orc = oracle_lib.Oracle(lib_path)
+    frames = wl.host.copy()
+    n = wl.n
+    # parity of the sample: oracle vs the GPU output of the same batch
+    exp = orc.tcp4_batch(frames.copy(), n, stride=STRIDE)
+    parity = bool(np.array_equal(exp, gpu_out))
+    ncpu = len(os.sched_getaffinity(0))
+    threads = min(16, ncpu)  # the box's CPU share for one GPU
+    t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=1)
+    reps1 = max(3, min(200, int(budget_s * 0.4 / max(t1, 1e-6))))
+    t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=reps1)
+    tn = orc.bench(1, frames, n, stride=STRIDE, threads=threads, reps=1)
+    repsn = max(3, min(2000, int(budget_s * 0.4 / max(tn, 1e-6))))
+    tn = orc.bench(1, frames, n, stride=STRIDE, threads=threads, reps=repsn)
+    alg = n * (IP_TOTAL + 4)
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    if lib_path is not None:
+        shutil.rmtree(lib_path.parent, ignore_errors=True)
+    return {
+        "value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
+        "sample": f"the 64K-frame TCP4 batch (98.6 MB algorithmic), per-frame oracle_tcp_checksums "
+                  f"(DPDK 19.11 restatement), median of {repsn} passes on {threads} pinned threads; "
+                  f"1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}; CPU {model}, "
+                  f"{ncpu} cpus visible",
+        "single_core_value": alg / t1 / GIB,
+        "parity_vs_gpu": "bit-exact" if parity else "MISMATCH",
+    }
+
+
+def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
+    """HBM bytes per launch from rocprofv3 PMC counters, one counter per pass
+    (guide: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950 -> x2;
+    WRITE_SIZE exact for wide stores; both in KiB)."""
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(rocprof).exists():
+        return None
+    res = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        outdir = Path(tempfile.mkdtemp(prefix=f"pmc_{ctr}_"))
+        cmd = [rocprof, "--pmc", ctr, "--output-format", "csv", "-d", str(outdir), "-o", "run", "--",
+               sys.executable, str(ROOT / "bench.py"), "--pmc-child", mode, "--steps", str(launches)]
+        env = dict(os.environ)
+        env.pop("WORLD_SIZE", None)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+        if r.returncode != 0:
+            return {"error": f"rocprofv3 {ctr} rc={r.returncode}: {r.stderr[-400:]}"}
+        vals = []
+        for csvf in outdir.rglob("*counter_collection.csv"):
+            import csv
+            with open(csvf) as fh:
+                for row in csv.DictReader(fh):
+                    if kernel_name in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
+                        vals.append(float(row["Counter_Value"]))
+        shutil.rmtree(outdir, ignore_errors=True)
+        if not vals:
+            return {"error": f"no {ctr} rows for {kernel_name}"}
+        res[ctr] = float(np.median(vals))
+    fetch = res["FETCH_SIZE"] * 1024 * 2
+    write = res["WRITE_SIZE"] * 1024
+    return {"FETCH_SIZE_kib": res["FETCH_SIZE"], "WRITE_SIZE_kib": res["WRITE_SIZE"],
+            "hbm_bytes_per_launch": fetch + write}
+
+
+def pmc_child(mode: str, steps: int):
+    torch.cuda.set_device(0)
+    xsum.lib()
+    wl = Tcp4Workload(16, pktgen.SEED) if mode == "tcp4" else RawWorkload(16, pktgen.SEED)
+    launch = wl.launcher()
+    for k in range(steps):
+        launch(k)
+    torch.cuda.synchronize()
+
+
+# ---------------------------------------------------------------------------
+
+def roofline(bytes_per_launch: int, kern_ms: list[float], traffic):
+    avg_s = float(np.mean(kern_ms)) / 1e3
+    achieved = bytes_per_launch / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel_avg_us": round(avg_s * 1e6, 3), "kernel_median_us": round(float(np.median(kern_ms)) * 1e3, 3),
+            "algorithmic_bytes_per_launch": bytes_per_launch}
+
+
+def main():
+    args = parse()
+    if args.pmc_child:
+        pmc_child(args.pmc_child, args.steps)
+        return
+    ws, rank, local = dist_setup()
+    xsum.lib()
+    rot = max(1, args.rotate)
+
+    wl = Tcp4Workload(rot, pktgen.SEED + rank)
+    bytes_per_step = wl.bytes_per_step
+    dt, kern_ms = timed_run(wl, args.steps, args.warmup, ws)
+    dt_max = max_over_ranks(dt, ws)
+    total_bytes = sum_over_ranks(float(bytes_per_step * args.steps), ws)
+    value = total_bytes / dt_max / GIB
+
+    extra = {}
+    raw = None
+    if not args.no_raw:
+        rw = RawWorkload(rot, pktgen.SEED + 1000 + rank)
+        rdt, rkern = timed_run(rw, args.steps, args.warmup, ws)
+        rdt = max_over_ranks(rdt, ws)
+        rtotal = sum_over_ranks(float(rw.bytes_per_step * args.steps), ws)
+        raw = {"value": rtotal / rdt / GIB, "unit": "GiB/s", "ms_per_step": rdt / args.steps * 1e3,
+               "workload": rw.desc, "roofline": roofline(rw.bytes_per_step, rkern, None)}
+        del rw
+
+    traffic = None
+    if rank == 0 and ws == 1:
+        torch.cuda.synchronize()
+        gpu_out = wl.outs[0].cpu().numpy().view(np.uint16).copy()
+        if not args.no_cpu_baseline:
+            extra["cpu_baseline"] = cpu_baseline_leg(wl, gpu_out, args.cpu_seconds)
+        if not args.no_e2e:
+            extra["e2e"] = e2e_leg()
+        if args.pmc:
+            del wl
+            torch.cuda.empty_cache()
+            p = pmc_leg("tcp4", "tcp4_cksum_kernel", 64)
+            extra["pmc"] = p
+            if p and "hbm_bytes_per_launch" in p:
+                traffic = int(p["hbm_bytes_per_launch"])
+            if raw is not None:
+                pr = pmc_leg("raw", "raw_cksum_kernel", 64)
+                if pr and "hbm_bytes_per_launch" in pr:
+                    raw["roofline"]["traffic"] = int(pr["hbm_bytes_per_launch"])
+                raw["pmc"] = pr
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64-seeded frames, pktgen.py)",
+            "config": {"workload": Tcp4Workload.desc, "frames_per_gpu_step": N_FRAMES,
+                       "algorithmic_bytes_per_frame": IP_TOTAL + 4, "rotation_batches": rot,
+                       "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
+            "roofline": roofline(bytes_per_step, kern_ms, traffic),
+            "cpu_baseline": extra.get("cpu_baseline"),
+        }
+        if raw is not None:
+            line["raw"] = raw
+        if "e2e" in extra:
+            line["e2e"] = extra["e2e"]
+        if "pmc" in extra:
+            line["pmc"] = extra["pmc"]
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+/*
+ * tasx_xsum.h -- C ABI of libtasx, the MI355X (gfx950) implementation of TAS's
+ * software TCP/IP checksum path (TAS run with --fp-no-xsumoffload).
+ *
+ * What it replaces in the reference (/root/reference):
+ *   - tcp_checksums(nbh, p, ip_s, ip_d, l3_paylen), flag-off branch,
+ *     tas/fast/fast_flows.c:1058-1069 (decl :75-76)      -> tasx_tcp_checksums
+ *   - fast_flows_kernelxsums(nbh, p), tas/fast/fast_flows.c:1071-1076,
+ *     declared tas/fast/fastemu.h:70-71                   -> tasx_fast_flows_kernelxsums
+ *   - the per-frame DPDK calls it makes, rte_ipv4_cksum + rte_ipv4_udptcp_cksum
+ *     (DPDK 19.11 rte_ip.h, not vendored; called at fast_flows.c:1066-1067)
+ *     -> batched on the GPU by tasx_tcp4_cksum_batch_dev / _host
+ *   - rte_raw_cksum over packet payloads
+ *     -> tasx_raw_cksum_batch_dev / _host
+ *   - the batch boundary tx_flush(ctx), tas/fast/fastemu.c:544-566 -> tasx_flush
+ *
+ * Conventions:
+ *   - Plain C types only.  `stream` is a hipStream_t passed as void* (NULL =
+ *     the null stream).  Device-resident (_dev) entry points are asynchronous
+ *     on that stream; everything else returns after the work is complete.
+ *   - Return 0 on success or a negative errno (-EINVAL bad argument, -ENOMEM,
+ *     -ENODEV no usable GPU, -EIO a HIP runtime error; tasx_last_error()
+ *     describes the last one).  There is NO CPU fallback: a frame whose
+ *     checksum could not be computed on the GPU is reported, never silently
+ *     computed elsewhere.  The reference's per-frame calls cannot fail
+ *     (void); TAS's integration aborts on a non-zero
+ *     return, as it does on its other invariant violations (fastemu.h:86-89).
+ *   - Checksum results are native (little-endian) uint16 values, exactly what
+ *     tcp_checksums() stores into ip.chksum / tcp.chksum
+ *     (include/packet_defs.h:96,165): their bytes are the network-order
+ *     RFC 1071 checksum.
+ *   - Arithmetic is bit-exact with DPDK 19.11: rte_raw_cksum (folded, not
+ *     inverted, 0 only for all-zero input), rte_ipv4_cksum (20 B, IHL ignored,
+ *     0xffff kept), rte_ipv4_udptcp_cksum (L4 length from ip.total_length,
+ *     0 when total_length < 20, result 0 -> 0xffff).
+ */
+#ifndef TASX_XSUM_H_
+#define TASX_XSUM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TASX_ABI_VERSION 1
+
+/* flags for the TCP4 batch entry points */
+#define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
+
+/* largest RAW packet: DPDK's 32-bit accumulator cannot wrap below this
+ * (65536 words * 0xffff + 0xff < 2^32), so results stay bit-exact. */
+#define TASX_RAW_MAX_LEN 131073u
+
+/* TAS frame layout (struct pkt_tcp, include/packet_defs.h:215-219) */
+#define TASX_TAS_IP_OFF 14u
+#define TASX_TAS_L4_OFF 34u
+
+/* Maximum fast-path contexts (fp_cores_max <= FLEXNIC_PL_APPST_CTX_MCS = 16,
+ * tas/fast/fastemu.c:87-91). */
+#define TASX_MAX_CTX 16u
+
+int tasx_abi_version(void);
+const char *tasx_last_error(void);
+/* number of visible GPUs (-EIO on runtime failure) */
+int tasx_device_count(void);
+
+/* ---------------------------------------------------------------------- */
+/* Device-resident batches.  All pointers are device pointers (or host memory
+ * the device can address).  Packet i starts at base + off[i], or at
+ * base + i * stride when off == NULL.  Asynchronous on `stream`. */
+
+/* RAW: out[i] = rte_raw_cksum(base + off_i, len_i); len_i = len[i], or len0
+ * when len == NULL; len_i <= TASX_RAW_MAX_LEN (device-side lengths are the
+ * caller's responsibility). */
+int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *len, uint32_t len0, uint32_t n,
+    uint16_t *out, void *stream);
+
+/* TCP4: for each frame, the flag-off branch of tcp_checksums(): with
+ * ip = frame + ip_off and tcp = frame + l4_off (ip.chksum and tcp.chksum
+ * taken as zero), out[2i] = rte_ipv4_cksum(ip), out[2i+1] =
+ * rte_ipv4_udptcp_cksum(ip, tcp).  `out` (4-byte aligned) may be NULL when
+ * TASX_F_INPLACE is set.  Frames must not overlap. */
+int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Per-fast-path-core contexts (one per dataplane_context, no shared state,
+ * no locks: tas/fast/fastemu.c:87-91).  A context owns a GPU, streams, pinned
+ * host staging and device buffers sized for `max_batch_bytes` per pipeline
+ * slot (0 = 64 MiB). */
+int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes);
+int tasx_ctx_destroy(unsigned ctx_id);
+
+/* Host-memory batches, end to end: pinned hipMemcpyAsync H2D of the frames,
+ * GPU checksum, D2H of the results, pipelined over the context's slots.
+ * Frames are read from [base + off_i, base + off_i + extent) where extent is
+ * `stride` (stride mode) -- i.e. whole mbuf data rooms are copied.
+ * Register `base` with tasx_host_register (or allocate it with
+ * tasx_host_alloc) for full PCIe speed. */
+int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
+    uint32_t flags);
+int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
+    uint64_t stride, uint32_t len0, uint32_t n, uint16_t *out);
+
+/* Deferred per-frame surface.  tasx_tcp_checksums() has the reference's
+ * argument list plus the context id; it only records the frame (no device
+ * work, safe under the per-flow spinlock).  tasx_flush() -- called where TAS
+ * calls tx_flush(), outside any flow lock -- checksums every recorded frame
+ * on the GPU and stores ip.chksum / tcp.chksum into the frames before it
+ * returns.  Frames must stay valid and unmodified until then.
+ * Recorded frames are read up to ip_off + ip.total_length. */
+int tasx_tcp_checksums(unsigned ctx_id, void *nbh, void *p, uint32_t ip_s,
+    uint32_t ip_d, uint16_t l3_paylen);
+int tasx_fast_flows_kernelxsums(unsigned ctx_id, void *nbh, void *p);
+int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off,
+    uint16_t l4_off);
+/* frames recorded and not yet flushed */
+int tasx_pending(unsigned ctx_id);
+int tasx_flush(unsigned ctx_id);
+
+/* ---------------------------------------------------------------------- */
+/* Memory helpers (plumbing for callers without their own HIP code). */
+void *tasx_host_alloc(size_t bytes);          /* pinned host memory */
+int tasx_host_free(void *p);
+int tasx_host_register(void *p, size_t bytes);  /* pin existing memory */
+int tasx_host_unregister(void *p);
+void *tasx_dev_alloc(int device, size_t bytes);
+int tasx_dev_free(void *p);
+int tasx_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int tasx_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int tasx_stream_sync(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

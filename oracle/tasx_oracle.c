@@ -1,0 +1,307 @@
+/*
+ * tasx_oracle.c -- TEST INFRASTRUCTURE ONLY (see tasx_oracle.h for the rules
+ * and the parity status).  CPU restatement of:
+ *   - DPDK 19.11 lib/librte_net/rte_ip.h: __rte_raw_cksum, __rte_raw_cksum_reduce,
+ *     rte_raw_cksum, rte_ipv4_cksum, rte_ipv4_phdr_cksum, rte_ipv4_udptcp_cksum
+ *     (third-party, not vendored in the reference; restated from the published
+ *     algorithm);
+ *   - TAS tcp_checksums() flag-off branch, tas/fast/fast_flows.c:1058-1069;
+ *   - TAS network_ip_phdr_xsum(), tas/fast/network.h:157-173.
+ * Compiled with the reference's flags (-std=gnu99 -O3 -march=native,
+ * /root/reference/Makefile:8).  Host is little-endian x86: every "u16 word" is
+ * a native LE load of two consecutive bytes counted from the buffer start.
+ */
+#define _GNU_SOURCE
+#include "tasx_oracle.h"
+
+#include <pthread.h>
+#include <sched.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+static inline uint16_t ld16(const uint8_t *p)
+{
+  uint16_t v;
+  memcpy(&v, p, 2); /* the may_alias u16 load of rte_ip.h */
+  return v;
+}
+
+/* a1: __rte_raw_cksum.  4-word unrolled loop, 1-word loop, odd tail byte
+ * added as the low byte of a zero-padded LE word.  32-bit accumulator. */
+uint32_t oracle_raw_cksum_acc(const void *buf, size_t len, uint32_t sum)
+{
+  const uint8_t *b = (const uint8_t *) buf;
+
+  while (len >= 8) {
+    sum += ld16(b);
+    sum += ld16(b + 2);
+    sum += ld16(b + 4);
+    sum += ld16(b + 6);
+    len -= 8;
+    b += 8;
+  }
+  while (len >= 2) {
+    sum += ld16(b);
+    len -= 2;
+    b += 2;
+  }
+  if (len == 1)
+    sum += *b;
+  return sum;
+}
+
+/* __rte_raw_cksum_reduce: two end-around folds, no inversion. */
+uint16_t oracle_raw_cksum_reduce(uint32_t sum)
+{
+  sum = ((sum & 0xffff0000u) >> 16) + (sum & 0xffffu);
+  sum = ((sum & 0xffff0000u) >> 16) + (sum & 0xffffu);
+  return (uint16_t) sum;
+}
+
+/* a2: rte_raw_cksum */
+uint16_t oracle_raw_cksum(const void *buf, size_t len)
+{
+  return oracle_raw_cksum_reduce(oracle_raw_cksum_acc(buf, len, 0));
+}
+
+/* a3: rte_ipv4_cksum -- fixed 20-byte header, 0xffff kept, else inverted. */
+uint16_t oracle_ipv4_cksum(const void *ip_hdr)
+{
+  uint16_t c = oracle_raw_cksum(ip_hdr, 20);
+  return (c == 0xffff) ? c : (uint16_t) ~c;
+}
+
+/* a4: rte_ipv4_phdr_cksum.  12-byte pseudo header {src, dst, 0, proto,
+ * htons(total_length - 20)}; length 0 under PKT_TX_TCP_SEG. */
+uint16_t oracle_ipv4_phdr_cksum(const void *ip_hdr, uint64_t ol_flags)
+{
+  const uint8_t *ip = (const uint8_t *) ip_hdr;
+  uint8_t psd[12];
+  uint16_t tl = (uint16_t) ((ip[2] << 8) | ip[3]);
+  uint16_t l4 = (uint16_t) (tl - 20);
+
+  memcpy(psd, ip + 12, 4);      /* src_addr */
+  memcpy(psd + 4, ip + 16, 4);  /* dst_addr */
+  psd[8] = 0;                   /* zero */
+  psd[9] = ip[9];               /* proto (next_proto_id) */
+  if (ol_flags & ORACLE_PKT_TX_TCP_SEG) {
+    psd[10] = 0;
+    psd[11] = 0;
+  } else {
+    psd[10] = (uint8_t) (l4 >> 8); /* rte_cpu_to_be_16 */
+    psd[11] = (uint8_t) l4;
+  }
+  return oracle_raw_cksum(psd, sizeof(psd));
+}
+
+/* a5: rte_ipv4_udptcp_cksum, DPDK 19.11 semantics: l3 < 20 -> 0; L4 length
+ * from ip.total_length; one fold; invert; 0 -> 0xffff. */
+uint16_t oracle_ipv4_udptcp_cksum(const void *ip_hdr, const void *l4_hdr)
+{
+  const uint8_t *ip = (const uint8_t *) ip_hdr;
+  uint32_t l3_len = (uint32_t) ((ip[2] << 8) | ip[3]);
+  uint32_t cksum;
+
+  if (l3_len < 20)
+    return 0;
+  cksum = oracle_raw_cksum(l4_hdr, l3_len - 20);
+  cksum += oracle_ipv4_phdr_cksum(ip_hdr, 0);
+  cksum = ((cksum & 0xffff0000u) >> 16) + (cksum & 0xffffu);
+  cksum = (~cksum) & 0xffffu;
+  if (cksum == 0)
+    cksum = 0xffff;
+  return (uint16_t) cksum;
+}
+
+/* a6: tcp_checksums(), fp_xsumoffload == 0 branch (fast_flows.c:1061-1067).
+ * Order as in the reference: ip.chksum = 0; tcp.chksum = 0; ip.chksum =
+ * a3(ip); tcp.chksum = a5(ip, tcp).  Stores are native (LE) u16. */
+void oracle_tcp_checksums(void *ip_hdr, void *l4_hdr)
+{
+  uint8_t *ip = (uint8_t *) ip_hdr;
+  uint8_t *tcp = (uint8_t *) l4_hdr;
+  uint16_t v;
+
+  memset(ip + 10, 0, 2);
+  memset(tcp + 16, 0, 2);
+  v = oracle_ipv4_cksum(ip);
+  memcpy(ip + 10, &v, 2);
+  v = oracle_ipv4_udptcp_cksum(ip, tcp);
+  memcpy(tcp + 16, &v, 2);
+}
+
+/* a8: network_ip_phdr_xsum (offload branch's pseudo-header fold).  The
+ * beui32 .x fields hold network-order bytes read as a native LE u32. */
+uint16_t oracle_ip_phdr_xsum(uint32_t ip_src_be, uint32_t ip_dst_be,
+    uint8_t proto, uint16_t l3_paylen)
+{
+  uint32_t sum = 0;
+  sum += ip_src_be & 0xffff;
+  sum += (ip_src_be >> 16) & 0xffff;
+  sum += ip_dst_be & 0xffff;
+  sum += (ip_dst_be >> 16) & 0xffff;
+  sum += ((uint16_t) proto) << 8;
+  sum += (uint16_t) __builtin_bswap16(l3_paylen); /* t_beui16(l3_paylen).x */
+  sum = ((sum & 0xffff0000u) >> 16) + (sum & 0xffffu);
+  sum = ((sum & 0xffff0000u) >> 16) + (sum & 0xffffu);
+  return (uint16_t) sum;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Batch drivers (one reference-style call per packet). */
+
+static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, size_t i)
+{
+  return off ? off[i] : (uint64_t) i * stride;
+}
+
+void oracle_raw_batch(const uint8_t *base, const uint64_t *off,
+    const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
+    uint16_t *out)
+{
+  size_t i;
+  for (i = 0; i < n; i++)
+    out[i] = oracle_raw_cksum(base + pkt_off(off, stride, i),
+        len ? len[i] : len0);
+}
+
+void oracle_tcp4_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
+    size_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out, int inplace)
+{
+  size_t i;
+  for (i = 0; i < n; i++) {
+    uint8_t *f = base + pkt_off(off, stride, i);
+    uint8_t save_ip[2], save_tcp[2];
+    if (!inplace) {
+      memcpy(save_ip, f + ip_off + 10, 2);
+      memcpy(save_tcp, f + l4_off + 16, 2);
+    }
+    oracle_tcp_checksums(f + ip_off, f + l4_off);
+    memcpy(&out[2 * i], f + ip_off + 10, 2);
+    memcpy(&out[2 * i + 1], f + l4_off + 16, 2);
+    if (!inplace) {
+      memcpy(f + ip_off + 10, save_ip, 2);
+      memcpy(f + l4_off + 16, save_tcp, 2);
+    }
+  }
+}
+
+/* ---------------------------------------------------------------------- */
+/* CPU baseline timing. */
+
+struct bench_arg {
+  int mode, cpu;
+  uint8_t *base;
+  const uint64_t *off;
+  const uint32_t *len;
+  uint64_t stride;
+  uint32_t len0, ip_off, l4_off;
+  size_t lo, hi;
+  uint16_t *out;
+  pthread_barrier_t *bar;
+  double t0, t1;
+};
+
+static double now_s(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+static void *bench_worker(void *p)
+{
+  struct bench_arg *a = (struct bench_arg *) p;
+  size_t i;
+  if (a->cpu >= 0) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    CPU_SET(a->cpu, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+  }
+  pthread_barrier_wait(a->bar);
+  a->t0 = now_s();
+  if (a->mode == 0) {
+    for (i = a->lo; i < a->hi; i++)
+      a->out[i] = oracle_raw_cksum(a->base + pkt_off(a->off, a->stride, i),
+          a->len ? a->len[i] : a->len0);
+  } else {
+    /* in place, exactly what tcp_checksums() does to each TX frame */
+    for (i = a->lo; i < a->hi; i++) {
+      uint8_t *f = a->base + pkt_off(a->off, a->stride, i);
+      oracle_tcp_checksums(f + a->ip_off, f + a->l4_off);
+    }
+  }
+  a->t1 = now_s();
+  return NULL;
+}
+
+static int cmp_d(const void *x, const void *y)
+{
+  double a = *(const double *) x, b = *(const double *) y;
+  return (a > b) - (a < b);
+}
+
+double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
+    const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
+    uint32_t ip_off, uint32_t l4_off, uint16_t *out, int threads, int reps)
+{
+  pthread_t *th;
+  struct bench_arg *args;
+  pthread_barrier_t bar;
+  double *times, med;
+  cpu_set_t avail;
+  int t, r, ncpu_avail = 0, cpus[1024];
+
+  if (threads < 1)
+    threads = 1;
+  if (reps < 1)
+    reps = 1;
+  /* pin to the cpus this process may run on, in order */
+  CPU_ZERO(&avail);
+  if (sched_getaffinity(0, sizeof(avail), &avail) == 0) {
+    for (t = 0; t < CPU_SETSIZE && ncpu_avail < 1024; t++)
+      if (CPU_ISSET(t, &avail))
+        cpus[ncpu_avail++] = t;
+  }
+  th = calloc((size_t) threads, sizeof(*th));
+  args = calloc((size_t) threads, sizeof(*args));
+  times = calloc((size_t) reps, sizeof(*times));
+  for (r = 0; r < reps; r++) {
+    double t0 = 1e300, t1 = 0;
+    pthread_barrier_init(&bar, NULL, (unsigned) threads);
+    for (t = 0; t < threads; t++) {
+      struct bench_arg *a = &args[t];
+      a->mode = mode;
+      a->cpu = ncpu_avail ? cpus[t % ncpu_avail] : -1;
+      a->base = base;
+      a->off = off;
+      a->len = len;
+      a->stride = stride;
+      a->len0 = len0;
+      a->ip_off = ip_off;
+      a->l4_off = l4_off;
+      a->lo = n * (size_t) t / (size_t) threads;
+      a->hi = n * (size_t) (t + 1) / (size_t) threads;
+      a->out = out;
+      a->bar = &bar;
+      pthread_create(&th[t], NULL, bench_worker, a);
+    }
+    for (t = 0; t < threads; t++) {
+      pthread_join(th[t], NULL);
+      if (args[t].t0 < t0)
+        t0 = args[t].t0;
+      if (args[t].t1 > t1)
+        t1 = args[t].t1;
+    }
+    pthread_barrier_destroy(&bar);
+    times[r] = t1 - t0;
+  }
+  qsort(times, (size_t) reps, sizeof(double), cmp_d);
+  med = times[reps / 2];
+  free(th);
+  free(args);
+  free(times);
+  return med;
+}

@@ -1,0 +1,95 @@
+"""TEST INFRASTRUCTURE ONLY -- independent numpy restatement of the checksum path.
+
+This second restatement is written from RFC 1071 arithmetic (exact integer sum
+of little-endian 16-bit words, then the closed form of the end-around-carry
+fold) rather than from DPDK's loop structure, so that it cross-checks
+`oracle/tasx_oracle.c` instead of repeating it.  It follows the same reference
+semantics:
+
+* rte_raw_cksum (DPDK 19.11 rte_ip.h): folded, not
+  inverted; 0 only for an all-zero buffer, otherwise in [1, 0xffff].
+* rte_ipv4_cksum (a3), rte_ipv4_phdr_cksum (a4), rte_ipv4_udptcp_cksum (a5).
+* tcp_checksums flag-off branch, /root/reference tas/fast/fast_flows.c:1058-1069.
+* network_ip_phdr_xsum, /root/reference tas/fast/network.h:157-173.
+
+Only tests/ (and tests/golden/gen_golden.py) import this module.  Parity status:
+see oracle/tasx_oracle.h -- the reference's own tests pin no checksum value.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+PKT_TX_TCP_SEG = 1 << 50
+
+
+def _fold_exact(total: int) -> int:
+    """Closed form of repeated 16-bit end-around folding of a non-negative sum."""
+    if total == 0:
+        return 0
+    return ((total - 1) % 0xFFFF) + 1
+
+
+def word_sum(buf) -> int:
+    """Exact integer sum of LE u16 words counted from the buffer start; an odd
+    tail byte is the low byte of a zero-padded word."""
+    b = np.frombuffer(bytes(buf), dtype=np.uint8)
+    if b.size & 1:
+        b = np.concatenate([b, np.zeros(1, np.uint8)])
+    return int(b.view("<u2").astype(np.int64).sum())
+
+
+def raw_cksum(buf) -> int:
+    return _fold_exact(word_sum(buf))
+
+
+def ipv4_cksum(ip: bytes) -> int:
+    c = raw_cksum(ip[:20])
+    return c if c == 0xFFFF else (~c) & 0xFFFF
+
+
+def ipv4_phdr_cksum(ip: bytes, ol_flags: int = 0) -> int:
+    tl = (ip[2] << 8) | ip[3]
+    l4 = 0 if (ol_flags & PKT_TX_TCP_SEG) else ((tl - 20) & 0xFFFF)
+    psd = bytes(ip[12:20]) + bytes([0, ip[9], l4 >> 8, l4 & 0xFF])
+    return raw_cksum(psd)
+
+
+def ipv4_udptcp_cksum(ip: bytes, l4: bytes) -> int:
+    l3 = (ip[2] << 8) | ip[3]
+    if l3 < 20:
+        return 0
+    c = raw_cksum(l4[: l3 - 20]) + ipv4_phdr_cksum(ip, 0)
+    c = (c >> 16) + (c & 0xFFFF)
+    c = (~c) & 0xFFFF
+    return 0xFFFF if c == 0 else c
+
+
+def tcp_checksums(frame: bytearray, ip_off: int = 14, l4_off: int = 34) -> tuple[int, int]:
+    """In-place flag-off branch of tcp_checksums(); returns (ip.chksum, tcp.chksum)
+    as the native u16 values the reference stores."""
+    frame[ip_off + 10: ip_off + 12] = b"\0\0"
+    frame[l4_off + 16: l4_off + 18] = b"\0\0"
+    ip = bytes(frame[ip_off: ip_off + 20])
+    ipc = ipv4_cksum(ip)
+    frame[ip_off + 10: ip_off + 12] = ipc.to_bytes(2, "little")
+    tl = (frame[ip_off + 2] << 8) | frame[ip_off + 3]
+    l4 = bytes(frame[l4_off: l4_off + max(tl - 20, 0)])
+    tcpc = ipv4_udptcp_cksum(bytes(frame[ip_off: ip_off + 20]), l4)
+    frame[l4_off + 16: l4_off + 18] = tcpc.to_bytes(2, "little")
+    return ipc, tcpc
+
+
+def ip_phdr_xsum(ip_src_be: int, ip_dst_be: int, proto: int, l3_paylen: int) -> int:
+    s = (ip_src_be & 0xFFFF) + (ip_src_be >> 16) + (ip_dst_be & 0xFFFF) + (ip_dst_be >> 16)
+    s += proto << 8
+    s += ((l3_paylen & 0xFF) << 8) | (l3_paylen >> 8)
+    return _fold_exact(s)
+
+
+def raw_batch(buf: np.ndarray, offsets, lengths) -> np.ndarray:
+    """Vectorised-by-packet reference for RAW batches (uint16 per packet)."""
+    out = np.empty(len(offsets), np.uint16)
+    mv = memoryview(np.ascontiguousarray(buf, dtype=np.uint8))
+    for i, (o, n) in enumerate(zip(offsets, lengths)):
+        out[i] = raw_cksum(mv[int(o): int(o) + int(n)])
+    return out

@@ -1,0 +1,541 @@
+/*
+ * tasx_host.c -- C host layer of libtasx: argument checking, per-fast-path-core
+ * contexts, the deferred tcp_checksums()/tx_flush() surface and the
+ * end-to-end (host memory, PCIe) batch pipeline.  Kernels live in
+ * xsum_kernels.hip.  See include/tasx_xsum.h for the contract and the
+ * reference interfaces each entry point replaces.
+ *
+ * No CPU checksum code exists in this library: every checksum is computed by
+ * the GPU kernels, and a HIP failure is returned to the caller.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "tasx_kernels.h"
+
+#define NSLOT 3
+#define DEFAULT_SLOT_BYTES (64u << 20)
+#define DEFER_MAX_FRAME 65536u /* ip_off + 65535-byte datagram */
+
+static __thread char g_err[256];
+
+static int set_err(int code, const char *fmt, ...)
+{
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+static int hip_err(hipError_t e, const char *what)
+{
+  return set_err(-EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIPCHK(call)                                   \
+  do {                                                 \
+    hipError_t e_ = (call);                            \
+    if (e_ != hipSuccess)                              \
+      return hip_err(e_, #call);                       \
+  } while (0)
+
+int tasx_abi_version(void) { return TASX_ABI_VERSION; }
+const char *tasx_last_error(void) { return g_err; }
+
+int tasx_device_count(void)
+{
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess)
+    return hip_err(e, "hipGetDeviceCount");
+  return n;
+}
+
+/* ---------------------------------------------------------------------- */
+/* device-resident batches */
+
+/* lanes per packet: enough chunks per lane to keep loads in flight, the
+ * whole wave for jumbo / TSO segments */
+static int pick_group(uint32_t typical_len)
+{
+  if (typical_len >= 8192)
+    return 64;
+  return 16;
+}
+
+int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *len, uint32_t len0, uint32_t n,
+    uint16_t *out, void *stream)
+{
+  tasx_raw_params p;
+  int r;
+  if (n == 0)
+    return 0;
+  if (!out || (!base && !off))
+    return set_err(-EINVAL, "raw batch: NULL out/base");
+  if (!len && len0 > TASX_RAW_MAX_LEN)
+    return set_err(-EINVAL, "raw batch: len0 %u > %u", len0, TASX_RAW_MAX_LEN);
+  p.base = (const uint8_t *) base;
+  p.off = off;
+  p.len = len;
+  p.out = out;
+  p.stride = stride;
+  p.len0 = len0;
+  p.n = n;
+  r = tasx_launch_raw(&p, pick_group(len ? 1500 : len0), stream);
+  if (r != 0)
+    return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
+  return 0;
+}
+
+int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags, void *stream)
+{
+  tasx_tcp4_params p;
+  int r;
+  if (n == 0)
+    return 0;
+  if ((!base && !off) || (!out && !(flags & TASX_F_INPLACE)))
+    return set_err(-EINVAL, "tcp4 batch: NULL base/out");
+  if (out && ((uintptr_t) out & 3))
+    return set_err(-EINVAL, "tcp4 batch: out must be 4-byte aligned");
+  if (flags & ~TASX_F_INPLACE)
+    return set_err(-EINVAL, "tcp4 batch: unknown flags 0x%x", flags);
+  p.base = (uint8_t *) base;
+  p.off = off;
+  p.out = out;
+  p.stride = stride;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  p.flags = flags;
+  r = tasx_launch_tcp4(&p, 16, stream);
+  if (r != 0)
+    return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* contexts */
+
+struct tasx_ctx {
+  int in_use;
+  int device;
+  size_t slot_bytes;
+  hipStream_t st[NSLOT];
+  uint8_t *d_buf[NSLOT];
+  uint64_t *d_off[NSLOT];
+  uint16_t *d_out[NSLOT];
+  uint8_t *h_stage[NSLOT];
+  uint64_t *h_off[NSLOT];
+  uint16_t *h_out[NSLOT];
+  uint32_t slot_frames; /* offsets / results capacity per slot */
+  /* deferred frames */
+  uint8_t **pend_ip;
+  uint8_t **pend_l4;
+  uint32_t npend;
+};
+
+static struct tasx_ctx g_ctx[TASX_MAX_CTX];
+
+static struct tasx_ctx *get_ctx(unsigned id)
+{
+  if (id >= TASX_MAX_CTX || !g_ctx[id].in_use)
+    return NULL;
+  return &g_ctx[id];
+}
+
+static void ctx_release(struct tasx_ctx *c)
+{
+  int s;
+  for (s = 0; s < NSLOT; s++) {
+    if (c->st[s])
+      hipStreamDestroy(c->st[s]);
+    if (c->d_buf[s])
+      hipFree(c->d_buf[s]);
+    if (c->d_off[s])
+      hipFree(c->d_off[s]);
+    if (c->d_out[s])
+      hipFree(c->d_out[s]);
+    if (c->h_stage[s])
+      hipHostFree(c->h_stage[s]);
+    if (c->h_off[s])
+      hipHostFree(c->h_off[s]);
+    if (c->h_out[s])
+      hipHostFree(c->h_out[s]);
+  }
+  free(c->pend_ip);
+  free(c->pend_l4);
+  memset(c, 0, sizeof(*c));
+}
+
+int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
+{
+  struct tasx_ctx *c;
+  int s, ndev = 0;
+  hipError_t e;
+
+  if (ctx_id >= TASX_MAX_CTX)
+    return set_err(-EINVAL, "ctx id %u >= %u", ctx_id, TASX_MAX_CTX);
+  c = &g_ctx[ctx_id];
+  if (c->in_use)
+    return set_err(-EINVAL, "ctx %u already initialised", ctx_id);
+  e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess)
+    return hip_err(e, "hipGetDeviceCount");
+  if (device < 0 || device >= ndev)
+    return set_err(-ENODEV, "device %d not present (%d GPUs)", device, ndev);
+  memset(c, 0, sizeof(*c));
+  c->device = device;
+  c->slot_bytes = max_batch_bytes ? max_batch_bytes : DEFAULT_SLOT_BYTES;
+  /* one result pair / offset per 64 staged bytes is the densest TAS batch
+   * (minimum frame 60 B) */
+  c->slot_frames = (uint32_t) (c->slot_bytes / 64 + 1);
+  HIPCHK(hipSetDevice(device));
+  for (s = 0; s < NSLOT; s++) {
+    if ((e = hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipMalloc((void **) &c->d_buf[s], c->slot_bytes)) != hipSuccess ||
+        (e = hipMalloc((void **) &c->d_off[s], (size_t) c->slot_frames * 8)) != hipSuccess ||
+        (e = hipMalloc((void **) &c->d_out[s], (size_t) c->slot_frames * 4)) != hipSuccess ||
+        (e = hipHostMalloc((void **) &c->h_stage[s], c->slot_bytes, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void **) &c->h_off[s], (size_t) c->slot_frames * 8, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void **) &c->h_out[s], (size_t) c->slot_frames * 4, 0)) != hipSuccess) {
+      ctx_release(c);
+      return hip_err(e, "tasx_ctx_init allocation");
+    }
+  }
+  c->pend_ip = calloc(c->slot_frames, sizeof(*c->pend_ip));
+  c->pend_l4 = calloc(c->slot_frames, sizeof(*c->pend_l4));
+  if (!c->pend_ip || !c->pend_l4) {
+    ctx_release(c);
+    return set_err(-ENOMEM, "tasx_ctx_init: out of host memory");
+  }
+  c->in_use = 1;
+  return 0;
+}
+
+int tasx_ctx_destroy(unsigned ctx_id)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  hipSetDevice(c->device);
+  for (int s = 0; s < NSLOT; s++)
+    hipStreamSynchronize(c->st[s]);
+  ctx_release(c);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* end-to-end host batches: chunk -> H2D -> kernel -> D2H, NSLOT in flight */
+
+struct chunk_job {
+  uint32_t first, cnt;
+};
+
+static void finish_tcp4_chunk(struct tasx_ctx *c, int s, const struct chunk_job *j,
+    uint8_t *base, uint64_t stride, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags)
+{
+  const uint16_t *r = c->h_out[s];
+  if (out)
+    memcpy(out + 2 * (size_t) j->first, r, (size_t) j->cnt * 4);
+  if (flags & TASX_F_INPLACE) {
+    for (uint32_t k = 0; k < j->cnt; k++) {
+      uint8_t *f = base + (uint64_t) (j->first + k) * stride;
+      memcpy(f + ip_off + 10, &r[2 * k], 2);
+      memcpy(f + l4_off + 16, &r[2 * k + 1], 2);
+    }
+  }
+}
+
+int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
+    uint32_t flags)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  struct chunk_job jobs[NSLOT];
+  uint32_t per, first, k = 0;
+  int rc = 0;
+
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (n == 0)
+    return 0;
+  if (!base || stride == 0 || stride > c->slot_bytes || (!out && !(flags & TASX_F_INPLACE)))
+    return set_err(-EINVAL, "tcp4 host batch: bad base/stride/out");
+  if ((uint64_t) l4_off + 18 > stride || (uint64_t) ip_off + 20 > stride)
+    return set_err(-EINVAL, "tcp4 host batch: headers exceed the stride");
+  if (flags & ~TASX_F_INPLACE)
+    return set_err(-EINVAL, "tcp4 host batch: unknown flags 0x%x", flags);
+  HIPCHK(hipSetDevice(c->device));
+  per = (uint32_t) (c->slot_bytes / stride);
+  if (per > c->slot_frames)
+    per = c->slot_frames;
+  for (first = 0; first < n; first += per, k++) {
+    const int s = (int) (k % NSLOT);
+    tasx_tcp4_params p;
+    if (k >= NSLOT) {
+      HIPCHK(hipStreamSynchronize(c->st[s]));
+      finish_tcp4_chunk(c, s, &jobs[s], (uint8_t *) base, stride, ip_off, l4_off, out, flags);
+    }
+    jobs[s].first = first;
+    jobs[s].cnt = (n - first < per) ? n - first : per;
+    HIPCHK(hipMemcpyAsync(c->d_buf[s], (uint8_t *) base + (uint64_t) first * stride,
+        (size_t) jobs[s].cnt * stride, hipMemcpyHostToDevice, c->st[s]));
+    p.base = c->d_buf[s];
+    p.off = NULL;
+    p.out = c->d_out[s];
+    p.stride = stride;
+    p.n = jobs[s].cnt;
+    p.ip_off = ip_off;
+    p.l4_off = l4_off;
+    p.flags = 0;
+    if (tasx_launch_tcp4(&p, 16, c->st[s]) != 0)
+      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 4,
+        hipMemcpyDeviceToHost, c->st[s]));
+  }
+  /* drain: the last min(k, NSLOT) chunks, in submission order */
+  for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
+    const int s = (int) (d % NSLOT);
+    HIPCHK(hipStreamSynchronize(c->st[s]));
+    finish_tcp4_chunk(c, s, &jobs[s], (uint8_t *) base, stride, ip_off, l4_off, out, flags);
+  }
+  return rc;
+}
+
+int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
+    uint64_t stride, uint32_t len0, uint32_t n, uint16_t *out)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  struct chunk_job jobs[NSLOT];
+  uint32_t per, first, k = 0;
+
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (n == 0)
+    return 0;
+  if (!base || !out || len0 > TASX_RAW_MAX_LEN || stride < len0 || stride > c->slot_bytes)
+    return set_err(-EINVAL, "raw host batch: bad base/out/stride/len0");
+  HIPCHK(hipSetDevice(c->device));
+  per = (uint32_t) (c->slot_bytes / (stride ? stride : 1));
+  if (per > c->slot_frames)
+    per = c->slot_frames;
+  if (per == 0)
+    return set_err(-EINVAL, "raw host batch: stride larger than a slot");
+  for (first = 0; first < n; first += per, k++) {
+    const int s = (int) (k % NSLOT);
+    tasx_raw_params p;
+    if (k >= NSLOT) {
+      HIPCHK(hipStreamSynchronize(c->st[s]));
+      memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
+    }
+    jobs[s].first = first;
+    jobs[s].cnt = (n - first < per) ? n - first : per;
+    /* the last packet of a chunk only needs len0 bytes */
+    HIPCHK(hipMemcpyAsync(c->d_buf[s], (const uint8_t *) base + (uint64_t) first * stride,
+        (size_t) (jobs[s].cnt - 1) * stride + len0, hipMemcpyHostToDevice, c->st[s]));
+    p.base = c->d_buf[s];
+    p.off = NULL;
+    p.len = NULL;
+    p.out = c->d_out[s];
+    p.stride = stride;
+    p.len0 = len0;
+    p.n = jobs[s].cnt;
+    if (tasx_launch_raw(&p, pick_group(len0), c->st[s]) != 0)
+      return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
+    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 2,
+        hipMemcpyDeviceToHost, c->st[s]));
+  }
+  for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
+    const int s = (int) (d % NSLOT);
+    HIPCHK(hipStreamSynchronize(c->st[s]));
+    memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* deferred per-frame surface */
+
+int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off, uint16_t l4_off)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!frame || l4_off < ip_off + 20u)
+    return set_err(-EINVAL, "defer: NULL frame or l4_off < ip_off + 20");
+  if (c->npend >= c->slot_frames)
+    return set_err(-ENOSPC, "defer: %u frames pending", c->npend);
+  c->pend_ip[c->npend] = (uint8_t *) frame + ip_off;
+  c->pend_l4[c->npend] = (uint8_t *) frame + l4_off;
+  c->npend++;
+  return 0;
+}
+
+int tasx_tcp_checksums(unsigned ctx_id, void *nbh, void *p, uint32_t ip_s,
+    uint32_t ip_d, uint16_t l3_paylen)
+{
+  /* the flag-off branch uses only the frame; ip_s/ip_d/l3_paylen feed the
+   * offload branch (fast_flows.c:1062-1063), which stays in TAS */
+  (void) nbh;
+  (void) ip_s;
+  (void) ip_d;
+  (void) l3_paylen;
+  return tasx_defer_tcp4(ctx_id, p, TASX_TAS_IP_OFF, TASX_TAS_L4_OFF);
+}
+
+int tasx_fast_flows_kernelxsums(unsigned ctx_id, void *nbh, void *p)
+{
+  (void) nbh;
+  return tasx_defer_tcp4(ctx_id, p, TASX_TAS_IP_OFF, TASX_TAS_L4_OFF);
+}
+
+int tasx_pending(unsigned ctx_id)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  return (int) c->npend;
+}
+
+/* Gather every pending frame as [20-byte IPv4 header | L4 segment] into
+ * pinned staging (16-byte aligned records: the sum is relative to the header
+ * / segment start, so where a record sits does not change it), run the TCP4
+ * kernel with ip_off 0 / l4_off 20, and store the two results into the
+ * frames. */
+int tasx_flush(unsigned ctx_id)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  uint32_t i, start = 0;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (c->npend == 0)
+    return 0;
+  HIPCHK(hipSetDevice(c->device));
+  while (start < c->npend) {
+    const int s = 0;
+    uint8_t *stage = c->h_stage[s];
+    uint64_t *offs = c->h_off[s];
+    size_t pos = 0;
+    tasx_tcp4_params p;
+    uint32_t cnt = 0;
+    for (i = start; i < c->npend; i++) {
+      const uint8_t *ip = c->pend_ip[i];
+      uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+      uint32_t l4len = tl > 20 ? tl - 20 : 0;
+      /* the kernel reads the checksum field of short segments too */
+      uint32_t cp = l4len < 18 ? 18 : l4len;
+      size_t rec = (20 + (size_t) cp + 15) & ~(size_t) 15;
+      if (pos + rec > c->slot_bytes) {
+        if (cnt == 0)
+          return set_err(-EINVAL, "flush: frame of %zu B exceeds the staging slot", rec);
+        break;
+      }
+      memcpy(stage + pos, ip, 20);
+      memcpy(stage + pos + 20, c->pend_l4[i], cp);
+      offs[cnt++] = pos;
+      pos += rec;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_buf[s], stage, pos, hipMemcpyHostToDevice, c->st[s]));
+    HIPCHK(hipMemcpyAsync(c->d_off[s], offs, (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
+    p.base = c->d_buf[s];
+    p.off = c->d_off[s];
+    p.out = c->d_out[s];
+    p.stride = 0;
+    p.n = cnt;
+    p.ip_off = 0;
+    p.l4_off = 20;
+    p.flags = 0;
+    if (tasx_launch_tcp4(&p, 16, c->st[s]) != 0)
+      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4,
+        hipMemcpyDeviceToHost, c->st[s]));
+    HIPCHK(hipStreamSynchronize(c->st[s]));
+    for (i = 0; i < cnt; i++) {
+      memcpy(c->pend_ip[start + i] + 10, &c->h_out[s][2 * i], 2);
+      memcpy(c->pend_l4[start + i] + 16, &c->h_out[s][2 * i + 1], 2);
+    }
+    start += cnt;
+  }
+  c->npend = 0;
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* memory helpers */
+
+void *tasx_host_alloc(size_t bytes)
+{
+  void *p = NULL;
+  hipError_t e = hipHostMalloc(&p, bytes, 0);
+  if (e != hipSuccess) {
+    hip_err(e, "hipHostMalloc");
+    return NULL;
+  }
+  return p;
+}
+
+int tasx_host_free(void *p)
+{
+  HIPCHK(hipHostFree(p));
+  return 0;
+}
+
+int tasx_host_register(void *p, size_t bytes)
+{
+  HIPCHK(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return 0;
+}
+
+int tasx_host_unregister(void *p)
+{
+  HIPCHK(hipHostUnregister(p));
+  return 0;
+}
+
+void *tasx_dev_alloc(int device, size_t bytes)
+{
+  void *p = NULL;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess)
+    e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    hip_err(e, "hipMalloc");
+    return NULL;
+  }
+  return p;
+}
+
+int tasx_dev_free(void *p)
+{
+  HIPCHK(hipFree(p));
+  return 0;
+}
+
+int tasx_memcpy_h2d(void *dst, const void *src, size_t bytes)
+{
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int tasx_memcpy_d2h(void *dst, const void *src, size_t bytes)
+{
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int tasx_stream_sync(void *stream)
+{
+  HIPCHK(hipStreamSynchronize((hipStream_t) stream));
+  return 0;
+}

@@ -1,0 +1,43 @@
+/* tasx_kernels.h -- internal interface between the C host layer (tasx_host.c)
+ * and the HIP kernels (xsum_kernels.hip).  Plain C structs, passed by value
+ * to the kernels. */
+#ifndef TASX_KERNELS_H_
+#define TASX_KERNELS_H_
+
+#include <stdint.h>
+
+#include "../../include/tasx_xsum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tasx_raw_params {
+  const uint8_t *base;   /* device pointer */
+  const uint64_t *off;   /* device, n entries, or NULL -> i * stride */
+  const uint32_t *len;   /* device, n entries, or NULL -> len0 */
+  uint16_t *out;         /* device, n entries */
+  uint64_t stride;
+  uint32_t len0;
+  uint32_t n;
+} tasx_raw_params;
+
+typedef struct tasx_tcp4_params {
+  uint8_t *base;         /* device pointer to frames */
+  const uint64_t *off;   /* device, n entries, or NULL -> i * stride */
+  uint16_t *out;         /* device, 2n entries (4-byte aligned) or NULL */
+  uint64_t stride;
+  uint32_t n;
+  uint32_t ip_off;       /* IPv4 header offset in the frame (TAS: 14) */
+  uint32_t l4_off;       /* TCP header offset in the frame (TAS: 34) */
+  uint32_t flags;        /* TASX_F_* */
+} tasx_tcp4_params;
+
+/* group = lanes per packet (16, 32 or 64); 0 on success */
+int tasx_launch_raw(const tasx_raw_params *p, int group, void *stream);
+int tasx_launch_tcp4(const tasx_tcp4_params *p, int group, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

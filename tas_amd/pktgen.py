@@ -1,0 +1,145 @@
+"""Seeded synthetic packet batches (BASELINE.md / SURVEY.md section 8d).
+
+All randomness is splitmix64 with a fixed seed, so CPU oracle, GPU kernels,
+tests and bench see identical bytes.  Frame layout follows the reference's TX
+segment builder, flow_tx_segment() (/root/reference/tas/fast/fast_flows.c:877-955):
+14 B Ethernet + 20 B IPv4 (IHL 5) + 20 B TCP + 12 B timestamp option
+(10 B + 2 B pad) + payload; ip.len = 52 + payload; a frame starts at the mbuf
+data room (BUFFER_SIZE 2048, tas/fast/internal.h:34).  The checksum fields are
+filled with random bytes on purpose: tcp_checksums() must treat them as zero.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x7A5C_5EED_2026_0001
+MTU_MIX = (64, 576, 1500, 9000)
+ETH_LEN, IP_LEN, TCP_LEN, TS_OPT_LEN = 14, 20, 20, 12
+HDRS_LEN = ETH_LEN + IP_LEN + TCP_LEN + TS_OPT_LEN  # 66, fast_flows.c:887-888
+TCP_MSS = 1448                                      # fast_flows.c:37
+MBUF_ROOM = 2048                                    # tas/fast/internal.h:34
+
+_C1 = np.uint64(0x9E3779B97F4A7C15)
+_C2 = np.uint64(0xBF58476D1CE4E5B9)
+_C3 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(seed: int, n: int, start: int = 0) -> np.ndarray:
+    """n outputs of splitmix64 (Steele/Lea/Flood 2014) from `seed`, skipping `start`."""
+    i = np.arange(start + 1, start + n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + i * _C1
+        z = (z ^ (z >> np.uint64(30))) * _C2
+        z = (z ^ (z >> np.uint64(27))) * _C3
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def random_bytes(seed: int, nbytes: int, start_word: int = 0) -> np.ndarray:
+    words = splitmix64(seed, (nbytes + 7) // 8, start_word)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def raw_uniform(n: int, length: int = 1500, seed: int = SEED) -> tuple[np.ndarray, int]:
+    """n packed payloads of `length` bytes (stride == length). Returns (buf, stride)."""
+    return random_bytes(seed, n * length), length
+
+
+def mixed_lengths(n: int, seed: int = SEED, sizes=MTU_MIX) -> np.ndarray:
+    r = splitmix64(seed ^ 0x51ED, n)
+    return np.asarray(sizes, dtype=np.uint32)[(r % np.uint64(len(sizes))).astype(np.int64)]
+
+
+def raw_mixed(n: int, seed: int = SEED, sizes=MTU_MIX, align: int = 16, odd: bool = False):
+    """Mixed-MTU RAW batch in random order.  Offsets are `align`-aligned
+    (odd=True: lengths +/- 1 and offsets shifted by a random byte, for parity
+    of the odd-start / odd-tail paths).  Returns (buf, offsets u64, lengths u32)."""
+    lens = mixed_lengths(n, seed, sizes).astype(np.int64)
+    if odd:
+        jitter = (splitmix64(seed ^ 0x0DD, n) % np.uint64(3)).astype(np.int64) - 1
+        lens = np.maximum(lens + jitter, 0)
+        shift = (splitmix64(seed ^ 0x5A1F, n) % np.uint64(16)).astype(np.int64)
+    else:
+        shift = np.zeros(n, np.int64)
+    slot = (lens + shift + align - 1) // align * align
+    offs = np.zeros(n, np.int64)
+    np.cumsum(slot[:-1], out=offs[1:])
+    offs += shift
+    total = int(offs[-1] + lens[-1]) if n else 0
+    buf = random_bytes(seed ^ 0xB0F, total + 16)
+    return buf, offs.astype(np.uint64), lens.astype(np.uint32)
+
+
+def tcp4_frames(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SEED,
+                ip_total_len=None) -> np.ndarray:
+    """n TAS TX data segments at `stride` (one mbuf data room each).
+    `payload` is an int or a per-frame array; `ip_total_len` overrides ip.len
+    (e.g. 65535 for the TSO config, where stride must hold 14 + 65535 bytes)."""
+    payload = np.broadcast_to(np.asarray(payload, dtype=np.int64), (n,))
+    if ip_total_len is None:
+        tl = HDRS_LEN - ETH_LEN + payload
+    else:
+        tl = np.broadcast_to(np.asarray(ip_total_len, dtype=np.int64), (n,))
+    assert int((ETH_LEN + tl).max(initial=0)) <= stride or n == 0
+    buf = random_bytes(seed, n * stride)
+    f = buf.reshape(n, stride)
+    h = random_bytes(seed ^ 0x4EAD, n * 16).reshape(n, 16)  # per-frame header entropy
+    f[:, 12] = 0x08
+    f[:, 13] = 0x00                                   # eth.type = IP
+    ip = ETH_LEN
+    f[:, ip + 0] = 0x45                               # v4, IHL 5
+    f[:, ip + 1] = h[:, 0] & 0x3                      # tos: ECN bits only
+    f[:, ip + 2] = (tl >> 8) & 0xFF
+    f[:, ip + 3] = tl & 0xFF                          # ip.len
+    f[:, ip + 4] = 0
+    f[:, ip + 5] = 3                                  # ip.id = 3 (fast_flows.c:898)
+    f[:, ip + 6] = 0
+    f[:, ip + 7] = 0
+    f[:, ip + 8] = 0xFF                               # ttl
+    f[:, ip + 9] = 6                                  # proto TCP
+    # ip.chksum (ip+10..11) keeps random bytes
+    f[:, ip + 12: ip + 20] = h[:, 1:9]                # src, dst
+    t = ETH_LEN + IP_LEN
+    f[:, t + 12] = (5 + TS_OPT_LEN // 4) << 4          # hdrlen 8 words
+    f[:, t + 13] = 0x18                               # PSH|ACK
+    # tcp.chksum (t+16..17) keeps random bytes
+    f[:, t + 18] = 0
+    f[:, t + 19] = 0                                  # urgp
+    o = t + TCP_LEN
+    f[:, o + 0] = 8
+    f[:, o + 1] = 10                                  # TS option kind/len
+    f[:, o + 10] = 0
+    f[:, o + 11] = 0                                  # pad
+    return buf
+
+
+def kat_frame() -> bytearray:
+    """The window-update segment built by the reference unit test
+    test_rxbump_fc_reopen_notx (tests/tas_unit/fastpath.c:18-22,68-89,187-207
+    -> fast_flows_bump -> flow_tx_segment, fast_flows.c:886-928): zero MACs,
+    10.1.2.1:23456 -> 10.1.2.3:12345, seq 0, ack 0, wnd 1024, ip.id 3, TTL 255,
+    ip.len 52, TS opt val 0 ecr 0, no payload.  66 bytes."""
+    f = bytearray(HDRS_LEN)
+    f[12:14] = b"\x08\x00"
+    ip = ETH_LEN
+    f[ip] = 0x45
+    f[ip + 2: ip + 4] = (52).to_bytes(2, "big")
+    f[ip + 4: ip + 6] = (3).to_bytes(2, "big")
+    f[ip + 8] = 0xFF
+    f[ip + 9] = 6
+    f[ip + 12: ip + 16] = bytes([10, 1, 2, 1])
+    f[ip + 16: ip + 20] = bytes([10, 1, 2, 3])
+    t = ETH_LEN + IP_LEN
+    f[t: t + 2] = (23456).to_bytes(2, "big")
+    f[t + 2: t + 4] = (12345).to_bytes(2, "big")
+    f[t + 12: t + 14] = ((8 << 12) | 0x18).to_bytes(2, "big")
+    f[t + 14: t + 16] = (1024).to_bytes(2, "big")
+    f[t + 20] = 8
+    f[t + 21] = 10
+    return f
+
+
+# expected results for kat_frame(): network-order bytes a3 bb / cf d7
+# (hand-derived in SURVEY.md section 8c; stored as native LE u16)
+KAT_IP_CHKSUM = 0xBBA3
+KAT_TCP_CHKSUM = 0xD7CF

@@ -1,0 +1,228 @@
+"""Python host mirror of the checksum path's interface, over libtasx's C ABI.
+
+Names follow the reference (/root/reference):
+
+* ``tcp_checksums(ctx_id, frame)`` -- tcp_checksums() flag-off branch,
+  tas/fast/fast_flows.c:1058-1069: records the frame; ``tx_flush(ctx_id)``
+  (tas/fast/fastemu.c:544-566) checksums every recorded frame on the GPU and
+  stores ip.chksum / tcp.chksum into it.
+* ``fast_flows_kernelxsums(ctx_id, frame)`` -- tas/fast/fast_flows.c:1071-1076.
+* ``raw_cksum_batch`` / ``tcp4_cksum_batch`` -- device-resident batches of
+  rte_raw_cksum / (rte_ipv4_cksum, rte_ipv4_udptcp_cksum), the DPDK 19.11 calls
+  the reference makes per frame.
+
+PyTorch is plumbing here (device memory, streams); the checksum work is the HIP
+kernels in libtasx.so.  There is no CPU fallback: if the library cannot be
+loaded or a call fails, a ``TasxError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  -- must be imported first: libtasx then binds torch's HIP runtime
+
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libtasx.so"
+_lib = None
+
+TASX_F_INPLACE = 0x1
+TAS_IP_OFF = 14
+TAS_L4_OFF = 34
+RAW_MAX_LEN = 131073
+MAX_CTX = 16
+
+_c_int, _c_u16, _c_u32, _c_u64 = ctypes.c_int, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
+_vp, _sz, _uns = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint
+
+# name -> (restype, argtypes); mirrors include/tasx_xsum.h
+SIGNATURES = {
+    "tasx_abi_version": (_c_int, []),
+    "tasx_last_error": (ctypes.c_char_p, []),
+    "tasx_device_count": (_c_int, []),
+    "tasx_raw_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _vp, _vp]),
+    "tasx_tcp4_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp]),
+    "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
+    "tasx_ctx_destroy": (_c_int, [_uns]),
+    "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
+    "tasx_raw_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _vp]),
+    "tasx_tcp_checksums": (_c_int, [_uns, _vp, _vp, _c_u32, _c_u32, _c_u16]),
+    "tasx_fast_flows_kernelxsums": (_c_int, [_uns, _vp, _vp]),
+    "tasx_defer_tcp4": (_c_int, [_uns, _vp, _c_u16, _c_u16]),
+    "tasx_pending": (_c_int, [_uns]),
+    "tasx_flush": (_c_int, [_uns]),
+    "tasx_host_alloc": (_vp, [_sz]),
+    "tasx_host_free": (_c_int, [_vp]),
+    "tasx_host_register": (_c_int, [_vp, _sz]),
+    "tasx_host_unregister": (_c_int, [_vp]),
+    "tasx_dev_alloc": (_vp, [_c_int, _sz]),
+    "tasx_dev_free": (_c_int, [_vp]),
+    "tasx_memcpy_h2d": (_c_int, [_vp, _vp, _sz]),
+    "tasx_memcpy_d2h": (_c_int, [_vp, _vp, _sz]),
+    "tasx_stream_sync": (_c_int, [_vp]),
+}
+
+
+class TasxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        self.code = code
+        name = errno.errorcode.get(-code, str(code))
+        super().__init__(f"{what}: {name} ({last_error()})")
+
+
+def library_path() -> Path:
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    """Load libtasx.so (built in-tree by tas_amd.build / __graft_entry__.build)."""
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise RuntimeError(
+                f"libtasx.so not built ({_LIB_PATH}); run python -c 'import __graft_entry__ as g; g.build()'")
+        L = ctypes.CDLL(str(_LIB_PATH), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    if _lib is None:
+        return ""
+    s = _lib.tasx_last_error()
+    return s.decode() if s else ""
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise TasxError(rc, what)
+    return rc
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+# ---------------------------------------------------------------------------
+# device-resident batches
+
+def raw_cksum_batch(buf: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
+                    lengths: torch.Tensor | None = None, stride: int = 0, len0: int = 0,
+                    out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """out[i] = rte_raw_cksum(buf + off_i, len_i) on the GPU; int16 tensor holding
+    the uint16 results (view as uint16 on the host)."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=buf.device)
+    if offsets is not None:
+        assert offsets.dtype in (torch.int64,) and offsets.numel() >= n
+    if lengths is not None:
+        assert lengths.dtype == torch.int32 and lengths.numel() >= n
+    assert out.numel() >= n and out.element_size() == 2
+    _check(lib().tasx_raw_cksum_batch_dev(_ptr(buf), _ptr(offsets), stride, _ptr(lengths), len0,
+                                          n, _ptr(out), _stream(stream)), "tasx_raw_cksum_batch_dev")
+    return out
+
+
+def tcp4_cksum_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
+                     stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
+                     out: torch.Tensor | None = None, inplace: bool = False,
+                     want_out: bool = True, stream=None) -> torch.Tensor | None:
+    """tcp_checksums() flag-off branch for n frames on the GPU.  Returns an int16
+    tensor of 2n values: [ip.chksum, tcp.chksum] per frame (uint16 bit patterns)."""
+    if out is None and want_out:
+        out = torch.empty(2 * n, dtype=torch.int16, device=frames.device)
+    if offsets is not None:
+        assert offsets.dtype == torch.int64 and offsets.numel() >= n
+    flags = TASX_F_INPLACE if inplace else 0
+    _check(lib().tasx_tcp4_cksum_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
+                                           _ptr(out), flags, _stream(stream)),
+           "tasx_tcp4_cksum_batch_dev")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# contexts, deferred surface, end-to-end host batches
+
+def ctx_init(ctx_id: int, device: int = 0, max_batch_bytes: int = 0) -> None:
+    _check(lib().tasx_ctx_init(ctx_id, device, max_batch_bytes), "tasx_ctx_init")
+
+
+def ctx_destroy(ctx_id: int) -> None:
+    _check(lib().tasx_ctx_destroy(ctx_id), "tasx_ctx_destroy")
+
+
+def tcp_checksums(ctx_id: int, frame_addr: int, nbh: int | None = None, ip_s: int = 0,
+                  ip_d: int = 0, l3_paylen: int = 0) -> None:
+    _check(lib().tasx_tcp_checksums(ctx_id, nbh, frame_addr, ip_s, ip_d, l3_paylen),
+           "tasx_tcp_checksums")
+
+
+def fast_flows_kernelxsums(ctx_id: int, frame_addr: int, nbh: int | None = None) -> None:
+    _check(lib().tasx_fast_flows_kernelxsums(ctx_id, nbh, frame_addr), "tasx_fast_flows_kernelxsums")
+
+
+def defer_tcp4(ctx_id: int, frame_addr: int, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF) -> None:
+    _check(lib().tasx_defer_tcp4(ctx_id, frame_addr, ip_off, l4_off), "tasx_defer_tcp4")
+
+
+def pending(ctx_id: int) -> int:
+    return _check(lib().tasx_pending(ctx_id), "tasx_pending")
+
+
+def tx_flush(ctx_id: int) -> None:
+    _check(lib().tasx_flush(ctx_id), "tasx_flush")
+
+
+def tcp4_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, n: int, out_addr: int | None,
+                          ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
+                          inplace: bool = False) -> None:
+    flags = TASX_F_INPLACE if inplace else 0
+    _check(lib().tasx_tcp4_cksum_batch_host(ctx_id, base_addr, stride, n, ip_off, l4_off,
+                                            out_addr, flags), "tasx_tcp4_cksum_batch_host")
+
+
+def raw_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, len0: int, n: int,
+                         out_addr: int) -> None:
+    _check(lib().tasx_raw_cksum_batch_host(ctx_id, base_addr, stride, len0, n, out_addr),
+           "tasx_raw_cksum_batch_host")
+
+
+class PinnedBuffer:
+    """Pinned host memory from tasx_host_alloc, exposed as a numpy array."""
+
+    def __init__(self, nbytes: int):
+        import numpy as np
+        self.nbytes = nbytes
+        self.addr = lib().tasx_host_alloc(nbytes)
+        if not self.addr:
+            raise TasxError(-errno.ENOMEM, "tasx_host_alloc")
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.addr))
+
+    def free(self) -> None:
+        if self.addr:
+            lib().tasx_host_free(self.addr)
+            self.addr = 0
+            self.array = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -1,0 +1,100 @@
+"""libtasx C-ABI checks that need no GPU: the library builds and loads, exports
+every entry point include/tasx_xsum.h declares (and the Python mirror binds
+them all), carries no CPU checksum code, and rejects bad arguments before any
+device work."""
+import ctypes
+import errno
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = ROOT / "include" / "tasx_xsum.h"
+
+
+def header_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \t\*]*?\b(tasx_\w+)\s*\(", text, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    from tas_amd import build
+    return build.build()
+
+
+@pytest.fixture(scope="module")
+def L(libpath):
+    from tas_amd import xsum
+    return xsum.lib()
+
+
+def test_header_parses():
+    fns = header_functions()
+    assert "tasx_tcp_checksums" in fns and "tasx_flush" in fns
+    assert len(fns) >= 20
+
+
+def test_exports_every_declared_symbol(libpath):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(libpath)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (tasx_\w+)", out))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_python_mirror_binds_every_symbol(L):
+    from tas_amd import xsum
+    assert sorted(xsum.SIGNATURES) == header_functions()
+    for name in header_functions():
+        assert getattr(L, name) is not None
+
+
+def test_no_cpu_checksum_in_product(libpath):
+    """The product library must not contain or link the oracle (no CPU fallback)."""
+    syms = subprocess.run(["nm", "-D", str(libpath)], capture_output=True, text=True, check=True).stdout
+    assert "oracle" not in syms
+    dyn = subprocess.run(["readelf", "-d", str(libpath)], capture_output=True, text=True, check=True).stdout
+    assert "liboracle" not in dyn
+    assert "libamdhip64" in dyn
+
+
+def test_gfx950_code_object(libpath):
+    data = libpath.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # the .hip_fatbin code object
+    secs = subprocess.run(["readelf", "-S", str(libpath)], capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in secs
+
+
+def test_abi_version_and_errors_without_gpu(L):
+    assert L.tasx_abi_version() == 1
+    # argument errors are reported before any HIP call
+    rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
+    assert rc == -errno.EINVAL
+    rc = L.tasx_raw_cksum_batch_dev(ctypes.c_void_p(16), None, 0, None, 200000, 5,
+                                    ctypes.c_void_p(16), None)
+    assert rc == -errno.EINVAL  # len0 > TASX_RAW_MAX_LEN
+    rc = L.tasx_tcp4_cksum_batch_dev(ctypes.c_void_p(16), None, 2048, 4, 14, 34,
+                                     ctypes.c_void_p(18), 0, None)
+    assert rc == -errno.EINVAL  # misaligned out
+    rc = L.tasx_tcp4_cksum_batch_dev(ctypes.c_void_p(16), None, 2048, 4, 14, 34, None, 0, None)
+    assert rc == -errno.EINVAL  # no out and not in place
+    assert b"tcp4" in L.tasx_last_error()
+    # n == 0 is a no-op
+    assert L.tasx_raw_cksum_batch_dev(None, None, 0, None, 0, 0, None, None) == 0
+    # contexts: not initialised / out of range
+    assert L.tasx_defer_tcp4(3, ctypes.c_void_p(64), 14, 34) == -errno.EINVAL
+    assert L.tasx_flush(3) == -errno.EINVAL
+    assert L.tasx_pending(99) == -errno.EINVAL
+    assert L.tasx_ctx_destroy(0) == -errno.EINVAL
+
+
+def test_python_wrapper_raises(L):
+    from tas_amd import xsum
+    with pytest.raises(xsum.TasxError):
+        xsum.defer_tcp4(2, 4096)
+    with pytest.raises(xsum.TasxError):
+        xsum.tx_flush(2)

@@ -1,0 +1,323 @@
+"""GPU parity: the HIP kernels (through libtasx's C ABI) against the CPU oracle
+and the committed golden fixtures, bit-exact, at BASELINE.json's full sizes
+plus the edge cases the reference path has (odd starts / tails, empty and
+short segments, total_length < 20, the 0 -> 0xffff rules, in-place stores).
+
+Run on the MI355X box:  python -m pytest tests -m gpu -x -q
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from tas_amd import pktgen, xsum
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from tas_amd import build
+    build.build()
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    xsum.lib()
+    yield
+    torch.cuda.synchronize()
+
+
+def to_dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def u16(t: torch.Tensor) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint16)
+
+
+def dev_random(nbytes: int, seed: int) -> torch.Tensor:
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=DEV, generator=g)
+
+
+# ---------------------------------------------------------------------------
+# golden fixtures
+
+def test_golden_raw(raw_golden):
+    g = raw_golden
+    n = len(g["lengths"])
+    out = xsum.raw_cksum_batch(to_dev(g["buf"]), n, offsets=to_dev(g["offsets"].astype(np.int64)),
+                               lengths=to_dev(g["lengths"].astype(np.int32)))
+    np.testing.assert_array_equal(u16(out), g["expected"])
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3, 15])
+def test_golden_tcp4(tcp4_golden, shift):
+    g = tcp4_golden
+    n = len(g["offsets"])
+    buf = torch.zeros(g["frames"].size + 64, dtype=torch.uint8, device=DEV)
+    buf[shift:shift + g["frames"].size] = to_dev(g["frames"])
+    out = xsum.tcp4_cksum_batch(buf[shift:], n, stride=int(g["stride"]))
+    np.testing.assert_array_equal(u16(out), g["expected"])
+    # not in place: frames untouched
+    np.testing.assert_array_equal(buf[shift:shift + g["frames"].size].cpu().numpy(), g["frames"])
+
+
+def test_golden_tcp4_inplace(tcp4_golden, oracle):
+    g = tcp4_golden
+    n, stride = len(g["offsets"]), int(g["stride"])
+    dbuf = to_dev(g["frames"])
+    out = xsum.tcp4_cksum_batch(dbuf, n, stride=stride, inplace=True)
+    ref = g["frames"].copy()
+    oracle.tcp4_batch(ref, n, stride=stride, inplace=True)
+    np.testing.assert_array_equal(dbuf.cpu().numpy(), ref)
+    np.testing.assert_array_equal(u16(out), g["expected"])
+    # in place with no result array
+    dbuf2 = to_dev(g["frames"])
+    assert xsum.tcp4_cksum_batch(dbuf2, n, stride=stride, inplace=True, want_out=False) is None
+    np.testing.assert_array_equal(dbuf2.cpu().numpy(), ref)
+
+
+def test_kat_frame_on_gpu():
+    f = np.frombuffer(bytes(pktgen.kat_frame()) + bytes(30), np.uint8)
+    out = u16(xsum.tcp4_cksum_batch(to_dev(f), 1, stride=96))
+    assert (int(out[0]), int(out[1])) == (pktgen.KAT_IP_CHKSUM, pktgen.KAT_TCP_CHKSUM)
+
+
+# ---------------------------------------------------------------------------
+# RAW edge sweeps
+
+def test_raw_all_short_lengths_all_alignments(oracle):
+    lens, offs = [], []
+    pos = 0
+    for L in range(0, 300):
+        for sh in range(16):
+            pos = (pos + 15) // 16 * 16 + sh
+            offs.append(pos)
+            lens.append(L)
+            pos += L
+    buf = pktgen.random_bytes(5, pos + 32)
+    offs = np.asarray(offs, np.int64)
+    lens = np.asarray(lens, np.int32)
+    n = len(lens)
+    exp = oracle.raw_batch(buf, n, offsets=offs, lengths=lens)
+    got = u16(xsum.raw_cksum_batch(to_dev(buf), n, offsets=to_dev(offs), lengths=to_dev(lens)))
+    np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("fill", [0x00, 0xFF, 0x01])
+def test_raw_constant_buffers(fill):
+    """All-zero -> 0, all-0xff -> 0xffff (never 0), long buffers up to TASX_RAW_MAX_LEN."""
+    for L in (1, 2, 15, 16, 17, 1500, 65535, 131072, 131073):
+        buf = torch.full((L + 32,), fill, dtype=torch.uint8, device=DEV)
+        exp = _raw_np(bytes([fill]) * L)
+        for sh in (0, 1):
+            out = u16(xsum.raw_cksum_batch(buf[sh:], 1, len0=L, stride=0))
+            assert int(out[0]) == exp, (L, sh)
+        if fill == 0:
+            assert exp == 0
+        if fill == 0xFF and L % 2 == 0:
+            assert exp == 0xFFFF
+
+
+def _raw_np(b: bytes) -> int:
+    from oracle import xsum_ref
+    return xsum_ref.raw_cksum(b)
+
+
+def test_raw_uniform_stride_mode(oracle):
+    for L, stride in ((1500, 1500), (1500, 1504), (1499, 1501), (64, 64), (9000, 9000)):
+        n = 3000
+        buf = pktgen.random_bytes(L * 7 + stride, n * stride + 16)
+        exp = oracle.raw_batch(buf, n, stride=stride, len0=L)
+        got = u16(xsum.raw_cksum_batch(to_dev(buf), n, stride=stride, len0=L))
+        np.testing.assert_array_equal(got, exp, err_msg=f"L={L} stride={stride}")
+
+
+def test_raw_mixed_odd(oracle):
+    buf, offs, lens = pktgen.raw_mixed(20000, seed=11, odd=True)
+    n = len(lens)
+    exp = oracle.raw_batch(buf, n, offsets=offs, lengths=lens)
+    got = u16(xsum.raw_cksum_batch(to_dev(buf), n, offsets=to_dev(offs.astype(np.int64)),
+                                   lengths=to_dev(lens.astype(np.int32))))
+    np.testing.assert_array_equal(got, exp)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configs at full size, bit-exact against the C oracle
+
+def test_config2_raw_64k_1500(oracle):
+    n, L = 65536, 1500
+    d = dev_random(n * L, 2)
+    h = d.cpu().numpy()
+    exp = oracle.raw_batch(h, n, stride=L, len0=L)
+    got = u16(xsum.raw_cksum_batch(d, n, stride=L, len0=L))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_config2_tcp4_64k_tas_frames(oracle):
+    n = 65536
+    frames = pktgen.tcp4_frames(n, payload=pktgen.TCP_MSS, stride=2048)
+    exp = oracle.tcp4_batch(frames, n, stride=2048)
+    got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=2048))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_config3_mixed_mtu_1M(oracle):
+    n = 1 << 20
+    lens = pktgen.mixed_lengths(n, seed=3).astype(np.int64)
+    slot = (lens + 15) // 16 * 16
+    offs = np.zeros(n, np.int64)
+    np.cumsum(slot[:-1], out=offs[1:])
+    total = int(offs[-1] + slot[-1])
+    d = dev_random(total, 3)
+    h = d.cpu().numpy()
+    exp = oracle.raw_batch(h, n, offsets=offs, lengths=lens)
+    got = u16(xsum.raw_cksum_batch(d, n, offsets=to_dev(offs), lengths=to_dev(lens.astype(np.int32))))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_config4_shard_1M_1500(oracle):
+    """One GPU's shard of the 8M x 1500 B 8-GPU config (1,048,576 packets)."""
+    n, L = 1 << 20, 1500
+    d = dev_random(n * L, 4)
+    h = d.cpu().numpy()
+    exp = oracle.raw_batch(h, n, stride=L, len0=L)
+    got = u16(xsum.raw_cksum_batch(d, n, stride=L, len0=L))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_config5_tso_64k_segments(oracle):
+    """16,384 TSO-sized segments, ip.len 65535 (L4 65,515 B, odd tail)."""
+    n, stride = 16384, 65552
+    frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=5, ip_total_len=65535)
+    exp = oracle.tcp4_batch(frames, n, stride=stride)
+    d = to_dev(frames)
+    got = u16(xsum.tcp4_cksum_batch(d, n, stride=stride))
+    np.testing.assert_array_equal(got, exp)
+    # receiver-side property on the device: after in-place stores every IP header sums to 0xffff
+    xsum.tcp4_cksum_batch(d, n, stride=stride, inplace=True, want_out=False)
+    hdr = u16(xsum.raw_cksum_batch(d[14:], n, stride=stride, len0=20))
+    assert np.all(hdr == 0xFFFF)
+
+
+# ---------------------------------------------------------------------------
+# TCP4 edges
+
+def test_tcp4_varied_payloads_offsets(oracle):
+    n = 4096
+    pay = (pktgen.splitmix64(77, n) % np.uint64(1449)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=77)
+    # scatter the frames to random (odd and even) offsets in a bigger buffer
+    shift = (pktgen.splitmix64(78, n) % np.uint64(200)).astype(np.int64)
+    offs = np.arange(n, dtype=np.int64) * 2304 + shift
+    big = np.zeros(n * 2304 + 2048, np.uint8)
+    for i in range(n):
+        big[offs[i]:offs[i] + 2048] = frames[i * 2048:(i + 1) * 2048]
+    exp = oracle.tcp4_batch(big, n, offsets=offs)
+    got = u16(xsum.tcp4_cksum_batch(to_dev(big), n, offsets=to_dev(offs)))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_tcp4_ack_sized_and_short(oracle):
+    """ACKs (ip.len 52), SYN-sized (56), and total_length 0..60."""
+    n = 61 * 8
+    tl = np.tile(np.arange(61), 8)
+    frames = pktgen.tcp4_frames(n, payload=0, stride=128, seed=9, ip_total_len=tl)
+    exp = oracle.tcp4_batch(frames, n, stride=128)
+    got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=128))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_tcp4_nonstandard_offsets(oracle):
+    """ip/l4 offsets other than TAS's 14/34 (e.g. VLAN-tagged, IP options)."""
+    n = 1024
+    frames = pktgen.tcp4_frames(n, payload=700, stride=2048, seed=12)
+    exp = oracle.tcp4_batch(frames, n, stride=2048, ip_off=14, l4_off=38)
+    got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=2048, ip_off=14, l4_off=38))
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_deterministic_and_n0():
+    frames = pktgen.tcp4_frames(1000, stride=2048)
+    d = to_dev(frames)
+    a = u16(xsum.tcp4_cksum_batch(d, 1000, stride=2048))
+    b = u16(xsum.tcp4_cksum_batch(d, 1000, stride=2048))
+    np.testing.assert_array_equal(a, b)
+    assert xsum.raw_cksum_batch(d, 0, len0=5).numel() == 0
+
+
+# ---------------------------------------------------------------------------
+# host-memory surfaces: deferred tcp_checksums()/tx_flush and end-to-end batches
+
+def test_deferred_tcp_checksums_flush(oracle):
+    xsum.ctx_init(0, 0, 1 << 20)
+    try:
+        n = 32  # TXBUF_SIZE, tas/include/fastpath.h:38
+        pay = np.arange(n) * 45
+        frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=21)
+        ref = frames.copy()
+        oracle.tcp4_batch(ref, n, stride=2048, inplace=True)
+        base = frames.ctypes.data
+        for i in range(n):
+            if i % 2:
+                xsum.tcp_checksums(0, base + i * 2048)
+            else:
+                xsum.fast_flows_kernelxsums(0, base + i * 2048)
+        assert xsum.pending(0) == n
+        xsum.tx_flush(0)
+        assert xsum.pending(0) == 0
+        np.testing.assert_array_equal(frames, ref)
+        # many flushes of varying size, including a frame larger than a slot's share
+        for k in (1, 7, 200):
+            fr = pktgen.tcp4_frames(k, payload=1448, stride=2048, seed=100 + k)
+            rf = fr.copy()
+            oracle.tcp4_batch(rf, k, stride=2048, inplace=True)
+            for i in range(k):
+                xsum.defer_tcp4(0, fr.ctypes.data + i * 2048)
+            xsum.tx_flush(0)
+            np.testing.assert_array_equal(fr, rf)
+    finally:
+        xsum.ctx_destroy(0)
+
+
+def test_host_batch_end_to_end(oracle):
+    xsum.ctx_init(1, 0, 8 << 20)  # small slots: many pipelined chunks
+    try:
+        n = 20000
+        frames = pktgen.tcp4_frames(n, stride=2048, seed=31)
+        pin = xsum.PinnedBuffer(frames.size)
+        pin.array[:] = frames
+        out = np.empty(2 * n, np.uint16)
+        xsum.tcp4_cksum_batch_host(1, pin.addr, 2048, n, out.ctypes.data, inplace=True)
+        ref = frames.copy()
+        exp = oracle.tcp4_batch(ref, n, stride=2048, inplace=True)
+        np.testing.assert_array_equal(out, exp)
+        np.testing.assert_array_equal(pin.array, ref)
+        pin.free()
+        raw, stride = pktgen.raw_uniform(30000, 1500, seed=32)
+        pin = xsum.PinnedBuffer(raw.size)
+        pin.array[:] = raw
+        out = np.empty(30000, np.uint16)
+        xsum.raw_cksum_batch_host(1, pin.addr, 1500, 1500, 30000, out.ctypes.data)
+        np.testing.assert_array_equal(out, oracle.raw_batch(raw, 30000, stride=1500, len0=1500))
+        pin.free()
+    finally:
+        xsum.ctx_destroy(1)
+
+
+def test_ctx_errors():
+    with pytest.raises(xsum.TasxError):
+        xsum.ctx_init(0, 99)
+    xsum.ctx_init(2, 0, 1 << 20)
+    try:
+        with pytest.raises(xsum.TasxError):
+            xsum.ctx_init(2, 0)
+        f = np.zeros(64, np.uint8)
+        with pytest.raises(xsum.TasxError):
+            xsum.defer_tcp4(2, f.ctypes.data, 14, 20)  # l4_off < ip_off + 20
+    finally:
+        xsum.ctx_destroy(2)
