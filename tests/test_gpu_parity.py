@@ -20,8 +20,6 @@ DEV = "cuda:0"
 
 @pytest.fixture(scope="module", autouse=True)
 def _lib():
-    from tas_amd import build
-    build.build()
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
     xsum.lib()
     yield
