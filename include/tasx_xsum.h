@@ -87,6 +87,16 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint16_t *out, uint32_t flags, void *stream);
 
+/* Same, with frame-length hints: flen[i] (or flen0 when flen == NULL) is the
+ * frame's length from its start -- the mbuf data_len that tx_send() sets
+ * (tas/fast/fastemu.h:81-95) before tx_flush().  Hints only let the kernel
+ * issue a frame's data loads together with its header loads; results always
+ * follow ip.total_length, whatever the hint (0 = no hint). */
+int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
+    void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Per-fast-path-core contexts (one per dataplane_context, no shared state,
  * no locks: tas/fast/fastemu.c:87-91).  A context owns a GPU, streams, pinned
@@ -122,6 +132,13 @@ int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off,
 /* frames recorded and not yet flushed */
 int tasx_pending(unsigned ctx_id);
 int tasx_flush(unsigned ctx_id);
+
+/* ---------------------------------------------------------------------- */
+/* Kernel selection, for tuning and A/B tests (process-wide, not thread-safe
+ * against concurrent launches).  variant 0 = automatic (flat-stream kernel),
+ * 1 = wave-per-packet kernel, 2..7 = fixed shapes; ppg = packets per lane
+ * group for the flat-stream kernels (0 = automatic). */
+int tasx_set_kernel_config(int variant, unsigned ppg);
 
 /* ---------------------------------------------------------------------- */
 /* Memory helpers (plumbing for callers without their own HIP code). */

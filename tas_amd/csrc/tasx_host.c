@@ -61,13 +61,17 @@ int tasx_device_count(void)
 /* ---------------------------------------------------------------------- */
 /* device-resident batches */
 
-/* lanes per packet: enough chunks per lane to keep loads in flight, the
- * whole wave for jumbo / TSO segments */
-static int pick_group(uint32_t typical_len)
+/* kernel selection (tasx_set_kernel_config); 0/0 = automatic */
+static int g_variant = 0;
+static unsigned g_ppg = 0;
+
+int tasx_set_kernel_config(int variant, unsigned ppg)
 {
-  if (typical_len >= 8192)
-    return 64;
-  return 16;
+  if (variant < 0 || variant > 13 || ppg > 64)
+    return set_err(-EINVAL, "kernel config %d/%u out of range", variant, ppg);
+  g_variant = variant;
+  g_ppg = ppg;
+  return 0;
 }
 
 int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
@@ -89,15 +93,16 @@ int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
   p.stride = stride;
   p.len0 = len0;
   p.n = n;
-  r = tasx_launch_raw(&p, pick_group(len ? 1500 : len0), stream);
+  r = tasx_launch_raw(&p, g_variant, g_ppg, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
   return 0;
 }
 
-int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
-    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
-    uint16_t *out, uint32_t flags, void *stream)
+int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
+    void *stream)
 {
   tasx_tcp4_params p;
   int r;
@@ -109,6 +114,7 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
     return set_err(-EINVAL, "tcp4 batch: out must be 4-byte aligned");
   if (flags & ~TASX_F_INPLACE)
     return set_err(-EINVAL, "tcp4 batch: unknown flags 0x%x", flags);
+  memset(&p, 0, sizeof(p));
   p.base = (uint8_t *) base;
   p.off = off;
   p.out = out;
@@ -117,10 +123,20 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
   p.ip_off = ip_off;
   p.l4_off = l4_off;
   p.flags = flags;
-  r = tasx_launch_tcp4(&p, 16, stream);
+  p.flen = flen;
+  p.flen0 = flen0;
+  r = tasx_launch_tcp4(&p, g_variant, g_ppg, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
   return 0;
+}
+
+int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags, void *stream)
+{
+  return tasx_tcp4_cksum_batch_dev_hint(base, off, stride, NULL, 0, n, ip_off,
+      l4_off, out, flags, stream);
 }
 
 /* ---------------------------------------------------------------------- */
@@ -291,6 +307,7 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     jobs[s].cnt = (n - first < per) ? n - first : per;
     HIPCHK(hipMemcpyAsync(c->d_buf[s], (uint8_t *) base + (uint64_t) first * stride,
         (size_t) jobs[s].cnt * stride, hipMemcpyHostToDevice, c->st[s]));
+    memset(&p, 0, sizeof(p));
     p.base = c->d_buf[s];
     p.off = NULL;
     p.out = c->d_out[s];
@@ -299,7 +316,8 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     p.ip_off = ip_off;
     p.l4_off = l4_off;
     p.flags = 0;
-    if (tasx_launch_tcp4(&p, 16, c->st[s]) != 0)
+
+    if (tasx_launch_tcp4(&p, g_variant, g_ppg, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 4,
         hipMemcpyDeviceToHost, c->st[s]));
@@ -351,7 +369,7 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     p.stride = stride;
     p.len0 = len0;
     p.n = jobs[s].cnt;
-    if (tasx_launch_raw(&p, pick_group(len0), c->st[s]) != 0)
+    if (tasx_launch_raw(&p, g_variant, g_ppg, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 2,
         hipMemcpyDeviceToHost, c->st[s]));
@@ -448,6 +466,7 @@ int tasx_flush(unsigned ctx_id)
     }
     HIPCHK(hipMemcpyAsync(c->d_buf[s], stage, pos, hipMemcpyHostToDevice, c->st[s]));
     HIPCHK(hipMemcpyAsync(c->d_off[s], offs, (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
+    memset(&p, 0, sizeof(p));
     p.base = c->d_buf[s];
     p.off = c->d_off[s];
     p.out = c->d_out[s];
@@ -456,7 +475,7 @@ int tasx_flush(unsigned ctx_id)
     p.ip_off = 0;
     p.l4_off = 20;
     p.flags = 0;
-    if (tasx_launch_tcp4(&p, 16, c->st[s]) != 0)
+    if (tasx_launch_tcp4(&p, g_variant, g_ppg, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4,
         hipMemcpyDeviceToHost, c->st[s]));

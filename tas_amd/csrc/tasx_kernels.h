@@ -31,11 +31,15 @@ typedef struct tasx_tcp4_params {
   uint32_t ip_off;       /* IPv4 header offset in the frame (TAS: 14) */
   uint32_t l4_off;       /* TCP header offset in the frame (TAS: 34) */
   uint32_t flags;        /* TASX_F_* */
+  const uint32_t *flen;  /* device, n frame-length hints (bytes from the frame
+                          * start, the mbuf data_len), or NULL -> flen0 */
+  uint32_t flen0;        /* uniform hint; 0 = none */
 } tasx_tcp4_params;
 
-/* group = lanes per packet (16, 32 or 64); 0 on success */
-int tasx_launch_raw(const tasx_raw_params *p, int group, void *stream);
-int tasx_launch_tcp4(const tasx_tcp4_params *p, int group, void *stream);
+/* variant: 0 auto (flat-stream kernel), 1 / 7 wave-per-packet kernels,
+ * 2..6 flat-stream shapes; ppg: packets per group (0 auto).  0 on success. */
+int tasx_launch_raw(const tasx_raw_params *p, int variant, uint32_t ppg, void *stream);
+int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t ppg, void *stream);
 
 #ifdef __cplusplus
 }

@@ -258,6 +258,512 @@ __global__ __launch_bounds__(kBlock) void tcp4_cksum_kernel(tasx_tcp4_params p)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Flat-stream kernels (default).  A group of G lanes owns `ppg` consecutive
+// packets.  Phase 1: lane j reads packet j's descriptor (and, for TCP4, its
+// 20-byte IPv4 header, total_length and checksum-field bytes) -- one load
+// latency for the whole group instead of one per packet -- and the group
+// scans the packets' chunk counts into an LDS table.  Phase 2: the group walks
+// the concatenation of its packets' aligned chunks as ONE flat stream, lane gl
+// taking flat chunks gl, gl+G, ... (each wave instruction loads up to 1 KiB of
+// consecutive chunks, U instructions in flight per lane), so short and long
+// packets keep every lane busy.  A lane's chunks of one packet are
+// consecutive, so it keeps one running sum and parks it in LDS
+// part[packet][lane] when it moves on.  Phase 3: lane j adds row j of `part`
+// and finishes packet j: fold, odd-start swap, TCP4 result rules, one store.
+
+struct FlatEnt {
+  uint64_t cb;   // address of the packet's first aligned 16-byte chunk
+  uint32_t pre;  // exclusive prefix of chunk counts within the group
+  uint32_t info; // head offset (bits 0..3) | (tail bytes - 1) (bits 4..7)
+};
+
+template <int G, int P, int U, bool TCP4, typename Prm>
+__global__ __launch_bounds__(kBlock) void flat_cksum_kernel(Prm p, uint32_t ppg)
+{
+  static_assert(P <= G && (G & (G - 1)) == 0 && G <= 64, "group shape");
+  constexpr int NG = kBlock / G;
+  constexpr int ROW = G + 4; // +16 B per row: conflict-free ds_read_b128 in phase 3
+  __shared__ FlatEnt ent[NG][P + 1];
+  __shared__ __attribute__((aligned(16))) uint32_t part[NG][P][ROW];
+
+  const int lg = threadIdx.x / G;
+  const int gl = threadIdx.x % G;
+  const uint64_t first = ((uint64_t) blockIdx.x * NG + lg) * ppg;
+  const uint32_t cnt = first < p.n ? (uint32_t) min((uint64_t) ppg, (uint64_t) p.n - first) : 0u;
+  const bool own = (uint32_t) gl < cnt;
+  const uint32_t i = (uint32_t) (first + (uint32_t) gl);
+
+  // ---- phase 1: the lane's own packet
+  const uint8_t *s = nullptr;
+  uint32_t len = 0, tl = 0, c_ip = 0, c_ph = 0, fix = 0;
+  uint8_t *ipp = nullptr, *l4p = nullptr;
+  if (own) {
+    if constexpr (TCP4) {
+      uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+      ipp = f + p.ip_off;
+      l4p = f + p.l4_off;
+      uint32_t w[10];
+#pragma unroll
+      for (int k = 0; k < 10; ++k)
+        w[k] = ld8(ipp + 2 * k) | (ld8(ipp + 2 * k + 1) << 8);
+      tl = bswap16(w[1]);
+      len = tl >= 20 ? tl - 20 : 0;
+#pragma unroll
+      for (int k = 0; k < 10; ++k)
+        c_ip += (k == 5) ? 0u : w[k];             // ip.chksum taken as 0
+      c_ph = w[6] + w[7] + w[8] + w[9] + (w[4] & 0xff00u); // src, dst, proto<<8
+      if (len > 16) {                             // tcp.chksum taken as 0
+        uint32_t fw = ld8(l4p + 16);
+        if (len > 17)
+          fw |= ld8(l4p + 17) << 8;
+        fix = (~fw) & 0xffffu;
+      }
+      s = l4p;
+    } else {
+      s = p.base + pkt_offset(p.off, p.stride, i);
+      len = p.len ? ldg(p.len, i) : p.len0;
+    }
+  }
+  uint32_t nch = 0, info = 0;
+  uint64_t cb = 0;
+  if (len) {
+    const uintptr_t a0 = (uintptr_t) s, a1 = a0 + len;
+    cb = a0 & ~(uintptr_t) 15;
+    nch = (uint32_t) ((((a1 + 15) & ~(uintptr_t) 15) - cb) >> 4);
+    info = (uint32_t) (a0 & 15) | ((uint32_t) (a1 - ((a1 - 1) & ~(uintptr_t) 15) - 1) << 4);
+  }
+  uint32_t inc = nch;
+#pragma unroll
+  for (int d = 1; d < G; d <<= 1) {
+    const uint32_t t = __shfl_up(inc, d, G);
+    if (gl >= d)
+      inc += t;
+  }
+  const uint32_t T = __shfl(inc, G - 1, G);
+  if (own)
+    ent[lg][gl] = FlatEnt{cb, inc - nch, info};
+  if (gl == 0)
+    ent[lg][cnt].pre = T; // sentinel
+  for (uint32_t k = 0; k < cnt; ++k)
+    part[lg][k][gl] = 0;
+  __syncthreads();
+
+  // ---- phase 2: flat stream over the group's chunks
+  if (cnt) {
+    uint64_t acc = 0;
+    int kacc = -1, k = 0;
+    FlatEnt e = ent[lg][0];
+    uint32_t knext = ent[lg][1].pre;
+    for (uint32_t f0 = (uint32_t) gl; f0 < T; f0 += (uint32_t) (G * U)) {
+      u32x4 v[U];
+      int ku[U], lo[U], hi[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t f = f0 + (uint32_t) (u * G);
+        ku[u] = -1;
+        lo[u] = 0;
+        hi[u] = 16;
+        v[u] = u32x4{0, 0, 0, 0};
+        if (f < T) {
+          while (f >= knext) {
+            ++k;
+            e = ent[lg][k];
+            knext = ent[lg][k + 1].pre;
+          }
+          const uint32_t c = f - e.pre;
+          ku[u] = k;
+          if (c == 0)
+            lo[u] = (int) (e.info & 15u);
+          if (f + 1 == knext)
+            hi[u] = (int) (e.info >> 4) + 1;
+          v[u] = ld16((const u32x4 *) e.cb, c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ku[u] >= 0) {
+          if (ku[u] != kacc) {
+            if (kacc >= 0)
+              part[lg][kacc][gl] = fold64_to_18(acc);
+            acc = 0;
+            kacc = ku[u];
+          }
+          if (lo[u] != 0 || hi[u] != 16)
+            v[u] = mask_chunk(v[u], lo[u], hi[u]);
+          acc = add_chunk(acc, v[u]);
+        }
+      }
+    }
+    if (kacc >= 0)
+      part[lg][kacc][gl] = fold64_to_18(acc);
+  }
+  __syncthreads();
+
+  // ---- phase 3: lane j finishes packet j
+  if (own) {
+    uint32_t sum = 0;
+    const u32x4 *row = (const u32x4 *) &part[lg][gl][0];
+#pragma unroll
+    for (int l = 0; l < G / 4; ++l) {
+      const u32x4 q = row[l];
+      sum += q.x + q.y + q.z + q.w;
+    }
+    uint32_t r = fold32_to_16(sum); // sum < G * 2^18 <= 2^24
+    if (info & 1u)
+      r = bswap16(r);
+    if constexpr (TCP4) {
+      const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
+      uint32_t tcpc = 0;
+      if (tl >= 20)
+        tcpc = inv_result(residue(fold32_to_16(r + fix + c_ph + bswap16(len))));
+      if (p.out)
+        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+      if (p.flags & TASX_F_INPLACE) {
+        st8(ipp + 10, ipc);
+        st8(ipp + 11, ipc >> 8);
+        st8(l4p + 16, tcpc);
+        st8(l4p + 17, tcpc >> 8);
+      }
+    } else {
+      stg(p.out, i, (uint16_t) r);
+    }
+  }
+}
+
+template <int G, int P, int U, bool TCP4, typename Prm>
+int launch_flat(const Prm &p, uint32_t ppg, hipStream_t s)
+{
+  constexpr int NG = kBlock / G;
+  if (ppg == 0 || ppg > (uint32_t) P)
+    ppg = P;
+  const uint64_t groups = ((uint64_t) p.n + ppg - 1) / ppg;
+  const uint64_t blocks = (groups + NG - 1) / NG;
+  if (blocks == 0)
+    return 0;
+  if (blocks > 0x7fffffffull)
+    return -2;
+  hipLaunchKernelGGL((flat_cksum_kernel<G, P, U, TCP4, Prm>), dim3((uint32_t) blocks), dim3(kBlock), 0, s, p, ppg);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---------------------------------------------------------------------------
+// pkt16 kernels: 16-lane packet groups (one DPP row each), persistent grid.
+//   * loads: U clamped global_load_dwordx4 per lane, issued back to back with
+//     no branches (lanes past the packet re-read its last chunk -- same line,
+//     no extra HBM traffic -- and drop it with a select);
+//   * head / tail bytes: exact subtraction of the excluded bytes on the two
+//     lanes that hold the boundary chunks (lane sums are exact before folding);
+//   * reduction: 4 DPP row_shr adds per channel, total lands in lane 15;
+//   * TCP4: the next frame's header (total_length + header words) is
+//     prefetched while this frame's chunks are in flight, so the header ->
+//     length -> data dependency costs one load latency per group, not per frame.
+
+__device__ __forceinline__ uint32_t row_sum16(uint32_t v)
+{
+  // Hillis-Steele inclusive scan inside each 16-lane DPP row; lane 15 = row sum
+  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, false); // row_shr:1
+  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, false); // row_shr:2
+  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, false); // row_shr:4
+  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, false); // row_shr:8
+  return v;
+}
+
+// sum of the dwords of chunk v restricted to bytes [0, h) (0 <= h <= 16)
+__device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
+{
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = min(max(h - 4 * j, 0), 4);
+    s += w[j] & (uint32_t) ((1ull << (8 * b)) - 1ull);
+  }
+  return s;
+}
+
+template <int U>
+struct Chunks {
+  const u32x4 *c0p;
+  uint32_t nch;
+  int head, tail; // bytes dropped at the start of chunk 0 / kept in chunk nch-1
+};
+
+template <int U>
+__device__ __forceinline__ Chunks<U> chunk_range(const uint8_t *start, uint32_t len)
+{
+  Chunks<U> r;
+  const uintptr_t a0 = (uintptr_t) start, a1 = a0 + len;
+  r.c0p = (const u32x4 *) (a0 & ~(uintptr_t) 15);
+  r.nch = len ? (uint32_t) ((((a1 + 15) & ~(uintptr_t) 15) - (a0 & ~(uintptr_t) 15)) >> 4) : 0u;
+  r.head = (int) (a0 & 15);
+  r.tail = (int) (a1 - ((a1 - 1) & ~(uintptr_t) 15));
+  return r;
+}
+
+// this lane's exact partial over the group's chunks gl, gl+16, ...
+template <int U>
+__device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
+{
+  uint64_t acc = 0;
+  if (r.nch == 0)
+    return 0;
+  for (uint32_t c = (uint32_t) gl; c < r.nch; c += 16u * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16(r.c0p, min(c + 16u * u, r.nch - 1));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool keep = c + 16u * u < r.nch;
+      acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
+    }
+    // boundary fix-ups: drop bytes [0, head) of chunk 0, [tail, 16) of chunk nch-1
+    if (c == 0 && r.head)
+      acc -= chunk_prefix_sum(v[0], r.head);
+    const uint32_t last = r.nch - 1;
+    if (last >= c && last < c + 16u * U && ((last - c) & 15u) == 0 && r.tail < 16) {
+      const uint32_t ut = (last - c) >> 4;
+      u32x4 t = v[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        if (ut == (uint32_t) u)
+          t = v[u];
+      acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, r.tail);
+    }
+  }
+  return fold64_to_18(acc);
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void pkt16_raw_kernel(tasx_raw_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t ngroups = gridDim.x * (kBlock / 16);
+  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  // descriptor prefetch (every lane of the group reads the same word)
+  uint64_t off = 0;
+  uint32_t len = p.len0;
+  if (i < p.n) {
+    off = pkt_offset(p.off, p.stride, i);
+    if (p.len)
+      len = ldg(p.len, i);
+  }
+  for (; i < p.n; i += ngroups) {
+    const uint8_t *s = p.base + off;
+    const Chunks<U> r = chunk_range<U>(s, len);
+    const uint32_t inext = i + ngroups;
+    uint32_t part = group_lane_sum<U>(r, gl);
+    if (inext < p.n) {
+      off = pkt_offset(p.off, p.stride, inext);
+      if (p.len)
+        len = ldg(p.len, inext);
+    }
+    part = row_sum16(part);
+    if (gl == 15) {
+      uint32_t f = fold32_to_16(part);
+      if (r.head & 1)
+        f = bswap16(f);
+      stg(p.out, i, (uint16_t) f);
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void pkt16_tcp4_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t ngroups = gridDim.x * (kBlock / 16);
+  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  // header prefetch: every lane reads total_length; lanes 0..9 the header word gl
+  uint32_t tlb0 = 0, tlb1 = 0, wb0 = 0, wb1 = 0;
+  uint8_t *f = nullptr;
+  if (i < p.n) {
+    f = p.base + pkt_offset(p.off, p.stride, i);
+    const uint8_t *ip = f + p.ip_off;
+    tlb0 = ld8(ip + 2);
+    tlb1 = ld8(ip + 3);
+    if (gl < 10) {
+      wb0 = ld8(ip + 2 * gl);
+      wb1 = ld8(ip + 2 * gl + 1);
+    }
+  }
+  for (; i < p.n; i += ngroups) {
+    uint8_t *ip = f + p.ip_off;
+    uint8_t *l4 = f + p.l4_off;
+    const uint32_t tl = (tlb0 << 8) | tlb1;
+    const uint32_t len = tl >= 20 ? tl - 20 : 0;
+    const uint32_t w = wb0 | (wb1 << 8);
+    const Chunks<U> r = chunk_range<U>(l4, len);
+    // checksum-field bytes of the segment (lane 10), taken as zero
+    uint32_t fb0 = 0, fb1 = 0;
+    if (gl == 10 && len > 16) {
+      fb0 = ld8(l4 + 16);
+      if (len > 17)
+        fb1 = ld8(l4 + 17);
+    }
+    uint32_t part = group_lane_sum<U>(r, gl);
+    // prefetch the next frame's header
+    const uint32_t inext = i + ngroups;
+    uint8_t *fn = f;
+    if (inext < p.n) {
+      fn = p.base + pkt_offset(p.off, p.stride, inext);
+      const uint8_t *ipn = fn + p.ip_off;
+      tlb0 = ld8(ipn + 2);
+      tlb1 = ld8(ipn + 3);
+      if (gl < 10) {
+        wb0 = ld8(ipn + 2 * gl);
+        wb1 = ld8(ipn + 2 * gl + 1);
+      }
+    }
+    uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0u;
+    uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
+    if (gl == 10 && len > 16)
+      c_ph += (~(fb0 | (fb1 << 8))) & 0xffffu; // -field mod 0xffff
+    part = row_sum16(part);
+    c_ip = row_sum16(c_ip);
+    c_ph = row_sum16(c_ph);
+    if (gl == 15) {
+      const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
+      uint32_t tcpc = 0;
+      if (tl >= 20) {
+        uint32_t r4 = fold32_to_16(part);
+        if (r.head & 1)
+          r4 = bswap16(r4);
+        tcpc = inv_result(residue(fold32_to_16(r4 + c_ph + bswap16(len))));
+      }
+      if (p.out)
+        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+      if (p.flags & TASX_F_INPLACE) {
+        st8(ip + 10, ipc);
+        st8(ip + 11, ipc >> 8);
+        st8(l4 + 16, tcpc);
+        st8(l4 + 17, tcpc >> 8);
+      }
+    }
+    f = fn;
+  }
+}
+
+// TCP4 with frame-length hints: the frame length (mbuf data_len, set by
+// tx_send before tx_flush) predicts the L4 range, so the data loads are issued
+// together with the header loads instead of after them.  The hint drives only
+// the prefetch: results always follow ip.total_length (chunks past it are
+// dropped, chunks the hint missed are loaded after the header arrives).
+template <int U>
+__global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group (one DPP row) leaves together
+  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+  uint8_t *ip = f + p.ip_off;
+  uint8_t *l4 = f + p.l4_off;
+  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
+  // speculative chunk loads first, then the header bytes
+  const uint32_t slen = hint > p.l4_off ? min(hint - p.l4_off, 65535u) : 0u;
+  const Chunks<U> sr = chunk_range<U>(l4, slen);
+  u32x4 v[U];
+  if (sr.nch) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16(sr.c0p, min((uint32_t) gl + 16u * u, sr.nch - 1));
+  }
+  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  uint32_t w = 0;
+  if (gl < 10)
+    w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const Chunks<U> r = chunk_range<U>(l4, len);
+  uint32_t fb0 = 0, fb1 = 0;
+  if (gl == 10 && len > 16) {
+    fb0 = ld8(l4 + 16);
+    if (len > 17)
+      fb1 = ld8(l4 + 17);
+  }
+  // first 16*U chunks: reuse the speculative loads when they cover them
+  uint64_t acc = 0;
+  if (r.nch) {
+    const uint32_t need = min(r.nch, 16u * U);
+    if (sr.nch < need) { // hint too short (or absent): load now
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = ld16(r.c0p, min((uint32_t) gl + 16u * u, r.nch - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool keep = (uint32_t) gl + 16u * u < r.nch;
+      acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
+    }
+    if (gl == 0 && r.head)
+      acc -= chunk_prefix_sum(v[0], r.head);
+    const uint32_t last = r.nch - 1;
+    if (last < 16u * U && (last & 15u) == (uint32_t) gl && r.tail < 16) {
+      const uint32_t ut = last >> 4;
+      u32x4 t = v[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        if (ut == (uint32_t) u)
+          t = v[u];
+      acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, r.tail);
+    }
+  }
+  uint32_t part = fold64_to_18(acc);
+  if (r.nch > 16u * U) { // long segments: the rest in the plain loop
+    Chunks<U> rest = r;
+    rest.c0p = r.c0p + 16u * U;
+    rest.nch = r.nch - 16u * U;
+    rest.head = 0;
+    part += group_lane_sum<U>(rest, gl);
+  }
+  uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0u;
+  uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
+  if (gl == 10 && len > 16)
+    c_ph += (~(fb0 | (fb1 << 8))) & 0xffffu;
+  part = row_sum16(part);
+  c_ip = row_sum16(c_ip);
+  c_ph = row_sum16(c_ph);
+  if (gl == 15) {
+    const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
+    uint32_t tcpc = 0;
+    if (tl >= 20) {
+      uint32_t r4 = fold32_to_16(part);
+      if (r.head & 1)
+        r4 = bswap16(r4);
+      tcpc = inv_result(residue(fold32_to_16(r4 + c_ph + bswap16(len))));
+    }
+    if (p.out)
+      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+    if (p.flags & TASX_F_INPLACE) {
+      st8(ip + 10, ipc);
+      st8(ip + 11, ipc >> 8);
+      st8(l4 + 16, tcpc);
+      st8(l4 + 17, tcpc >> 8);
+    }
+  }
+}
+
+template <typename K, typename Prm>
+int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t s)
+{
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  uint64_t blocks = ((uint64_t) p.n + 15) / 16;
+  const uint64_t cap = (uint64_t) ncu * blocks_per_cu;
+  if (blocks_per_cu && blocks > cap)
+    blocks = cap;
+  if (blocks == 0)
+    return 0;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <typename K, typename P>
 int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStream_t s)
 {
@@ -275,26 +781,62 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-extern "C" int tasx_launch_raw(const tasx_raw_params *p, int group, void *stream)
+// variant: 0 = auto (RAW 11; TCP4 12 with hints, else 10), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
+// 8..11 = pkt16 persistent (ppg = blocks per CU for 8..10; 11 = one block per 16 packets)
+// ppg: packets per group for the flat kernels / blocks per CU for pkt16 (0 = auto)
+static uint32_t auto_ppg(uint32_t n, uint32_t P, uint32_t groups_per_block)
+{
+  // aim for ~8 blocks per CU of work in total (256 CUs)
+  const uint64_t want_groups = 256ull * 8 * groups_per_block;
+  uint64_t ppg = (n + want_groups - 1) / want_groups;
+  if (ppg < 1)
+    ppg = 1;
+  if (ppg > P)
+    ppg = P;
+  return (uint32_t) ppg;
+}
+
+extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, uint32_t ppg, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
   const int maxb = 256 * 64;
-  switch (group) {
-  case 16: return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
-  case 32: return launch(raw_cksum_kernel<32, 4>, *p, kBlock / 32, maxb, s);
-  case 64: return launch(raw_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
+  switch (variant) {
+  case 0:
+  case 11: return launch_persistent(pkt16_raw_kernel<6>, *p, 0, s);
+  case 8: return launch_persistent(pkt16_raw_kernel<6>, *p, ppg ? ppg : 8, s);
+  case 9: return launch_persistent(pkt16_raw_kernel<8>, *p, ppg ? ppg : 8, s);
+  case 10: return launch_persistent(pkt16_raw_kernel<4>, *p, ppg ? ppg : 8, s);
+  case 2: return launch_flat<64, 16, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
+  case 1: return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
+  case 3: return launch_flat<64, 16, 4, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
+  case 4: return launch_flat<16, 8, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
+  case 5: return launch_flat<16, 8, 4, false>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
+  case 6: return launch_flat<32, 16, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 8), s);
+  case 7: return launch(raw_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
   default: return -2;
   }
 }
 
-extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int group, void *stream)
+extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t ppg, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
   const int maxb = 256 * 64;
-  switch (group) {
-  case 16: return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
-  case 32: return launch(tcp4_cksum_kernel<32, 4>, *p, kBlock / 32, maxb, s);
-  case 64: return launch(tcp4_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
+  if (variant == 0) // frame-length hints -> speculative loads; else header prefetch
+    variant = (p->flen || p->flen0) ? 12 : 10;
+  switch (variant) {
+  case 8: return launch_persistent(pkt16_tcp4_kernel<6>, *p, ppg ? ppg : 8, s);
+  case 9: return launch_persistent(pkt16_tcp4_kernel<8>, *p, ppg ? ppg : 8, s);
+  case 10: return launch_persistent(pkt16_tcp4_kernel<4>, *p, ppg ? ppg : 12, s);
+  case 11: return launch_persistent(pkt16_tcp4_kernel<6>, *p, 0, s);
+  case 12: return launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s);
+  case 13: return launch_persistent(pkt16_tcp4_spec_kernel<8>, *p, 0, s);
+  case 2: return launch_flat<64, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
+  case 1: return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
+  case 3: return launch_flat<64, 16, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
+  case 4: return launch_flat<16, 8, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
+  case 5: return launch_flat<16, 8, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
+  case 6: return launch_flat<32, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 8), s);
+  case 7: return launch(tcp4_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
   default: return -2;
   }
 }

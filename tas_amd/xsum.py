@@ -43,6 +43,8 @@ SIGNATURES = {
     "tasx_device_count": (_c_int, []),
     "tasx_raw_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _vp, _vp]),
     "tasx_tcp4_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp]),
+    "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
+                                                _c_u32, _vp]),
     "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
     "tasx_ctx_destroy": (_c_int, [_uns]),
     "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
@@ -52,6 +54,7 @@ SIGNATURES = {
     "tasx_defer_tcp4": (_c_int, [_uns, _vp, _c_u16, _c_u16]),
     "tasx_pending": (_c_int, [_uns]),
     "tasx_flush": (_c_int, [_uns]),
+    "tasx_set_kernel_config": (_c_int, [_c_int, _uns]),
     "tasx_host_alloc": (_vp, [_sz]),
     "tasx_host_free": (_c_int, [_vp]),
     "tasx_host_register": (_c_int, [_vp, _sz]),
@@ -143,17 +146,30 @@ def raw_cksum_batch(buf: torch.Tensor, n: int, *, offsets: torch.Tensor | None =
 def tcp4_cksum_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
                      stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
                      out: torch.Tensor | None = None, inplace: bool = False,
-                     want_out: bool = True, stream=None) -> torch.Tensor | None:
+                     want_out: bool = True, frame_len: torch.Tensor | int | None = None,
+                     stream=None) -> torch.Tensor | None:
     """tcp_checksums() flag-off branch for n frames on the GPU.  Returns an int16
-    tensor of 2n values: [ip.chksum, tcp.chksum] per frame (uint16 bit patterns)."""
+    tensor of 2n values: [ip.chksum, tcp.chksum] per frame (uint16 bit patterns).
+    frame_len: optional frame-length hints (int32 tensor, or one int for all
+    frames) -- prefetch only, results never depend on it."""
     if out is None and want_out:
         out = torch.empty(2 * n, dtype=torch.int16, device=frames.device)
     if offsets is not None:
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
     flags = TASX_F_INPLACE if inplace else 0
-    _check(lib().tasx_tcp4_cksum_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
-                                           _ptr(out), flags, _stream(stream)),
-           "tasx_tcp4_cksum_batch_dev")
+    if frame_len is None:
+        _check(lib().tasx_tcp4_cksum_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
+                                               _ptr(out), flags, _stream(stream)),
+               "tasx_tcp4_cksum_batch_dev")
+    else:
+        if isinstance(frame_len, int):
+            flen, flen0 = None, frame_len
+        else:
+            assert frame_len.dtype == torch.int32 and frame_len.numel() >= n
+            flen, flen0 = frame_len, 0
+        _check(lib().tasx_tcp4_cksum_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
+                                                    n, ip_off, l4_off, _ptr(out), flags, _stream(stream)),
+               "tasx_tcp4_cksum_batch_dev_hint")
     return out
 
 
@@ -202,6 +218,11 @@ def raw_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, len0: int, n:
                          out_addr: int) -> None:
     _check(lib().tasx_raw_cksum_batch_host(ctx_id, base_addr, stride, len0, n, out_addr),
            "tasx_raw_cksum_batch_host")
+
+
+def set_kernel_config(variant: int = 0, ppg: int = 0) -> None:
+    """Select the kernel variant / packets-per-group (0, 0 = automatic)."""
+    _check(lib().tasx_set_kernel_config(variant, ppg), "tasx_set_kernel_config")
 
 
 class PinnedBuffer:

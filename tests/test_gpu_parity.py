@@ -239,6 +239,58 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 11, 12, 13])
+def test_tcp4_all_variants_and_hints(oracle, variant):
+    """Every kernel variant, with and without frame-length hints (exact, short,
+    long, zero, garbage): results follow ip.total_length only."""
+    n = 3000
+    pay = (pktgen.splitmix64(55, n) % np.uint64(1449)).astype(np.int64)
+    pay[::97] = 0
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=55)
+    tl = 52 + pay
+    tl[::101] = 10     # total_length < 20
+    tl[1::101] = 20
+    tl[2::101] = 37
+    f = frames.reshape(n, 2048)
+    f[:, 16] = (tl >> 8) & 0xFF
+    f[:, 17] = tl & 0xFF
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
+    d = to_dev(frames)
+    exact = (14 + tl).astype(np.int32)
+    noise = (pktgen.splitmix64(56, n) % np.uint64(4000)).astype(np.int32)
+    xsum.set_kernel_config(variant, 0)
+    try:
+        for hint in (None, 1514, 64, 2048, 0, to_dev(exact), to_dev(noise), to_dev(exact // 2)):
+            got = u16(xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=hint))
+            np.testing.assert_array_equal(got, exp, err_msg=f"variant {variant} hint {hint if isinstance(hint, (int, type(None))) else 'array'}")
+    finally:
+        xsum.set_kernel_config(0, 0)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 9, 10, 11])
+def test_raw_all_variants(oracle, variant):
+    buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
+    n = len(lens)
+    exp = oracle.raw_batch(buf, n, offsets=offs, lengths=lens)
+    xsum.set_kernel_config(variant, 0)
+    try:
+        got = u16(xsum.raw_cksum_batch(to_dev(buf), n, offsets=to_dev(offs.astype(np.int64)),
+                                       lengths=to_dev(lens.astype(np.int32))))
+        np.testing.assert_array_equal(got, exp)
+    finally:
+        xsum.set_kernel_config(0, 0)
+
+
+def test_tso_with_hints(oracle):
+    n, stride = 512, 65552
+    frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=58,
+                                ip_total_len=np.where(np.arange(n) % 3 == 0, 65535, 30000))
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=stride)
+    d = to_dev(frames)
+    for hint in (None, 65549, 1514, stride):
+        np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride, frame_len=hint)), exp)
+
+
 def test_deterministic_and_n0():
     frames = pktgen.tcp4_frames(1000, stride=2048)
     d = to_dev(frames)
