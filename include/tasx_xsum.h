@@ -139,6 +139,9 @@ int tasx_flush(unsigned ctx_id);
  * 1 = wave-per-packet kernel, 2..7 = fixed shapes; ppg = packets per lane
  * group for the flat-stream kernels (0 = automatic). */
 int tasx_set_kernel_config(int variant, unsigned ppg);
+/* Device buffer for the timestamp-diagnostic kernel variant (17): 4 x u64 per
+ * wave of s_memrealtime (100 MHz) stamps.  NULL disables. */
+int tasx_set_diag_buffer(void *dev_buf);
 
 /* ---------------------------------------------------------------------- */
 /* Memory helpers (plumbing for callers without their own HIP code). */

@@ -64,10 +64,17 @@ int tasx_device_count(void)
 /* kernel selection (tasx_set_kernel_config); 0/0 = automatic */
 static int g_variant = 0;
 static unsigned g_ppg = 0;
+static uint64_t *g_diag = NULL;
+
+int tasx_set_diag_buffer(void *dev_buf)
+{
+  g_diag = (uint64_t *) dev_buf;
+  return 0;
+}
 
 int tasx_set_kernel_config(int variant, unsigned ppg)
 {
-  if (variant < 0 || variant > 13 || ppg > 64)
+  if (variant < 0 || variant > 17 || ppg > 64)
     return set_err(-EINVAL, "kernel config %d/%u out of range", variant, ppg);
   g_variant = variant;
   g_ppg = ppg;
@@ -125,6 +132,7 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
   p.flags = flags;
   p.flen = flen;
   p.flen0 = flen0;
+  p.diag = g_diag;
   r = tasx_launch_tcp4(&p, g_variant, g_ppg, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");

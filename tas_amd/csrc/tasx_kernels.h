@@ -34,6 +34,7 @@ typedef struct tasx_tcp4_params {
   const uint32_t *flen;  /* device, n frame-length hints (bytes from the frame
                           * start, the mbuf data_len), or NULL -> flen0 */
   uint32_t flen0;        /* uniform hint; 0 = none */
+  uint64_t *diag;        /* diagnostic timestamp buffer (diag variants only) */
 } tasx_tcp4_params;
 
 /* variant: 0 auto (flat-stream kernel), 1 / 7 wave-per-packet kernels,

@@ -40,6 +40,12 @@ typedef __attribute__((address_space(1))) const uint8_t gcu8;
 typedef __attribute__((address_space(1))) uint8_t gu8;
 
 __device__ __forceinline__ u32x4 ld16(const u32x4 *p, uint32_t i) { return ((gcu4 *) p)[i]; }
+// streaming (non-temporal) 16-byte load: packet bytes are read exactly once
+// (MI355X_MICROARCH.md nt-weights: nt cuts issue->landed latency ~18%)
+__device__ __forceinline__ u32x4 ld16nt(const u32x4 *p, uint32_t i)
+{
+  return __builtin_nontemporal_load(&((gcu4 *) p)[i]);
+}
 __device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8 *) p; }
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t v) { *(gu8 *) p = (uint8_t) v; }
 template <typename T>
@@ -512,7 +518,7 @@ __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = ld16(r.c0p, min(c + 16u * u, r.nch - 1));
+      v[u] = ld16nt(r.c0p, min(c + 16u * u, r.nch - 1));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool keep = c + 16u * u < r.nch;
@@ -650,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_kernel(tasx_tcp4_params p)
 // together with the header loads instead of after them.  The hint drives only
 // the prefetch: results always follow ip.total_length (chunks past it are
 // dropped, chunks the hint missed are loaded after the header arrives).
-template <int U>
+template <int U, int DIAG = 0>
 __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -668,12 +674,16 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_param
   if (sr.nch) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = ld16(sr.c0p, min((uint32_t) gl + 16u * u, sr.nch - 1));
+      v[u] = ld16nt(sr.c0p, min((uint32_t) gl + 16u * u, sr.nch - 1));
   }
-  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
-  uint32_t w = 0;
-  if (gl < 10)
-    w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
+  uint32_t tl, w = 0;
+  if constexpr (DIAG == 1) { // timing diagnostic only: no header loads (wrong results)
+    tl = hint - p.ip_off;
+  } else {
+    tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+    if (gl < 10)
+      w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
+  }
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const Chunks<U> r = chunk_range<U>(l4, len);
   uint32_t fb0 = 0, fb1 = 0;
@@ -689,7 +699,7 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_param
     if (sr.nch < need) { // hint too short (or absent): load now
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        v[u] = ld16(r.c0p, min((uint32_t) gl + 16u * u, r.nch - 1));
+        v[u] = ld16nt(r.c0p, min((uint32_t) gl + 16u * u, r.nch - 1));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -744,6 +754,163 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_param
   }
 }
 
+// TCP4, TAS layout (l4_off == ip_off + 20): one chunk range [ip, ip + 20 +
+// L4 length) carries the IPv4 header, the pseudo-header fields and the
+// segment, so no byte loads are issued at all.  The lanes holding the chunks
+// that touch header bytes (ip-relative offsets < 38) split them into three
+// channels with byte masks:
+//   IP  = header bytes [0,10) + [12,20)            (ip.chksum taken as 0)
+//   PH  = proto (offset 9) + src/dst [12,20)       (pseudo-header fields)
+//   L4  = [20, 20+len) minus the tcp.chksum bytes [36,38)
+// total_length comes from the chunk holding offsets 2..3 (lane shuffle).
+// Without a frame-length hint the header chunks are loaded first and the
+// rest after total_length is known; with a hint everything is issued at once.
+
+// mask of the bytes of a dword (first byte at ip-relative offset `base`) that
+// fall in [lo, hi)
+__device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
+{
+  const int bl = min(max(lo - base, 0), 4);
+  const int bh = min(max(hi - base, 0), 4);
+  if (bh <= bl)
+    return 0u;
+  return (uint32_t) (((1ull << (8 * bh)) - 1ull) & ~((1ull << (8 * bl)) - 1ull));
+}
+
+__device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
+{
+  const uint32_t w = (b < 4) ? v.x : (b < 8) ? v.y : (b < 12) ? v.z : v.w;
+  return (w >> (8 * (b & 3))) & 0xffu;
+}
+
+__device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
+{
+  // 100 MHz global clock; one record of 4 stamps per wave
+  const uint64_t t = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    const uint64_t w = ((uint64_t) blockIdx.x * (kBlock / 64) + threadIdx.x / 64);
+    p.diag[w * 4 + slot] = t;
+  }
+}
+
+template <int U, int DIAG = 0>
+__global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params p)
+{
+  if constexpr (DIAG)
+    diag_stamp(p, 0);
+  const int gl = threadIdx.x & 15;
+  const int gbase = (threadIdx.x & 63) & ~15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group (one DPP row) leaves together
+  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+  uint8_t *ip = f + p.ip_off;
+  const uintptr_t A0 = (uintptr_t) ip & ~(uintptr_t) 15;
+  const u32x4 *c0p = (const u32x4 *) A0;
+  const int hb = (int) ((uintptr_t) ip & 15);
+  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
+  // chunks covering [ip, f + hint): the speculative range (at least the header)
+  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
+  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
+  // round 1: U loads back to back, no branches (lanes past the range re-read
+  // its last chunk: same line, no extra HBM traffic)
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, nld - 1));
+  // total_length: ip-relative bytes 2 and 3
+  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
+  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
+  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
+  const uint32_t tl = (ba << 8) | bb;
+  if constexpr (DIAG)
+    diag_stamp(p, 1);
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const int E = 20 + (int) len;                              // ip-relative end
+  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;        // chunks of [ip, ip+E)
+  const uint32_t need = min(nch, 16u * U);
+  // round 2 (no / short hint): wave-uniform branch, straight-line loads inside
+  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
+    const uint32_t top = max(need, nld);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, top - 1));
+  }
+  const int NS = (hb + 38 + 15) >> 4; // chunks holding ip-relative offsets < 38
+  uint64_t acc = 0, acc_ip = 0, acc_ph = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t c = (uint32_t) gl + 16u * u;
+    if (u == 0 && gl < NS) {
+      // header chunk: split by byte masks (ip-relative base of dword j)
+      const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int base = 16 * gl + 4 * j - hb;
+        const uint32_t m_ip = in_range(base, 0, 10) | in_range(base, 12, 20);
+        const uint32_t m_ph = in_range(base, 9, 10) | in_range(base, 12, 20);
+        const uint32_t m_l4 = in_range(base, 20, min(36, E)) | in_range(base, 38, E);
+        acc_ip += w[j] & m_ip;
+        acc_ph += w[j] & m_ph;
+        acc += w[j] & m_l4;
+      }
+    } else if (c < nch) {
+      acc += (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+  }
+  // tail chunk beyond the header chunks: drop bytes past ip + E
+  const uint32_t last = nch - 1;
+  const int tail = (int) (((uintptr_t) ip + E) - (((uintptr_t) ip + E - 1) & ~(uintptr_t) 15));
+  if (last >= (uint32_t) NS && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
+    const uint32_t ut = last >> 4;
+    u32x4 t = v[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u)
+      if (ut == (uint32_t) u)
+        t = v[u];
+    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
+  }
+  uint32_t part = fold64_to_18(acc);
+  if (nch > 16u * U) { // long segments: the rest in the plain loop (all L4 bytes)
+    Chunks<U> rest;
+    rest.c0p = c0p + 16u * U;
+    rest.nch = nch - 16u * U;
+    rest.head = 0;
+    rest.tail = tail;
+    part += group_lane_sum<U>(rest, gl);
+  }
+  uint32_t c_ip = fold64_to_18(acc_ip);
+  uint32_t c_ph = fold64_to_18(acc_ph);
+  if constexpr (DIAG)
+    diag_stamp(p, 2);
+  part = row_sum16(part);
+  c_ip = row_sum16(c_ip);
+  c_ph = row_sum16(c_ph);
+  if (gl == 15) {
+    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
+    if (hb & 1) { // address-aligned words -> header / segment relative words
+      ri = bswap16(ri);
+      rp = bswap16(rp);
+      r4 = bswap16(r4);
+    }
+    const uint32_t ipc = inv_result(residue(ri));
+    uint32_t tcpc = 0;
+    if (tl >= 20)
+      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
+    if (p.out)
+      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+    if (p.flags & TASX_F_INPLACE) {
+      uint8_t *l4 = ip + 20;
+      st8(ip + 10, ipc);
+      st8(ip + 11, ipc >> 8);
+      st8(l4 + 16, tcpc);
+      st8(l4 + 17, tcpc >> 8);
+    }
+  }
+  if constexpr (DIAG)
+    diag_stamp(p, 3);
+}
+
 template <typename K, typename Prm>
 int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t s)
 {
@@ -781,7 +948,7 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-// variant: 0 = auto (RAW 11; TCP4 12 with hints, else 10), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
+// variant: 0 = auto (RAW 11; TCP4 16 for TAS layout + hints, else 12), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
 // 8..11 = pkt16 persistent (ppg = blocks per CU for 8..10; 11 = one block per 16 packets)
 // ppg: packets per group for the flat kernels / blocks per CU for pkt16 (0 = auto)
 static uint32_t auto_ppg(uint32_t n, uint32_t P, uint32_t groups_per_block)
@@ -821,8 +988,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t
 {
   hipStream_t s = (hipStream_t) stream;
   const int maxb = 256 * 64;
-  if (variant == 0) // frame-length hints -> speculative loads; else header prefetch
-    variant = (p->flen || p->flen0) ? 12 : 10;
+  if (variant == 0) // TAS layout with hints -> header from the chunks; else byte loads
+    variant = (p->l4_off == p->ip_off + 20 && (p->flen || p->flen0)) ? 16 : 12;
+  if (variant >= 15 && p->l4_off != p->ip_off + 20)
+    variant = 12;
   switch (variant) {
   case 8: return launch_persistent(pkt16_tcp4_kernel<6>, *p, ppg ? ppg : 8, s);
   case 9: return launch_persistent(pkt16_tcp4_kernel<8>, *p, ppg ? ppg : 8, s);
@@ -830,6 +999,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t
   case 11: return launch_persistent(pkt16_tcp4_kernel<6>, *p, 0, s);
   case 12: return launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s);
   case 13: return launch_persistent(pkt16_tcp4_spec_kernel<8>, *p, 0, s);
+  case 14: return launch_persistent(pkt16_tcp4_spec_kernel<6, 1>, *p, 0, s); // timing diagnostic
+  case 15: return launch_persistent(pkt16_tcp4_tas_kernel<6>, *p, 0, s);
+  case 16: return launch_persistent(pkt16_tcp4_tas_kernel<8>, *p, 0, s);
+  case 17: return p->diag ? launch_persistent(pkt16_tcp4_tas_kernel<6, 1>, *p, 0, s) : -2;
   case 2: return launch_flat<64, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
   case 1: return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
   case 3: return launch_flat<64, 16, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);

@@ -55,6 +55,7 @@ SIGNATURES = {
     "tasx_pending": (_c_int, [_uns]),
     "tasx_flush": (_c_int, [_uns]),
     "tasx_set_kernel_config": (_c_int, [_c_int, _uns]),
+    "tasx_set_diag_buffer": (_c_int, [_vp]),
     "tasx_host_alloc": (_vp, [_sz]),
     "tasx_host_free": (_c_int, [_vp]),
     "tasx_host_register": (_c_int, [_vp, _sz]),

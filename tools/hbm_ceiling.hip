@@ -5,10 +5,10 @@
 // Pure streaming read + integer fold (the same VALU work per byte as the
 // checksum, no packet structure), over R rotating buffers of B bytes each so
 // every launch reads HBM.  Reports per-launch time (hipEvents around each
-// launch, and total / K) for several launch shapes.
+// launch, and total / K back-to-back) for several launch shapes.
 //
-//   hipcc --offload-arch=gfx950 -O3 -o hbm_ceiling tools/hbm_ceiling.hip
-//   ./hbm_ceiling [bytes_per_launch] [rotations] [launches]
+//   hipcc --offload-arch=gfx950 -O3 -o tools/bin/hbm_ceiling tools/hbm_ceiling.hip
+//   tools/bin/hbm_ceiling [bytes_per_launch] [rotations] [launches]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -22,41 +22,57 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gcu4;
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const gcu4 *g, uint64_t i)
+{
+  if constexpr (NT)
+    return __builtin_nontemporal_load(&g[i]);
+  else
+    return g[i];
+}
+
 // grid-stride: each thread U chunks in flight per iteration
-template <int U>
-__global__ __launch_bounds__(256) void stream_gs(const u32x4 *p, uint64_t nchunks, uint32_t *out)
+template <int U, int BS, bool NT>
+__global__ __launch_bounds__(BS) void stream_gs(const u32x4 *p, uint64_t nchunks, uint32_t *out)
 {
   const gcu4 *g = (const gcu4 *) p;
   uint64_t acc = 0;
-  const uint64_t T = (uint64_t) gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t T = (uint64_t) gridDim.x * BS;
+  uint64_t i = (uint64_t) blockIdx.x * BS + threadIdx.x;
   for (; i + (U - 1) * T < nchunks; i += U * T) {
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = g[i + u * T];
+    for (int u = 0; u < U; ++u) v[u] = ld<NT>(g, i + u * T);
 #pragma unroll
     for (int u = 0; u < U; ++u) { acc += v[u].x; acc += v[u].y; acc += v[u].z; acc += v[u].w; }
   }
-  for (; i < nchunks; i += T) { u32x4 v = g[i]; acc += v.x; acc += v.y; acc += v.z; acc += v.w; }
+  for (; i < nchunks; i += T) { u32x4 v = ld<NT>(g, i); acc += v.x; acc += v.y; acc += v.z; acc += v.w; }
   uint32_t r = (uint32_t) acc + (uint32_t) (acc >> 32);
-  if (r == 0x12345678u) out[0] = r;  // keep live, never true for random data
+  if (r == 0x12345678u) out[0] = r;  // keep live, never true for this data
 }
 
-// one-shot: block b reads a contiguous span of 256*U chunks, wave-contiguous 1 KiB per load
-template <int U>
-__global__ __launch_bounds__(256) void stream_blk(const u32x4 *p, uint64_t nchunks, uint32_t *out)
+// block-contiguous: block b reads chunks [b*S, (b+1)*S) with S = BS*U*iters,
+// wave-contiguous 1 KiB per load, U loads in flight per thread
+template <int U, int BS, bool NT>
+__global__ __launch_bounds__(BS) void stream_blk(const u32x4 *p, uint64_t nchunks, uint64_t per_block, uint32_t *out)
 {
   const gcu4 *g = (const gcu4 *) p;
-  uint64_t base = (uint64_t) blockIdx.x * 256 * U;
+  const uint64_t b0 = (uint64_t) blockIdx.x * per_block;
+  const uint64_t b1 = min(b0 + per_block, nchunks);
   uint64_t acc = 0;
-  u32x4 v[U];
+  for (uint64_t base = b0; base < b1; base += (uint64_t) BS * U) {
+    u32x4 v[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    uint64_t i = base + (uint64_t) u * 256 + threadIdx.x;
-    v[u] = i < nchunks ? g[i] : u32x4{0, 0, 0, 0};
+    for (int u = 0; u < U; ++u) {
+      uint64_t i = base + (uint64_t) u * BS + threadIdx.x;
+      v[u] = ld<NT>(g, i < b1 ? i : b0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      uint64_t i = base + (uint64_t) u * BS + threadIdx.x;
+      if (i < b1) { acc += v[u].x; acc += v[u].y; acc += v[u].z; acc += v[u].w; }
+    }
   }
-#pragma unroll
-  for (int u = 0; u < U; ++u) { acc += v[u].x; acc += v[u].y; acc += v[u].z; acc += v[u].w; }
   uint32_t r = (uint32_t) acc + (uint32_t) (acc >> 32);
   if (r == 0x12345678u) out[0] = r;
 }
@@ -71,25 +87,51 @@ Res run(F launch, int R, int K, hipStream_t s)
   hipEvent_t t0, t1; CHK(hipEventCreate(&t0)); CHK(hipEventCreate(&t1));
   for (int k = 0; k < 2 * R; ++k) launch(k % R);
   CHK(hipStreamSynchronize(s));
-  // pass 1: wall time over K launches, no per-launch events
   CHK(hipEventRecord(t0, s));
   for (int k = 0; k < K; ++k) launch(k % R);
   CHK(hipEventRecord(t1, s));
   CHK(hipEventSynchronize(t1));
   float tot; CHK(hipEventElapsedTime(&tot, t0, t1));
-  // pass 2: per-launch events
   for (int k = 0; k < K; ++k) { CHK(hipEventRecord(a[k], s)); launch(k % R); CHK(hipEventRecord(b[k], s)); }
   CHK(hipStreamSynchronize(s));
   std::vector<float> d(K);
   for (int k = 0; k < K; ++k) CHK(hipEventElapsedTime(&d[k], a[k], b[k]));
   std::sort(d.begin(), d.end());
-  for (int k = 0; k < K; ++k) { hipEventDestroy(a[k]); hipEventDestroy(b[k]); }
+  for (int k = 0; k < K; ++k) { (void) hipEventDestroy(a[k]); (void) hipEventDestroy(b[k]); }
+  (void) hipEventDestroy(t0); (void) hipEventDestroy(t1);
   return {d[K / 2] * 1e3, tot * 1e3 / K};
+}
+
+static uint64_t B;
+static void report(const char *name, Res r)
+{
+  printf("%-40s event-median %8.2f us %6.0f GB/s | wall/K %8.2f us %6.0f GB/s\n", name,
+         r.ev_us, B / r.ev_us / 1e3, r.wall_us, B / r.wall_us / 1e3);
+  fflush(stdout);
+}
+
+template <int U, int BS, bool NT>
+void gs_case(std::vector<u32x4 *> &buf, uint64_t nch, uint32_t *out, int R, int K, hipStream_t s, int ncu, int bpc)
+{
+  int grid = ncu * bpc;
+  char nm[96];
+  snprintf(nm, sizeof nm, "gs U=%d BS=%d %s %d blk/CU", U, BS, NT ? "nt" : "  ", bpc);
+  report(nm, run([&](int r) { hipLaunchKernelGGL((stream_gs<U, BS, NT>), dim3(grid), dim3(BS), 0, s, buf[r], nch, out); }, R, K, s));
+}
+
+template <int U, int BS, bool NT>
+void blk_case(std::vector<u32x4 *> &buf, uint64_t nch, uint32_t *out, int R, int K, hipStream_t s, uint64_t per_block)
+{
+  int grid = (int) ((nch + per_block - 1) / per_block);
+  char nm[96];
+  snprintf(nm, sizeof nm, "blk U=%d BS=%d %s %llu KiB/blk (%d blk)", U, BS, NT ? "nt" : "  ",
+           (unsigned long long) per_block / 64, grid);
+  report(nm, run([&](int r) { hipLaunchKernelGGL((stream_blk<U, BS, NT>), dim3(grid), dim3(BS), 0, s, buf[r], nch, per_block, out); }, R, K, s));
 }
 
 int main(int argc, char **argv)
 {
-  uint64_t B = argc > 1 ? strtoull(argv[1], 0, 0) : 98304000ull;
+  B = argc > 1 ? strtoull(argv[1], 0, 0) : 98304000ull;
   int R = argc > 2 ? atoi(argv[2]) : 16;
   int K = argc > 3 ? atoi(argv[3]) : 200;
   B &= ~15ull;
@@ -102,27 +144,24 @@ int main(int argc, char **argv)
   uint32_t *out; CHK(hipMalloc(&out, 64));
   hipStream_t s; CHK(hipStreamCreate(&s));
   hipDeviceProp_t prop; CHK(hipGetDeviceProperties(&prop, 0));
-  printf("device %s CUs %d, %llu B per launch, %d rotating buffers, %d launches\n",
-         prop.name, prop.multiProcessorCount, (unsigned long long) B, R, K);
-  auto report = [&](const char *name, Res r) {
-    printf("%-34s event-median %8.2f us  %7.0f GB/s | wall/K %8.2f us  %7.0f GB/s\n", name,
-           r.ev_us, B / r.ev_us / 1e3, r.wall_us, B / r.wall_us / 1e3);
-  };
-  for (int blocksPerCU : {2, 4, 8, 16}) {
-    int grid = prop.multiProcessorCount * blocksPerCU;
-    char nm[64];
-    snprintf(nm, sizeof nm, "grid-stride U=4 %d blk/CU", blocksPerCU);
-    report(nm, run([&](int r) { hipLaunchKernelGGL(stream_gs<4>, dim3(grid), dim3(256), 0, s, buf[r], nch, out); }, R, K, s));
-    snprintf(nm, sizeof nm, "grid-stride U=8 %d blk/CU", blocksPerCU);
-    report(nm, run([&](int r) { hipLaunchKernelGGL(stream_gs<8>, dim3(grid), dim3(256), 0, s, buf[r], nch, out); }, R, K, s));
+  int ncu = prop.multiProcessorCount;
+  printf("CUs %d, %llu B per launch, %d rotating buffers, %d launches\n", ncu, (unsigned long long) B, R, K);
+  for (int bpc : {2, 4, 8, 16}) {
+    gs_case<4, 256, false>(buf, nch, out, R, K, s, ncu, bpc);
+    gs_case<8, 256, false>(buf, nch, out, R, K, s, ncu, bpc);
+    gs_case<8, 256, true>(buf, nch, out, R, K, s, ncu, bpc);
   }
-  {
-    int grid = (int) ((nch + 256 * 4 - 1) / (256 * 4));
-    report("one-shot U=4", run([&](int r) { hipLaunchKernelGGL(stream_blk<4>, dim3(grid), dim3(256), 0, s, buf[r], nch, out); }, R, K, s));
-    grid = (int) ((nch + 256 * 8 - 1) / (256 * 8));
-    report("one-shot U=8", run([&](int r) { hipLaunchKernelGGL(stream_blk<8>, dim3(grid), dim3(256), 0, s, buf[r], nch, out); }, R, K, s));
-    grid = (int) ((nch + 256 * 16 - 1) / (256 * 16));
-    report("one-shot U=16", run([&](int r) { hipLaunchKernelGGL(stream_blk<16>, dim3(grid), dim3(256), 0, s, buf[r], nch, out); }, R, K, s));
+  for (int bpc : {1, 2, 4}) {
+    gs_case<4, 512, false>(buf, nch, out, R, K, s, ncu, bpc);
+    gs_case<8, 512, false>(buf, nch, out, R, K, s, ncu, bpc);
+    gs_case<4, 1024, false>(buf, nch, out, R, K, s, ncu, bpc);
+    gs_case<8, 1024, false>(buf, nch, out, R, K, s, ncu, bpc);
+  }
+  for (uint64_t kib : {4, 8, 16, 24, 32, 64}) {
+    blk_case<4, 256, false>(buf, nch, out, R, K, s, kib * 64);
+    blk_case<6, 256, false>(buf, nch, out, R, K, s, kib * 64);
+    blk_case<8, 256, false>(buf, nch, out, R, K, s, kib * 64);
+    blk_case<8, 256, true>(buf, nch, out, R, K, s, kib * 64);
   }
   return 0;
 }
