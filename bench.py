@@ -1,28 +1,34 @@
 """Benchmark: TAS software TCP/IP checksum path on MI355X (BASELINE.json metric
 "TCP/IP checksum GiB/s (device-resident), 1500B MTU batch, 1/2/4/8 GPU").
 
-One step = one launch of the TCP4 checksum kernel (tcp_checksums() flag-off
-branch: rte_ipv4_cksum + rte_ipv4_udptcp_cksum per frame) over one batch of
-65,536 TAS TX data segments (1514 B frames, ip.len 1500, one per 2048 B mbuf
-data room: BASELINE.json configs[1] / BASELINE.md).  Inputs are resident in HBM
-before the timed region; steps rotate over R distinct batches (R x 134 MB >>
-the 256 MiB Infinity Cache) so every step reads HBM, not MALL.
+Headline step = one launch of the TCP4 checksum kernel (tcp_checksums()
+flag-off branch: rte_ipv4_cksum + rte_ipv4_udptcp_cksum per frame) over one
+batch of 65,536 TAS TX data segments (1514 B frames, ip.len 1500, one per
+2048 B mbuf data room: BASELINE.json configs[1] / BASELINE.md), with the frame
+length (the mbuf data_len tx_send() sets before tx_flush) as the prefetch hint.
+Inputs are resident in HBM before the timed region; steps rotate over R
+distinct batches (R x 134 MB >> the 256 MiB Infinity Cache) so every step
+reads HBM, not the MALL.
 
 Algorithmic bytes per frame = ip.total_length (1500, the bytes summed) + 4
-(results written) -- SURVEY.md section 8d.  GiB/s = bytes / s / 2^30.
+(results written) -- SURVEY.md section 8d.  value = GiB/s = bytes / s / 2^30.
 
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 One process per GPU, each with its own batches and stream (weak scaling, no
-data-path collective); the timed region is barrier + synchronize on both sides
-and the MAX over ranks is taken.  Rank 0 prints one JSON line.
+data-path collective: the path shards); the timed region is
+barrier + synchronize on both sides and the MAX over ranks is taken.  Rank 0
+prints one JSON line.
 
-Extra legs (rank 0, N == 1): the RAW payload fold (rte_raw_cksum over 64K x
-1500 B), the end-to-end host-memory rate through pinned hipMemcpyAsync, the
-CPU oracle baseline, and (--pmc) HBM traffic from rocprofv3 counters.
+Extra legs (rank 0, N == 1): the same frames without the hint, the RAW payload
+fold (rte_raw_cksum over 64K x 1500 B), the end-to-end host-memory rate through
+pinned hipMemcpyAsync, the CPU oracle baseline, and (--pmc) HBM traffic from
+rocprofv3 counters.  --workload {shard8m,mixed,tso} measures the other
+BASELINE.json configs instead (one JSON line each).
 """
 from __future__ import annotations
 
 import argparse
+import csv
 import json
 import os
 import shutil
@@ -39,36 +45,37 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from tas_amd import pktgen, xsum  # noqa: E402
+from tas_amd import pktgen, shard, xsum  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 METRIC = "TCP/IP checksum GiB/s (device-resident), 1500B MTU batch, 1/2/4/8 GPU"
 
 N_FRAMES = 65536
-STRIDE = pktgen.MBUF_ROOM      # 2048
+STRIDE = pktgen.MBUF_ROOM              # 2048
 IP_TOTAL = 1500
 FRAME_LEN = pktgen.ETH_LEN + IP_TOTAL  # 1514, the mbuf data_len tx_send() sets
 RAW_LEN = 1500
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rotate", type=int, default=16, help="distinct device batches cycled through")
+    ap.add_argument("--workload", default="tcp4", choices=["tcp4", "shard8m", "mixed", "tso"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--pmc", action="store_true", help="collect HBM traffic via rocprofv3 child runs")
     ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # ---------------------------------------------------------------------------
-# distributed plumbing (one process per GPU)
+# distributed plumbing (one process per GPU; control only, never data)
 
 def dist_setup():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -82,6 +89,10 @@ def dist_setup():
     return ws, rank, local
 
 
+def _red_device():
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
 def barrier(ws):
     if ws > 1:
         dist.barrier()
@@ -90,7 +101,7 @@ def barrier(ws):
 def max_over_ranks(x: float, ws: int) -> float:
     if ws == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device())
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -98,60 +109,88 @@ def max_over_ranks(x: float, ws: int) -> float:
 def sum_over_ranks(x: float, ws: int) -> float:
     if ws == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device())
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
 
 # ---------------------------------------------------------------------------
-# workloads
+# workloads: device-resident batches + a zero-overhead launcher
+
+def device_random(nbytes: int, seed: int) -> torch.Tensor:
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def device_tcp4_frames(n: int, stride: int, ip_total: int, seed: int) -> torch.Tensor:
+    """Random frame bytes generated on the device, then the 66-byte TAS headers
+    (pktgen.tcp4_frames layout, ip.len = ip_total) written over each frame."""
+    buf = device_random(n * stride, seed)
+    hdr = pktgen.tcp4_frames(n, payload=0, stride=128, seed=seed).reshape(n, 128)[:, :pktgen.HDRS_LEN].copy()
+    hdr[:, 16] = (ip_total >> 8) & 0xFF
+    hdr[:, 17] = ip_total & 0xFF
+    buf.view(n, stride)[:, :pktgen.HDRS_LEN] = torch.from_numpy(hdr).cuda()
+    return buf
+
 
 class Tcp4Workload:
-    name = "tcp4"
     desc = (f"{N_FRAMES} TAS TX segments (1514 B frames, ip.len {IP_TOTAL}, {STRIDE} B mbuf stride), "
-            "tcp_checksums() flag-off per frame, frame length (mbuf data_len) passed as the prefetch hint")
+            "tcp_checksums() flag-off per frame, frame length (mbuf data_len) as the prefetch hint")
 
-    def __init__(self, rotate: int, seed: int, hint: bool = True):
-        self.hint = FRAME_LEN if hint else 0
-        self.n = N_FRAMES
-        self.host = pktgen.tcp4_frames(self.n, payload=IP_TOTAL - 52, stride=STRIDE, seed=seed)
-        first = torch.from_numpy(self.host).cuda()
+    def __init__(self, rotate: int, seed: int, n: int = N_FRAMES, stride: int = STRIDE,
+                 ip_total: int = IP_TOTAL, hint: int | None = None, host: bool = True):
+        self.n, self.stride, self.ip_total = n, stride, ip_total
+        self.hint = pktgen.ETH_LEN + ip_total if hint is None else hint
+        if host:
+            self.host = pktgen.tcp4_frames(n, payload=ip_total - 52, stride=stride, seed=seed)
+            first = torch.from_numpy(self.host).cuda()
+        else:
+            self.host = None
+            first = device_tcp4_frames(n, stride, ip_total, seed)
         self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
-        self.outs = [torch.empty(2 * self.n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
-        self.bytes_per_step = self.n * (IP_TOTAL + 4)
+        self.outs = [torch.empty(2 * n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
+        self.bytes_per_step = n * (ip_total + 4)
 
     def launcher(self):
-        L = xsum.lib()
-        fn = L.tasx_tcp4_cksum_batch_dev_hint
+        fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
         stream = torch.cuda.current_stream().cuda_stream
-        args = [(b.data_ptr(), None, STRIDE, None, self.hint, self.n, pktgen.ETH_LEN,
+        args = [(b.data_ptr(), None, self.stride, None, self.hint, self.n, pktgen.ETH_LEN,
                  pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), 0, stream) for b, o in zip(self.bufs, self.outs)]
         R = len(args)
 
         def launch(k):
             rc = fn(*args[k % R])
             if rc:
-                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev")
+                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev_hint")
         return launch
 
 
 class RawWorkload:
-    name = "raw"
     desc = f"{N_FRAMES} x {RAW_LEN} B packed payloads, rte_raw_cksum per packet"
 
-    def __init__(self, rotate: int, seed: int):
-        self.n = N_FRAMES
-        self.host, _ = pktgen.raw_uniform(self.n, RAW_LEN, seed=seed)
-        first = torch.from_numpy(self.host).cuda()
+    def __init__(self, rotate: int, seed: int, n: int = N_FRAMES, length: int = RAW_LEN,
+                 offsets=None, lengths=None, total_bytes: int | None = None):
+        self.n = n
+        self.len0 = length
+        if offsets is None:
+            first = device_random(n * length, seed)
+            self.off = self.lens = None
+            self.bytes_per_step = n * (length + 2)
+        else:
+            first = device_random(total_bytes, seed)
+            self.off = torch.from_numpy(np.ascontiguousarray(offsets, np.int64)).cuda()
+            self.lens = torch.from_numpy(np.ascontiguousarray(lengths, np.int32)).cuda()
+            self.bytes_per_step = int(np.asarray(lengths, np.int64).sum()) + 2 * n
         self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
-        self.outs = [torch.empty(self.n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
-        self.bytes_per_step = self.n * (RAW_LEN + 2)
+        self.outs = [torch.empty(n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
 
     def launcher(self):
-        L = xsum.lib()
-        fn = L.tasx_raw_cksum_batch_dev
+        fn = xsum.lib().tasx_raw_cksum_batch_dev
         stream = torch.cuda.current_stream().cuda_stream
-        args = [(b.data_ptr(), None, RAW_LEN, None, RAW_LEN, self.n, o.data_ptr(), stream)
+        op = self.off.data_ptr() if self.off is not None else None
+        lp = self.lens.data_ptr() if self.lens is not None else None
+        args = [(b.data_ptr(), op, self.len0 if op is None else 0, lp, self.len0, self.n, o.data_ptr(), stream)
                 for b, o in zip(self.bufs, self.outs)]
         R = len(args)
 
@@ -162,12 +201,25 @@ class RawWorkload:
         return launch
 
 
+def prewarm(launch, seconds: float = 0.25):
+    """Bring the GPU out of idle clocks before any measured step (not part of
+    W or K)."""
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(32):
+            launch(k)
+            k += 1
+        torch.cuda.synchronize()
+
+
 def timed_run(wl, steps: int, warmup: int, ws: int):
     """W untimed steps, then exactly K timed steps between barrier+sync pairs.
     A HIP event pair on the launch stream around the K back-to-back launches
-    gives the average launch duration (kernel + the ~1 us launch boundary; no
-    per-launch events, which would add their own gaps)."""
+    gives the average launch duration (no per-launch events, which would add
+    gaps of their own)."""
     launch = wl.launcher()
+    prewarm(launch)
     for k in range(warmup):
         launch(k)
     torch.cuda.synchronize()
@@ -182,15 +234,31 @@ def timed_run(wl, steps: int, warmup: int, ws: int):
     torch.cuda.synchronize()
     barrier(ws)
     t1 = time.perf_counter()
-    avg_ms = e0.elapsed_time(e1) / steps
-    return t1 - t0, avg_ms
+    return t1 - t0, e0.elapsed_time(e1) / steps
+
+
+def roofline(bytes_per_launch: int, avg_ms: float, traffic):
+    avg_s = avg_ms / 1e3
+    achieved = bytes_per_launch / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "launch_avg_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": bytes_per_launch}
+
+
+def leg(wl, args, ws, desc):
+    dt, avg_ms = timed_run(wl, args.steps, args.warmup, ws)
+    dt = max_over_ranks(dt, ws)
+    total = sum_over_ranks(float(wl.bytes_per_step * args.steps), ws)
+    return {"value": total / dt / GIB, "unit": "GiB/s", "ms_per_step": dt / args.steps * 1e3,
+            "workload": desc, "roofline": roofline(wl.bytes_per_step, avg_ms, None)}
 
 
 # ---------------------------------------------------------------------------
-# extra legs
+# rank-0 extra legs
 
 def e2e_leg(reps: int = 5) -> dict:
-    """Host-memory frames -> pinned H2D -> kernel -> D2H results (tasx_*_host)."""
+    """Host-memory frames -> pinned H2D -> kernel -> D2H results (tasx_*_host),
+    and the deferred tcp_checksums()/tx_flush() surface at TAS's batch size."""
     n = N_FRAMES
     frames = pktgen.tcp4_frames(n, payload=IP_TOTAL - 52, stride=STRIDE, seed=41)
     pin = xsum.PinnedBuffer(frames.size)
@@ -204,11 +272,10 @@ def e2e_leg(reps: int = 5) -> dict:
             t0 = time.perf_counter()
             xsum.tcp4_cksum_batch_host(0, pin.addr, STRIDE, n, out.ctypes.data)
             ts.append(time.perf_counter() - t0)
-        # deferred per-frame surface with TAS's own batch size (TXBUF_SIZE 32)
         frames32 = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
         base = frames32.ctypes.data
         fl = []
-        for r in range(50):
+        for _ in range(50):
             t0 = time.perf_counter()
             for i in range(32):
                 xsum.defer_tcp4(0, base + i * STRIDE)
@@ -221,8 +288,7 @@ def e2e_leg(reps: int = 5) -> dict:
     alg = n * (IP_TOTAL + 4)
     return {
         "value": alg / t / GIB, "unit": "GiB/s",
-        "pcie_h2d_bytes": n * STRIDE, "pcie_d2h_bytes": n * 4,
-        "ms_per_batch": t * 1e3,
+        "pcie_h2d_bytes": n * STRIDE, "pcie_d2h_bytes": n * 4, "ms_per_batch": t * 1e3,
         "desc": "64K TAS frames in pinned host memory: chunked hipMemcpyAsync H2D (whole 2048 B mbuf rooms) "
                 "-> kernel -> D2H of results, 3 slots pipelined; median of 5",
         "defer_flush_32_us": float(np.median(fl)) * 1e6,
@@ -233,9 +299,8 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
     """The oracle (C restatement of the reference path, per-frame calls) timed on
     this box's host cores, on a bounded sample of the same workload."""
     from oracle import oracle_lib
-    lib_path = None
+    tmp = Path(tempfile.mkdtemp(prefix="tasx_oracle_"))
     try:  # the reference's own flags: -O3 -march=native, built for THIS host
-        tmp = Path(tempfile.mkdtemp(prefix="tasx_oracle_"))
         lib_path = oracle_lib.build(out_dir=tmp, march="native")
         kind_note = "-O3 -march=native (built on this host)"
     except Exception:
@@ -244,7 +309,6 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
     orc = oracle_lib.Oracle(lib_path)
     frames = wl.host.copy()
     n = wl.n
-    # parity of the sample: oracle vs the GPU output of the same batch
     exp = orc.tcp4_batch(frames.copy(), n, stride=STRIDE)
     parity = bool(np.array_equal(exp, gpu_out))
     ncpu = len(os.sched_getaffinity(0))
@@ -260,8 +324,7 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:
         model = "unknown"
-    if lib_path is not None:
-        shutil.rmtree(lib_path.parent, ignore_errors=True)
+    shutil.rmtree(tmp, ignore_errors=True)
     return {
         "value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
         "sample": f"the 64K-frame TCP4 batch (98.6 MB algorithmic), per-frame oracle_tcp_checksums "
@@ -275,8 +338,8 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
 
 def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
     """HBM bytes per launch from rocprofv3 PMC counters, one counter per pass
-    (guide: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950 -> x2;
-    WRITE_SIZE exact for wide stores; both in KiB)."""
+    (MI355X_MICROARCH.md HBM: FETCH_SIZE reads 1/2 of a wide streaming read on
+    gfx950 -> x2; WRITE_SIZE exact for wide stores; both in KiB)."""
     rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not Path(rocprof).exists():
         return None
@@ -286,13 +349,13 @@ def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
         cmd = [rocprof, "--pmc", ctr, "--output-format", "csv", "-d", str(outdir), "-o", "run", "--",
                sys.executable, str(ROOT / "bench.py"), "--pmc-child", mode, "--steps", str(launches)]
         env = dict(os.environ)
-        env.pop("WORLD_SIZE", None)
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
         if r.returncode != 0:
             return {"error": f"rocprofv3 {ctr} rc={r.returncode}: {r.stderr[-400:]}"}
         vals = []
         for csvf in outdir.rglob("*counter_collection.csv"):
-            import csv
             with open(csvf) as fh:
                 for row in csv.DictReader(fh):
                     if kernel_name in row.get("Kernel_Name", "") and row.get("Counter_Name") == ctr:
@@ -304,7 +367,8 @@ def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
     fetch = res["FETCH_SIZE"] * 1024 * 2
     write = res["WRITE_SIZE"] * 1024
     return {"FETCH_SIZE_kib": res["FETCH_SIZE"], "WRITE_SIZE_kib": res["WRITE_SIZE"],
-            "hbm_bytes_per_launch": fetch + write}
+            "hbm_bytes_per_launch": fetch + write,
+            "method": "median over launches; FETCH_SIZE x 2 (gfx950 wide-read correction) + WRITE_SIZE, KiB x 1024"}
 
 
 def pmc_child(mode: str, steps: int):
@@ -318,14 +382,38 @@ def pmc_child(mode: str, steps: int):
 
 
 # ---------------------------------------------------------------------------
+# other BASELINE.json configs (--workload)
 
-def roofline(bytes_per_launch: int, avg_ms: float, traffic):
-    avg_s = avg_ms / 1e3
-    achieved = bytes_per_launch / avg_s / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "launch_avg_us": round(avg_s * 1e6, 3),
-            "algorithmic_bytes_per_launch": bytes_per_launch}
+def other_workload(args, ws, rank):
+    name = args.workload
+    if name == "shard8m":
+        total = 8 * (1 << 20)
+        a, b = shard.shard_ranges(total, ws)[rank]
+        wl = RawWorkload(1, pktgen.SEED + rank, n=b - a, length=RAW_LEN)
+        desc = f"8,388,608 x 1500 B payloads sharded over {ws} GPU(s): {b - a} packets on this rank"
+        scaling = "strong"
+    elif name == "mixed":
+        n = 1 << 20
+        lens = pktgen.mixed_lengths(n, seed=pktgen.SEED + rank).astype(np.int64)
+        slot = (lens + 15) // 16 * 16
+        offs = np.zeros(n, np.int64)
+        np.cumsum(slot[:-1], out=offs[1:])
+        wl = RawWorkload(1, pktgen.SEED + rank, n=n, offsets=offs, lengths=lens,
+                         total_bytes=int(offs[-1] + slot[-1]))
+        desc = "1,048,576 RAW packets per GPU, sizes uniform over {64,576,1500,9000} B in random order"
+        scaling = "weak"
+    else:  # tso
+        wl = Tcp4Workload(2, pktgen.SEED + rank, n=16384, stride=65552, ip_total=65535, host=False)
+        desc = "16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B), tcp_checksums() flag-off, hinted"
+        scaling = "weak"
+    r = leg(wl, args, ws, desc)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(r["value"], 2), "unit": "GiB/s", "n_gpus": ws,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
+                          "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+                          "data": "synthetic (device-generated random bytes)",
+                          "config": {"workload": desc, "parallelism": f"shard{ws}"},
+                          "roofline": r["roofline"]}), flush=True)
 
 
 def main():
@@ -335,36 +423,27 @@ def main():
         return
     ws, rank, local = dist_setup()
     xsum.lib()
+    if args.workload != "tcp4":
+        other_workload(args, ws, rank)
+        if ws > 1:
+            dist.destroy_process_group()
+        return
     rot = max(1, args.rotate)
 
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
-    bytes_per_step = wl.bytes_per_step
-    dt, kern_ms = timed_run(wl, args.steps, args.warmup, ws)
-    # the same batch without the frame-length hint (frames only)
+    head = leg(wl, args, ws, Tcp4Workload.desc)
     wl.hint = 0
-    ndt, nkern = timed_run(wl, args.steps, args.warmup, ws)
+    nohint = leg(wl, args, ws, "same frames, tasx_tcp4_cksum_batch_dev (frames only, no hint)")
     wl.hint = FRAME_LEN
-    ndt = max_over_ranks(ndt, ws)
-    nohint = {"value": sum_over_ranks(float(bytes_per_step * args.steps), ws) / ndt / GIB, "unit": "GiB/s",
-              "ms_per_step": ndt / args.steps * 1e3, "roofline": roofline(bytes_per_step, nkern, None),
-              "workload": "same frames, tasx_tcp4_cksum_batch_dev (no hint)"}
-    dt_max = max_over_ranks(dt, ws)
-    total_bytes = sum_over_ranks(float(bytes_per_step * args.steps), ws)
-    value = total_bytes / dt_max / GIB
-
-    extra = {}
     raw = None
     if not args.no_raw:
         rw = RawWorkload(rot, pktgen.SEED + 1000 + rank)
-        rdt, rkern = timed_run(rw, args.steps, args.warmup, ws)
-        rdt = max_over_ranks(rdt, ws)
-        rtotal = sum_over_ranks(float(rw.bytes_per_step * args.steps), ws)
-        raw = {"value": rtotal / rdt / GIB, "unit": "GiB/s", "ms_per_step": rdt / args.steps * 1e3,
-               "algorithmic_bytes_per_packet": RAW_LEN + 2,
-               "workload": rw.desc, "roofline": roofline(rw.bytes_per_step, rkern, None)}
+        raw = leg(rw, args, ws, RawWorkload.desc)
+        raw["algorithmic_bytes_per_packet"] = RAW_LEN + 2
         del rw
+        torch.cuda.empty_cache()
 
-    traffic = None
+    extra = {}
     if rank == 0 and ws == 1:
         torch.cuda.synchronize()
         gpu_out = wl.outs[0].cpu().numpy().view(np.uint16).copy()
@@ -378,7 +457,7 @@ def main():
             p = pmc_leg("tcp4", "tcp4", 64)
             extra["pmc"] = p
             if p and "hbm_bytes_per_launch" in p:
-                traffic = int(p["hbm_bytes_per_launch"])
+                head["roofline"]["traffic"] = int(p["hbm_bytes_per_launch"])
             if raw is not None:
                 pr = pmc_leg("raw", "_raw_", 64)
                 if pr and "hbm_bytes_per_launch" in pr:
@@ -387,17 +466,17 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": ws,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3,
+            "metric": METRIC, "value": round(head["value"], 2), "unit": "GiB/s", "n_gpus": ws,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (splitmix64-seeded frames, pktgen.py)",
+            "data": "synthetic (splitmix64-seeded frames, tas_amd/pktgen.py)",
             "config": {"workload": Tcp4Workload.desc, "frames_per_gpu_step": N_FRAMES,
                        "algorithmic_bytes_per_frame": IP_TOTAL + 4, "rotation_batches": rot,
                        "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
-            "roofline": roofline(bytes_per_step, kern_ms, traffic),
+            "roofline": head["roofline"],
             "cpu_baseline": extra.get("cpu_baseline"),
+            "tcp4_nohint": nohint,
         }
-        line["tcp4_nohint"] = nohint
         if raw is not None:
             line["raw"] = raw
         if "e2e" in extra:
