@@ -74,7 +74,7 @@ int tasx_set_diag_buffer(void *dev_buf)
 
 int tasx_set_kernel_config(int variant, unsigned ppg)
 {
-  if (variant < 0 || variant > 17 || ppg > 64)
+  if (variant < 0 || variant > 25 || ppg > 160)
     return set_err(-EINVAL, "kernel config %d/%u out of range", variant, ppg);
   g_variant = variant;
   g_ppg = ppg;

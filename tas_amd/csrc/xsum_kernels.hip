@@ -541,12 +541,12 @@ __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
   return fold64_to_18(acc);
 }
 
-template <int U>
-__global__ __launch_bounds__(kBlock) void pkt16_raw_kernel(tasx_raw_params p)
+template <int U, int BS = kBlock>
+__global__ __launch_bounds__(BS) void pkt16_raw_kernel(tasx_raw_params p)
 {
   const int gl = threadIdx.x & 15;
-  const uint32_t ngroups = gridDim.x * (kBlock / 16);
-  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  const uint32_t ngroups = gridDim.x * (BS / 16);
+  uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
   // descriptor prefetch (every lane of the group reads the same word)
   uint64_t off = 0;
   uint32_t len = p.len0;
@@ -783,24 +783,25 @@ __device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
   return (w >> (8 * (b & 3))) & 0xffu;
 }
 
+template <int BS>
 __device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
 {
   // 100 MHz global clock; one record of 4 stamps per wave
   const uint64_t t = __builtin_amdgcn_s_memrealtime();
   if ((threadIdx.x & 63) == 0) {
-    const uint64_t w = ((uint64_t) blockIdx.x * (kBlock / 64) + threadIdx.x / 64);
+    const uint64_t w = ((uint64_t) blockIdx.x * (BS / 64) + threadIdx.x / 64);
     p.diag[w * 4 + slot] = t;
   }
 }
 
-template <int U, int DIAG = 0>
-__global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params p)
+template <int U, int DIAG = 0, int BS = kBlock>
+__global__ __launch_bounds__(BS) void pkt16_tcp4_tas_kernel(tasx_tcp4_params p)
 {
-  if constexpr (DIAG)
-    diag_stamp(p, 0);
+  if constexpr (DIAG == 1)
+    diag_stamp<BS>(p, 0);
   const int gl = threadIdx.x & 15;
   const int gbase = (threadIdx.x & 63) & ~15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return; // whole 16-lane group (one DPP row) leaves together
   uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
@@ -819,12 +820,17 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params
   for (int u = 0; u < U; ++u)
     v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, nld - 1));
   // total_length: ip-relative bytes 2 and 3
-  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
-  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
-  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
-  const uint32_t tl = (ba << 8) | bb;
-  if constexpr (DIAG)
-    diag_stamp(p, 1);
+  uint32_t tl;
+  if constexpr (DIAG >= 2) { // timing diagnostic: length from the hint (wrong results)
+    tl = hint - p.ip_off;
+  } else {
+    const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
+    const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
+    const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
+    tl = (ba << 8) | bb;
+  }
+  if constexpr (DIAG == 1)
+    diag_stamp<BS>(p, 1);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const int E = 20 + (int) len;                              // ip-relative end
   const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;        // chunks of [ip, ip+E)
@@ -841,7 +847,7 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t c = (uint32_t) gl + 16u * u;
-    if (u == 0 && gl < NS) {
+    if (DIAG < 3 && u == 0 && gl < NS) {
       // header chunk: split by byte masks (ip-relative base of dword j)
       const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
 #pragma unroll
@@ -881,8 +887,8 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params
   }
   uint32_t c_ip = fold64_to_18(acc_ip);
   uint32_t c_ph = fold64_to_18(acc_ph);
-  if constexpr (DIAG)
-    diag_stamp(p, 2);
+  if constexpr (DIAG == 1)
+    diag_stamp<BS>(p, 2);
   part = row_sum16(part);
   c_ip = row_sum16(c_ip);
   c_ph = row_sum16(c_ph);
@@ -907,12 +913,302 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_tas_kernel(tasx_tcp4_params
       st8(l4 + 17, tcpc >> 8);
     }
   }
-  if constexpr (DIAG)
-    diag_stamp(p, 3);
+  if constexpr (DIAG == 1)
+    diag_stamp<BS>(p, 3);
 }
 
-template <typename K, typename Prm>
-int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t s)
+// Header-channel byte masks for the TAS-layout kernel, precomputed at compile
+// time: [ip & 15][chunk 0..3][channel IP, PH, L4][dword].  Channels over
+// ip-relative byte offsets: IP = [0,10)+[12,20), PH = {9}+[12,20),
+// L4 = [20,36)+[38,inf) (the segment minus tcp.chksum; its end is applied by the
+// tail fix-up).  One 48-byte table row per lane replaces ~300 VALU of mask math.
+struct HdrMasks {
+  uint32_t m[16][4][3][4];
+};
+
+constexpr uint32_t cx_in_range(int base, int lo, int hi)
+{
+  int bl = lo - base < 0 ? 0 : (lo - base > 4 ? 4 : lo - base);
+  int bh = hi - base < 0 ? 0 : (hi - base > 4 ? 4 : hi - base);
+  uint32_t m = 0;
+  for (int b = bl; b < bh; ++b)
+    m |= 0xffu << (8 * b);
+  return m;
+}
+
+constexpr HdrMasks make_hdr_masks()
+{
+  HdrMasks t{};
+  for (int hb = 0; hb < 16; ++hb)
+    for (int c = 0; c < 4; ++c)
+      for (int j = 0; j < 4; ++j) {
+        const int base = 16 * c + 4 * j - hb;
+        t.m[hb][c][0][j] = cx_in_range(base, 0, 10) | cx_in_range(base, 12, 20);
+        t.m[hb][c][1][j] = cx_in_range(base, 9, 10) | cx_in_range(base, 12, 20);
+        t.m[hb][c][2][j] = cx_in_range(base, 20, 36) | cx_in_range(base, 38, 1 << 20);
+      }
+  return t;
+}
+
+__constant__ HdrMasks kHdrMasks = make_hdr_masks();
+
+__device__ __forceinline__ uint64_t masked_sum(u32x4 v, u32x4 m)
+{
+  return (uint64_t) (v.x & m.x) + (v.y & m.y) + (uint64_t) (v.z & m.z) + (v.w & m.w);
+}
+
+// bytes [t, 16) of a chunk as a dword mask vector
+__device__ __forceinline__ u32x4 suffix_mask(int t)
+{
+  u32x4 m;
+  m.x = in_range(0, t, 16);
+  m.y = in_range(4, t, 16);
+  m.z = in_range(8, t, 16);
+  m.w = in_range(12, t, 16);
+  return m;
+}
+
+template <int U, int BS = kBlock>
+__global__ __launch_bounds__(BS) void pkt16_tcp4_tasm_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const int gbase = (threadIdx.x & 63) & ~15;
+  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group (one DPP row) leaves together
+  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+  uint8_t *ip = f + p.ip_off;
+  const uintptr_t A0 = (uintptr_t) ip & ~(uintptr_t) 15;
+  const u32x4 *c0p = (const u32x4 *) A0;
+  const int hb = (int) ((uintptr_t) ip & 15);
+  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
+  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
+  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, nld - 1));
+  // this lane's header-channel masks (lanes 0..3 only; L1/L2-resident table)
+  u32x4 mip = u32x4{0, 0, 0, 0}, mph = mip, ml4 = mip;
+  if (gl < 4) {
+    const u32x4 *mt = (const u32x4 *) &kHdrMasks.m[hb][gl][0][0];
+    mip = mt[0];
+    mph = mt[1];
+    ml4 = mt[2];
+  }
+  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
+  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
+  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
+  const uint32_t tl = (ba << 8) | bb;
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const int E = 20 + (int) len;
+  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
+  const uint32_t need = min(nch, 16u * U);
+  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
+    const uint32_t top = max(need, nld);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, top - 1));
+  }
+  const uint32_t last = nch - 1;
+  const int tail = (int) (((uintptr_t) ip + E) - (((uintptr_t) ip + E - 1) & ~(uintptr_t) 15));
+  uint64_t acc = 0;
+  uint64_t acc_ip = masked_sum(v[0], mip), acc_ph = masked_sum(v[0], mph);
+  // chunk gl (u == 0): the header lanes add their L4 bytes through the mask
+  if (gl < 4) {
+    if ((uint32_t) gl <= last) {
+      acc += masked_sum(v[0], ml4);
+      if ((uint32_t) gl == last && tail < 16) // short segment ends in a header chunk
+        acc -= masked_sum(v[0], ml4 & suffix_mask(tail));
+    }
+  } else if ((uint32_t) gl < nch) {
+    acc += (uint64_t) v[0].x + v[0].y + v[0].z + v[0].w;
+  }
+#pragma unroll
+  for (int u = 1; u < U; ++u) {
+    const uint32_t c = (uint32_t) gl + 16u * u;
+    acc += c < nch ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
+  }
+  if (last >= 4u && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
+    const uint32_t ut = last >> 4;
+    u32x4 t = v[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u)
+      if (ut == (uint32_t) u)
+        t = v[u];
+    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
+  }
+  uint32_t part = fold64_to_18(acc);
+  if (nch > 16u * U) {
+    Chunks<U> rest;
+    rest.c0p = c0p + 16u * U;
+    rest.nch = nch - 16u * U;
+    rest.head = 0;
+    rest.tail = tail;
+    part += group_lane_sum<U>(rest, gl);
+  }
+  uint32_t c_ip = fold64_to_18(acc_ip);
+  uint32_t c_ph = fold64_to_18(acc_ph);
+  part = row_sum16(part);
+  c_ip = row_sum16(c_ip);
+  c_ph = row_sum16(c_ph);
+  if (gl == 15) {
+    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
+    if (hb & 1) {
+      ri = bswap16(ri);
+      rp = bswap16(rp);
+      r4 = bswap16(r4);
+    }
+    const uint32_t ipc = inv_result(residue(ri));
+    uint32_t tcpc = 0;
+    if (tl >= 20)
+      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
+    if (p.out)
+      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+    if (p.flags & TASX_F_INPLACE) {
+      uint8_t *l4 = ip + 20;
+      st8(ip + 10, ipc);
+      st8(ip + 11, ipc >> 8);
+      st8(l4 + 16, tcpc);
+      st8(l4 + 17, tcpc >> 8);
+    }
+  }
+}
+
+// Lean TAS-layout TCP4 kernel: 32-bit byte offsets from the (16-byte aligned)
+// batch base, so every load is global_load_dwordx4 v, v_off, s[base] (one VGPR
+// per address), and the header-channel byte masks come from three 64-bit
+// constants (bit x+16 = ip-relative byte x is in the channel) expanded with
+// one multiply -- no tables, no 64-bit shifts per byte range.
+constexpr uint64_t kPatIP = (((1ull << 10) - 1) << 16) | (((1ull << 8) - 1) << 28);  // [0,10)+[12,20)
+constexpr uint64_t kPatPH = (1ull << 25) | (((1ull << 8) - 1) << 28);                // {9}+[12,20)
+constexpr uint64_t kPatNL4 = ((1ull << 36) - 1) | (3ull << 52);                     // [-16,20)+{36,37}
+
+__device__ __forceinline__ uint32_t expand4(uint32_t bits)
+{
+  return ((bits * 0x204081u) & 0x01010101u) * 0xffu; // 4 bits -> 4 byte masks
+}
+
+__device__ __forceinline__ uint32_t pat_bits(uint64_t pat, int s)
+{
+  return s < 64 ? (uint32_t) (pat >> s) & 0xfu : 0u;
+}
+
+__device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
+{
+  return __builtin_nontemporal_load((gcu4 *) (base + off));
+}
+
+template <int U, int BS = kBlock>
+__global__ __launch_bounds__(BS) void pkt16_tcp4_lean_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const int gbase = (threadIdx.x & 63) & ~15;
+  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
+  const uint32_t fo = (uint32_t) pkt_offset(p.off, p.stride, i);
+  const uint32_t ipo = fo + p.ip_off;
+  const uint32_t a0 = ipo & ~15u;
+  const int hb = (int) (ipo & 15u);
+  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
+  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
+  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
+  // round 1: U loads back to back, no branches (lanes past the hinted range
+  // re-read its last chunk: same line, no extra HBM traffic)
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + 16u * u, nld - 1));
+  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
+  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
+  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
+  const uint32_t tl = (ba << 8) | bb;
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const int E = 20 + (int) len;
+  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
+  const uint32_t need = min(nch, 16u * U);
+  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
+    const uint32_t top = max(need, nld);
+    if ((uint32_t) gl >= nld) // lanes below nld already hold chunk gl
+      v[0] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl, top - 1));
+#pragma unroll
+    for (int u = 1; u < U; ++u)
+      v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + 16u * u, top - 1));
+  }
+  const uint32_t last = nch - 1;
+  const int tail = (int) ((ipo + (uint32_t) E) - ((ipo + (uint32_t) E - 1) & ~15u));
+  uint64_t acc = 0, acc_ip = 0, acc_ph = 0;
+  if (gl < 4) {
+    const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
+    const bool l4ok = (uint32_t) gl <= last;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int sft = 16 * gl + 4 * j - hb + 16;
+      acc_ip += w[j] & expand4(pat_bits(kPatIP, sft));
+      acc_ph += w[j] & expand4(pat_bits(kPatPH, sft));
+      uint32_t ml4 = ~expand4(pat_bits(kPatNL4, sft));
+      if ((uint32_t) gl == last) // a short segment ends in this chunk: bytes < tail only
+        ml4 &= in_range(4 * j, 0, tail);
+      acc += l4ok ? (w[j] & ml4) : 0u;
+    }
+  } else if ((uint32_t) gl < nch) {
+    acc += (uint64_t) v[0].x + v[0].y + v[0].z + v[0].w;
+  }
+#pragma unroll
+  for (int u = 1; u < U; ++u) {
+    const uint32_t c = (uint32_t) gl + 16u * u;
+    acc += c < nch ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
+  }
+  if (last >= 4u && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
+    const uint32_t ut = last >> 4;
+    u32x4 t = v[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u)
+      if (ut == (uint32_t) u)
+        t = v[u];
+    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
+  }
+  uint32_t part = fold64_to_18(acc);
+  if (nch > 16u * U) {
+    Chunks<U> rest;
+    rest.c0p = (const u32x4 *) (base + a0) + 16u * U;
+    rest.nch = nch - 16u * U;
+    rest.head = 0;
+    rest.tail = tail;
+    part += group_lane_sum<U>(rest, gl);
+  }
+  uint32_t c_ip = fold64_to_18(acc_ip);
+  uint32_t c_ph = fold64_to_18(acc_ph);
+  part = row_sum16(part);
+  c_ip = row_sum16(c_ip);
+  c_ph = row_sum16(c_ph);
+  if (gl == 15) {
+    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
+    if (hb & 1) {
+      ri = bswap16(ri);
+      rp = bswap16(rp);
+      r4 = bswap16(r4);
+    }
+    const uint32_t ipc = inv_result(residue(ri));
+    uint32_t tcpc = 0;
+    if (tl >= 20)
+      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
+    if (p.out)
+      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+    if (p.flags & TASX_F_INPLACE) {
+      uint8_t *ip = p.base + ipo;
+      st8(ip + 10, ipc);
+      st8(ip + 11, ipc >> 8);
+      st8(ip + 36, tcpc);
+      st8(ip + 37, tcpc >> 8);
+    }
+  }
+}
+
+template <int BS = kBlock, typename K, typename Prm>
+int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t s, uint32_t lds_bytes = 0)
 {
   static int ncu = 0;
   if (ncu == 0) {
@@ -921,13 +1217,16 @@ int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t 
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       ncu = 256;
   }
-  uint64_t blocks = ((uint64_t) p.n + 15) / 16;
+  constexpr uint64_t fpb = BS / 16; // 16-lane groups (frames) per block
+  uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
   const uint64_t cap = (uint64_t) ncu * blocks_per_cu;
   if (blocks_per_cu && blocks > cap)
     blocks = cap;
   if (blocks == 0)
     return 0;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
+  // lds_bytes: dynamic LDS reserved only to cap blocks per CU (occupancy
+  // experiments); the kernels use none
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds_bytes, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -948,7 +1247,15 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-// variant: 0 = auto (RAW 11; TCP4 16 for TAS layout + hints, else 12), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
+// lean kernel preconditions: 16-byte aligned base, stride mode, every frame's
+// bytes within 4 GiB of the base
+static bool lean_ok(const tasx_tcp4_params &p)
+{
+  return ((uintptr_t) p.base & 15u) == 0 && p.off == nullptr &&
+         (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
+}
+
+// variant: 0 = auto (RAW 11; TCP4 25 (lean, falls back to 12) for TAS layout + hints, else 12), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
 // 8..11 = pkt16 persistent (ppg = blocks per CU for 8..10; 11 = one block per 16 packets)
 // ppg: packets per group for the flat kernels / blocks per CU for pkt16 (0 = auto)
 static uint32_t auto_ppg(uint32_t n, uint32_t P, uint32_t groups_per_block)
@@ -969,7 +1276,10 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, uint32_t p
   const int maxb = 256 * 64;
   switch (variant) {
   case 0:
-  case 11: return launch_persistent(pkt16_raw_kernel<6>, *p, 0, s);
+  case 11: return launch_persistent(pkt16_raw_kernel<6>, *p, 0, s, ppg * 1024u);
+  case 18: return launch_persistent<64>(pkt16_raw_kernel<6, 64>, *p, 0, s);
+  case 19: return launch_persistent<128>(pkt16_raw_kernel<6, 128>, *p, 0, s);
+  case 20: return launch_persistent<512>(pkt16_raw_kernel<6, 512>, *p, 0, s);
   case 8: return launch_persistent(pkt16_raw_kernel<6>, *p, ppg ? ppg : 8, s);
   case 9: return launch_persistent(pkt16_raw_kernel<8>, *p, ppg ? ppg : 8, s);
   case 10: return launch_persistent(pkt16_raw_kernel<4>, *p, ppg ? ppg : 8, s);
@@ -989,20 +1299,30 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t
   hipStream_t s = (hipStream_t) stream;
   const int maxb = 256 * 64;
   if (variant == 0) // TAS layout with hints -> header from the chunks; else byte loads
-    variant = (p->l4_off == p->ip_off + 20 && (p->flen || p->flen0)) ? 16 : 12;
-  if (variant >= 15 && p->l4_off != p->ip_off + 20)
+    variant = (p->l4_off == p->ip_off + 20 && (p->flen || p->flen0)) ? 25 : 12;
+  if (((variant >= 15 && variant <= 22) || variant == 23 || variant == 24 || variant == 25) &&
+      p->l4_off != p->ip_off + 20)
     variant = 12;
   switch (variant) {
   case 8: return launch_persistent(pkt16_tcp4_kernel<6>, *p, ppg ? ppg : 8, s);
   case 9: return launch_persistent(pkt16_tcp4_kernel<8>, *p, ppg ? ppg : 8, s);
   case 10: return launch_persistent(pkt16_tcp4_kernel<4>, *p, ppg ? ppg : 12, s);
   case 11: return launch_persistent(pkt16_tcp4_kernel<6>, *p, 0, s);
-  case 12: return launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s);
+  case 12: return launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s, ppg * 1024u);
   case 13: return launch_persistent(pkt16_tcp4_spec_kernel<8>, *p, 0, s);
   case 14: return launch_persistent(pkt16_tcp4_spec_kernel<6, 1>, *p, 0, s); // timing diagnostic
-  case 15: return launch_persistent(pkt16_tcp4_tas_kernel<6>, *p, 0, s);
-  case 16: return launch_persistent(pkt16_tcp4_tas_kernel<8>, *p, 0, s);
+  case 15: return launch_persistent(pkt16_tcp4_tas_kernel<6>, *p, 0, s, ppg * 1024u);
+  case 16: return launch_persistent(pkt16_tcp4_tas_kernel<8>, *p, 0, s, ppg * 1024u);
   case 17: return p->diag ? launch_persistent(pkt16_tcp4_tas_kernel<6, 1>, *p, 0, s) : -2;
+  case 18: return launch_persistent<64>(pkt16_tcp4_tas_kernel<8, 0, 64>, *p, 0, s);
+  case 19: return launch_persistent<128>(pkt16_tcp4_tas_kernel<8, 0, 128>, *p, 0, s);
+  case 20: return launch_persistent<512>(pkt16_tcp4_tas_kernel<8, 0, 512>, *p, 0, s);
+  case 21: return launch_persistent(pkt16_tcp4_tas_kernel<6, 2>, *p, 0, s); // diag: no shuffles
+  case 22: return launch_persistent(pkt16_tcp4_tas_kernel<6, 3>, *p, 0, s); // diag: + no header split
+  case 23: return launch_persistent(pkt16_tcp4_tasm_kernel<6>, *p, 0, s);
+  case 24: return launch_persistent(pkt16_tcp4_tasm_kernel<8>, *p, 0, s);
+  case 25: return lean_ok(*p) ? launch_persistent(pkt16_tcp4_lean_kernel<6>, *p, 0, s)
+                              : launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s);
   case 2: return launch_flat<64, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
   case 1: return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
   case 3: return launch_flat<64, 16, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);

@@ -239,7 +239,7 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 11, 12, 13, 15, 16])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 11, 12, 13, 15, 16, 18, 19, 20, 23, 24, 25])
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
