@@ -133,14 +133,28 @@ int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off,
 int tasx_pending(unsigned ctx_id);
 int tasx_flush(unsigned ctx_id);
 
+/* Zero-copy frames: declare the host region the context's frames live in
+ * (TAS: the per-core mbuf mempool, tas/fast/network.c:320-330).  It is pinned
+ * with hipHostRegister unless it already is (tasx_host_alloc).  A flush whose
+ * frames all lie in the region (TAS layout, tcp = ip + 20) is done without any
+ * copy: the kernel reads the frames over PCIe and stores both checksum fields
+ * in place.  Other flushes take the staged path. */
+int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes);
+/* counts of zero-copy and staged flushes since tasx_ctx_init */
+int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
+    uint32_t *staged_flushes);
+
 /* ---------------------------------------------------------------------- */
-/* Kernel selection, for tuning and A/B tests (process-wide, not thread-safe
- * against concurrent launches).  variant 0 = automatic (flat-stream kernel),
- * 1 = wave-per-packet kernel, 2..7 = fixed shapes; ppg = packets per lane
- * group for the flat-stream kernels (0 = automatic). */
-int tasx_set_kernel_config(int variant, unsigned ppg);
-/* Device buffer for the timestamp-diagnostic kernel variant (17): 4 x u64 per
- * wave of s_memrealtime (100 MHz) stamps.  NULL disables. */
+/* Kernel selection, for A/B tests (process-wide; set it before launching).
+ *   0 automatic: RAW -> 2; TCP4 -> 3 for the TAS layout in stride mode with a
+ *     frame-length hint, else 2
+ *   1 first-generation group-per-packet kernels (A/B baseline)
+ *   2 raw_group_kernel / tcp4_frame_kernel (any layout)
+ *   3 tcp4_tas_kernel (TAS layout, stride mode; falls back to 2)
+ *   4 tcp4_tas_kernel with wave-timeline stamps into the diag buffer */
+int tasx_set_kernel_variant(int variant);
+/* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
+ * wave.  NULL disables. */
 int tasx_set_diag_buffer(void *dev_buf);
 
 /* ---------------------------------------------------------------------- */
@@ -148,6 +162,8 @@ int tasx_set_diag_buffer(void *dev_buf);
 void *tasx_host_alloc(size_t bytes);          /* pinned host memory */
 int tasx_host_free(void *p);
 int tasx_host_register(void *p, size_t bytes);  /* pin existing memory */
+/* the device's address of pinned host memory (zero-copy kernel access) */
+void *tasx_host_device_pointer(void *p);
 int tasx_host_unregister(void *p);
 void *tasx_dev_alloc(int device, size_t bytes);
 int tasx_dev_free(void *p);

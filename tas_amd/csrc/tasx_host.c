@@ -61,9 +61,8 @@ int tasx_device_count(void)
 /* ---------------------------------------------------------------------- */
 /* device-resident batches */
 
-/* kernel selection (tasx_set_kernel_config); 0/0 = automatic */
+/* kernel selection (tasx_set_kernel_variant); 0 = automatic */
 static int g_variant = 0;
-static unsigned g_ppg = 0;
 static uint64_t *g_diag = NULL;
 
 int tasx_set_diag_buffer(void *dev_buf)
@@ -72,12 +71,11 @@ int tasx_set_diag_buffer(void *dev_buf)
   return 0;
 }
 
-int tasx_set_kernel_config(int variant, unsigned ppg)
+int tasx_set_kernel_variant(int variant)
 {
-  if (variant < 0 || variant > 25 || ppg > 160)
-    return set_err(-EINVAL, "kernel config %d/%u out of range", variant, ppg);
+  if (variant < 0 || variant > 4)
+    return set_err(-EINVAL, "kernel variant %d out of range", variant);
   g_variant = variant;
-  g_ppg = ppg;
   return 0;
 }
 
@@ -100,7 +98,7 @@ int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
   p.stride = stride;
   p.len0 = len0;
   p.n = n;
-  r = tasx_launch_raw(&p, g_variant, g_ppg, stream);
+  r = tasx_launch_raw(&p, g_variant, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
   return 0;
@@ -133,7 +131,7 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
   p.flen = flen;
   p.flen0 = flen0;
   p.diag = g_diag;
-  r = tasx_launch_tcp4(&p, g_variant, g_ppg, stream);
+  r = tasx_launch_tcp4(&p, g_variant, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
   return 0;
@@ -166,6 +164,15 @@ struct tasx_ctx {
   uint8_t **pend_ip;
   uint8_t **pend_l4;
   uint32_t npend;
+  /* zero-copy frame region (tasx_ctx_register_frames) */
+  uint8_t *zc_host;
+  uint8_t *zc_dev;
+  size_t zc_bytes;
+  int zc_registered; /* we called hipHostRegister on it */
+  uint64_t *d_hoff;  /* device view of h_off[0] (pinned) */
+  uint32_t *h_flen;  /* pinned frame-length hints, and its device view */
+  uint32_t *d_hflen;
+  uint32_t n_zerocopy_flushes, n_staged_flushes;
 };
 
 static struct tasx_ctx g_ctx[TASX_MAX_CTX];
@@ -196,6 +203,10 @@ static void ctx_release(struct tasx_ctx *c)
     if (c->h_out[s])
       hipHostFree(c->h_out[s]);
   }
+  if (c->h_flen)
+    hipHostFree(c->h_flen);
+  if (c->zc_registered)
+    hipHostUnregister(c->zc_host);
   free(c->pend_ip);
   free(c->pend_l4);
   memset(c, 0, sizeof(*c));
@@ -235,6 +246,12 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
       ctx_release(c);
       return hip_err(e, "tasx_ctx_init allocation");
     }
+  }
+  if ((e = hipHostMalloc((void **) &c->h_flen, (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &c->d_hoff, c->h_off[0], 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &c->d_hflen, c->h_flen, 0)) != hipSuccess) {
+    ctx_release(c);
+    return hip_err(e, "tasx_ctx_init pinned descriptors");
   }
   c->pend_ip = calloc(c->slot_frames, sizeof(*c->pend_ip));
   c->pend_l4 = calloc(c->slot_frames, sizeof(*c->pend_l4));
@@ -325,7 +342,7 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     p.l4_off = l4_off;
     p.flags = 0;
 
-    if (tasx_launch_tcp4(&p, g_variant, g_ppg, c->st[s]) != 0)
+    if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 4,
         hipMemcpyDeviceToHost, c->st[s]));
@@ -377,7 +394,7 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     p.stride = stride;
     p.len0 = len0;
     p.n = jobs[s].cnt;
-    if (tasx_launch_raw(&p, g_variant, g_ppg, c->st[s]) != 0)
+    if (tasx_launch_raw(&p, g_variant, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 2,
         hipMemcpyDeviceToHost, c->st[s]));
@@ -434,6 +451,98 @@ int tasx_pending(unsigned ctx_id)
   return (int) c->npend;
 }
 
+int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  void *dev = NULL;
+  hipError_t e;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!base || bytes == 0)
+    return set_err(-EINVAL, "register_frames: empty region");
+  if (c->zc_host)
+    return set_err(-EINVAL, "ctx %u already has a frame region", ctx_id);
+  HIPCHK(hipSetDevice(c->device));
+  /* already pinned (tasx_host_alloc / hipHostMalloc)?  else pin it */
+  e = hipHostGetDevicePointer(&dev, base, 0);
+  if (e != hipSuccess) {
+    (void) hipGetLastError();
+    HIPCHK(hipHostRegister(base, bytes, hipHostRegisterMapped));
+    c->zc_registered = 1;
+    e = hipHostGetDevicePointer(&dev, base, 0);
+    if (e != hipSuccess) {
+      hipHostUnregister(base);
+      c->zc_registered = 0;
+      return hip_err(e, "hipHostGetDevicePointer");
+    }
+  }
+  c->zc_host = (uint8_t *) base;
+  c->zc_dev = (uint8_t *) dev;
+  c->zc_bytes = bytes;
+  return 0;
+}
+
+int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged_flushes)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (zerocopy_flushes)
+    *zerocopy_flushes = c->n_zerocopy_flushes;
+  if (staged_flushes)
+    *staged_flushes = c->n_staged_flushes;
+  return 0;
+}
+
+/* Zero-copy flush: every pending frame lies in the registered region and has
+ * the TAS layout (tcp = ip + 20).  The kernel reads the frames straight from
+ * host memory over PCIe (only the bytes it sums), writes both checksum fields
+ * in place, and the descriptors (offset, frame-length hint) are read from
+ * pinned memory: one launch + one synchronize, no copies. */
+static int flush_zerocopy(struct tasx_ctx *c)
+{
+  tasx_tcp4_params p;
+  uint32_t i, n = c->npend;
+  for (i = 0; i < n; i++) {
+    const uint8_t *ip = c->pend_ip[i];
+    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+    c->h_off[0][i] = (uint64_t) (ip - c->zc_host);
+    c->h_flen[i] = (tl < 20 ? 20 : tl);
+  }
+  memset(&p, 0, sizeof(p));
+  p.base = c->zc_dev;
+  p.off = c->d_hoff;
+  p.out = NULL;
+  p.n = n;
+  p.ip_off = 0;
+  p.l4_off = 20;
+  p.flags = TASX_F_INPLACE;
+  p.flen = c->d_hflen;
+  if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
+    return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+  HIPCHK(hipStreamSynchronize(c->st[0]));
+  c->n_zerocopy_flushes++;
+  c->npend = 0;
+  return 0;
+}
+
+static int zerocopy_ok(const struct tasx_ctx *c)
+{
+  uint32_t i;
+  if (!c->zc_host)
+    return 0;
+  for (i = 0; i < c->npend; i++) {
+    const uint8_t *ip = c->pend_ip[i];
+    uint32_t tl;
+    if (c->pend_l4[i] != ip + 20 || ip < c->zc_host || ip + 20 > c->zc_host + c->zc_bytes)
+      return 0;
+    tl = ((uint32_t) ip[2] << 8) | ip[3];
+    if (ip + (tl < 38 ? 38 : tl) > c->zc_host + c->zc_bytes)
+      return 0;
+  }
+  return 1;
+}
+
 /* Gather every pending frame as [20-byte IPv4 header | L4 segment] into
  * pinned staging (16-byte aligned records: the sum is relative to the header
  * / segment start, so where a record sits does not change it), run the TCP4
@@ -448,6 +557,9 @@ int tasx_flush(unsigned ctx_id)
   if (c->npend == 0)
     return 0;
   HIPCHK(hipSetDevice(c->device));
+  if (zerocopy_ok(c))
+    return flush_zerocopy(c);
+  c->n_staged_flushes++;
   while (start < c->npend) {
     const int s = 0;
     uint8_t *stage = c->h_stage[s];
@@ -483,7 +595,7 @@ int tasx_flush(unsigned ctx_id)
     p.ip_off = 0;
     p.l4_off = 20;
     p.flags = 0;
-    if (tasx_launch_tcp4(&p, g_variant, g_ppg, c->st[s]) != 0)
+    if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
     HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4,
         hipMemcpyDeviceToHost, c->st[s]));
@@ -516,6 +628,17 @@ int tasx_host_free(void *p)
 {
   HIPCHK(hipHostFree(p));
   return 0;
+}
+
+void *tasx_host_device_pointer(void *p)
+{
+  void *d = NULL;
+  hipError_t e = hipHostGetDevicePointer(&d, p, 0);
+  if (e != hipSuccess) {
+    hip_err(e, "hipHostGetDevicePointer");
+    return NULL;
+  }
+  return d;
 }
 
 int tasx_host_register(void *p, size_t bytes)

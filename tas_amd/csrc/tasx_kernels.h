@@ -37,10 +37,9 @@ typedef struct tasx_tcp4_params {
   uint64_t *diag;        /* diagnostic timestamp buffer (diag variants only) */
 } tasx_tcp4_params;
 
-/* variant: 0 auto (flat-stream kernel), 1 / 7 wave-per-packet kernels,
- * 2..6 flat-stream shapes; ppg: packets per group (0 auto).  0 on success. */
-int tasx_launch_raw(const tasx_raw_params *p, int variant, uint32_t ppg, void *stream);
-int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t ppg, void *stream);
+/* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
+int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
+int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 
 #ifdef __cplusplus
 }

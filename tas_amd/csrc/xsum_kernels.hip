@@ -4,11 +4,13 @@
 //
 // Bandwidth-bound integer fold, no MFMA.  Layout and arithmetic:
 //   * A packet (RAW payload, or the L4 segment of a TCP4 frame) is covered by
-//     the naturally aligned 16-byte chunks [start & ~15, end rounded up).  Each
-//     lane of a G-lane packet group loads whole chunks with global_load_dwordx4
-//     (1 KiB per wave instruction, fully coalesced); only the first and the last
-//     chunk are byte-masked.  Reading an aligned chunk that contains a valid
-//     byte never crosses a page, so it cannot fault.
+//     the naturally aligned 16-byte chunks [start & ~15, end rounded up).  A
+//     16-lane group (one DPP row) owns a packet; lane gl loads chunks gl,
+//     gl+16, ... with non-temporal global_load_dwordx4, U per lane issued back
+//     to back with no branches (lanes past the packet re-read its last chunk:
+//     same line, no extra HBM traffic, dropped by a select).  Reading an
+//     aligned chunk that contains a valid byte never crosses a page, so it
+//     cannot fault.
 //   * Sums are taken over ADDRESS-aligned LE 16-bit words.  DPDK sums words
 //     counted from the buffer start; for an odd start the two frames differ by
 //     a byte swap of the folded result (RFC 1071 section 2(B)), applied at the end.
@@ -17,11 +19,18 @@
 //     the dword sum is congruent to the 16-bit word sum, and every end-around
 //     fold keeps both the residue mod 0xffff and "zero iff all words zero" --
 //     which is exactly what rte_raw_cksum returns.
-//   * Group reduction: xor-shuffles inside the G-lane group.
+//     Bytes before / after the packet in its first / last chunk are removed by
+//     exact subtraction on the lane that holds that chunk.
+//   * Group reduction: 4 DPP row_shr adds; the total lands in lane 15.
 //   * TCP4 (rte_ipv4_cksum + rte_ipv4_udptcp_cksum) depends only on the
 //     residue mod 0xffff of (header sum) and of (L4 sum + pseudo-header), so the
-//     zeroed checksum fields are handled by subtracting their bytes modulo
-//     0xffff instead of masking the loads.
+//     zeroed checksum fields are handled by masking or by subtracting their
+//     bytes modulo 0xffff.
+//
+// Kernels (tasx_set_kernel_variant): 2 = raw_group_kernel / tcp4_frame_kernel
+// (any layout), 3 = tcp4_tas_kernel (TAS frame layout, stride mode), 1 = the
+// first-generation group-per-packet kernels (kept as the A/B baseline),
+// 4 = tcp4_tas_kernel with wave-timeline stamps (diagnostic).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -169,6 +178,8 @@ __device__ __forceinline__ uint64_t pkt_offset(const uint64_t *off, uint64_t str
 }
 
 // ---------------------------------------------------------------------------
+// First-generation kernels (variant 1, the A/B baseline): one G-lane group per
+// packet, xor-shuffle reductions, byte loads for the TCP4 header.
 // RAW: out[i] = rte_raw_cksum(base + off_i, len_i)   
 
 template <int G, int U>
@@ -265,205 +276,7 @@ __global__ __launch_bounds__(kBlock) void tcp4_cksum_kernel(tasx_tcp4_params p)
 }
 
 // ---------------------------------------------------------------------------
-// Flat-stream kernels (default).  A group of G lanes owns `ppg` consecutive
-// packets.  Phase 1: lane j reads packet j's descriptor (and, for TCP4, its
-// 20-byte IPv4 header, total_length and checksum-field bytes) -- one load
-// latency for the whole group instead of one per packet -- and the group
-// scans the packets' chunk counts into an LDS table.  Phase 2: the group walks
-// the concatenation of its packets' aligned chunks as ONE flat stream, lane gl
-// taking flat chunks gl, gl+G, ... (each wave instruction loads up to 1 KiB of
-// consecutive chunks, U instructions in flight per lane), so short and long
-// packets keep every lane busy.  A lane's chunks of one packet are
-// consecutive, so it keeps one running sum and parks it in LDS
-// part[packet][lane] when it moves on.  Phase 3: lane j adds row j of `part`
-// and finishes packet j: fold, odd-start swap, TCP4 result rules, one store.
-
-struct FlatEnt {
-  uint64_t cb;   // address of the packet's first aligned 16-byte chunk
-  uint32_t pre;  // exclusive prefix of chunk counts within the group
-  uint32_t info; // head offset (bits 0..3) | (tail bytes - 1) (bits 4..7)
-};
-
-template <int G, int P, int U, bool TCP4, typename Prm>
-__global__ __launch_bounds__(kBlock) void flat_cksum_kernel(Prm p, uint32_t ppg)
-{
-  static_assert(P <= G && (G & (G - 1)) == 0 && G <= 64, "group shape");
-  constexpr int NG = kBlock / G;
-  constexpr int ROW = G + 4; // +16 B per row: conflict-free ds_read_b128 in phase 3
-  __shared__ FlatEnt ent[NG][P + 1];
-  __shared__ __attribute__((aligned(16))) uint32_t part[NG][P][ROW];
-
-  const int lg = threadIdx.x / G;
-  const int gl = threadIdx.x % G;
-  const uint64_t first = ((uint64_t) blockIdx.x * NG + lg) * ppg;
-  const uint32_t cnt = first < p.n ? (uint32_t) min((uint64_t) ppg, (uint64_t) p.n - first) : 0u;
-  const bool own = (uint32_t) gl < cnt;
-  const uint32_t i = (uint32_t) (first + (uint32_t) gl);
-
-  // ---- phase 1: the lane's own packet
-  const uint8_t *s = nullptr;
-  uint32_t len = 0, tl = 0, c_ip = 0, c_ph = 0, fix = 0;
-  uint8_t *ipp = nullptr, *l4p = nullptr;
-  if (own) {
-    if constexpr (TCP4) {
-      uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-      ipp = f + p.ip_off;
-      l4p = f + p.l4_off;
-      uint32_t w[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k)
-        w[k] = ld8(ipp + 2 * k) | (ld8(ipp + 2 * k + 1) << 8);
-      tl = bswap16(w[1]);
-      len = tl >= 20 ? tl - 20 : 0;
-#pragma unroll
-      for (int k = 0; k < 10; ++k)
-        c_ip += (k == 5) ? 0u : w[k];             // ip.chksum taken as 0
-      c_ph = w[6] + w[7] + w[8] + w[9] + (w[4] & 0xff00u); // src, dst, proto<<8
-      if (len > 16) {                             // tcp.chksum taken as 0
-        uint32_t fw = ld8(l4p + 16);
-        if (len > 17)
-          fw |= ld8(l4p + 17) << 8;
-        fix = (~fw) & 0xffffu;
-      }
-      s = l4p;
-    } else {
-      s = p.base + pkt_offset(p.off, p.stride, i);
-      len = p.len ? ldg(p.len, i) : p.len0;
-    }
-  }
-  uint32_t nch = 0, info = 0;
-  uint64_t cb = 0;
-  if (len) {
-    const uintptr_t a0 = (uintptr_t) s, a1 = a0 + len;
-    cb = a0 & ~(uintptr_t) 15;
-    nch = (uint32_t) ((((a1 + 15) & ~(uintptr_t) 15) - cb) >> 4);
-    info = (uint32_t) (a0 & 15) | ((uint32_t) (a1 - ((a1 - 1) & ~(uintptr_t) 15) - 1) << 4);
-  }
-  uint32_t inc = nch;
-#pragma unroll
-  for (int d = 1; d < G; d <<= 1) {
-    const uint32_t t = __shfl_up(inc, d, G);
-    if (gl >= d)
-      inc += t;
-  }
-  const uint32_t T = __shfl(inc, G - 1, G);
-  if (own)
-    ent[lg][gl] = FlatEnt{cb, inc - nch, info};
-  if (gl == 0)
-    ent[lg][cnt].pre = T; // sentinel
-  for (uint32_t k = 0; k < cnt; ++k)
-    part[lg][k][gl] = 0;
-  __syncthreads();
-
-  // ---- phase 2: flat stream over the group's chunks
-  if (cnt) {
-    uint64_t acc = 0;
-    int kacc = -1, k = 0;
-    FlatEnt e = ent[lg][0];
-    uint32_t knext = ent[lg][1].pre;
-    for (uint32_t f0 = (uint32_t) gl; f0 < T; f0 += (uint32_t) (G * U)) {
-      u32x4 v[U];
-      int ku[U], lo[U], hi[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t f = f0 + (uint32_t) (u * G);
-        ku[u] = -1;
-        lo[u] = 0;
-        hi[u] = 16;
-        v[u] = u32x4{0, 0, 0, 0};
-        if (f < T) {
-          while (f >= knext) {
-            ++k;
-            e = ent[lg][k];
-            knext = ent[lg][k + 1].pre;
-          }
-          const uint32_t c = f - e.pre;
-          ku[u] = k;
-          if (c == 0)
-            lo[u] = (int) (e.info & 15u);
-          if (f + 1 == knext)
-            hi[u] = (int) (e.info >> 4) + 1;
-          v[u] = ld16((const u32x4 *) e.cb, c);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (ku[u] >= 0) {
-          if (ku[u] != kacc) {
-            if (kacc >= 0)
-              part[lg][kacc][gl] = fold64_to_18(acc);
-            acc = 0;
-            kacc = ku[u];
-          }
-          if (lo[u] != 0 || hi[u] != 16)
-            v[u] = mask_chunk(v[u], lo[u], hi[u]);
-          acc = add_chunk(acc, v[u]);
-        }
-      }
-    }
-    if (kacc >= 0)
-      part[lg][kacc][gl] = fold64_to_18(acc);
-  }
-  __syncthreads();
-
-  // ---- phase 3: lane j finishes packet j
-  if (own) {
-    uint32_t sum = 0;
-    const u32x4 *row = (const u32x4 *) &part[lg][gl][0];
-#pragma unroll
-    for (int l = 0; l < G / 4; ++l) {
-      const u32x4 q = row[l];
-      sum += q.x + q.y + q.z + q.w;
-    }
-    uint32_t r = fold32_to_16(sum); // sum < G * 2^18 <= 2^24
-    if (info & 1u)
-      r = bswap16(r);
-    if constexpr (TCP4) {
-      const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
-      uint32_t tcpc = 0;
-      if (tl >= 20)
-        tcpc = inv_result(residue(fold32_to_16(r + fix + c_ph + bswap16(len))));
-      if (p.out)
-        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-      if (p.flags & TASX_F_INPLACE) {
-        st8(ipp + 10, ipc);
-        st8(ipp + 11, ipc >> 8);
-        st8(l4p + 16, tcpc);
-        st8(l4p + 17, tcpc >> 8);
-      }
-    } else {
-      stg(p.out, i, (uint16_t) r);
-    }
-  }
-}
-
-template <int G, int P, int U, bool TCP4, typename Prm>
-int launch_flat(const Prm &p, uint32_t ppg, hipStream_t s)
-{
-  constexpr int NG = kBlock / G;
-  if (ppg == 0 || ppg > (uint32_t) P)
-    ppg = P;
-  const uint64_t groups = ((uint64_t) p.n + ppg - 1) / ppg;
-  const uint64_t blocks = (groups + NG - 1) / NG;
-  if (blocks == 0)
-    return 0;
-  if (blocks > 0x7fffffffull)
-    return -2;
-  hipLaunchKernelGGL((flat_cksum_kernel<G, P, U, TCP4, Prm>), dim3((uint32_t) blocks), dim3(kBlock), 0, s, p, ppg);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// ---------------------------------------------------------------------------
-// pkt16 kernels: 16-lane packet groups (one DPP row each), persistent grid.
-//   * loads: U clamped global_load_dwordx4 per lane, issued back to back with
-//     no branches (lanes past the packet re-read its last chunk -- same line,
-//     no extra HBM traffic -- and drop it with a select);
-//   * head / tail bytes: exact subtraction of the excluded bytes on the two
-//     lanes that hold the boundary chunks (lane sums are exact before folding);
-//   * reduction: 4 DPP row_shr adds per channel, total lands in lane 15;
-//   * TCP4: the next frame's header (total_length + header words) is
-//     prefetched while this frame's chunks are in flight, so the header ->
-//     length -> data dependency costs one load latency per group, not per frame.
+// 16-lane packet groups (one DPP row each), one block per 16 packets.
 
 __device__ __forceinline__ uint32_t row_sum16(uint32_t v)
 {
@@ -541,12 +354,13 @@ __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
   return fold64_to_18(acc);
 }
 
-template <int U, int BS = kBlock>
-__global__ __launch_bounds__(BS) void pkt16_raw_kernel(tasx_raw_params p)
+// RAW, any layout: out[i] = rte_raw_cksum(base + off_i, len_i)
+template <int U>
+__global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
 {
   const int gl = threadIdx.x & 15;
-  const uint32_t ngroups = gridDim.x * (BS / 16);
-  uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  const uint32_t ngroups = gridDim.x * (kBlock / 16);
+  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   // descriptor prefetch (every lane of the group reads the same word)
   uint64_t off = 0;
   uint32_t len = p.len0;
@@ -574,90 +388,14 @@ __global__ __launch_bounds__(BS) void pkt16_raw_kernel(tasx_raw_params p)
     }
   }
 }
-
+// TCP4, any frame layout: header words and the checksum-field bytes by byte
+// loads, then the segment chunks.  With a frame-length hint (the mbuf
+// data_len tx_send() sets before tx_flush) the chunk loads are issued together
+// with the header loads; the hint drives only the prefetch: results always
+// follow ip.total_length (chunks past it are dropped, chunks the hint missed
+// are loaded after the header arrives).
 template <int U>
-__global__ __launch_bounds__(kBlock) void pkt16_tcp4_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t ngroups = gridDim.x * (kBlock / 16);
-  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  // header prefetch: every lane reads total_length; lanes 0..9 the header word gl
-  uint32_t tlb0 = 0, tlb1 = 0, wb0 = 0, wb1 = 0;
-  uint8_t *f = nullptr;
-  if (i < p.n) {
-    f = p.base + pkt_offset(p.off, p.stride, i);
-    const uint8_t *ip = f + p.ip_off;
-    tlb0 = ld8(ip + 2);
-    tlb1 = ld8(ip + 3);
-    if (gl < 10) {
-      wb0 = ld8(ip + 2 * gl);
-      wb1 = ld8(ip + 2 * gl + 1);
-    }
-  }
-  for (; i < p.n; i += ngroups) {
-    uint8_t *ip = f + p.ip_off;
-    uint8_t *l4 = f + p.l4_off;
-    const uint32_t tl = (tlb0 << 8) | tlb1;
-    const uint32_t len = tl >= 20 ? tl - 20 : 0;
-    const uint32_t w = wb0 | (wb1 << 8);
-    const Chunks<U> r = chunk_range<U>(l4, len);
-    // checksum-field bytes of the segment (lane 10), taken as zero
-    uint32_t fb0 = 0, fb1 = 0;
-    if (gl == 10 && len > 16) {
-      fb0 = ld8(l4 + 16);
-      if (len > 17)
-        fb1 = ld8(l4 + 17);
-    }
-    uint32_t part = group_lane_sum<U>(r, gl);
-    // prefetch the next frame's header
-    const uint32_t inext = i + ngroups;
-    uint8_t *fn = f;
-    if (inext < p.n) {
-      fn = p.base + pkt_offset(p.off, p.stride, inext);
-      const uint8_t *ipn = fn + p.ip_off;
-      tlb0 = ld8(ipn + 2);
-      tlb1 = ld8(ipn + 3);
-      if (gl < 10) {
-        wb0 = ld8(ipn + 2 * gl);
-        wb1 = ld8(ipn + 2 * gl + 1);
-      }
-    }
-    uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0u;
-    uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
-    if (gl == 10 && len > 16)
-      c_ph += (~(fb0 | (fb1 << 8))) & 0xffffu; // -field mod 0xffff
-    part = row_sum16(part);
-    c_ip = row_sum16(c_ip);
-    c_ph = row_sum16(c_ph);
-    if (gl == 15) {
-      const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
-      uint32_t tcpc = 0;
-      if (tl >= 20) {
-        uint32_t r4 = fold32_to_16(part);
-        if (r.head & 1)
-          r4 = bswap16(r4);
-        tcpc = inv_result(residue(fold32_to_16(r4 + c_ph + bswap16(len))));
-      }
-      if (p.out)
-        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-      if (p.flags & TASX_F_INPLACE) {
-        st8(ip + 10, ipc);
-        st8(ip + 11, ipc >> 8);
-        st8(l4 + 16, tcpc);
-        st8(l4 + 17, tcpc >> 8);
-      }
-    }
-    f = fn;
-  }
-}
-
-// TCP4 with frame-length hints: the frame length (mbuf data_len, set by
-// tx_send before tx_flush) predicts the L4 range, so the data loads are issued
-// together with the header loads instead of after them.  The hint drives only
-// the prefetch: results always follow ip.total_length (chunks past it are
-// dropped, chunks the hint missed are loaded after the header arrives).
-template <int U, int DIAG = 0>
-__global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_params p)
+__global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
@@ -676,14 +414,10 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_param
     for (int u = 0; u < U; ++u)
       v[u] = ld16nt(sr.c0p, min((uint32_t) gl + 16u * u, sr.nch - 1));
   }
-  uint32_t tl, w = 0;
-  if constexpr (DIAG == 1) { // timing diagnostic only: no header loads (wrong results)
-    tl = hint - p.ip_off;
-  } else {
-    tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
-    if (gl < 10)
-      w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
-  }
+  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  uint32_t w = 0;
+  if (gl < 10)
+    w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const Chunks<U> r = chunk_range<U>(l4, len);
   uint32_t fb0 = 0, fb1 = 0;
@@ -754,18 +488,6 @@ __global__ __launch_bounds__(kBlock) void pkt16_tcp4_spec_kernel(tasx_tcp4_param
   }
 }
 
-// TCP4, TAS layout (l4_off == ip_off + 20): one chunk range [ip, ip + 20 +
-// L4 length) carries the IPv4 header, the pseudo-header fields and the
-// segment, so no byte loads are issued at all.  The lanes holding the chunks
-// that touch header bytes (ip-relative offsets < 38) split them into three
-// channels with byte masks:
-//   IP  = header bytes [0,10) + [12,20)            (ip.chksum taken as 0)
-//   PH  = proto (offset 9) + src/dst [12,20)       (pseudo-header fields)
-//   L4  = [20, 20+len) minus the tcp.chksum bytes [36,38)
-// total_length comes from the chunk holding offsets 2..3 (lane shuffle).
-// Without a frame-length hint the header chunks are loaded first and the
-// rest after total_length is known; with a hint everything is issued at once.
-
 // mask of the bytes of a dword (first byte at ip-relative offset `base`) that
 // fall in [lo, hi)
 __device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
@@ -794,292 +516,19 @@ __device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
   }
 }
 
-template <int U, int DIAG = 0, int BS = kBlock>
-__global__ __launch_bounds__(BS) void pkt16_tcp4_tas_kernel(tasx_tcp4_params p)
-{
-  if constexpr (DIAG == 1)
-    diag_stamp<BS>(p, 0);
-  const int gl = threadIdx.x & 15;
-  const int gbase = (threadIdx.x & 63) & ~15;
-  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return; // whole 16-lane group (one DPP row) leaves together
-  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  uint8_t *ip = f + p.ip_off;
-  const uintptr_t A0 = (uintptr_t) ip & ~(uintptr_t) 15;
-  const u32x4 *c0p = (const u32x4 *) A0;
-  const int hb = (int) ((uintptr_t) ip & 15);
-  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
-  // chunks covering [ip, f + hint): the speculative range (at least the header)
-  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
-  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
-  // round 1: U loads back to back, no branches (lanes past the range re-read
-  // its last chunk: same line, no extra HBM traffic)
-  u32x4 v[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, nld - 1));
-  // total_length: ip-relative bytes 2 and 3
-  uint32_t tl;
-  if constexpr (DIAG >= 2) { // timing diagnostic: length from the hint (wrong results)
-    tl = hint - p.ip_off;
-  } else {
-    const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
-    const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
-    const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
-    tl = (ba << 8) | bb;
-  }
-  if constexpr (DIAG == 1)
-    diag_stamp<BS>(p, 1);
-  const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  const int E = 20 + (int) len;                              // ip-relative end
-  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;        // chunks of [ip, ip+E)
-  const uint32_t need = min(nch, 16u * U);
-  // round 2 (no / short hint): wave-uniform branch, straight-line loads inside
-  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
-    const uint32_t top = max(need, nld);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, top - 1));
-  }
-  const int NS = (hb + 38 + 15) >> 4; // chunks holding ip-relative offsets < 38
-  uint64_t acc = 0, acc_ip = 0, acc_ph = 0;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t c = (uint32_t) gl + 16u * u;
-    if (DIAG < 3 && u == 0 && gl < NS) {
-      // header chunk: split by byte masks (ip-relative base of dword j)
-      const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int base = 16 * gl + 4 * j - hb;
-        const uint32_t m_ip = in_range(base, 0, 10) | in_range(base, 12, 20);
-        const uint32_t m_ph = in_range(base, 9, 10) | in_range(base, 12, 20);
-        const uint32_t m_l4 = in_range(base, 20, min(36, E)) | in_range(base, 38, E);
-        acc_ip += w[j] & m_ip;
-        acc_ph += w[j] & m_ph;
-        acc += w[j] & m_l4;
-      }
-    } else if (c < nch) {
-      acc += (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w;
-    }
-  }
-  // tail chunk beyond the header chunks: drop bytes past ip + E
-  const uint32_t last = nch - 1;
-  const int tail = (int) (((uintptr_t) ip + E) - (((uintptr_t) ip + E - 1) & ~(uintptr_t) 15));
-  if (last >= (uint32_t) NS && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
-    const uint32_t ut = last >> 4;
-    u32x4 t = v[0];
-#pragma unroll
-    for (int u = 1; u < U; ++u)
-      if (ut == (uint32_t) u)
-        t = v[u];
-    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
-  }
-  uint32_t part = fold64_to_18(acc);
-  if (nch > 16u * U) { // long segments: the rest in the plain loop (all L4 bytes)
-    Chunks<U> rest;
-    rest.c0p = c0p + 16u * U;
-    rest.nch = nch - 16u * U;
-    rest.head = 0;
-    rest.tail = tail;
-    part += group_lane_sum<U>(rest, gl);
-  }
-  uint32_t c_ip = fold64_to_18(acc_ip);
-  uint32_t c_ph = fold64_to_18(acc_ph);
-  if constexpr (DIAG == 1)
-    diag_stamp<BS>(p, 2);
-  part = row_sum16(part);
-  c_ip = row_sum16(c_ip);
-  c_ph = row_sum16(c_ph);
-  if (gl == 15) {
-    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
-    if (hb & 1) { // address-aligned words -> header / segment relative words
-      ri = bswap16(ri);
-      rp = bswap16(rp);
-      r4 = bswap16(r4);
-    }
-    const uint32_t ipc = inv_result(residue(ri));
-    uint32_t tcpc = 0;
-    if (tl >= 20)
-      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
-    if (p.out)
-      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-    if (p.flags & TASX_F_INPLACE) {
-      uint8_t *l4 = ip + 20;
-      st8(ip + 10, ipc);
-      st8(ip + 11, ipc >> 8);
-      st8(l4 + 16, tcpc);
-      st8(l4 + 17, tcpc >> 8);
-    }
-  }
-  if constexpr (DIAG == 1)
-    diag_stamp<BS>(p, 3);
-}
-
-// Header-channel byte masks for the TAS-layout kernel, precomputed at compile
-// time: [ip & 15][chunk 0..3][channel IP, PH, L4][dword].  Channels over
-// ip-relative byte offsets: IP = [0,10)+[12,20), PH = {9}+[12,20),
-// L4 = [20,36)+[38,inf) (the segment minus tcp.chksum; its end is applied by the
-// tail fix-up).  One 48-byte table row per lane replaces ~300 VALU of mask math.
-struct HdrMasks {
-  uint32_t m[16][4][3][4];
-};
-
-constexpr uint32_t cx_in_range(int base, int lo, int hi)
-{
-  int bl = lo - base < 0 ? 0 : (lo - base > 4 ? 4 : lo - base);
-  int bh = hi - base < 0 ? 0 : (hi - base > 4 ? 4 : hi - base);
-  uint32_t m = 0;
-  for (int b = bl; b < bh; ++b)
-    m |= 0xffu << (8 * b);
-  return m;
-}
-
-constexpr HdrMasks make_hdr_masks()
-{
-  HdrMasks t{};
-  for (int hb = 0; hb < 16; ++hb)
-    for (int c = 0; c < 4; ++c)
-      for (int j = 0; j < 4; ++j) {
-        const int base = 16 * c + 4 * j - hb;
-        t.m[hb][c][0][j] = cx_in_range(base, 0, 10) | cx_in_range(base, 12, 20);
-        t.m[hb][c][1][j] = cx_in_range(base, 9, 10) | cx_in_range(base, 12, 20);
-        t.m[hb][c][2][j] = cx_in_range(base, 20, 36) | cx_in_range(base, 38, 1 << 20);
-      }
-  return t;
-}
-
-__constant__ HdrMasks kHdrMasks = make_hdr_masks();
-
-__device__ __forceinline__ uint64_t masked_sum(u32x4 v, u32x4 m)
-{
-  return (uint64_t) (v.x & m.x) + (v.y & m.y) + (uint64_t) (v.z & m.z) + (v.w & m.w);
-}
-
-// bytes [t, 16) of a chunk as a dword mask vector
-__device__ __forceinline__ u32x4 suffix_mask(int t)
-{
-  u32x4 m;
-  m.x = in_range(0, t, 16);
-  m.y = in_range(4, t, 16);
-  m.z = in_range(8, t, 16);
-  m.w = in_range(12, t, 16);
-  return m;
-}
-
-template <int U, int BS = kBlock>
-__global__ __launch_bounds__(BS) void pkt16_tcp4_tasm_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const int gbase = (threadIdx.x & 63) & ~15;
-  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return; // whole 16-lane group (one DPP row) leaves together
-  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  uint8_t *ip = f + p.ip_off;
-  const uintptr_t A0 = (uintptr_t) ip & ~(uintptr_t) 15;
-  const u32x4 *c0p = (const u32x4 *) A0;
-  const int hb = (int) ((uintptr_t) ip & 15);
-  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
-  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
-  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
-  u32x4 v[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, nld - 1));
-  // this lane's header-channel masks (lanes 0..3 only; L1/L2-resident table)
-  u32x4 mip = u32x4{0, 0, 0, 0}, mph = mip, ml4 = mip;
-  if (gl < 4) {
-    const u32x4 *mt = (const u32x4 *) &kHdrMasks.m[hb][gl][0][0];
-    mip = mt[0];
-    mph = mt[1];
-    ml4 = mt[2];
-  }
-  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
-  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
-  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
-  const uint32_t tl = (ba << 8) | bb;
-  const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  const int E = 20 + (int) len;
-  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
-  const uint32_t need = min(nch, 16u * U);
-  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
-    const uint32_t top = max(need, nld);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(c0p, min((uint32_t) gl + 16u * u, top - 1));
-  }
-  const uint32_t last = nch - 1;
-  const int tail = (int) (((uintptr_t) ip + E) - (((uintptr_t) ip + E - 1) & ~(uintptr_t) 15));
-  uint64_t acc = 0;
-  uint64_t acc_ip = masked_sum(v[0], mip), acc_ph = masked_sum(v[0], mph);
-  // chunk gl (u == 0): the header lanes add their L4 bytes through the mask
-  if (gl < 4) {
-    if ((uint32_t) gl <= last) {
-      acc += masked_sum(v[0], ml4);
-      if ((uint32_t) gl == last && tail < 16) // short segment ends in a header chunk
-        acc -= masked_sum(v[0], ml4 & suffix_mask(tail));
-    }
-  } else if ((uint32_t) gl < nch) {
-    acc += (uint64_t) v[0].x + v[0].y + v[0].z + v[0].w;
-  }
-#pragma unroll
-  for (int u = 1; u < U; ++u) {
-    const uint32_t c = (uint32_t) gl + 16u * u;
-    acc += c < nch ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
-  }
-  if (last >= 4u && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
-    const uint32_t ut = last >> 4;
-    u32x4 t = v[0];
-#pragma unroll
-    for (int u = 1; u < U; ++u)
-      if (ut == (uint32_t) u)
-        t = v[u];
-    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
-  }
-  uint32_t part = fold64_to_18(acc);
-  if (nch > 16u * U) {
-    Chunks<U> rest;
-    rest.c0p = c0p + 16u * U;
-    rest.nch = nch - 16u * U;
-    rest.head = 0;
-    rest.tail = tail;
-    part += group_lane_sum<U>(rest, gl);
-  }
-  uint32_t c_ip = fold64_to_18(acc_ip);
-  uint32_t c_ph = fold64_to_18(acc_ph);
-  part = row_sum16(part);
-  c_ip = row_sum16(c_ip);
-  c_ph = row_sum16(c_ph);
-  if (gl == 15) {
-    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
-    if (hb & 1) {
-      ri = bswap16(ri);
-      rp = bswap16(rp);
-      r4 = bswap16(r4);
-    }
-    const uint32_t ipc = inv_result(residue(ri));
-    uint32_t tcpc = 0;
-    if (tl >= 20)
-      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
-    if (p.out)
-      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-    if (p.flags & TASX_F_INPLACE) {
-      uint8_t *l4 = ip + 20;
-      st8(ip + 10, ipc);
-      st8(ip + 11, ipc >> 8);
-      st8(l4 + 16, tcpc);
-      st8(l4 + 17, tcpc >> 8);
-    }
-  }
-}
-
-// Lean TAS-layout TCP4 kernel: 32-bit byte offsets from the (16-byte aligned)
-// batch base, so every load is global_load_dwordx4 v, v_off, s[base] (one VGPR
-// per address), and the header-channel byte masks come from three 64-bit
-// constants (bit x+16 = ip-relative byte x is in the channel) expanded with
-// one multiply -- no tables, no 64-bit shifts per byte range.
+// TCP4, TAS frame layout (tcp = ip + 20), stride mode: one chunk range
+// [ip, ip + 20 + L4 length) carries the IPv4 header, the pseudo-header fields
+// and the segment, so no byte loads are issued at all.  The (up to 4) lanes
+// holding chunks with header bytes split them into three channels:
+//   IP = header bytes [0,10) + [12,20)            (ip.chksum taken as 0)
+//   PH = proto (offset 9) + src/dst [12,20)       (pseudo-header fields)
+//   L4 = [20, 20+len) minus the tcp.chksum bytes [36,38)
+// with byte masks from three 64-bit constants (bit x+16 = ip-relative byte x
+// is in the channel) expanded by one multiply.  total_length comes from the
+// chunk holding offsets 2..3 by a lane shuffle.  32-bit byte offsets from the
+// 16-byte aligned batch base make every load global_load_dwordx4 v, v_off,
+// s[base] (one VGPR per address).  With a frame-length hint all chunk loads
+// are issued at once; without one, after total_length is known.
 constexpr uint64_t kPatIP = (((1ull << 10) - 1) << 16) | (((1ull << 8) - 1) << 28);  // [0,10)+[12,20)
 constexpr uint64_t kPatPH = (1ull << 25) | (((1ull << 8) - 1) << 28);                // {9}+[12,20)
 constexpr uint64_t kPatNL4 = ((1ull << 36) - 1) | (3ull << 52);                     // [-16,20)+{36,37}
@@ -1099,12 +548,14 @@ __device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
   return __builtin_nontemporal_load((gcu4 *) (base + off));
 }
 
-template <int U, int BS = kBlock>
-__global__ __launch_bounds__(BS) void pkt16_tcp4_lean_kernel(tasx_tcp4_params p)
+template <int U, int DIAG = 0>
+__global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 {
+  if constexpr (DIAG)
+    diag_stamp<kBlock>(p, 0);
   const int gl = threadIdx.x & 15;
   const int gbase = (threadIdx.x & 63) & ~15;
-  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
   const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
@@ -1125,16 +576,16 @@ __global__ __launch_bounds__(BS) void pkt16_tcp4_lean_kernel(tasx_tcp4_params p)
   const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
   const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
   const uint32_t tl = (ba << 8) | bb;
+  if constexpr (DIAG)
+    diag_stamp<kBlock>(p, 1);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const int E = 20 + (int) len;
   const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
   const uint32_t need = min(nch, 16u * U);
   if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
     const uint32_t top = max(need, nld);
-    if ((uint32_t) gl >= nld) // lanes below nld already hold chunk gl
-      v[0] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl, top - 1));
 #pragma unroll
-    for (int u = 1; u < U; ++u)
+    for (int u = 0; u < U; ++u)
       v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + 16u * u, top - 1));
   }
   const uint32_t last = nch - 1;
@@ -1181,6 +632,8 @@ __global__ __launch_bounds__(BS) void pkt16_tcp4_lean_kernel(tasx_tcp4_params p)
   }
   uint32_t c_ip = fold64_to_18(acc_ip);
   uint32_t c_ph = fold64_to_18(acc_ph);
+  if constexpr (DIAG)
+    diag_stamp<kBlock>(p, 2);
   part = row_sum16(part);
   c_ip = row_sum16(c_ip);
   c_ph = row_sum16(c_ph);
@@ -1205,28 +658,23 @@ __global__ __launch_bounds__(BS) void pkt16_tcp4_lean_kernel(tasx_tcp4_params p)
       st8(ip + 37, tcpc >> 8);
     }
   }
+  if constexpr (DIAG)
+    diag_stamp<kBlock>(p, 3);
 }
 
-template <int BS = kBlock, typename K, typename Prm>
-int launch_persistent(K kern, const Prm &p, uint32_t blocks_per_cu, hipStream_t s, uint32_t lds_bytes = 0)
+template <typename K, typename Prm>
+int launch_groups(K kern, const Prm &p, hipStream_t s)
 {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
-  constexpr uint64_t fpb = BS / 16; // 16-lane groups (frames) per block
-  uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
-  const uint64_t cap = (uint64_t) ncu * blocks_per_cu;
-  if (blocks_per_cu && blocks > cap)
-    blocks = cap;
+  // one 16-lane group per packet, 16 groups per 256-thread block: the grid
+  // covers the batch once (measured faster than persistent grids at these
+  // batch sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
+  constexpr uint64_t fpb = kBlock / 16;
+  const uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
   if (blocks == 0)
     return 0;
-  // lds_bytes: dynamic LDS reserved only to cap blocks per CU (occupancy
-  // experiments); the kernels use none
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds_bytes, s, p);
+  if (blocks > 0x7fffffffull)
+    return -2;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1247,89 +695,47 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-// lean kernel preconditions: 16-byte aligned base, stride mode, every frame's
-// bytes within 4 GiB of the base
-static bool lean_ok(const tasx_tcp4_params &p)
+// tcp4_tas_kernel preconditions: TAS layout, 16-byte aligned base, stride mode,
+// every frame within 4 GiB of the base (32-bit offsets)
+static bool tas_kernel_ok(const tasx_tcp4_params &p)
 {
-  return ((uintptr_t) p.base & 15u) == 0 && p.off == nullptr &&
+  return p.l4_off == p.ip_off + 20 && ((uintptr_t) p.base & 15u) == 0 && p.off == nullptr &&
          (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
 }
 
-// variant: 0 = auto (RAW 11; TCP4 25 (lean, falls back to 12) for TAS layout + hints, else 12), 1/7 = v1 group-per-packet, 2..6 = flat-stream shapes,
-// 8..11 = pkt16 persistent (ppg = blocks per CU for 8..10; 11 = one block per 16 packets)
-// ppg: packets per group for the flat kernels / blocks per CU for pkt16 (0 = auto)
-static uint32_t auto_ppg(uint32_t n, uint32_t P, uint32_t groups_per_block)
-{
-  // aim for ~8 blocks per CU of work in total (256 CUs)
-  const uint64_t want_groups = 256ull * 8 * groups_per_block;
-  uint64_t ppg = (n + want_groups - 1) / want_groups;
-  if (ppg < 1)
-    ppg = 1;
-  if (ppg > P)
-    ppg = P;
-  return (uint32_t) ppg;
-}
-
-extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, uint32_t ppg, void *stream)
+extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  const int maxb = 256 * 64;
   switch (variant) {
   case 0:
-  case 11: return launch_persistent(pkt16_raw_kernel<6>, *p, 0, s, ppg * 1024u);
-  case 18: return launch_persistent<64>(pkt16_raw_kernel<6, 64>, *p, 0, s);
-  case 19: return launch_persistent<128>(pkt16_raw_kernel<6, 128>, *p, 0, s);
-  case 20: return launch_persistent<512>(pkt16_raw_kernel<6, 512>, *p, 0, s);
-  case 8: return launch_persistent(pkt16_raw_kernel<6>, *p, ppg ? ppg : 8, s);
-  case 9: return launch_persistent(pkt16_raw_kernel<8>, *p, ppg ? ppg : 8, s);
-  case 10: return launch_persistent(pkt16_raw_kernel<4>, *p, ppg ? ppg : 8, s);
-  case 2: return launch_flat<64, 16, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
-  case 1: return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
-  case 3: return launch_flat<64, 16, 4, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
-  case 4: return launch_flat<16, 8, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
-  case 5: return launch_flat<16, 8, 4, false>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
-  case 6: return launch_flat<32, 16, 8, false>(*p, ppg ? ppg : auto_ppg(p->n, 16, 8), s);
-  case 7: return launch(raw_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
-  default: return -2;
+  case 2:
+  case 3:
+    return launch_groups(raw_group_kernel<6>, *p, s);
+  case 1:
+    return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+  default:
+    return -2;
   }
 }
 
-extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, uint32_t ppg, void *stream)
+extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  const int maxb = 256 * 64;
-  if (variant == 0) // TAS layout with hints -> header from the chunks; else byte loads
-    variant = (p->l4_off == p->ip_off + 20 && (p->flen || p->flen0)) ? 25 : 12;
-  if (((variant >= 15 && variant <= 22) || variant == 23 || variant == 24 || variant == 25) &&
-      p->l4_off != p->ip_off + 20)
-    variant = 12;
+  const bool tas_ok = tas_kernel_ok(*p);
+  if (variant == 0) // TAS layout + frame-length hints -> tcp4_tas_kernel
+    variant = (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
+  if ((variant == 3 || variant == 4) && !tas_ok)
+    variant = 2;
   switch (variant) {
-  case 8: return launch_persistent(pkt16_tcp4_kernel<6>, *p, ppg ? ppg : 8, s);
-  case 9: return launch_persistent(pkt16_tcp4_kernel<8>, *p, ppg ? ppg : 8, s);
-  case 10: return launch_persistent(pkt16_tcp4_kernel<4>, *p, ppg ? ppg : 12, s);
-  case 11: return launch_persistent(pkt16_tcp4_kernel<6>, *p, 0, s);
-  case 12: return launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s, ppg * 1024u);
-  case 13: return launch_persistent(pkt16_tcp4_spec_kernel<8>, *p, 0, s);
-  case 14: return launch_persistent(pkt16_tcp4_spec_kernel<6, 1>, *p, 0, s); // timing diagnostic
-  case 15: return launch_persistent(pkt16_tcp4_tas_kernel<6>, *p, 0, s, ppg * 1024u);
-  case 16: return launch_persistent(pkt16_tcp4_tas_kernel<8>, *p, 0, s, ppg * 1024u);
-  case 17: return p->diag ? launch_persistent(pkt16_tcp4_tas_kernel<6, 1>, *p, 0, s) : -2;
-  case 18: return launch_persistent<64>(pkt16_tcp4_tas_kernel<8, 0, 64>, *p, 0, s);
-  case 19: return launch_persistent<128>(pkt16_tcp4_tas_kernel<8, 0, 128>, *p, 0, s);
-  case 20: return launch_persistent<512>(pkt16_tcp4_tas_kernel<8, 0, 512>, *p, 0, s);
-  case 21: return launch_persistent(pkt16_tcp4_tas_kernel<6, 2>, *p, 0, s); // diag: no shuffles
-  case 22: return launch_persistent(pkt16_tcp4_tas_kernel<6, 3>, *p, 0, s); // diag: + no header split
-  case 23: return launch_persistent(pkt16_tcp4_tasm_kernel<6>, *p, 0, s);
-  case 24: return launch_persistent(pkt16_tcp4_tasm_kernel<8>, *p, 0, s);
-  case 25: return lean_ok(*p) ? launch_persistent(pkt16_tcp4_lean_kernel<6>, *p, 0, s)
-                              : launch_persistent(pkt16_tcp4_spec_kernel<6>, *p, 0, s);
-  case 2: return launch_flat<64, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
-  case 1: return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, maxb, s);
-  case 3: return launch_flat<64, 16, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 4), s);
-  case 4: return launch_flat<16, 8, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
-  case 5: return launch_flat<16, 8, 4, true>(*p, ppg ? ppg : auto_ppg(p->n, 8, 16), s);
-  case 6: return launch_flat<32, 16, 8, true>(*p, ppg ? ppg : auto_ppg(p->n, 16, 8), s);
-  case 7: return launch(tcp4_cksum_kernel<64, 4>, *p, kBlock / 64, maxb, s);
-  default: return -2;
+  case 1:
+    return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+  case 2:
+    return launch_groups(tcp4_frame_kernel<6>, *p, s);
+  case 3:
+    return launch_groups(tcp4_tas_kernel<6>, *p, s);
+  case 4:
+    return p->diag ? launch_groups(tcp4_tas_kernel<6, 1>, *p, s) : -2;
+  default:
+    return -2;
   }
 }

@@ -54,11 +54,14 @@ SIGNATURES = {
     "tasx_defer_tcp4": (_c_int, [_uns, _vp, _c_u16, _c_u16]),
     "tasx_pending": (_c_int, [_uns]),
     "tasx_flush": (_c_int, [_uns]),
-    "tasx_set_kernel_config": (_c_int, [_c_int, _uns]),
+    "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
+    "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
+    "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_set_diag_buffer": (_c_int, [_vp]),
     "tasx_host_alloc": (_vp, [_sz]),
     "tasx_host_free": (_c_int, [_vp]),
     "tasx_host_register": (_c_int, [_vp, _sz]),
+    "tasx_host_device_pointer": (_vp, [_vp]),
     "tasx_host_unregister": (_c_int, [_vp]),
     "tasx_dev_alloc": (_vp, [_c_int, _sz]),
     "tasx_dev_free": (_c_int, [_vp]),
@@ -207,6 +210,17 @@ def tx_flush(ctx_id: int) -> None:
     _check(lib().tasx_flush(ctx_id), "tasx_flush")
 
 
+def register_frames(ctx_id: int, base_addr: int, nbytes: int) -> None:
+    """Zero-copy region for the context's frames (tasx_ctx_register_frames)."""
+    _check(lib().tasx_ctx_register_frames(ctx_id, base_addr, nbytes), "tasx_ctx_register_frames")
+
+
+def ctx_stats(ctx_id: int) -> tuple[int, int]:
+    z, st = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().tasx_ctx_stats(ctx_id, ctypes.byref(z), ctypes.byref(st)), "tasx_ctx_stats")
+    return z.value, st.value
+
+
 def tcp4_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, n: int, out_addr: int | None,
                           ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
                           inplace: bool = False) -> None:
@@ -221,9 +235,9 @@ def raw_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, len0: int, n:
            "tasx_raw_cksum_batch_host")
 
 
-def set_kernel_config(variant: int = 0, ppg: int = 0) -> None:
-    """Select the kernel variant / packets-per-group (0, 0 = automatic)."""
-    _check(lib().tasx_set_kernel_config(variant, ppg), "tasx_set_kernel_config")
+def set_kernel_variant(variant: int = 0) -> None:
+    """Select the kernel variant (0 = automatic; see include/tasx_xsum.h)."""
+    _check(lib().tasx_set_kernel_variant(variant), "tasx_set_kernel_variant")
 
 
 class PinnedBuffer:
@@ -236,6 +250,9 @@ class PinnedBuffer:
         if not self.addr:
             raise TasxError(-errno.ENOMEM, "tasx_host_alloc")
         self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(self.addr))
+        self.dev_addr = lib().tasx_host_device_pointer(self.addr)
+        if not self.dev_addr:
+            raise TasxError(-errno.EIO, "tasx_host_device_pointer")
 
     def free(self) -> None:
         if self.addr:

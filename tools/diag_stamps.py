@@ -1,5 +1,5 @@
-"""Wave-timeline diagnostic for the TCP4 TAS-layout kernel (variant 17: the
-production kernel plus s_memrealtime stamps, 100 MHz).  Tuning aid only.
+"""Wave-timeline diagnostic for the TCP4 TAS-layout kernel (variant 4: the
+production tcp4_tas_kernel plus s_memrealtime stamps, 100 MHz).  Tuning aid only.
 
 Per wave: t0 entry, t1 total_length known (header chunks landed), t2 data
 accumulated, t3 stored.  Prints the dispatch ramp, phase latencies under load
@@ -28,14 +28,14 @@ def run(hint: int, rotate: int = 16):
     diag = torch.zeros(waves * 4, dtype=torch.int64, device="cuda")
     L = xsum.lib()
     L.tasx_set_diag_buffer(diag.data_ptr())
-    xsum.set_kernel_config(17, 0)
+    xsum.set_kernel_variant(4)
     st = torch.cuda.current_stream().cuda_stream
     for k in range(3 * rotate):
         assert L.tasx_tcp4_cksum_batch_dev_hint(bufs[k % rotate].data_ptr(), None, stride, None, hint, n, 14, 34,
                                                 out.data_ptr(), 0, st) == 0
     torch.cuda.synchronize()
     d = diag.cpu().numpy().reshape(-1, 4).astype(np.int64)
-    xsum.set_kernel_config(0, 0)
+    xsum.set_kernel_variant(0)
     L.tasx_set_diag_buffer(None)
     d = d[(d > 0).all(axis=1)]
     t = (d - d[:, 0].min()) * 10 / 1000.0  # us

@@ -1,6 +1,6 @@
 """Kernel-variant sweep on the GPU box (tuning aid, not part of the product).
 
-For each (mode, variant, ppg): K back-to-back launches over R rotating batches,
+For each (mode, variant): K back-to-back launches over R rotating batches,
 GPU time measured by one event pair around the K launches (us/launch, includes
 the ~1 us launch boundaries) and by per-launch event pairs (median); results
 are checked bit-exact against the oracle on the first batch.
@@ -133,8 +133,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rotate", type=int, default=16)
     ap.add_argument("--modes", default="tcp4,raw")
-    ap.add_argument("--variants", default="1,2,3,4,5,6,7")
-    ap.add_argument("--ppg", default="0")
+    ap.add_argument("--variants", default="1,2,3")
     ap.add_argument("--rounds", type=int, default=3, help="interleaved rounds per config (median)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
@@ -144,18 +143,15 @@ def main():
         fn, fargs, outs, nbytes, exp = make(mode, args.rotate)
         configs = []
         for v in map(int, args.variants.split(",")):
-            for ppg in map(int, args.ppg.split(",")):
-                if v in (1, 7) and ppg:
-                    continue
-                xsum.set_kernel_config(v, ppg)
-                outs[0].zero_()
-                if fn(*fargs[0]) != 0:  # variant not available for this mode
-                    continue
-                torch.cuda.synchronize()
-                got = outs[0].cpu().numpy().view(np.uint16)
-                configs.append((v, ppg, bool(np.array_equal(got, exp))))
+            xsum.set_kernel_variant(v)
+            outs[0].zero_()
+            if fn(*fargs[0]) != 0:  # variant not available for this mode
+                continue
+            torch.cuda.synchronize()
+            got = outs[0].cpu().numpy().view(np.uint16)
+            configs.append((v, 0, bool(np.array_equal(got, exp))))
         # prewarm the clocks, then interleave rounds over all configs (rule 24)
-        xsum.set_kernel_config(*configs[0][:2])
+        xsum.set_kernel_variant(configs[0][0])
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 0.3:
             for k in range(32):
@@ -165,7 +161,7 @@ def main():
         res = {c: [] for c in configs}
         for _ in range(args.rounds):
             for c in configs:
-                xsum.set_kernel_config(c[0], c[1])
+                xsum.set_kernel_variant(c[0])
                 res[c].append(measure(fn, fargs, steps))
         for c in configs:
             wall = float(np.median([w for w, _ in res[c]]))
@@ -178,7 +174,7 @@ def main():
             print(json.dumps(row), flush=True)
         del fn, fargs, outs
         torch.cuda.empty_cache()
-    xsum.set_kernel_config(0, 0)
+    xsum.set_kernel_variant(0)
 
 
 if __name__ == "__main__":
