@@ -78,12 +78,20 @@ def parse(argv=None):
 # distributed plumbing (one process per GPU; control only, never data)
 
 def dist_setup():
+    """One process per GPU.  The process group carries only the barrier and two
+    scalar reductions (RCCL as "nccl"; TASX_DIST_BACKEND=gloo runs the same
+    control plane on the CPU, e.g. to rehearse N ranks on a one-GPU box)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        backend = os.environ.get("TASX_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
