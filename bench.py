@@ -174,6 +174,29 @@ class Tcp4Workload:
         return launch
 
 
+class RxVerifyWorkload:
+    """Receive-side verification over a Tcp4Workload's (checksummed) frames."""
+
+    def __init__(self, wl: Tcp4Workload):
+        self.wl = wl
+        wl.rx_flags = [torch.empty(wl.n, dtype=torch.uint8, device="cuda") for _ in wl.bufs]
+        self.bytes_per_step = wl.n * (wl.ip_total + 1)
+
+    def launcher(self):
+        fn = xsum.lib().tasx_tcp4_verify_batch_dev
+        stream = torch.cuda.current_stream().cuda_stream
+        wl = self.wl
+        args = [(b.data_ptr(), None, wl.stride, wl.n, pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN,
+                 f.data_ptr(), stream) for b, f in zip(wl.bufs, wl.rx_flags)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_tcp4_verify_batch_dev")
+        return launch
+
+
 class RawWorkload:
     desc = f"{N_FRAMES} x {RAW_LEN} B packed payloads, rte_raw_cksum per packet"
 
@@ -470,6 +493,17 @@ def main():
     wl.hint = 0
     nohint = leg(wl, args, ws, "same frames, tasx_tcp4_cksum_batch_dev (frames only, no hint)")
     wl.hint = FRAME_LEN
+    # receive-side verification of the same frames (after in-place TX checksums)
+    xsum.tcp4_cksum_batch(wl.bufs[0], wl.n, stride=wl.stride, inplace=True, want_out=False)
+    for b in wl.bufs[1:]:
+        b.copy_(wl.bufs[0])
+    rx = leg(RxVerifyWorkload(wl), args, ws, "same frames after TX checksums, tasx_tcp4_verify_batch_dev")
+    torch.cuda.synchronize()
+    rx["all_frames_verified"] = bool((wl.rx_flags[0] == 3).all().item())
+    src = torch.from_numpy(wl.host).cuda()
+    for b in wl.bufs:  # restore the un-checksummed frames for the legs below
+        b.copy_(src)
+    del src
     raw = None
     if not args.no_raw:
         rw = RawWorkload(rot, pktgen.SEED + 1000 + rank)
@@ -511,6 +545,7 @@ def main():
             "roofline": head["roofline"],
             "cpu_baseline": extra.get("cpu_baseline"),
             "tcp4_nohint": nohint,
+            "rx_verify": rx,
         }
         if raw is not None:
             line["raw"] = raw

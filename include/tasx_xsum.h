@@ -97,6 +97,20 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
     uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
     void *stream);
 
+/* Receive-side verification (new behaviour: TAS never verifies RX checksums,
+ * tas/fast/fast_flows.c:242-251, and requests no RX offloads,
+ * tas/fast/network.c:174).  flags[i] bit 0: the 20-byte IPv4 header folds to
+ * 0xffff; bit 1: DPDK (>= 21.11) rte_ipv4_udptcp_cksum_verify() passes, i.e.
+ * fold(rte_raw_cksum(L4) + rte_ipv4_phdr_cksum()) == 0xffff (total_length < 20
+ * fails); bit 2: IHL != 5 (TAS drops such frames, fast_flows.c:247).
+ * Asynchronous on `stream`. */
+#define TASX_RX_IP_OK 0x1u
+#define TASX_RX_L4_OK 0x2u
+#define TASX_RX_IHL_NOT5 0x4u
+int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint8_t *flags, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Per-fast-path-core contexts (one per dataplane_context, no shared state,
  * no locks: tas/fast/fastemu.c:87-91).  A context owns a GPU, streams, pinned

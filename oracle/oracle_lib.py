@@ -44,6 +44,10 @@ class Oracle:
             "oracle_ip_phdr_xsum": (ctypes.c_uint16, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint8, ctypes.c_uint16]),
             "oracle_raw_batch": (None, [_u8p, _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_size_t, _u8p]),
             "oracle_tcp4_batch": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_int]),
+            "oracle_ipv4_hdr_verify": (ctypes.c_int, [_u8p]),
+            "oracle_ipv4_udptcp_cksum_verify": (ctypes.c_int, [_u8p, _u8p]),
+            "oracle_tcp4_verify_batch": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
+                                                ctypes.c_uint32, _u8p]),
             "oracle_bench": (ctypes.c_double, [ctypes.c_int, _u8p, _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_int, ctypes.c_int]),
         }
@@ -107,6 +111,14 @@ class Oracle:
         o = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
         self.L.oracle_tcp4_batch(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n,
                                  ip_off, l4_off, out.ctypes.data, 1 if inplace else 0)
+        return out
+
+    def tcp4_verify_batch(self, buf: np.ndarray, n: int, offsets=None, stride: int = 0, ip_off: int = 14,
+                          l4_off: int = 34) -> np.ndarray:
+        out = np.empty(n, np.uint8)
+        o = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
+        self.L.oracle_tcp4_verify_batch(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n,
+                                        ip_off, l4_off, out.ctypes.data)
         return out
 
     def bench(self, mode: int, buf: np.ndarray, n: int, *, offsets=None, lengths=None, stride=0,

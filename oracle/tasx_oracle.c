@@ -148,6 +148,25 @@ uint16_t oracle_ip_phdr_xsum(uint32_t ip_src_be, uint32_t ip_dst_be,
   return (uint16_t) sum;
 }
 
+/* Receive-side verification (new behaviour; see tasx_oracle.h). */
+int oracle_ipv4_hdr_verify(const void *ip_hdr)
+{
+  return oracle_raw_cksum(ip_hdr, 20) == 0xffff;
+}
+
+int oracle_ipv4_udptcp_cksum_verify(const void *ip_hdr, const void *l4_hdr)
+{
+  const uint8_t *ip = (const uint8_t *) ip_hdr;
+  uint32_t l3_len = (uint32_t) ((ip[2] << 8) | ip[3]);
+  uint32_t cksum;
+  if (l3_len < 20)
+    return 0; /* __rte_ipv4_udptcp_cksum returns 0, which is not 0xffff */
+  cksum = oracle_raw_cksum(l4_hdr, l3_len - 20);
+  cksum += oracle_ipv4_phdr_cksum(ip_hdr, 0);
+  cksum = ((cksum & 0xffff0000u) >> 16) + (cksum & 0xffffu);
+  return (uint16_t) cksum == 0xffff;
+}
+
 /* ---------------------------------------------------------------------- */
 /* Batch drivers (one reference-style call per packet). */
 
@@ -184,6 +203,23 @@ void oracle_tcp4_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
       memcpy(f + ip_off + 10, save_ip, 2);
       memcpy(f + l4_off + 16, save_tcp, 2);
     }
+  }
+}
+
+void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags)
+{
+  size_t i;
+  for (i = 0; i < n; i++) {
+    const uint8_t *f = base + pkt_off(off, stride, i);
+    uint8_t v = 0;
+    if (oracle_ipv4_hdr_verify(f + ip_off))
+      v |= 1;
+    if (oracle_ipv4_udptcp_cksum_verify(f + ip_off, f + l4_off))
+      v |= 2;
+    if ((f[ip_off] & 0x0f) != 5)
+      v |= 4;
+    flags[i] = v;
   }
 }
 

@@ -49,6 +49,17 @@ void oracle_tcp_checksums(void *ip_hdr, void *l4_hdr);
 uint16_t oracle_ip_phdr_xsum(uint32_t ip_src_be, uint32_t ip_dst_be,
     uint8_t proto, uint16_t l3_paylen);
 
+/* Receive-side verification (new behaviour).
+ * hdr: rte_raw_cksum of the 20-byte header (checksum included) == 0xffff.
+ * l4: DPDK 21.11 rte_ipv4_udptcp_cksum_verify for IHL 5 (published algorithm,
+ * third-party): l3 < 20 fails; fold1(rte_raw_cksum(l4, l3-20) +
+ * rte_ipv4_phdr_cksum(ip, 0)) == 0xffff. */
+int oracle_ipv4_hdr_verify(const void *ip_hdr);
+int oracle_ipv4_udptcp_cksum_verify(const void *ip_hdr, const void *l4_hdr);
+/* flags[i] = hdr_ok | l4_ok << 1 | (IHL != 5) << 2 */
+void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags);
+
 /* PKT_TX_TCP_SEG bit of DPDK 19.11 rte_mbuf_core.h (1ULL << 50) */
 #define ORACLE_PKT_TX_TCP_SEG (1ULL << 50)
 

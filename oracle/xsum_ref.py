@@ -93,3 +93,29 @@ def raw_batch(buf: np.ndarray, offsets, lengths) -> np.ndarray:
     for i, (o, n) in enumerate(zip(offsets, lengths)):
         out[i] = raw_cksum(mv[int(o): int(o) + int(n)])
     return out
+
+
+def ipv4_hdr_verify(ip: bytes) -> bool:
+    """Receive-side header check: the 20-byte header (checksum included) folds to 0xffff."""
+    return raw_cksum(ip[:20]) == 0xFFFF
+
+
+def ipv4_udptcp_cksum_verify(ip: bytes, l4: bytes) -> bool:
+    """DPDK 21.11 rte_ipv4_udptcp_cksum_verify for IHL 5 (published algorithm)."""
+    l3 = (ip[2] << 8) | ip[3]
+    if l3 < 20:
+        return False
+    c = raw_cksum(l4[: l3 - 20]) + ipv4_phdr_cksum(ip, 0)
+    c = (c >> 16) + (c & 0xFFFF)
+    return c == 0xFFFF
+
+
+def tcp4_verify(frame: bytes, ip_off: int = 14, l4_off: int = 34) -> int:
+    ip = bytes(frame[ip_off: ip_off + 20])
+    tl = (ip[2] << 8) | ip[3]
+    v = 1 if ipv4_hdr_verify(ip) else 0
+    if ipv4_udptcp_cksum_verify(ip, bytes(frame[l4_off: l4_off + max(tl - 20, 0)])):
+        v |= 2
+    if (ip[0] & 0x0F) != 5:
+        v |= 4
+    return v

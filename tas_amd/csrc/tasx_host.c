@@ -145,6 +145,28 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
       l4_off, out, flags, stream);
 }
 
+int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint8_t *flags, void *stream)
+{
+  tasx_tcp4_params p;
+  if (n == 0)
+    return 0;
+  if ((!base && !off) || !flags)
+    return set_err(-EINVAL, "tcp4 verify: NULL base/flags");
+  memset(&p, 0, sizeof(p));
+  p.base = (uint8_t *) base;
+  p.off = off;
+  p.out = (uint16_t *) (void *) flags;
+  p.stride = stride;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  if (tasx_launch_tcp4_verify(&p, stream) != 0)
+    return hip_err(hipGetLastError(), "tcp4 verify kernel launch");
+  return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* contexts */
 

@@ -40,6 +40,8 @@ typedef struct tasx_tcp4_params {
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
+/* receive-side verification; p->out points to n flag bytes */
+int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream);
 
 #ifdef __cplusplus
 }

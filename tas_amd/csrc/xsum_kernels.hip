@@ -301,6 +301,13 @@ __device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
   return s;
 }
 
+// byte b (0..15) of a 16-byte chunk
+__device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
+{
+  const uint32_t w = (b < 4) ? v.x : (b < 8) ? v.y : (b < 12) ? v.z : v.w;
+  return (w >> (8 * (b & 3))) & 0xffu;
+}
+
 template <int U>
 struct Chunks {
   const u32x4 *c0p;
@@ -394,7 +401,14 @@ __global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
 // with the header loads; the hint drives only the prefetch: results always
 // follow ip.total_length (chunks past it are dropped, chunks the hint missed
 // are loaded after the header arrives).
-template <int U>
+//
+// VERIFY = true is the receive-side check (TAS itself
+// never verifies, fast_flows.c:242-251): the checksum fields are summed as they
+// are, and out[i] gets a flag byte: bit 0 = the header folds to 0xffff, bit 1
+// = rte_ipv4_udptcp_cksum_verify passes (DPDK >= 21.11: fold1(raw(L4) +
+// phdr) == 0xffff; total_length < 20 fails), bit 2 = IHL != 5 (TAS drops
+// such frames, fast_flows.c:247; bits 0/1 then describe a 20-byte header).
+template <int U, bool VERIFY = false>
 __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -420,12 +434,6 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
     w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const Chunks<U> r = chunk_range<U>(l4, len);
-  uint32_t fb0 = 0, fb1 = 0;
-  if (gl == 10 && len > 16) {
-    fb0 = ld8(l4 + 16);
-    if (len > 17)
-      fb1 = ld8(l4 + 17);
-  }
   // first 16*U chunks: reuse the speculative loads when they cover them
   uint64_t acc = 0;
   if (r.nch) {
@@ -453,6 +461,15 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
       acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, r.tail);
     }
   }
+  if (!VERIFY && len > 16) {
+    // tcp.chksum (segment bytes 16, 17) is taken as zero: subtract its bytes
+    // exactly on the lane that holds their chunk (chunk index <= 2, so u = 0)
+    const int p16 = r.head + 16, p17 = p16 + 1;
+    if (gl == (p16 >> 4))
+      acc -= (uint64_t) chunk_byte(v[0], p16 & 15) << (8 * (p16 & 3));
+    if (len > 17 && gl == (p17 >> 4))
+      acc -= (uint64_t) chunk_byte(v[0], p17 & 15) << (8 * (p17 & 3));
+  }
   uint32_t part = fold64_to_18(acc);
   if (r.nch > 16u * U) { // long segments: the rest in the plain loop
     Chunks<U> rest = r;
@@ -461,14 +478,30 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
     rest.head = 0;
     part += group_lane_sum<U>(rest, gl);
   }
-  uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0u;
+  uint32_t c_ip = (gl < 10 && (VERIFY || gl != 5)) ? w : 0u;
   uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
-  if (gl == 10 && len > 16)
-    c_ph += (~(fb0 | (fb1 << 8))) & 0xffffu;
+  const uint32_t w0 = (uint32_t) __shfl((int) w, (threadIdx.x & 63) & ~15, 64); // version/IHL byte
   part = row_sum16(part);
   c_ip = row_sum16(c_ip);
   c_ph = row_sum16(c_ph);
-  if (gl == 15) {
+  if (VERIFY && gl == 15) {
+    // exact rte_raw_cksum values: every sum above is exact and non-negative
+    const uint32_t ri = fold32_to_16(c_ip);
+    uint32_t flags = (ri == 0xffffu) ? 1u : 0u;
+    if (tl >= 20) {
+      uint32_t r4 = fold32_to_16(part);
+      if (r.head & 1)
+        r4 = bswap16(r4);
+      const uint32_t ph = fold32_to_16(c_ph + bswap16(len)); // rte_ipv4_phdr_cksum
+      uint32_t c = r4 + ph;
+      c = (c >> 16) + (c & 0xffffu);
+      flags |= (c == 0xffffu) ? 2u : 0u;
+    }
+    if ((w0 & 0x0fu) != 5u)
+      flags |= 4u;
+    stg((uint8_t *) p.out, i, (uint8_t) flags);
+  }
+  if (!VERIFY && gl == 15) {
     const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
     uint32_t tcpc = 0;
     if (tl >= 20) {
@@ -497,12 +530,6 @@ __device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
   if (bh <= bl)
     return 0u;
   return (uint32_t) (((1ull << (8 * bh)) - 1ull) & ~((1ull << (8 * bl)) - 1ull));
-}
-
-__device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
-{
-  const uint32_t w = (b < 4) ? v.x : (b < 8) ? v.y : (b < 12) ? v.z : v.w;
-  return (w >> (8 * (b & 3))) & 0xffu;
 }
 
 template <int BS>
@@ -716,6 +743,11 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
   default:
     return -2;
   }
+}
+
+extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream)
+{
+  return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)

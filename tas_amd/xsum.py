@@ -45,6 +45,7 @@ SIGNATURES = {
     "tasx_tcp4_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp]),
     "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                 _c_u32, _vp]),
+    "tasx_tcp4_verify_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
     "tasx_ctx_destroy": (_c_int, [_uns]),
     "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
@@ -174,6 +175,23 @@ def tcp4_cksum_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | No
         _check(lib().tasx_tcp4_cksum_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
                                                     n, ip_off, l4_off, _ptr(out), flags, _stream(stream)),
                "tasx_tcp4_cksum_batch_dev_hint")
+    return out
+
+
+RX_IP_OK, RX_L4_OK, RX_IHL_NOT5 = 0x1, 0x2, 0x4
+
+
+def tcp4_verify_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
+                      stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
+                      out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Receive-side checksum verification of n frames: uint8 flags per frame
+    (RX_IP_OK | RX_L4_OK | RX_IHL_NOT5)."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint8, device=frames.device)
+    if offsets is not None:
+        assert offsets.dtype == torch.int64 and offsets.numel() >= n
+    _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
+                                            _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
     return out
 
 

@@ -27,7 +27,10 @@ def _lib():
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
-    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:
+        a = a.copy()
+    return torch.from_numpy(a).to(DEV)
 
 
 def u16(t: torch.Tensor) -> np.ndarray:
@@ -441,3 +444,46 @@ def test_ctx_errors():
             xsum.defer_tcp4(2, f.ctypes.data, 14, 20)  # l4_off < ip_off + 20
     finally:
         xsum.ctx_destroy(2)
+
+
+# ---------------------------------------------------------------------------
+# receive-side verification
+
+def test_verify_roundtrip_64k(oracle):
+    """TX kernel stores -> RX verification kernel: every frame verifies; random
+    single-bit corruption is caught exactly as the oracle reports it."""
+    n = 65536
+    frames = pktgen.tcp4_frames(n, payload=(np.arange(n) * 7) % 1449, stride=2048, seed=81)
+    d = to_dev(frames)
+    xsum.tcp4_cksum_batch(d, n, stride=2048, inplace=True, want_out=False)
+    flags = xsum.tcp4_verify_batch(d, n, stride=2048)
+    torch.cuda.synchronize()
+    assert bool((flags == 3).all())
+    h = d.cpu().numpy()
+    rng = pktgen.splitmix64(82, n)
+    tl = 52 + (np.arange(n) * 7) % 1449
+    pos = 14 + (rng % tl.astype(np.uint64)).astype(np.int64)
+    bit = (rng >> np.uint64(61)).astype(np.int64)
+    sel = np.arange(0, n, 3)
+    h2 = h.copy()
+    h2[sel * 2048 + pos[sel]] ^= (1 << bit[sel]).astype(np.uint8)
+    got = xsum.tcp4_verify_batch(to_dev(h2), n, stride=2048).cpu().numpy()
+    exp = oracle.tcp4_verify_batch(h2, n, stride=2048)
+    np.testing.assert_array_equal(got, exp)
+    assert np.all(got[sel] != 3) and np.all(np.delete(got, sel) == 3)
+
+
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_verify_edges(oracle, tcp4_golden, shift):
+    g = tcp4_golden
+    n, stride = len(g["offsets"]), int(g["stride"])
+    good = g["frames"].copy()
+    oracle.tcp4_batch(good, n, stride=stride, inplace=True)
+    mixed = np.concatenate([good, g["frames"]])  # checksummed + raw (random fields) frames
+    f = mixed.reshape(2 * n, stride)
+    f[::5, 14] = 0x46                          # IHL 6
+    f[1::7, 16:18] = 0                         # total_length 0
+    buf = torch.zeros(mixed.size + 64, dtype=torch.uint8, device=DEV)
+    buf[shift:shift + mixed.size] = to_dev(mixed)
+    got = xsum.tcp4_verify_batch(buf[shift:], 2 * n, stride=stride).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.tcp4_verify_batch(mixed, 2 * n, stride=stride))

@@ -156,3 +156,41 @@ def test_oracle_bench_runs(oracle):
     fr = pktgen.tcp4_frames(256)
     t = oracle.bench(1, fr, 256, stride=2048, threads=1, reps=3)
     assert 0 < t < 5
+
+
+# ---------------------------------------------------------------------------
+# receive-side verification
+
+def test_verify_kat_and_corruption(oracle):
+    f = pktgen.kat_frame()
+    oracle.tcp_checksums(f)
+    arr = np.frombuffer(bytes(f), np.uint8).copy()
+    assert oracle.tcp4_verify_batch(arr, 1, stride=len(f))[0] == 3
+    assert R.tcp4_verify(bytes(f)) == 3
+    for pos, expect in ((14 + 8, 2), (34 + 5, 1), (14 + 13, 0)):  # ttl; seq; src addr (in both)
+        g = arr.copy()
+        g[pos] ^= 0x10
+        assert oracle.tcp4_verify_batch(g, 1, stride=len(f))[0] == expect, pos
+        assert R.tcp4_verify(bytes(g)) == expect
+    g = arr.copy()
+    g[14] = 0x46  # IHL 6
+    assert oracle.tcp4_verify_batch(g, 1, stride=len(f))[0] & 4
+
+
+def test_verify_batch_cross_restatement(oracle):
+    n = 300
+    frames = pktgen.tcp4_frames(n, payload=(np.arange(n) * 5) % 1449, stride=2048, seed=71)
+    good = frames.copy()
+    oracle.tcp4_batch(good, n, stride=2048, inplace=True)
+    flags = oracle.tcp4_verify_batch(good, n, stride=2048)
+    assert np.all(flags == 3)
+    bad = good.copy()
+    rng = pktgen.splitmix64(72, n)
+    for i in range(n):
+        tl = 52 + (i * 5) % 1449
+        pos = 14 + int(rng[i] % np.uint64(tl))
+        bad[i * 2048 + pos] ^= 1 << int(rng[i] >> np.uint64(61))
+    fl = oracle.tcp4_verify_batch(bad, n, stride=2048)
+    assert np.all(fl != 3)  # a single flipped bit is always detected
+    for i in range(0, n, 7):
+        assert fl[i] == R.tcp4_verify(bytes(bad[i * 2048:(i + 1) * 2048]))
