@@ -111,6 +111,36 @@ int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream);
 
+/* Fused TX segment build: the payload copy of
+ * flow_tx_segment() -- flow_tx_read() from the flow's circular transmit buffer
+ * in the shared-memory region, wrap-around split included
+ * (tas/fast/fast_flows.c:833-846, dma_read tas/fast/dma.h:39-53, placement
+ * :930-933) -- fused with the tcp_checksums() that follows it (:936 ->
+ * :1058-1069), in one pass over the payload.  The host has already filled the
+ * headers (:891-928).  Per segment, one 32-byte descriptor: */
+typedef struct tasx_tx_seg {
+  uint64_t frame_off; /* frame start, offset from `frames` */
+  uint64_t tx_base;   /* fs->tx_base: the flow's TX buffer, offset in shm */
+  uint32_t tx_len;    /* fs->tx_len */
+  uint32_t pos;       /* payload_pos, the read position in the TX buffer */
+  uint16_t payload;   /* payload bytes */
+  uint16_t hdrs_len;  /* payload offset in the frame (66 in TAS data segments) */
+  uint32_t reserved;  /* 0 */
+} tasx_tx_seg;
+/* For each segment: copy `payload` bytes from shm + tx_base at circular
+ * position pos into frame + hdrs_len, then store ip.chksum / tcp.chksum into
+ * the frame exactly as tcp_checksums() would over the finished frame (lengths
+ * from ip.total_length).  out[i] (optional, 4-byte aligned) = ip.chksum |
+ * tcp.chksum << 16.  A descriptor that dma_read()'s assertions would reject
+ * (pos >= tx_len with payload > 0, payload > tx_len, tx_base + tx_len >
+ * shm_len) or with hdrs_len < l4_off + 20 leaves its frame untouched and gets
+ * out[i] = 0, which no valid segment produces (ip.chksum is never 0).
+ * shm, frames, segs and out are device (or device-mapped host) pointers.
+ * Frames must not overlap.  Asynchronous on `stream`. */
+int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
+    const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint32_t *out, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Per-fast-path-core contexts (one per dataplane_context, no shared state,
  * no locks: tas/fast/fastemu.c:87-91).  A context owns a GPU, streams, pinned

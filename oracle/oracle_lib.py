@@ -48,6 +48,11 @@ class Oracle:
             "oracle_ipv4_udptcp_cksum_verify": (ctypes.c_int, [_u8p, _u8p]),
             "oracle_tcp4_verify_batch": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
                                                 ctypes.c_uint32, _u8p]),
+            "oracle_tx_segment_batch": (None, [_u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_size_t,
+                                               ctypes.c_uint32, ctypes.c_uint32, _u8p]),
+            "oracle_bench_tx_segment": (ctypes.c_double, [_u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_size_t,
+                                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                                          ctypes.c_int]),
             "oracle_bench": (ctypes.c_double, [ctypes.c_int, _u8p, _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_int, ctypes.c_int]),
         }
@@ -120,6 +125,20 @@ class Oracle:
         self.L.oracle_tcp4_verify_batch(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n,
                                         ip_off, l4_off, out.ctypes.data)
         return out
+
+    def tx_segment_batch(self, shm: np.ndarray, shm_len: int, frames: np.ndarray, segs: np.ndarray,
+                         ip_off: int = 14, l4_off: int = 34) -> np.ndarray:
+        """In place on `frames`; returns ip.chksum | tcp.chksum << 16 (0 = rejected)."""
+        assert frames.flags.c_contiguous and segs.flags.c_contiguous and segs.dtype.itemsize == 32
+        out = np.zeros(len(segs), np.uint32)
+        self.L.oracle_tx_segment_batch(shm.ctypes.data, shm_len, frames.ctypes.data, segs.ctypes.data,
+                                       len(segs), ip_off, l4_off, out.ctypes.data)
+        return out
+
+    def bench_tx_segment(self, shm: np.ndarray, shm_len: int, frames: np.ndarray, segs: np.ndarray,
+                         ip_off: int = 14, l4_off: int = 34, threads: int = 1, reps: int = 5) -> float:
+        return self.L.oracle_bench_tx_segment(shm.ctypes.data, shm_len, frames.ctypes.data, segs.ctypes.data,
+                                              len(segs), ip_off, l4_off, threads, reps)
 
     def bench(self, mode: int, buf: np.ndarray, n: int, *, offsets=None, lengths=None, stride=0,
               len0=0, ip_off=14, l4_off=34, threads=1, reps=5) -> float:

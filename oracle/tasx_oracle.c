@@ -224,6 +224,61 @@ void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
 }
 
 /* ---------------------------------------------------------------------- */
+/* TX segment build. */
+
+/* flow_tx_read(), tas/fast/fast_flows.c:833-846: read len bytes at circular
+ * position pos of the flow's TX buffer; dma_read() (tas/fast/dma.h:39-53) is a
+ * bounds-asserted rte_memcpy from the shared-memory region. */
+static void oracle_flow_tx_read(const uint8_t *shm, uint64_t tx_base,
+    uint32_t tx_len, uint32_t pos, uint16_t len, uint8_t *dst)
+{
+  uint32_t part;
+  if (pos + len <= tx_len) {
+    memcpy(dst, shm + tx_base + pos, len);
+  } else {
+    part = tx_len - pos;
+    memcpy(dst, shm + tx_base + pos, part);
+    memcpy(dst + part, shm + tx_base, len - part);
+  }
+}
+
+/* the descriptor checks that stand in for dma_read()'s assertions */
+static int oracle_tx_seg_ok(const struct oracle_tx_seg *d, uint64_t shm_len,
+    uint32_t l4_off)
+{
+  return (d->payload == 0 || d->pos < d->tx_len) && d->payload <= d->tx_len &&
+      d->tx_base <= shm_len && d->tx_len <= shm_len - d->tx_base &&
+      d->hdrs_len >= l4_off + 20;
+}
+
+void oracle_tx_segment_batch(const uint8_t *shm, uint64_t shm_len,
+    uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,
+    uint32_t ip_off, uint32_t l4_off, uint32_t *out)
+{
+  size_t i;
+  for (i = 0; i < n; i++) {
+    const struct oracle_tx_seg *d = &segs[i];
+    uint8_t *f = frames + d->frame_off;
+    uint16_t ipc, tcpc;
+    if (!oracle_tx_seg_ok(d, shm_len, l4_off)) {
+      if (out)
+        out[i] = 0;
+      continue;
+    }
+    /* flow_tx_segment(): payload at hdrs_len (:930-933), then the checksums
+     * over the finished frame (:936 -> tcp_checksums, :1058-1069) */
+    if (d->payload > 0)
+      oracle_flow_tx_read(shm, d->tx_base, d->tx_len, d->pos, d->payload,
+          f + d->hdrs_len);
+    oracle_tcp_checksums(f + ip_off, f + l4_off);
+    memcpy(&ipc, f + ip_off + 10, 2);
+    memcpy(&tcpc, f + l4_off + 16, 2);
+    if (out)
+      out[i] = (uint32_t) ipc | ((uint32_t) tcpc << 16);
+  }
+}
+
+/* ---------------------------------------------------------------------- */
 /* CPU baseline timing. */
 
 struct bench_arg {
@@ -235,6 +290,9 @@ struct bench_arg {
   uint32_t len0, ip_off, l4_off;
   size_t lo, hi;
   uint16_t *out;
+  const uint8_t *shm;
+  uint64_t shm_len;
+  const struct oracle_tx_seg *segs;
   pthread_barrier_t *bar;
   double t0, t1;
 };
@@ -262,6 +320,10 @@ static void *bench_worker(void *p)
     for (i = a->lo; i < a->hi; i++)
       a->out[i] = oracle_raw_cksum(a->base + pkt_off(a->off, a->stride, i),
           a->len ? a->len[i] : a->len0);
+  } else if (a->mode == 2) {
+    /* flow_tx_segment()'s payload copy + tcp_checksums(), per segment */
+    oracle_tx_segment_batch(a->shm, a->shm_len, a->base, a->segs + a->lo,
+        a->hi - a->lo, a->ip_off, a->l4_off, NULL);
   } else {
     /* in place, exactly what tcp_checksums() does to each TX frame */
     for (i = a->lo; i < a->hi; i++) {
@@ -279,9 +341,8 @@ static int cmp_d(const void *x, const void *y)
   return (a > b) - (a < b);
 }
 
-double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
-    const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
-    uint32_t ip_off, uint32_t l4_off, uint16_t *out, int threads, int reps)
+static double bench_run(const struct bench_arg *proto, size_t n, int threads,
+    int reps)
 {
   pthread_t *th;
   struct bench_arg *args;
@@ -309,18 +370,10 @@ double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
     pthread_barrier_init(&bar, NULL, (unsigned) threads);
     for (t = 0; t < threads; t++) {
       struct bench_arg *a = &args[t];
-      a->mode = mode;
+      *a = *proto;
       a->cpu = ncpu_avail ? cpus[t % ncpu_avail] : -1;
-      a->base = base;
-      a->off = off;
-      a->len = len;
-      a->stride = stride;
-      a->len0 = len0;
-      a->ip_off = ip_off;
-      a->l4_off = l4_off;
       a->lo = n * (size_t) t / (size_t) threads;
       a->hi = n * (size_t) (t + 1) / (size_t) threads;
-      a->out = out;
       a->bar = &bar;
       pthread_create(&th[t], NULL, bench_worker, a);
     }
@@ -340,4 +393,38 @@ double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
   free(args);
   free(times);
   return med;
+}
+
+double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
+    const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
+    uint32_t ip_off, uint32_t l4_off, uint16_t *out, int threads, int reps)
+{
+  struct bench_arg a;
+  memset(&a, 0, sizeof(a));
+  a.mode = mode;
+  a.base = base;
+  a.off = off;
+  a.len = len;
+  a.stride = stride;
+  a.len0 = len0;
+  a.ip_off = ip_off;
+  a.l4_off = l4_off;
+  a.out = out;
+  return bench_run(&a, n, threads, reps);
+}
+
+double oracle_bench_tx_segment(const uint8_t *shm, uint64_t shm_len,
+    uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,
+    uint32_t ip_off, uint32_t l4_off, int threads, int reps)
+{
+  struct bench_arg a;
+  memset(&a, 0, sizeof(a));
+  a.mode = 2;
+  a.base = frames;
+  a.shm = shm;
+  a.shm_len = shm_len;
+  a.segs = segs;
+  a.ip_off = ip_off;
+  a.l4_off = l4_off;
+  return bench_run(&a, n, threads, reps);
 }

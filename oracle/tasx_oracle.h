@@ -60,6 +60,21 @@ int oracle_ipv4_udptcp_cksum_verify(const void *ip_hdr, const void *l4_hdr);
 void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
     uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags);
 
+/* TX segment build: flow_tx_segment()'s payload
+ * copy, flow_tx_read() (tas/fast/fast_flows.c:833-846, :930-933), then
+ * tcp_checksums() over the frame (:936).  Same 32-byte descriptor as
+ * tasx_tx_seg (include/tasx_xsum.h).  Rejected descriptors: out[i] = 0, frame
+ * untouched.  out may be NULL. */
+struct oracle_tx_seg {
+  uint64_t frame_off, tx_base;
+  uint32_t tx_len, pos;
+  uint16_t payload, hdrs_len;
+  uint32_t reserved;
+};
+void oracle_tx_segment_batch(const uint8_t *shm, uint64_t shm_len,
+    uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,
+    uint32_t ip_off, uint32_t l4_off, uint32_t *out);
+
 /* PKT_TX_TCP_SEG bit of DPDK 19.11 rte_mbuf_core.h (1ULL << 50) */
 #define ORACLE_PKT_TX_TCP_SEG (1ULL << 50)
 
@@ -80,6 +95,10 @@ void oracle_tcp4_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
 double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
     const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
     uint32_t ip_off, uint32_t l4_off, uint16_t *out, int threads, int reps);
+/* same for the TX segment build (copy + checksums per segment) */
+double oracle_bench_tx_segment(const uint8_t *shm, uint64_t shm_len,
+    uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,
+    uint32_t ip_off, uint32_t l4_off, int threads, int reps);
 
 #ifdef __cplusplus
 }

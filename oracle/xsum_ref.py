@@ -119,3 +119,35 @@ def tcp4_verify(frame: bytes, ip_off: int = 14, l4_off: int = 34) -> int:
     if (ip[0] & 0x0F) != 5:
         v |= 4
     return v
+
+
+def flow_tx_read(shm, tx_base: int, tx_len: int, pos: int, n: int) -> bytes:
+    """flow_tx_read(), /root/reference tas/fast/fast_flows.c:833-846."""
+    mv = memoryview(shm)
+    if pos + n <= tx_len:
+        return bytes(mv[tx_base + pos: tx_base + pos + n])
+    part = tx_len - pos
+    return bytes(mv[tx_base + pos: tx_base + tx_len]) + bytes(mv[tx_base: tx_base + n - part])
+
+
+def tx_segment(shm, shm_len: int, frames: np.ndarray, segs: np.ndarray, ip_off: int = 14,
+               l4_off: int = 34) -> np.ndarray:
+    """flow_tx_segment()'s payload copy + tcp_checksums() per descriptor, in
+    place on `frames` (uint8); returns ip.chksum | tcp.chksum << 16 per segment,
+    0 for a descriptor dma_read()'s assertions would reject."""
+    out = np.zeros(len(segs), np.uint32)
+    shm = np.ascontiguousarray(shm, dtype=np.uint8)
+    for i, d in enumerate(segs):
+        fo, tb, tlen, pos, pay, hl = (int(d["frame_off"]), int(d["tx_base"]), int(d["tx_len"]),
+                                      int(d["pos"]), int(d["payload"]), int(d["hdrs_len"]))
+        if not ((pay == 0 or pos < tlen) and pay <= tlen and tb <= shm_len and tlen <= shm_len - tb
+                and hl >= l4_off + 20):
+            continue
+        if pay:
+            frames[fo + hl: fo + hl + pay] = np.frombuffer(flow_tx_read(shm, tb, tlen, pos, pay), np.uint8)
+        fr = bytearray(frames[fo: fo + max(l4_off + 18, ip_off + 20, hl + pay,
+                                           ip_off + ((int(frames[fo + ip_off + 2]) << 8) | int(frames[fo + ip_off + 3])))])
+        ipc, tcpc = tcp_checksums(fr, ip_off, l4_off)
+        frames[fo: fo + len(fr)] = np.frombuffer(bytes(fr), np.uint8)
+        out[i] = ipc | (tcpc << 16)
+    return out

@@ -167,6 +167,33 @@ int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
   return 0;
 }
 
+int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
+    const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint32_t *out, void *stream)
+{
+  tasx_txseg_params p;
+  if (n == 0)
+    return 0;
+  if (!shm || !frames || !segs)
+    return set_err(-EINVAL, "tx segment: NULL shm/frames/segs");
+  if (((uintptr_t) segs & 15u) || ((uintptr_t) out & 3u))
+    return set_err(-EINVAL, "tx segment: segs must be 16-byte, out 4-byte aligned");
+  if (l4_off < ip_off + 20 || l4_off > 0xffff)
+    return set_err(-EINVAL, "tx segment: need ip_off + 20 <= l4_off <= 65535");
+  memset(&p, 0, sizeof(p));
+  p.shm = (const uint8_t *) shm;
+  p.shm_len = shm_len;
+  p.frames = (uint8_t *) frames;
+  p.segs = segs;
+  p.out = out;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  if (tasx_launch_txseg(&p, stream) != 0)
+    return hip_err(hipGetLastError(), "tx segment kernel launch");
+  return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* contexts */
 

@@ -37,11 +37,24 @@ typedef struct tasx_tcp4_params {
   uint64_t *diag;        /* diagnostic timestamp buffer (diag variants only) */
 } tasx_tcp4_params;
 
+typedef struct tasx_txseg_params {
+  const uint8_t *shm;      /* device view of the shared-memory region */
+  uint64_t shm_len;
+  uint8_t *frames;         /* device pointer; segment frames at frame_off */
+  const tasx_tx_seg *segs; /* device, n descriptors (16-byte aligned) */
+  uint32_t *out;           /* device, n entries, or NULL */
+  uint32_t n;
+  uint32_t ip_off;
+  uint32_t l4_off;
+} tasx_txseg_params;
+
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 /* receive-side verification; p->out points to n flag bytes */
 int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream);
+/* fused TX segment build (txseg_kernels.hip) */
+int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 
 #ifdef __cplusplus
 }

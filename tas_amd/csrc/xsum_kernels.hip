@@ -36,146 +36,9 @@
 
 #include "tasx_kernels.h"
 
+#include "xsum_device.h"
+
 namespace {
-
-constexpr int kBlock = 256;
-
-// Global-address-space views: plain pointers taken from a by-value struct are
-// generic to the compiler and would lower to flat_load; these lower to
-// global_load_dwordx4 / global_load_ubyte / global_store_*.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 gcu4;
-typedef __attribute__((address_space(1))) const uint8_t gcu8;
-typedef __attribute__((address_space(1))) uint8_t gu8;
-
-__device__ __forceinline__ u32x4 ld16(const u32x4 *p, uint32_t i) { return ((gcu4 *) p)[i]; }
-// streaming (non-temporal) 16-byte load: packet bytes are read exactly once
-// (MI355X_MICROARCH.md nt-weights: nt cuts issue->landed latency ~18%)
-__device__ __forceinline__ u32x4 ld16nt(const u32x4 *p, uint32_t i)
-{
-  return __builtin_nontemporal_load(&((gcu4 *) p)[i]);
-}
-__device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8 *) p; }
-__device__ __forceinline__ void st8(uint8_t *p, uint32_t v) { *(gu8 *) p = (uint8_t) v; }
-template <typename T>
-__device__ __forceinline__ T ldg(const T *p, uint32_t i) { return ((__attribute__((address_space(1))) const T *) p)[i]; }
-template <typename T>
-__device__ __forceinline__ void stg(T *p, uint32_t i, T v) { ((__attribute__((address_space(1))) T *) p)[i] = v; }
-
-// ---------------------------------------------------------------------------
-// small integer helpers
-
-__device__ __forceinline__ uint32_t fold64_to_18(uint64_t a)
-{
-  // 64 -> <= 2^33 -> < 2^18, congruent mod 0xffff, positive iff a > 0
-  a = (a & 0xffffffffull) + (a >> 32);
-  a = (a & 0xffffull) + (a >> 16);
-  return (uint32_t) a;
-}
-
-__device__ __forceinline__ uint32_t fold32_to_16(uint32_t x)
-{
-  // x < 2^24 -> [0, 0xffff], 0 iff x == 0
-  x = (x & 0xffffu) + (x >> 16);
-  x = (x & 0xffffu) + (x >> 16);
-  return x;
-}
-
-__device__ __forceinline__ uint32_t bswap16(uint32_t x)
-{
-  return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
-}
-
-// residue in [0, 0xfffe] of a folded value in [0, 0xffff]
-__device__ __forceinline__ uint32_t residue(uint32_t f)
-{
-  return f == 0xffffu ? 0u : f;
-}
-
-// DPDK's inverted results (rte_ipv4_cksum, rte_ipv4_udptcp_cksum) as a
-// function of the residue r of their folded sum: 0xffff when r == 0, else ~r.
-__device__ __forceinline__ uint32_t inv_result(uint32_t r)
-{
-  return r == 0u ? 0xffffu : (0xffffu - r);
-}
-
-// keep bytes [lo, hi) (0 <= lo <= hi <= 16) of a 16-byte chunk
-__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi)
-{
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int l = min(max(lo - 4 * j, 0), 4);
-    int h = min(max(hi - 4 * j, 0), 4);
-    uint64_t mh = (1ull << (8 * h)) - 1ull;
-    uint64_t ml = (1ull << (8 * l)) - 1ull;
-    w[j] &= (uint32_t) (mh & ~ml);
-  }
-  return u32x4{w[0], w[1], w[2], w[3]};
-}
-
-__device__ __forceinline__ uint64_t add_chunk(uint64_t acc, u32x4 v)
-{
-  acc += v.x;
-  acc += v.y;
-  acc += v.z;
-  acc += v.w;
-  return acc;
-}
-
-template <int G>
-__device__ __forceinline__ uint32_t group_sum(uint32_t v)
-{
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1)
-    v += __shfl_xor(v, m, 64);
-  return v;
-}
-
-// Sum of the aligned-word frame over bytes [start, start + len), spread over
-// the G lanes of a group (lane gl), U chunks per lane per iteration.  Returns
-// this lane's partial (not yet reduced), < 2^18.
-template <int G, int U>
-__device__ __forceinline__ uint32_t lane_partial(const uint8_t *start, uint32_t len, int gl)
-{
-  if (len == 0)
-    return 0;
-  const uintptr_t a0 = (uintptr_t) start;
-  const uintptr_t a1 = a0 + len;
-  const u32x4 *c0p = (const u32x4 *) (a0 & ~(uintptr_t) 15);
-  const uint32_t nch = (uint32_t) (((a1 + 15) & ~(uintptr_t) 15) - (a0 & ~(uintptr_t) 15)) >> 4;
-  const int head = (int) (a0 & 15);                 // bytes to drop in chunk 0
-  const int tail = (int) (a1 - ((a1 - 1) & ~(uintptr_t) 15)); // bytes kept in last chunk (1..16)
-  uint64_t acc = 0;
-
-  for (uint32_t c = (uint32_t) gl; c < nch; c += (uint32_t) (G * U)) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t cc = c + (uint32_t) (u * G);
-      if (cc < nch)
-        v[u] = ld16(c0p, cc);
-      else
-        v[u] = u32x4{0, 0, 0, 0};
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t cc = c + (uint32_t) (u * G);
-      if (cc == 0 || cc == nch - 1) {
-        const int lo = (cc == 0) ? head : 0;
-        const int hi = (cc == nch - 1) ? tail : 16;
-        v[u] = mask_chunk(v[u], lo, hi);
-      }
-      acc = add_chunk(acc, v[u]);
-    }
-  }
-  return fold64_to_18(acc);
-}
-
-__device__ __forceinline__ uint64_t pkt_offset(const uint64_t *off, uint64_t stride, uint32_t i)
-{
-  return off ? ldg(off, i) : (uint64_t) i * stride;
-}
 
 // ---------------------------------------------------------------------------
 // First-generation kernels (variant 1, the A/B baseline): one G-lane group per
@@ -273,92 +136,6 @@ __global__ __launch_bounds__(kBlock) void tcp4_cksum_kernel(tasx_tcp4_params p)
       }
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// 16-lane packet groups (one DPP row each), one block per 16 packets.
-
-__device__ __forceinline__ uint32_t row_sum16(uint32_t v)
-{
-  // Hillis-Steele inclusive scan inside each 16-lane DPP row; lane 15 = row sum
-  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x111, 0xf, 0xf, false); // row_shr:1
-  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x112, 0xf, 0xf, false); // row_shr:2
-  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x114, 0xf, 0xf, false); // row_shr:4
-  v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x118, 0xf, 0xf, false); // row_shr:8
-  return v;
-}
-
-// sum of the dwords of chunk v restricted to bytes [0, h) (0 <= h <= 16)
-__device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
-{
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  uint64_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int b = min(max(h - 4 * j, 0), 4);
-    s += w[j] & (uint32_t) ((1ull << (8 * b)) - 1ull);
-  }
-  return s;
-}
-
-// byte b (0..15) of a 16-byte chunk
-__device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
-{
-  const uint32_t w = (b < 4) ? v.x : (b < 8) ? v.y : (b < 12) ? v.z : v.w;
-  return (w >> (8 * (b & 3))) & 0xffu;
-}
-
-template <int U>
-struct Chunks {
-  const u32x4 *c0p;
-  uint32_t nch;
-  int head, tail; // bytes dropped at the start of chunk 0 / kept in chunk nch-1
-};
-
-template <int U>
-__device__ __forceinline__ Chunks<U> chunk_range(const uint8_t *start, uint32_t len)
-{
-  Chunks<U> r;
-  const uintptr_t a0 = (uintptr_t) start, a1 = a0 + len;
-  r.c0p = (const u32x4 *) (a0 & ~(uintptr_t) 15);
-  r.nch = len ? (uint32_t) ((((a1 + 15) & ~(uintptr_t) 15) - (a0 & ~(uintptr_t) 15)) >> 4) : 0u;
-  r.head = (int) (a0 & 15);
-  r.tail = (int) (a1 - ((a1 - 1) & ~(uintptr_t) 15));
-  return r;
-}
-
-// this lane's exact partial over the group's chunks gl, gl+16, ...
-template <int U>
-__device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
-{
-  uint64_t acc = 0;
-  if (r.nch == 0)
-    return 0;
-  for (uint32_t c = (uint32_t) gl; c < r.nch; c += 16u * U) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(r.c0p, min(c + 16u * u, r.nch - 1));
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool keep = c + 16u * u < r.nch;
-      acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
-    }
-    // boundary fix-ups: drop bytes [0, head) of chunk 0, [tail, 16) of chunk nch-1
-    if (c == 0 && r.head)
-      acc -= chunk_prefix_sum(v[0], r.head);
-    const uint32_t last = r.nch - 1;
-    if (last >= c && last < c + 16u * U && ((last - c) & 15u) == 0 && r.tail < 16) {
-      const uint32_t ut = (last - c) >> 4;
-      u32x4 t = v[0];
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        if (ut == (uint32_t) u)
-          t = v[u];
-      acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, r.tail);
-    }
-  }
-  return fold64_to_18(acc);
 }
 
 // RAW, any layout: out[i] = rte_raw_cksum(base + off_i, len_i)

@@ -113,6 +113,55 @@ def tcp4_frames(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SE
     return buf
 
 
+# struct tasx_tx_seg (include/tasx_xsum.h), 32 bytes
+TX_SEG_DTYPE = np.dtype([("frame_off", "<u8"), ("tx_base", "<u8"), ("tx_len", "<u4"), ("pos", "<u4"),
+                         ("payload", "<u2"), ("hdrs_len", "<u2"), ("reserved", "<u4")])
+
+
+def tx_segments(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SEED,
+                nflows: int | None = None, tx_len: int = 16384, odd: bool = False,
+                make_shm: bool = True):
+    """n TX data segments the way fast_flows_qman -> flow_tx_segment() builds
+    them (/root/reference/tas/fast/fast_flows.c:877-955): headers filled (as
+    tcp4_frames), payload still to be read from the flow's circular TX buffer.
+    Segment i belongs to flow i % nflows; a flow's segments read consecutive
+    payload from a random start position, wrapping at tx_len.  odd=True gives
+    odd buffer lengths and odd, unaligned buffer bases.
+    Returns (shm u8, frames u8, segs TX_SEG_DTYPE, shm_bytes)."""
+    payload = np.broadcast_to(np.asarray(payload, dtype=np.int64), (n,)).copy()
+    nflows = nflows or max(1, n // 8)
+    tlen = np.full(nflows, tx_len, np.int64)
+    if odd:
+        tlen -= (splitmix64(seed ^ 0x0DDF, nflows) % np.uint64(7)).astype(np.int64)
+    assert int(payload.max(initial=0)) <= int(tlen.min(initial=tx_len))
+    slot = tlen + (16 if odd else 0)
+    base = np.zeros(nflows, np.int64)
+    np.cumsum(slot[:-1], out=base[1:])
+    if odd:
+        base += (splitmix64(seed ^ 0xBA5E, nflows) % np.uint64(16)).astype(np.int64)
+    shm_bytes = int(base[-1] + tlen[-1]) + 16 if nflows else 16
+    start = (splitmix64(seed ^ 0x5747, nflows) % tlen.astype(np.uint64)).astype(np.int64)
+    flow = np.arange(n, dtype=np.int64) % nflows
+    # bytes the flow sent before segment i: exclusive cumsum within each flow
+    order = np.lexsort((np.arange(n), flow))
+    ps = payload[order]
+    cs = np.cumsum(ps) - ps
+    first = np.r_[True, flow[order][1:] != flow[order][:-1]] if n else np.zeros(0, bool)
+    grp0 = np.maximum.accumulate(np.where(first, np.arange(n), 0)) if n else np.zeros(0, np.int64)
+    before = np.empty(n, np.int64)
+    before[order] = cs - cs[grp0]
+    segs = np.zeros(n, TX_SEG_DTYPE)
+    segs["frame_off"] = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    segs["tx_base"] = base[flow]
+    segs["tx_len"] = tlen[flow]
+    segs["pos"] = (start[flow] + before) % tlen[flow]
+    segs["payload"] = payload
+    segs["hdrs_len"] = HDRS_LEN
+    frames = tcp4_frames(n, payload, stride, seed)
+    shm = random_bytes(seed ^ 0x7E5B, shm_bytes) if make_shm else None
+    return shm, frames, segs, shm_bytes
+
+
 def kat_frame() -> bytearray:
     """The window-update segment built by the reference unit test
     test_rxbump_fc_reopen_notx (tests/tas_unit/fastpath.c:18-22,68-89,187-207

@@ -46,6 +46,7 @@ SIGNATURES = {
     "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                 _c_u32, _vp]),
     "tasx_tcp4_verify_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
+    "tasx_tx_segment_batch_dev": (_c_int, [_vp, _c_u64, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
     "tasx_ctx_destroy": (_c_int, [_uns]),
     "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
@@ -192,6 +193,23 @@ def tcp4_verify_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | N
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
     _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
                                             _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
+    return out
+
+
+def tx_segment_batch(shm: torch.Tensor, frames: torch.Tensor, segs: torch.Tensor, n: int, *,
+                     ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
+                     out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Fused TX segment build: flow_tx_read() of each segment's payload from the
+    shared-memory TX buffers into its frame, then tcp_checksums() in place
+    (tas/fast/fast_flows.c:930-936).  `segs` holds n 32-byte tasx_tx_seg
+    descriptors (pktgen.TX_SEG_DTYPE bytes, 16-byte aligned on the device).
+    Returns int32 ip.chksum | tcp.chksum << 16 per segment (0 = rejected)."""
+    assert segs.numel() * segs.element_size() >= 32 * n
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=frames.device)
+    _check(lib().tasx_tx_segment_batch_dev(_ptr(shm), shm.numel() * shm.element_size(), _ptr(frames),
+                                           _ptr(segs), n, ip_off, l4_off, _ptr(out), _stream(stream)),
+           "tasx_tx_segment_batch_dev")
     return out
 
 

@@ -134,6 +134,52 @@ def tcp4_fixture():
                 expected=exp)
 
 
+def txseg_fixture():
+    """Fused TX segment build (flow_tx_read + tcp_checksums, SURVEY.md section 8f
+    row 1): odd-length / odd-based circular TX buffers small enough that many
+    payloads wrap, plus rejected descriptors, zero payloads, other header
+    lengths and ip.total_length that disagrees with the payload."""
+    stride = 1536
+    pay = np.asarray([0, 1, 2, 15, 16, 17, 100, 1447, 1448] + list(range(200, 1449, 97)))
+    n_reg = len(pay)
+    shm, frames, segs, shm_len = pktgen.tx_segments(n_reg, payload=pay, stride=stride, seed=SEED,
+                                                    nflows=5, tx_len=1600, odd=True)
+    segs = list(segs)
+    fr = [bytearray(frames[i * stride:(i + 1) * stride].tobytes()) for i in range(n_reg)]
+
+    def add(f: bytearray, d):
+        d = d.copy()
+        d["frame_off"] = len(fr) * stride
+        fr.append(f)
+        segs.append(d)
+
+    base = segs[7]  # a full-MSS segment
+    f0 = fr[7]
+    d = base.copy(); d["payload"] = 0; d["pos"] = d["tx_len"] + 3          # no payload: pos unused
+    g = bytearray(f0); g[16:18] = (52).to_bytes(2, "big"); add(g, d)
+    d = base.copy(); d["pos"] = d["tx_len"]; d["payload"] = 5; add(bytearray(f0), d)    # rejected
+    d = base.copy(); d["payload"] = d["tx_len"] + 1; add(bytearray(f0), d)              # rejected
+    d = base.copy(); d["tx_base"] = shm_len - d["tx_len"] + 1; add(bytearray(f0), d)    # rejected
+    d = base.copy(); d["hdrs_len"] = 53; add(bytearray(f0), d)                           # rejected
+    for delta in (7, -100):                                         # ip.len disagrees
+        g = bytearray(f0); g[16:18] = (52 + int(base["payload"]) + delta).to_bytes(2, "big")
+        add(g, base)
+    g = bytearray(f0); g[16:18] = (10).to_bytes(2, "big"); add(g, base)      # total_length < 20
+    for hl in (54, 67, 80):                                         # other header lengths
+        d = base.copy(); d["hdrs_len"] = hl; d["payload"] = 1400
+        g = bytearray(f0); g[16:18] = (hl - 14 + 1400).to_bytes(2, "big"); add(g, d)
+    d = base.copy(); d["pos"] = d["tx_len"] - 1; d["payload"] = 300   # wraps after 1 byte
+    g = bytearray(f0); g[16:18] = (52 + 300).to_bytes(2, "big"); add(g, d)
+    d = base.copy(); d["pos"] = 0; d["payload"] = d["tx_len"] if d["tx_len"] <= 1448 else 1448
+    g = bytearray(f0); g[16:18] = (52 + int(d["payload"])).to_bytes(2, "big"); add(g, d)
+    segs = np.asarray(segs, pktgen.TX_SEG_DTYPE)
+    frames_in = np.frombuffer(b"".join(bytes(x) for x in fr), np.uint8).copy()
+    frames_out = frames_in.copy()
+    exp = R.tx_segment(shm, shm_len, frames_out, segs)
+    return dict(shm=shm, shm_len=np.uint64(shm_len), frames_in=frames_in, segs=segs.view(np.uint8),
+                frames_out=frames_out, expected=exp)
+
+
 def main():
     raw = raw_fixture()
     np.savez_compressed(HERE / "raw_vectors.npz", **raw)
@@ -150,8 +196,11 @@ def main():
                       "flow_tx_segment, tas/fast/fast_flows.c:886-928); values hand-derived "
                       "in SURVEY.md section 8c"},
     }
+    tx = txseg_fixture()
+    np.savez_compressed(HERE / "txseg_vectors.npz", **tx)
     (HERE / "kat.json").write_text(json.dumps(kat, indent=2) + "\n")
-    print("raw:", len(raw["lengths"]), "vectors;", "tcp4:", len(tcp["offsets"]), "frames")
+    print("raw:", len(raw["lengths"]), "vectors;", "tcp4:", len(tcp["offsets"]), "frames;",
+          "txseg:", len(tx["expected"]), "segments")
 
 
 if __name__ == "__main__":

@@ -1,0 +1,181 @@
+"""Fused TX segment build: flow_tx_segment()'s
+payload copy from the flow's circular TX buffer (flow_tx_read,
+/root/reference/tas/fast/fast_flows.c:833-846, :930-933) fused with
+tcp_checksums() (:936 -> :1058-1069).
+
+CPU tests pin the C oracle against the committed fixture (made by the numpy
+restatement) and against the numpy restatement on seeded batches.  GPU tests
+run tasx_tx_segment_batch_dev through the C ABI and compare the WHOLE frames
+buffer (payload copy, checksum fields, and every byte the build must leave
+alone) and the per-segment results with the oracle, bit-exact.
+"""
+import numpy as np
+import pytest
+
+from tas_amd import pktgen
+
+GOLDEN = "txseg_vectors.npz"
+
+
+@pytest.fixture(scope="module")
+def txseg_golden():
+    from conftest import GOLDEN as G
+    with np.load(G / GOLDEN) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _segs(g):
+    return g["segs"].view(pktgen.TX_SEG_DTYPE)
+
+
+# ---------------------------------------------------------------------------
+# oracle (CPU)
+
+def test_oracle_txseg_golden(oracle, txseg_golden):
+    g = txseg_golden
+    fr = g["frames_in"].copy()
+    out = oracle.tx_segment_batch(g["shm"], int(g["shm_len"]), fr, _segs(g))
+    np.testing.assert_array_equal(out, g["expected"])
+    np.testing.assert_array_equal(fr, g["frames_out"])
+    assert (out == 0).sum() == 4  # the four rejected descriptors
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_oracle_txseg_vs_numpy(oracle, odd):
+    from oracle import xsum_ref as R
+    pay = (np.arange(150) * 37) % 1449
+    shm, fr, segs, sl = pktgen.tx_segments(150, payload=pay, tx_len=2000, nflows=9, odd=odd, seed=0x1234 + odd)
+    a, b = fr.copy(), fr.copy()
+    np.testing.assert_array_equal(oracle.tx_segment_batch(shm, sl, a, segs), R.tx_segment(shm, sl, b, segs))
+    np.testing.assert_array_equal(a, b)
+
+
+def test_oracle_txseg_matches_tcp4_path(oracle):
+    """After the build, the frames' checksums are what tcp_checksums gives the
+    finished frames (the fused op is copy-then-checksum)."""
+    shm, fr, segs, sl = pktgen.tx_segments(64, tx_len=3000, nflows=4)
+    out = oracle.tx_segment_batch(shm, sl, fr, segs)
+    again = oracle.tcp4_batch(fr.copy(), 64, stride=pktgen.MBUF_ROOM)
+    np.testing.assert_array_equal(out, again.view(np.uint32))
+
+
+def test_generator_wraps_and_flows():
+    shm, fr, segs, sl = pktgen.tx_segments(4096, tx_len=16384, nflows=512)
+    wraps = (segs["pos"].astype(np.int64) + segs["payload"]) > segs["tx_len"]
+    assert 0 < wraps.sum() < 4096 // 4
+    assert (segs["pos"] < segs["tx_len"]).all()
+    assert segs.dtype.itemsize == 32 and sl == len(shm)
+
+
+# ---------------------------------------------------------------------------
+# GPU parity
+
+def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
+    import torch
+    from tas_amd import xsum
+    dev = "cuda:0"
+    dshm = torch.from_numpy(np.ascontiguousarray(shm)).to(dev)
+    fr = np.ascontiguousarray(frames)
+    dfr = torch.zeros(fr.size + frame_shift + 16, dtype=torch.uint8, device=dev)
+    dfr[frame_shift:frame_shift + fr.size] = torch.from_numpy(fr).to(dev)
+    s = segs.copy()
+    s["frame_off"] += np.uint64(frame_shift)
+    dsegs = torch.from_numpy(s.view(np.uint8).copy()).to(dev)
+    out = xsum.tx_segment_batch(dshm[:shm_len], dfr, dsegs, len(s), ip_off=ip_off, l4_off=l4_off)
+    torch.cuda.synchronize()
+    got = dfr.cpu().numpy()
+    assert not got[:frame_shift].any() and not got[frame_shift + fr.size:].any(), "wrote outside the frames"
+    return out.cpu().numpy().view(np.uint32), got[frame_shift:frame_shift + fr.size]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 2, 7])
+def test_gpu_txseg_golden(txseg_golden, shift):
+    g = txseg_golden
+    out, fr = _gpu_run(g["shm"], int(g["shm_len"]), g["frames_in"], _segs(g), frame_shift=shift)
+    np.testing.assert_array_equal(out, g["expected"])
+    np.testing.assert_array_equal(fr, g["frames_out"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("odd,tx_len,nflows", [(False, 16384, 512), (True, 16384, 512), (True, 1500, 7),
+                                               (False, 1448, 3)])
+def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows):
+    n = 4096
+    pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 131) % 1449, pktgen.TCP_MSS)
+    pay = np.minimum(pay, tx_len - (7 if odd else 0))
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=tx_len, nflows=nflows, odd=odd,
+                                           seed=0xC0FFEE + tx_len)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(got, exp_fr)
+
+
+@pytest.mark.gpu
+def test_gpu_txseg_packed_odd_frames(oracle):
+    """Frames packed back to back at an odd stride (chunks shared between
+    neighbours): the build must not clobber a neighbour's bytes."""
+    n, stride = 1024, 1515
+    pay = (np.arange(n) * 7) % 1449
+    shm, fr0, segs, sl = pktgen.tx_segments(n, payload=pay, stride=2048, tx_len=3001, nflows=13, odd=True)
+    fr = np.zeros(n * stride + 1, np.uint8)
+    for i in range(n):  # repack to the odd stride, trailing bytes random
+        fr[i * stride:(i + 1) * stride] = fr0[i * 2048:i * 2048 + stride]
+    segs["frame_off"] = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=3)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(got, exp_fr)
+
+
+@pytest.mark.gpu
+def test_gpu_txseg_tso(oracle):
+    """64 KB segments: payload 65483 (ip.len 65535), wrap inside."""
+    n, pay = 64, 65535 - 52
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, stride=65536 + 64, tx_len=98304 + 5, nflows=8,
+                                           odd=True)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(got, exp_fr)
+
+
+@pytest.mark.gpu
+def test_gpu_txseg_other_layouts(oracle):
+    """Staged-record layout (ip_off 0, l4_off 20) and a gap between IP and TCP."""
+    for ip_off, l4_off in ((0, 20), (14, 40)):
+        n = 512
+        shm, fr, segs, sl = pktgen.tx_segments(n, tx_len=5000, nflows=11, odd=True, seed=ip_off + l4_off)
+        segs["hdrs_len"] = l4_off + 32
+        fr = fr.reshape(n, -1)
+        # rebuild each header at the layout: ip header copied to ip_off, ip.len for this hdrs_len
+        hdr = fr[:, 14:34].copy()
+        fr[:, ip_off:ip_off + 20] = hdr
+        tl = segs["hdrs_len"].astype(np.int64) - ip_off + segs["payload"]
+        fr[:, ip_off + 2] = (tl >> 8) & 0xFF
+        fr[:, ip_off + 3] = tl & 0xFF
+        fr = fr.reshape(-1)
+        exp_fr = fr.copy()
+        exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs, ip_off=ip_off, l4_off=l4_off)
+        out, got = _gpu_run(shm, sl, fr, segs, ip_off=ip_off, l4_off=l4_off)
+        np.testing.assert_array_equal(out, exp)
+        np.testing.assert_array_equal(got, exp_fr)
+
+
+@pytest.mark.gpu
+def test_gpu_txseg_errors():
+    import torch
+    from tas_amd import xsum
+    dev = "cuda:0"
+    shm = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    fr = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    segs = torch.zeros(64, dtype=torch.uint8, device=dev)
+    with pytest.raises(xsum.TasxError):
+        xsum.tx_segment_batch(shm, fr, segs, 1, ip_off=14, l4_off=30)   # l4 inside the IP header
+    with pytest.raises(xsum.TasxError):
+        xsum.tx_segment_batch(shm, fr, segs[8:], 1)                      # misaligned descriptors
+    assert xsum.tx_segment_batch(shm, fr, segs, 0).numel() == 0
