@@ -68,6 +68,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-raw", action="store_true")
+    ap.add_argument("--no-txseg", action="store_true")
     ap.add_argument("--pmc", action="store_true", help="collect HBM traffic via rocprofv3 child runs")
     ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -230,6 +231,68 @@ class RawWorkload:
             if rc:
                 raise xsum.TasxError(rc, "tasx_raw_cksum_batch_dev")
         return launch
+
+
+class TxSegWorkload:
+    """Fused TX segment build: per segment, the
+    payload read from the flow's circular TX buffer in shm, written into the
+    frame, and both checksums stored (flow_tx_read + tcp_checksums,
+    tas/fast/fast_flows.c:930-936).  Headers are pre-filled; shm and frames are
+    device-resident.  Algorithmic bytes per segment: payload read + payload
+    written + the 20 B IP header and hdrs_len - l4_off L4 header bytes read +
+    4 B of checksums written."""
+    desc = (f"{N_FRAMES} TAS TX segments of {pktgen.TCP_MSS} B payload from 8192 flows' 16 KiB circular TX "
+            f"buffers (wraps included) into 1514 B frames at {STRIDE} B stride, checksums in place")
+
+    def __init__(self, rotate: int, seed: int, n: int = N_FRAMES):
+        self.n = n
+        _, _, segs, shm_len = pktgen.tx_segments(n, seed=seed, nflows=8192, tx_len=16384, make_shm=False)
+        self.segs_np, self.shm_len = segs, shm_len
+        self.segs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
+        self.shms = [device_random(shm_len, seed + 7 + r) for r in range(rotate)]
+        first = device_tcp4_frames(n, STRIDE, IP_TOTAL, seed)
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.outs = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(rotate)]
+        hdr = pktgen.HDRS_LEN - pktgen.ETH_LEN - pktgen.IP_LEN
+        self.bytes_per_seg = 2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4
+        self.bytes_per_step = n * self.bytes_per_seg
+
+    def launcher(self):
+        fn = xsum.lib().tasx_tx_segment_batch_dev
+        stream = torch.cuda.current_stream().cuda_stream
+        args = [(sh.data_ptr(), self.shm_len, b.data_ptr(), self.segs.data_ptr(), self.n, pktgen.ETH_LEN,
+                 pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), stream)
+                for sh, b, o in zip(self.shms, self.bufs, self.outs)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_tx_segment_batch_dev")
+        return launch
+
+    def cpu_check(self, budget_s: float) -> dict:
+        """The oracle's copy + tcp_checksums per segment on this box's cores, on
+        rotation 0's inputs, and a bit-exact comparison of the built frames."""
+        from oracle import oracle_lib
+        orc = oracle_lib.Oracle()
+        torch.cuda.synchronize()
+        shm = self.shms[0].cpu().numpy()
+        gpu_frames = self.bufs[0].cpu().numpy()
+        frames = gpu_frames.copy()
+        # un-build: the oracle must produce the built frames from scratch
+        f2 = frames.reshape(self.n, STRIDE)
+        f2[:, pktgen.HDRS_LEN:FRAME_LEN] ^= 0x5A
+        f2[:, 24:26] = 0
+        f2[:, 50:52] = 0
+        threads = min(16, len(os.sched_getaffinity(0)))
+        t = orc.bench_tx_segment(shm, self.shm_len, frames, self.segs_np, threads=threads, reps=1)
+        reps = max(3, min(500, int(budget_s / max(t, 1e-6))))
+        t = orc.bench_tx_segment(shm, self.shm_len, frames, self.segs_np, threads=threads, reps=reps)
+        return {"value": self.bytes_per_step / t / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
+                "sample": f"rotation 0's {self.n} segments, oracle flow_tx_read + tcp_checksums per segment, "
+                          f"median of {reps} passes",
+                "parity_vs_gpu": "bit-exact" if np.array_equal(frames, gpu_frames) else "MISMATCH"}
 
 
 def prewarm(launch, seconds: float = 0.25):
@@ -512,6 +575,18 @@ def main():
         del rw
         torch.cuda.empty_cache()
 
+    txseg = None
+    if not args.no_txseg:
+        del wl.bufs[1:], wl.outs[1:]
+        torch.cuda.empty_cache()
+        tw = TxSegWorkload(rot, pktgen.SEED + 2000 + rank)
+        txseg = leg(tw, args, ws, TxSegWorkload.desc)
+        txseg["algorithmic_bytes_per_segment"] = tw.bytes_per_seg
+        if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+            txseg["cpu_baseline"] = tw.cpu_check(3.0)
+        del tw
+        torch.cuda.empty_cache()
+
     extra = {}
     if rank == 0 and ws == 1:
         torch.cuda.synchronize()
@@ -549,6 +624,8 @@ def main():
         }
         if raw is not None:
             line["raw"] = raw
+        if txseg is not None:
+            line["tx_segment"] = txseg
         if "e2e" in extra:
             line["e2e"] = extra["e2e"]
         if "pmc" in extra:

@@ -189,6 +189,14 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   p.n = n;
   p.ip_off = ip_off;
   p.l4_off = l4_off;
+  {
+    static int dbg = -1;
+    if (dbg < 0) {
+      const char *e = getenv("TASX_TXSEG_DEBUG");
+      dbg = e ? atoi(e) : 0;
+    }
+    p.dbg = (uint32_t) dbg;
+  }
   if (tasx_launch_txseg(&p, stream) != 0)
     return hip_err(hipGetLastError(), "tx segment kernel launch");
   return 0;

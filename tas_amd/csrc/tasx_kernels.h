@@ -46,6 +46,7 @@ typedef struct tasx_txseg_params {
   uint32_t n;
   uint32_t ip_off;
   uint32_t l4_off;
+  uint32_t dbg;            /* diagnostics: TASX_TXSEG_DEBUG (0 = product) */
 } tasx_txseg_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */

@@ -61,26 +61,67 @@ __device__ __forceinline__ u32x4 clear_byte(u32x4 v, int b)
                j == 3 ? v.w & m : v.w};
 }
 
-// store bytes [lo, hi) of v into the 16-byte aligned chunk at cp
-__device__ __forceinline__ void store_range(uint8_t *cp, u32x4 v, int lo, int hi)
+// byte b of v set to x (no-op unless 0 <= b < 16)
+__device__ __forceinline__ u32x4 put_byte(u32x4 v, int b, uint32_t x)
 {
+  const uint32_t sh = 8u * (uint32_t) (b & 3), m = ~(0xffu << sh), y = (x & 0xffu) << sh;
+  const int j = b >> 2;
+  return u32x4{j == 0 ? (v.x & m) | y : v.x, j == 1 ? (v.y & m) | y : v.y, j == 2 ? (v.z & m) | y : v.z,
+               j == 3 ? (v.w & m) | y : v.w};
+}
+
+// store bytes [lo, hi) of v into the 16-byte aligned chunk at cp: whole
+// dwords as dword stores, the rest as byte stores (constant offsets from one
+// address)
+__device__ __forceinline__ void store_range(uint8_t *cp, u32x4 v, int lo, int hi, bool nt = true)
+{
+  if (lo >= hi)
+    return;
   if (lo == 0 && hi == 16) {
-    __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
+    if (nt)
+      __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
+    else
+      *(__attribute__((address_space(1))) u32x4 *) cp = v;
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int l = min(max(lo - 4 * j, 0), 4), h = min(max(hi - 4 * j, 0), 4);
-    if (l == 0 && h == 4)
+    if (lo <= 4 * j && 4 * j + 4 <= hi) {
       stg((uint32_t *) cp, (uint32_t) j, w[j]);
-    else
-      for (int b = l; b < h; ++b)
-        st8(cp + 4 * j + b, w[j] >> (8 * b));
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * j + q >= lo && 4 * j + q < hi)
+          st8(cp + 4 * j + q, w[j] >> (8 * q));
+    }
   }
 }
 
-template <int U>
+// The aligned chunk pair whose funnel gives the 16-byte window starting at
+// byte address S, of which bytes [lo, hi) (0 <= lo < hi <= 16) are wanted:
+// each chunk holds at least one wanted byte, so neither load can fault.
+__device__ __forceinline__ void window_pair(uintptr_t S, int lo, int hi, const u32x4 *&pa, const u32x4 *&pb)
+{
+  const uintptr_t a = (S + (uintptr_t) lo) & ~(uintptr_t) 15;
+  const uintptr_t b1 = (S & ~(uintptr_t) 15) + 16, b2 = (S + (uintptr_t) hi - 1) & ~(uintptr_t) 15;
+  pa = (const u32x4 *) a;
+  pb = (const u32x4 *) (b1 < b2 ? b1 : b2);
+}
+
+// One 16-lane group per segment.  l4-relative coordinates (l4 = frame +
+// l4_off): payload D = [dlo, dhi), summed bytes [0, send); chunk c covers
+// [16c - head, +16).  The header chunks (the frame's bytes [0, hdrs_len)) are
+// read by lane k and written back whole at the end with both checksums
+// inserted -- the frame's first cache lines are then written in full, which
+// avoids the HBM read-modify-write of a partly written line.  Payload chunks
+// [cp0, nend) go to lane (c - cp0) % 16, slot (c - cp0) / 16.  A chunk holding
+// both (the first payload chunk) is summed and stored in two parts.  All
+// loads of a round are issued before any is consumed, so a segment costs one
+// memory latency after its descriptor (plus one per extra 96-chunk round).
+// MODE (diagnostics, TASX_TXSEG_DEBUG): bit 0 = no full-chunk payload stores,
+// bit 1 = temporal instead of non-temporal stores.
+template <int U, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -99,88 +140,124 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
       stg(p.out, i, 0u);
     return;
   }
-  uint8_t *f = p.frames + frame_off;
-  uint8_t *ip = f + p.ip_off;
-  uint8_t *l4 = f + p.l4_off;
-  const uint8_t *src = p.shm + tx_base; // the flow's TX buffer
-  // header words (bytes never written by this kernel before the final stores)
-  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
-  uint32_t w = 0;
-  if (gl < 10)
-    w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
-  // l4-relative coordinates: payload D = [dlo, dhi), checksummed S = [0, slen)
+  uint8_t *const f = p.frames + frame_off;
+  uint8_t *const ip = f + p.ip_off;
+  uint8_t *const l4 = f + p.l4_off;
   const int dlo = (int) (hl - p.l4_off), dhi = dlo + (int) pay;
-  const Chunks<U> r = chunk_range<U>(l4, (uint32_t) dhi);
-  const int wrap = (int) (tx_len - pos); // payload index of the buffer wrap
-  const uintptr_t s1 = (uintptr_t) src + pos;      // payload byte j at s1 + j (j < wrap)
-  const uintptr_t s2 = (uintptr_t) src - wrap;     // ... or at s2 + j (j >= wrap)
-  const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  const int send = min((int) len, dhi); // main pass sums [0, send)
-  const int p16 = r.head + 16;          // chunk position of tcp.chksum
+  const int head = (int) ((uintptr_t) l4 & 15);
+  const u32x4 *const c0p = (const u32x4 *) ((uintptr_t) l4 & ~(uintptr_t) 15);
+  const uint32_t cp0 = (uint32_t) ((head + dlo) >> 4);                 // first payload chunk
+  const uint32_t nend = pay ? (uint32_t) ((head + dhi + 15) >> 4) : cp0; // payload chunks [cp0, nend)
+  const int wrap = (int) (tx_len - pos);           // payload index where the buffer wraps
+  const uintptr_t s1 = (uintptr_t) p.shm + tx_base + pos; // payload byte j at s1 + j (j < wrap)
+  const uintptr_t s2 = s1 - tx_len;                       // ... or at s2 + j (j >= wrap)
+  // the chunk holding payload bytes from both sides of the wrap, if any
+  const int pw = dlo + wrap;
+  const uint32_t cs = (wrap < (int) pay && ((head + pw) & 15)) ? (uint32_t) ((head + pw) >> 4) : 0xffffffffu;
 
+  // ---- loads, all unconditional (clamped to valid addresses) so that none is
+  // sunk into a branch: header bytes, header chunks, the straddle chunk's
+  // second piece
+  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  const int wl = min(gl, 9);
+  const uint32_t w_ = ld8(ip + 2 * wl) | (ld8(ip + 2 * wl + 1) << 8);
+  const uint32_t w = gl < 10 ? w_ : 0u;
+  // header chunks: the frame's bytes [0, hl), written back whole at the end
+  // with the checksums inserted (the frame's first cache lines are then
+  // written in full)
+  const int fh = (int) ((uintptr_t) f & 15);
+  const u32x4 *const f0p = (const u32x4 *) ((uintptr_t) f & ~(uintptr_t) 15);
+  const uint32_t nhc = (uint32_t) ((fh + (int) hl + 15) >> 4);
+  u32x4 hv = ld16nt(f0p, min((uint32_t) gl, nhc - 1));
+  const bool own_cs = cs != 0xffffffffu && ((cs - cp0) & 15u) == (uint32_t) gl;
+  const u32x4 *xpa = f0p, *xpb = f0p;
+  {
+    const int o = 16 * (int) cs - head, j0 = o - dlo;
+    const u32x4 *pa, *pb;
+    window_pair(s2 + (intptr_t) j0, wrap - j0, min(dhi - o, 16), pa, pb);
+    xpa = own_cs ? pa : xpa;
+    xpb = own_cs ? pb : xpb;
+  }
+  const u32x4 xa = ld16nt(xpa, 0), xb = ld16nt(xpb, 0);
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const int send = min((int) len, dhi);
+
+  // ---- payload chunks: gather, store, sum
   uint64_t acc = 0;
-  for (uint32_t c = (uint32_t) gl; c < r.nch; c += 16u * U) {
-    u32x4 fa[U], sa[U], sb[U];
-    // issue every load of this round first
+  u32x4 vfirst = u32x4{0, 0, 0, 0}, vlast = vfirst;
+  for (uint32_t base = cp0; base < nend; base += 16u * U) {
+    u32x4 a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t cc = c + 16u * u;
-      const int o = 16 * (int) cc - r.head; // l4-relative offset of chunk byte 0
-      const int blo = min(max(dlo - o, 0), 16), bhi = min(max(dhi - o, 0), 16);
-      fa[u] = sa[u] = sb[u] = u32x4{0, 0, 0, 0};
-      if (cc < r.nch && o < dlo)
-        fa[u] = ld16nt(r.c0p, cc);
-      if (cc < r.nch && blo < bhi) {
-        const int j0 = o - dlo;
-        const bool p2 = j0 + blo >= wrap;
-        const uintptr_t S = (p2 ? s2 : s1) + (intptr_t) j0;
-        const uintptr_t ca = S & ~(uintptr_t) 15;
-        // a window straddling the buffer end is byte-gathered below; its
-        // chunk loads stay inside the first piece
-        const int bh = (!p2 && j0 + bhi > wrap) ? wrap - j0 : bhi;
-        const uintptr_t lo_c = (S + blo) & ~(uintptr_t) 15, hi_c = (S + bh - 1) & ~(uintptr_t) 15;
-        sa[u] = ld16nt((const u32x4 *) lo_c, 0);
-        sb[u] = ld16nt((const u32x4 *) (ca + 16 < hi_c ? ca + 16 : hi_c), 0);
-      }
+    for (int u = 0; u < U; ++u) { // clamped: lanes past the end re-read the last chunk
+      const uint32_t cc = min(base + (uint32_t) gl + 16u * u, nend - 1);
+      const int o = 16 * (int) cc - head, j0 = o - dlo;
+      const int blo = max(-j0, 0), bhi = min(dhi - o, 16);
+      const bool p2 = j0 + blo >= wrap;
+      const int hi = p2 ? bhi : min(bhi, wrap - j0); // wanted bytes in this piece
+      const u32x4 *pa, *pb;
+      window_pair((p2 ? s2 : s1) + (intptr_t) j0, blo, hi, pa, pb);
+      a[u] = ld16nt(pa, 0);
+      b[u] = ld16nt(pb, 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t cc = c + 16u * u;
-      if (cc >= r.nch)
-        continue;
-      const int o = 16 * (int) cc - r.head;
-      const int blo = min(max(dlo - o, 0), 16), bhi = min(max(dhi - o, 0), 16);
-      u32x4 val = fa[u];
-      if (blo < bhi) {
-        const int j0 = o - dlo;
-        u32x4 g;
-        if (j0 + blo < wrap && j0 + bhi > wrap) {
-          // the window straddles the end of the circular buffer: byte gather
-          uint32_t gw[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (int b = 0; b < 16; ++b) {
-            const int j = j0 + b;
-            if (b >= blo && b < bhi)
-              gw[b >> 2] |= ld8((const uint8_t *) ((j < wrap ? s1 : s2) + (intptr_t) j)) << (8 * (b & 3));
-          }
-          g = u32x4{gw[0], gw[1], gw[2], gw[3]};
-        } else {
-          const uintptr_t S = ((j0 + blo >= wrap) ? s2 : s1) + (intptr_t) j0;
-          g = funnel16(sa[u], sb[u], (int) (S & 15));
-        }
-        store_range((uint8_t *) (r.c0p + cc), g, blo, bhi);
-        val = merge_at(val, g, blo);
+      const uint32_t c = base + (uint32_t) gl + 16u * u;
+      const bool valid = c < nend;
+      const uint32_t cc = valid ? c : nend - 1;
+      const int o = 16 * (int) cc - head, j0 = o - dlo;
+      const int blo = max(-j0, 0), bhi = min(dhi - o, 16);
+      const bool p2 = j0 + blo >= wrap;
+      u32x4 v = funnel16(a[u], b[u], (int) (((p2 ? s2 : s1) + (intptr_t) j0) & 15));
+      if (cc == cs) // bytes from the wrap on come from the buffer start
+        v = merge_at(v, funnel16(xa, xb, (int) ((s2 + (intptr_t) j0) & 15)), wrap - j0);
+      uint8_t *const cp = (uint8_t *) (c0p + cc);
+      if (valid && blo == 0 && bhi == 16) {
+        if (MODE & 2)
+          *(__attribute__((address_space(1))) u32x4 *) cp = v;
+        else if (!(MODE & 1))
+          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
       }
-      // checksummed bytes of this chunk: [0, send), tcp.chksum taken as zero
-      const int lo = min(max(-o, 0), 16), hi = min(max(send - o, 0), 16);
-      if (lo > 0 || hi < 16)
-        val = mask_chunk(val, lo, hi);
-      if ((int) cc == (p16 >> 4))
-        val = clear_byte(val, p16 & 15);
-      if ((int) cc == ((p16 + 1) >> 4))
-        val = clear_byte(val, (p16 + 1) & 15);
-      acc += (uint64_t) val.x + val.y + val.z + val.w;
+      // the (at most two) partial payload chunks are stored after the loop
+      if (valid && cc == cp0)
+        vfirst = v;
+      if (valid && cc == nend - 1)
+        vlast = v;
+      const int sh = valid ? min(bhi, send - o) : blo; // summed: [blo, sh)
+      if (blo > 0 || sh < 16)
+        v = mask_chunk(v, blo, max(sh, blo));
+      acc += (uint64_t) v.x + v.y + v.z + v.w;
     }
+  }
+  if (nend > cp0) {
+    // partial first / last payload chunks (lanes 0 and (nend - 1 - cp0) % 16)
+    if (gl == 0) {
+      const int o = 16 * (int) cp0 - head;
+      store_range((uint8_t *) (c0p + cp0), vfirst, max(dlo - o, 0), min(dhi - o, 16));
+    }
+    if (((nend - 1 - cp0) & 15u) == (uint32_t) gl && nend - 1 > cp0) {
+      const int o = 16 * (int) (nend - 1) - head;
+      if (MODE & 4) { // diagnostic: pad the frame's last cache line (needs room)
+        uint8_t *e = (uint8_t *) (c0p + (nend - 1));
+        store_range(e, vlast, 0, 16);
+        for (e += 16; ((uintptr_t) e & 127) != 0; e += 16)
+          store_range(e, u32x4{0, 0, 0, 0}, 0, 16);
+      } else {
+        store_range((uint8_t *) (c0p + (nend - 1)), vlast, 0, min(dhi - o, 16));
+      }
+    }
+  }
+  // ---- header chunks: L4 bytes [0, min(dlo, send)) summed, tcp.chksum as zero
+  const int hend = min(dlo, send);
+  const int hbase = fh + (int) p.l4_off; // chunk k's byte b is l4 byte 16k + b - hbase
+  for (uint32_t k = (uint32_t) gl; k < nhc; k += 16u) {
+    u32x4 v = k < 16u ? hv : ld16nt(f0p, k); // > 16 header chunks: rare, loaded here
+    const int o = 16 * (int) k - hbase;
+    v = mask_chunk(v, min(max(-o, 0), 16), min(max(hend - o, 0), 16));
+    if (16 - o >= 0 && 16 - o < 16)
+      v = clear_byte(v, 16 - o);
+    if (17 - o >= 0 && 17 - o < 16)
+      v = clear_byte(v, 17 - o);
+    acc += (uint64_t) v.x + v.y + v.z + v.w;
   }
   uint32_t part = fold64_to_18(acc);
   if ((int) len > dhi) { // total_length reaches past the payload: frame bytes
@@ -191,21 +268,28 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   const uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
   part = row_sum16(part);
   const uint32_t s_ip = row_sum16(c_ip), s_ph = row_sum16(c_ph);
-  if (gl == 15) {
-    const uint32_t ipc = inv_result(residue(fold32_to_16(s_ip)));
-    uint32_t tcpc = 0;
-    if (tl >= 20) {
-      uint32_t r4 = fold32_to_16(part);
-      if (r.head & 1)
-        r4 = bswap16(r4);
-      tcpc = inv_result(residue(fold32_to_16(r4 + s_ph + bswap16(len))));
-    }
-    st8(ip + 10, ipc);
-    st8(ip + 11, ipc >> 8);
-    st8(l4 + 16, tcpc);
-    st8(l4 + 17, tcpc >> 8);
-    if (p.out)
-      stg(p.out, i, ipc | (tcpc << 16));
+  // results, valid in lane 15 of the group, then broadcast to the group
+  const uint32_t ipc = inv_result(residue(fold32_to_16(s_ip)));
+  uint32_t tcpc = 0;
+  if (tl >= 20) {
+    uint32_t r4 = fold32_to_16(part);
+    if (head & 1)
+      r4 = bswap16(r4);
+    tcpc = inv_result(residue(fold32_to_16(r4 + s_ph + bswap16(len))));
+  }
+  const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
+  if (gl == 15 && p.out)
+    stg(p.out, i, res);
+  // header write-back: bytes [0, hl) of the frame, checksum fields inserted
+  const int fi = (int) p.ip_off + 10 + fh, ft = (int) p.l4_off + 16 + fh; // chunk-grid positions
+  for (uint32_t k = (uint32_t) gl; k < nhc; k += 16u) {
+    u32x4 v = k < 16u ? hv : ld16nt(f0p, k);
+    const int b0 = 16 * (int) k;
+    v = put_byte(v, fi - b0, res);
+    v = put_byte(v, fi + 1 - b0, res >> 8);
+    v = put_byte(v, ft - b0, res >> 16);
+    v = put_byte(v, ft + 1 - b0, res >> 24);
+    store_range((uint8_t *) (f0p + k), v, max(fh - b0, 0), min(fh + (int) hl - b0, 16), false);
   }
 }
 
@@ -217,7 +301,17 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   const uint64_t blocks = ((uint64_t) p->n + spb - 1) / spb;
   if (blocks == 0)
     return 0;
-  hipLaunchKernelGGL(tx_segment_kernel<6>, dim3((uint32_t) blocks), dim3(kBlock), 0,
-                     (hipStream_t) stream, *p);
+  const dim3 grid((uint32_t) blocks), block(kBlock);
+  hipStream_t s = (hipStream_t) stream;
+  switch (p->dbg) {
+  case 1: hipLaunchKernelGGL((tx_segment_kernel<3, 1>), grid, block, 0, s, *p); break;
+  case 2: hipLaunchKernelGGL((tx_segment_kernel<3, 2>), grid, block, 0, s, *p); break;
+  case 3: hipLaunchKernelGGL((tx_segment_kernel<2, 0>), grid, block, 0, s, *p); break;
+  case 4: hipLaunchKernelGGL((tx_segment_kernel<4, 0>), grid, block, 0, s, *p); break;
+  case 5: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;
+  case 6: hipLaunchKernelGGL((tx_segment_kernel<1, 0>), grid, block, 0, s, *p); break;
+  case 7: hipLaunchKernelGGL((tx_segment_kernel<6, 4>), grid, block, 0, s, *p); break;
+  default: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
