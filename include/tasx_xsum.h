@@ -135,8 +135,11 @@ typedef struct tasx_tx_seg {
  * (pos >= tx_len with payload > 0, payload > tx_len, tx_base + tx_len >
  * shm_len) or with hdrs_len < l4_off + 20 leaves its frame untouched and gets
  * out[i] = 0, which no valid segment produces (ip.chksum is never 0).
- * shm, frames, segs and out are device (or device-mapped host) pointers.
- * Frames must not overlap.  Asynchronous on `stream`. */
+ * shm, frames, segs and out are device (or device-mapped host) pointers;
+ * shm_len < 4 GiB (TAS's shared region is far smaller); l4_off >= ip_off + 20.
+ * Frames must not overlap.  Besides the payload and the two checksum fields,
+ * the header bytes [0, hdrs_len) are rewritten with their own values (whole
+ * cache lines avoid HBM read-modify-write).  Asynchronous on `stream`. */
 int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
     const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint32_t *out, void *stream);

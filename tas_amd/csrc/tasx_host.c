@@ -180,6 +180,8 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
     return set_err(-EINVAL, "tx segment: segs must be 16-byte, out 4-byte aligned");
   if (l4_off < ip_off + 20 || l4_off > 0xffff)
     return set_err(-EINVAL, "tx segment: need ip_off + 20 <= l4_off <= 65535");
+  if (shm_len > 0xffffffffull)
+    return set_err(-EINVAL, "tx segment: shm_len must be below 4 GiB");
   memset(&p, 0, sizeof(p));
   p.shm = (const uint8_t *) shm;
   p.shm_len = shm_len;

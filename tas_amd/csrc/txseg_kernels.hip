@@ -46,6 +46,12 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, int s)
                __builtin_amdgcn_alignbyte(o[3], o[2], r), __builtin_amdgcn_alignbyte(o[4], o[3], r)};
 }
 
+// row_ror:15 -- lane k of each 16-lane row gets lane (k + 1) % 16's value
+__device__ __forceinline__ uint32_t ror15(uint32_t x)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x12f, 0xf, 0xf, false);
+}
+
 // bytes [0, k) from a, [k, 16) from b
 __device__ __forceinline__ u32x4 merge_at(u32x4 a, u32x4 b, int k)
 {
@@ -149,15 +155,39 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   const uint32_t cp0 = (uint32_t) ((head + dlo) >> 4);                 // first payload chunk
   const uint32_t nend = pay ? (uint32_t) ((head + dhi + 15) >> 4) : cp0; // payload chunks [cp0, nend)
   const int wrap = (int) (tx_len - pos);           // payload index where the buffer wraps
-  const uintptr_t s1 = (uintptr_t) p.shm + tx_base + pos; // payload byte j at s1 + j (j < wrap)
-  const uintptr_t s2 = s1 - tx_len;                       // ... or at s2 + j (j >= wrap)
-  // the chunk holding payload bytes from both sides of the wrap, if any
+  // Source offsets are 32-bit, relative to shm (shm_len < 4 GiB, checked by
+  // the host): payload piece 1 = indices [0, min(wrap, pay)) at s1 + j, piece 2
+  // = [wrap, pay) at s2 + j (modular u32 arithmetic; only valid j are used).
+  // Chunk c's window starts at payload index j0 = 16c - head - dlo, in the
+  // piece of its first payload byte; the lane owning c loads L_c, the aligned
+  // chunk holding that window start with j clamped into the piece (so it cannot
+  // fault), and takes the window's second chunk from the lane owning c + 1 (DPP
+  // row rotate): one source load per chunk.  Exceptions: the chunk ce at the
+  // piece switch (the straddle chunk cs, or the last piece-1 chunk when the
+  // wrap falls on a chunk boundary) loads its own second chunk (xb1); the
+  // straddle chunk's bytes past the wrap come from a piece-2 pair (xa2, xb2).
+  const uint8_t *const shm = p.shm;
+  const uint32_t s1 = (uint32_t) (tx_base + pos), s2 = s1 - tx_len;
+  const bool wraps = wrap < (int) pay;
+  const int end1 = min(wrap, (int) pay) - 1; // last piece-1 index
   const int pw = dlo + wrap;
-  const uint32_t cs = (wrap < (int) pay && ((head + pw) & 15)) ? (uint32_t) ((head + pw) >> 4) : 0xffffffffu;
+  const uint32_t kw = (uint32_t) ((head + pw) >> 4);
+  const bool straddle = wraps && ((head + pw) & 15);
+  const uint32_t cs = straddle ? kw : 0xffffffffu;
+  const uint32_t ce = wraps ? (straddle ? kw : kw - 1) : 0xffffffffu;
+  // chunk c: shm offset of L_c, and the window start's byte position (sh)
+  auto window = [&](uint32_t c, int &sh) -> uint32_t {
+    const int j0 = 16 * (int) c - head - dlo, blo = max(-j0, 0);
+    const bool p2 = wraps && j0 + blo >= wrap;
+    const uint32_t sb = p2 ? s2 : s1;
+    const int jc = min(max(j0, p2 ? wrap : 0), p2 ? (int) pay - 1 : end1);
+    sh = (int) ((sb + (uint32_t) j0) & 15u);
+    return (sb + (uint32_t) jc) & ~15u;
+  };
+  auto shm_chunk = [&](uint32_t off) -> u32x4 { return ld16nt((const u32x4 *) (shm + off), 0); };
 
   // ---- loads, all unconditional (clamped to valid addresses) so that none is
-  // sunk into a branch: header bytes, header chunks, the straddle chunk's
-  // second piece
+  // sunk into a branch: header bytes, header chunks, the exception chunks
   const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
   const int wl = min(gl, 9);
   const uint32_t w_ = ld8(ip + 2 * wl) | (ld8(ip + 2 * wl + 1) << 8);
@@ -169,16 +199,21 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   const u32x4 *const f0p = (const u32x4 *) ((uintptr_t) f & ~(uintptr_t) 15);
   const uint32_t nhc = (uint32_t) ((fh + (int) hl + 15) >> 4);
   u32x4 hv = ld16nt(f0p, min((uint32_t) gl, nhc - 1));
-  const bool own_cs = cs != 0xffffffffu && ((cs - cp0) & 15u) == (uint32_t) gl;
-  const u32x4 *xpa = f0p, *xpb = f0p;
+  const bool own_ce = ce != 0xffffffffu && ((ce - cp0) & 15u) == (uint32_t) gl;
+  uint32_t o1 = 0, oa = 0, ob = 0; // exception chunks (offset 0 on other lanes)
   {
-    const int o = 16 * (int) cs - head, j0 = o - dlo;
-    const u32x4 *pa, *pb;
-    window_pair(s2 + (intptr_t) j0, wrap - j0, min(dhi - o, 16), pa, pb);
-    xpa = own_cs ? pa : xpa;
-    xpb = own_cs ? pb : xpb;
+    const int j0 = 16 * (int) ce - head - dlo;
+    o1 = own_ce ? ((s1 + (uint32_t) min(j0 + 16, end1)) & ~15u) : 0u;
+    // straddle: piece-2 bytes [wrap - j0, bhi) of the window at s2 + j0,
+    // i.e. buffer indices [0, j0 + bhi - wrap): chunks of tx_base and of the
+    // window's second slot, clamped to the last wanted byte
+    const int bhi = min(dhi - (16 * (int) cs - head), 16);
+    const int64_t S = (int64_t) tx_base + (j0 - wrap);
+    const int64_t b1 = (S & ~(int64_t) 15) + 16, b2 = ((int64_t) tx_base + (j0 + bhi - wrap) - 1) & ~(int64_t) 15;
+    oa = (own_ce && straddle) ? (uint32_t) (tx_base & ~(uint64_t) 15) : 0u;
+    ob = (own_ce && straddle) ? (uint32_t) (b1 < b2 ? b1 : b2) : 0u;
   }
-  const u32x4 xa = ld16nt(xpa, 0), xb = ld16nt(xpb, 0);
+  const u32x4 xb1 = shm_chunk(o1), xa2 = shm_chunk(oa), xb2 = shm_chunk(ob);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const int send = min((int) len, dhi);
 
@@ -186,31 +221,30 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   uint64_t acc = 0;
   u32x4 vfirst = u32x4{0, 0, 0, 0}, vlast = vfirst;
   for (uint32_t base = cp0; base < nend; base += 16u * U) {
-    u32x4 a[U], b[U];
+    u32x4 a[U];
+    int sh;
 #pragma unroll
-    for (int u = 0; u < U; ++u) { // clamped: lanes past the end re-read the last chunk
-      const uint32_t cc = min(base + (uint32_t) gl + 16u * u, nend - 1);
-      const int o = 16 * (int) cc - head, j0 = o - dlo;
-      const int blo = max(-j0, 0), bhi = min(dhi - o, 16);
-      const bool p2 = j0 + blo >= wrap;
-      const int hi = p2 ? bhi : min(bhi, wrap - j0); // wanted bytes in this piece
-      const u32x4 *pa, *pb;
-      window_pair((p2 ? s2 : s1) + (intptr_t) j0, blo, hi, pa, pb);
-      a[u] = ld16nt(pa, 0);
-      b[u] = ld16nt(pb, 0);
-    }
+    for (int u = 0; u < U; ++u)
+      a[u] = shm_chunk(window(base + (uint32_t) gl + 16u * u, sh));
+    const u32x4 ext = shm_chunk(window(base + 16u * U, sh)); // lane 15's last neighbour
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = base + (uint32_t) gl + 16u * u;
       const bool valid = c < nend;
-      const uint32_t cc = valid ? c : nend - 1;
-      const int o = 16 * (int) cc - head, j0 = o - dlo;
+      const int o = 16 * (int) c - head, j0 = o - dlo;
       const int blo = max(-j0, 0), bhi = min(dhi - o, 16);
-      const bool p2 = j0 + blo >= wrap;
-      u32x4 v = funnel16(a[u], b[u], (int) (((p2 ? s2 : s1) + (intptr_t) j0) & 15));
-      if (cc == cs) // bytes from the wrap on come from the buffer start
-        v = merge_at(v, funnel16(xa, xb, (int) ((s2 + (intptr_t) j0) & 15)), wrap - j0);
-      uint8_t *const cp = (uint8_t *) (c0p + cc);
+      // second chunk: a[u] of lane (gl + 1) % 16 (lane 15: slot u + 1 of lane 0)
+      const u32x4 nx = (u + 1 < U) ? a[u + 1 < U ? u + 1 : u] : ext;
+      const u32x4 t0 = u32x4{ror15(a[u].x), ror15(a[u].y), ror15(a[u].z), ror15(a[u].w)};
+      const u32x4 t1 = u32x4{ror15(nx.x), ror15(nx.y), ror15(nx.z), ror15(nx.w)};
+      u32x4 bn = gl == 15 ? ((u + 1 < U) ? t1 : ext) : t0;
+      if (c == ce)
+        bn = xb1;
+      window(c, sh);
+      u32x4 v = funnel16(a[u], bn, sh);
+      if (c == cs) // bytes from the wrap on come from the buffer start
+        v = merge_at(v, funnel16(xa2, xb2, (int) ((s2 + (uint32_t) j0) & 15u)), wrap - j0);
+      uint8_t *const cp = (uint8_t *) (c0p + c);
       if (valid && blo == 0 && bhi == 16) {
         if (MODE & 2)
           *(__attribute__((address_space(1))) u32x4 *) cp = v;
@@ -218,9 +252,9 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
           __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
       }
       // the (at most two) partial payload chunks are stored after the loop
-      if (valid && cc == cp0)
+      if (valid && c == cp0)
         vfirst = v;
-      if (valid && cc == nend - 1)
+      if (valid && c == nend - 1)
         vlast = v;
       const int sh = valid ? min(bhi, send - o) : blo; // summed: [blo, sh)
       if (blo > 0 || sh < 16)
@@ -228,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
       acc += (uint64_t) v.x + v.y + v.z + v.w;
     }
   }
-  if (nend > cp0) {
+  if (!(MODE & 16) && nend > cp0) {
     // partial first / last payload chunks (lanes 0 and (nend - 1 - cp0) % 16)
     if (gl == 0) {
       const int o = 16 * (int) cp0 - head;
@@ -289,7 +323,8 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
     v = put_byte(v, fi + 1 - b0, res >> 8);
     v = put_byte(v, ft - b0, res >> 16);
     v = put_byte(v, ft + 1 - b0, res >> 24);
-    store_range((uint8_t *) (f0p + k), v, max(fh - b0, 0), min(fh + (int) hl - b0, 16), false);
+    if (!(MODE & 8))
+      store_range((uint8_t *) (f0p + k), v, max(fh - b0, 0), min(fh + (int) hl - b0, 16), false);
   }
 }
 
@@ -311,6 +346,9 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 5: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;
   case 6: hipLaunchKernelGGL((tx_segment_kernel<1, 0>), grid, block, 0, s, *p); break;
   case 7: hipLaunchKernelGGL((tx_segment_kernel<6, 4>), grid, block, 0, s, *p); break;
+  case 8: hipLaunchKernelGGL((tx_segment_kernel<3, 8>), grid, block, 0, s, *p); break;
+  case 9: hipLaunchKernelGGL((tx_segment_kernel<3, 16>), grid, block, 0, s, *p); break;
+  case 10: hipLaunchKernelGGL((tx_segment_kernel<3, 25>), grid, block, 0, s, *p); break;
   default: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
