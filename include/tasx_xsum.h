@@ -144,6 +144,34 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
     const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint32_t *out, void *stream);
 
+/* RX flow lookup: the batch hash-table lookup
+ * of fast_flows_packet_fss() (tas/fast/fast_flows.c:1084-1163).  For frame i
+ * (ip = frame + ip_off, tcp = frame + l4_off) the key is (local = ip.dest /
+ * tcp.dest, remote = ip.src / tcp.src) and its hash flow_hash()
+ * (:1078-1082): CRC32C (Castagnoli, SSE4.2 crc32 semantics: no pre/post
+ * inversion) with initial value 0 over the 12 bytes ip.dest, ip.src,
+ * tcp.dest, tcp.src in packet order.  Up to TASX_FLOWHT_NBSZ entries
+ * flowht[(h + j) % ht_entries] are probed in order; an entry matches when it
+ * is valid, its flow_hash equals h, and the 4-tuple stored in the flow state
+ * of its flow id (low 29 bits) equals the key.  fid_out[i] = that flow id, or
+ * TASX_FLOW_NONE (fss[i] = NULL in the reference).  hash_out (optional) gets
+ * h.  Layouts are TAS's: flowht = struct flextcp_pl_flowhte {u32 flow_id, u32
+ * flow_hash}[ht_entries] (include/tas_memif.h:320-327); flow state i at flowst
+ * + i * fs_stride holds local_ip, remote_ip (network order), local_port,
+ * remote_port at fs_key_off (struct flextcp_pl_flowst: stride 128, offset 32,
+ * tas_memif.h:231-252).  A flow id >= fs_num never matches (the reference
+ * would read past the array).  fs_stride and fs_key_off are multiples of 4;
+ * flowht is 8-byte and flowst 4-byte aligned.  Asynchronous on `stream`. */
+#define TASX_FLOWHT_NBSZ 4u          /* FLEXNIC_PL_FLOWHT_NBSZ */
+#define TASX_FLOWHTE_VALID 0x80000000u /* FLEXNIC_PL_FLOWHTE_VALID */
+#define TASX_FLOWHTE_POSSHIFT 29     /* FLEXNIC_PL_FLOWHTE_POSSHIFT */
+#define TASX_FLOW_NONE 0xffffffffu
+int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    const void *flowht, uint32_t ht_entries, const void *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* Per-fast-path-core contexts (one per dataplane_context, no shared state,
  * no locks: tas/fast/fastemu.c:87-91).  A context owns a GPU, streams, pinned

@@ -53,6 +53,16 @@ class Oracle:
             "oracle_bench_tx_segment": (ctypes.c_double, [_u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_size_t,
                                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                                           ctypes.c_int]),
+            "oracle_crc32c_u32": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
+            "oracle_crc32c_u64": (ctypes.c_uint32, [ctypes.c_uint64, ctypes.c_uint32]),
+            "oracle_flow_hash": (ctypes.c_uint32, [_u8p, _u8p]),
+            "oracle_flow_lookup_batch": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
+                                                ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p]),
+            "oracle_bench_flow_lookup": (ctypes.c_double, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t,
+                                                           ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32,
+                                                           _u8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                           _u8p, ctypes.c_int, ctypes.c_int]),
             "oracle_bench": (ctypes.c_double, [ctypes.c_int, _u8p, _u8p, _u8p, ctypes.c_uint64, ctypes.c_uint32,
                                                ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_int, ctypes.c_int]),
         }
@@ -139,6 +149,30 @@ class Oracle:
                          ip_off: int = 14, l4_off: int = 34, threads: int = 1, reps: int = 5) -> float:
         return self.L.oracle_bench_tx_segment(shm.ctypes.data, shm_len, frames.ctypes.data, segs.ctypes.data,
                                               len(segs), ip_off, l4_off, threads, reps)
+
+    def flow_lookup_batch(self, buf: np.ndarray, n: int, flowht: np.ndarray, flowst: np.ndarray, *,
+                          fs_num: int, offsets=None, stride: int = 0, ip_off: int = 14, l4_off: int = 34,
+                          fs_stride: int = 128, fs_key_off: int = 32):
+        """Returns (hashes u32, flow ids u32; 0xffffffff = no flow)."""
+        ht = np.ascontiguousarray(flowht, np.uint32)
+        fs = np.ascontiguousarray(flowst, np.uint8)
+        h = np.empty(n, np.uint32)
+        fid = np.empty(n, np.uint32)
+        o = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
+        self.L.oracle_flow_lookup_batch(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n, ip_off,
+                                        l4_off, ht.ctypes.data, ht.size // 2, fs.ctypes.data, fs_num, fs_stride,
+                                        fs_key_off, h.ctypes.data, fid.ctypes.data)
+        return h, fid
+
+    def bench_flow_lookup(self, buf: np.ndarray, n: int, flowht: np.ndarray, flowst: np.ndarray, *, fs_num: int,
+                          stride: int, ip_off: int = 14, l4_off: int = 34, fs_stride: int = 128,
+                          fs_key_off: int = 32, threads: int = 1, reps: int = 5) -> float:
+        ht = np.ascontiguousarray(flowht, np.uint32)
+        fs = np.ascontiguousarray(flowst, np.uint8)
+        fid = np.empty(n, np.uint32)
+        return self.L.oracle_bench_flow_lookup(buf.ctypes.data, None, stride, n, ip_off, l4_off, ht.ctypes.data,
+                                               ht.size // 2, fs.ctypes.data, fs_num, fs_stride, fs_key_off,
+                                               fid.ctypes.data, threads, reps)
 
     def bench(self, mode: int, buf: np.ndarray, n: int, *, offsets=None, lengths=None, stride=0,
               len0=0, ip_off=14, l4_off=34, threads=1, reps=5) -> float:

@@ -279,6 +279,102 @@ void oracle_tx_segment_batch(const uint8_t *shm, uint64_t shm_len,
 }
 
 /* ---------------------------------------------------------------------- */
+/* RX flow lookup. */
+
+/* CRC32C (Castagnoli, reflected polynomial 0x82F63B78) as the SSE4.2 crc32
+ * instruction computes it: no pre/post inversion, the data operand consumed
+ * least-significant byte first.  DPDK's crc32c_sse42_u32 / _u64
+ * (rte_hash_crc.h, third-party, not vendored) wrap exactly that instruction;
+ * TAS's flow_hash() (tas/fast/fast_flows.c:1078-1082) and the slow path's
+ * rte_hash_crc() over the same 12 bytes (tas/slow/nicif.c:588-600) agree. */
+static uint32_t crc_table[256];
+static int crc_table_ready;
+
+static void crc_init(void)
+{
+  uint32_t i, k, c;
+  for (i = 0; i < 256; i++) {
+    c = i;
+    for (k = 0; k < 8; k++)
+      c = (c & 1) ? (c >> 1) ^ 0x82f63b78u : c >> 1;
+    crc_table[i] = c;
+  }
+  crc_table_ready = 1;
+}
+
+static uint32_t crc_bytes(uint32_t crc, uint64_t data, int nbytes)
+{
+  int b;
+  if (!crc_table_ready)
+    crc_init();
+  for (b = 0; b < nbytes; b++)
+    crc = crc_table[(crc ^ (uint32_t) (data >> (8 * b))) & 0xff] ^ (crc >> 8);
+  return crc;
+}
+
+uint32_t oracle_crc32c_u32(uint32_t data, uint32_t init)
+{
+  return crc_bytes(init, data, 4);
+}
+
+uint32_t oracle_crc32c_u64(uint64_t data, uint32_t init)
+{
+  return crc_bytes(init, data, 8);
+}
+
+/* flow_hash() of the key fast_flows_packet_fss() builds from a received
+ * frame (:1097-1101): local = destination, remote = source. */
+uint32_t oracle_flow_hash(const void *ip_hdr, const void *l4_hdr)
+{
+  const uint8_t *ip = (const uint8_t *) ip_hdr, *l4 = (const uint8_t *) l4_hdr;
+  uint32_t lip, rip;
+  uint16_t lp, rp;
+  memcpy(&lip, ip + 16, 4); /* ip.dest */
+  memcpy(&rip, ip + 12, 4); /* ip.src */
+  memcpy(&lp, l4 + 2, 2);   /* tcp.dest */
+  memcpy(&rp, l4, 2);       /* tcp.src */
+  return oracle_crc32c_u32((uint32_t) lp | ((uint32_t) rp << 16),
+      oracle_crc32c_u64((uint64_t) lip | ((uint64_t) rip << 32), 0));
+}
+
+void oracle_flow_lookup_batch(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *flowht, uint32_t ht_entries, const uint8_t *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out)
+{
+  size_t i;
+  uint32_t j;
+  for (i = 0; i < n; i++) {
+    const uint8_t *f = base + pkt_off(off, stride, i);
+    const uint8_t *ip = f + ip_off, *l4 = f + l4_off;
+    const uint32_t h = oracle_flow_hash(ip, l4);
+    uint32_t res = 0xffffffffu;
+    /* the last loop of fast_flows_packet_fss() (:1127-1162); the two before
+     * it only prefetch */
+    for (j = 0; j < 4; j++) {
+      const uint32_t k = (h + j) % ht_entries;
+      const uint32_t ffid = flowht[2 * k], eh = flowht[2 * k + 1];
+      const uint32_t fid = ffid & ((1u << 29) - 1);
+      const uint8_t *fs;
+      if ((ffid & 0x80000000u) == 0 || eh != h)
+        continue;
+      if (fid >= fs_num) /* the reference would read past flowst[] */
+        continue;
+      fs = flowst + (uint64_t) fid * fs_stride + fs_key_off;
+      if (memcmp(fs, ip + 16, 4) == 0 && memcmp(fs + 4, ip + 12, 4) == 0 &&
+          memcmp(fs + 8, l4 + 2, 2) == 0 && memcmp(fs + 10, l4, 2) == 0) {
+        res = fid;
+        break;
+      }
+    }
+    fid_out[i] = res;
+    if (hash_out)
+      hash_out[i] = h;
+  }
+}
+
+/* ---------------------------------------------------------------------- */
 /* CPU baseline timing. */
 
 struct bench_arg {
@@ -293,6 +389,10 @@ struct bench_arg {
   const uint8_t *shm;
   uint64_t shm_len;
   const struct oracle_tx_seg *segs;
+  const uint32_t *flowht;
+  const uint8_t *flowst;
+  uint32_t ht_entries, fs_num, fs_stride, fs_key_off;
+  uint32_t *fid_out;
   pthread_barrier_t *bar;
   double t0, t1;
 };
@@ -320,6 +420,13 @@ static void *bench_worker(void *p)
     for (i = a->lo; i < a->hi; i++)
       a->out[i] = oracle_raw_cksum(a->base + pkt_off(a->off, a->stride, i),
           a->len ? a->len[i] : a->len0);
+  } else if (a->mode == 3) {
+    /* fast_flows_packet_fss() per RX burst */
+    oracle_flow_lookup_batch(a->off ? a->base : a->base + a->lo * a->stride,
+        a->off ? a->off + a->lo : NULL, a->stride,
+        a->hi - a->lo, a->ip_off, a->l4_off, a->flowht, a->ht_entries,
+        a->flowst, a->fs_num, a->fs_stride, a->fs_key_off, NULL,
+        a->fid_out + a->lo);
   } else if (a->mode == 2) {
     /* flow_tx_segment()'s payload copy + tcp_checksums(), per segment */
     oracle_tx_segment_batch(a->shm, a->shm_len, a->base, a->segs + a->lo,
@@ -426,5 +533,29 @@ double oracle_bench_tx_segment(const uint8_t *shm, uint64_t shm_len,
   a.segs = segs;
   a.ip_off = ip_off;
   a.l4_off = l4_off;
+  return bench_run(&a, n, threads, reps);
+}
+
+double oracle_bench_flow_lookup(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *flowht, uint32_t ht_entries, const uint8_t *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *fid_out, int threads, int reps)
+{
+  struct bench_arg a;
+  memset(&a, 0, sizeof(a));
+  a.mode = 3;
+  a.base = (uint8_t *) base;
+  a.off = off;
+  a.stride = stride;
+  a.ip_off = ip_off;
+  a.l4_off = l4_off;
+  a.flowht = flowht;
+  a.ht_entries = ht_entries;
+  a.flowst = flowst;
+  a.fs_num = fs_num;
+  a.fs_stride = fs_stride;
+  a.fs_key_off = fs_key_off;
+  a.fid_out = fid_out;
   return bench_run(&a, n, threads, reps);
 }

@@ -75,6 +75,17 @@ void oracle_tx_segment_batch(const uint8_t *shm, uint64_t shm_len,
     uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,
     uint32_t ip_off, uint32_t l4_off, uint32_t *out);
 
+/* RX flow lookup: fast_flows_packet_fss(),
+ * tas/fast/fast_flows.c:1084-1163, and its CRC32C flow_hash (:1078-1082). */
+uint32_t oracle_crc32c_u32(uint32_t data, uint32_t init);
+uint32_t oracle_crc32c_u64(uint64_t data, uint32_t init);
+uint32_t oracle_flow_hash(const void *ip_hdr, const void *l4_hdr);
+void oracle_flow_lookup_batch(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *flowht, uint32_t ht_entries, const uint8_t *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out);
+
 /* PKT_TX_TCP_SEG bit of DPDK 19.11 rte_mbuf_core.h (1ULL << 50) */
 #define ORACLE_PKT_TX_TCP_SEG (1ULL << 50)
 
@@ -95,6 +106,12 @@ void oracle_tcp4_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
 double oracle_bench(int mode, uint8_t *base, const uint64_t *off,
     const uint32_t *len, uint64_t stride, uint32_t len0, size_t n,
     uint32_t ip_off, uint32_t l4_off, uint16_t *out, int threads, int reps);
+/* same for the RX flow lookup (mode 3) */
+double oracle_bench_flow_lookup(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *flowht, uint32_t ht_entries, const uint8_t *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *fid_out, int threads, int reps);
 /* same for the TX segment build (copy + checksums per segment) */
 double oracle_bench_tx_segment(const uint8_t *shm, uint64_t shm_len,
     uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,

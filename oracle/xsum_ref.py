@@ -151,3 +151,47 @@ def tx_segment(shm, shm_len: int, frames: np.ndarray, segs: np.ndarray, ip_off: 
         frames[fo: fo + len(fr)] = np.frombuffer(bytes(fr), np.uint8)
         out[i] = ipc | (tcpc << 16)
     return out
+
+
+# ---------------------------------------------------------------------------
+# RX flow lookup
+
+CRC32C_POLY = 0x82F63B78
+
+
+def crc32c(data: bytes, crc: int = 0) -> int:
+    """CRC32C bit by bit from the polynomial definition (reflected, no pre/post
+    inversion: the SSE4.2 crc32 instruction; DPDK crc32c_sse42_u32/_u64)."""
+    for b in data:
+        crc ^= b
+        for _ in range(8):
+            crc = (crc >> 1) ^ (CRC32C_POLY if crc & 1 else 0)
+    return crc
+
+
+def flow_hash(frame, ip_off: int = 14, l4_off: int = 34) -> int:
+    """flow_hash() of the key fast_flows_packet_fss() builds
+    (/root/reference tas/fast/fast_flows.c:1078-1082, :1097-1101): bytes
+    ip.dest, ip.src, tcp.dest, tcp.src."""
+    f = bytes(frame)
+    key = f[ip_off + 16: ip_off + 20] + f[ip_off + 12: ip_off + 16] + f[l4_off + 2: l4_off + 4] + f[l4_off: l4_off + 2]
+    return crc32c(key, 0)
+
+
+def flow_lookup(frame, flowht: np.ndarray, flowst: bytes, fs_num: int, ip_off: int = 14, l4_off: int = 34,
+                fs_stride: int = 128, fs_key_off: int = 32) -> tuple[int, int]:
+    """fast_flows_packet_fss() for one frame (:1127-1162): (hash, flow id or 0xffffffff)."""
+    f = bytes(frame)
+    h = flow_hash(f, ip_off, l4_off)
+    want = f[ip_off + 16: ip_off + 20] + f[ip_off + 12: ip_off + 16] + f[l4_off + 2: l4_off + 4] + f[l4_off: l4_off + 2]
+    ent = len(flowht) // 2
+    for j in range(4):
+        k = ((h + j) & 0xFFFFFFFF) % ent
+        ffid, eh = int(flowht[2 * k]), int(flowht[2 * k + 1])
+        fid = ffid & ((1 << 29) - 1)
+        if not (ffid & 0x80000000) or eh != h or fid >= fs_num:
+            continue
+        o = fid * fs_stride + fs_key_off
+        if bytes(flowst[o: o + 12]) == want:
+            return h, fid
+    return h, 0xFFFFFFFF

@@ -20,7 +20,7 @@ LIB = OUT_DIR / "libtasx.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
-HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip"]
+HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip", "flow_kernels.hip"]
 C_SRCS = ["tasx_host.c"]
 
 

@@ -204,6 +204,43 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   return 0;
 }
 
+int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    const void *flowht, uint32_t ht_entries, const void *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out, void *stream)
+{
+  tasx_flow_params p;
+  if (n == 0)
+    return 0;
+  if ((!base && !off) || !flowht || !flowst || !fid_out)
+    return set_err(-EINVAL, "flow lookup: NULL base/flowht/flowst/fid_out");
+  if (ht_entries == 0 || fs_num == 0)
+    return set_err(-EINVAL, "flow lookup: empty flow table");
+  if ((fs_stride & 3u) || (fs_key_off & 3u) || ((uintptr_t) flowst & 3u) || ((uintptr_t) flowht & 7u))
+    return set_err(-EINVAL, "flow lookup: misaligned flow table");
+  if (((uintptr_t) fid_out & 3u) || ((uintptr_t) hash_out & 3u))
+    return set_err(-EINVAL, "flow lookup: outputs must be 4-byte aligned");
+  memset(&p, 0, sizeof(p));
+  p.base = (const uint8_t *) base;
+  p.off = off;
+  p.stride = stride;
+  p.flowht = (const uint32_t *) flowht;
+  p.flowst = (const uint8_t *) flowst;
+  p.hash_out = hash_out;
+  p.fid_out = fid_out;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  p.ht_entries = ht_entries;
+  p.fs_num = fs_num;
+  p.fs_stride = fs_stride;
+  p.fs_key_off = fs_key_off;
+  if (tasx_launch_flow_lookup(&p, stream) != 0)
+    return hip_err(hipGetLastError(), "flow lookup kernel launch");
+  return 0;
+}
+
 /* ---------------------------------------------------------------------- */
 /* contexts */
 

@@ -49,11 +49,30 @@ typedef struct tasx_txseg_params {
   uint32_t dbg;            /* diagnostics: TASX_TXSEG_DEBUG (0 = product) */
 } tasx_txseg_params;
 
+typedef struct tasx_flow_params {
+  const uint8_t *base;     /* device pointer to RX frames */
+  const uint64_t *off;     /* device, n entries, or NULL -> i * stride */
+  uint64_t stride;
+  const uint32_t *flowht;  /* {flow_id, flow_hash} pairs */
+  const uint8_t *flowst;
+  uint32_t *hash_out;      /* or NULL */
+  uint32_t *fid_out;
+  uint32_t n;
+  uint32_t ip_off;
+  uint32_t l4_off;
+  uint32_t ht_entries;
+  uint32_t fs_num;
+  uint32_t fs_stride;
+  uint32_t fs_key_off;
+} tasx_flow_params;
+
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 /* receive-side verification; p->out points to n flag bytes */
 int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream);
+/* RX flow lookup (flow_kernels.hip) */
+int tasx_launch_flow_lookup(const tasx_flow_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 

@@ -162,6 +162,69 @@ def tx_segments(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SE
     return shm, frames, segs, shm_bytes
 
 
+# ---------------------------------------------------------------------------
+# RX flow lookup inputs (fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163)
+
+FLOWST_SIZE = 128     # sizeof(struct flextcp_pl_flowst), include/tas_memif.h:231-317
+FLOWST_KEY_OFF = 32   # local_ip, remote_ip, local_port, remote_port (:248-252)
+FLOWHT_NBSZ = 4       # FLEXNIC_PL_FLOWHT_NBSZ (:187)
+FLOWHTE_VALID = 1 << 31
+FLOWHTE_POSSHIFT = 29
+
+
+def flow_keys(nflows: int, seed: int = SEED) -> np.ndarray:
+    """nflows distinct 12-byte keys in flow-state order: local_ip, remote_ip
+    (network order), local_port, remote_port."""
+    raw = random_bytes(seed ^ 0xF10E, nflows * 16).reshape(nflows, 16)[:, :12].copy()
+    raw[:, 0:4] = np.frombuffer(np.arange(nflows, dtype=">u4").tobytes(), np.uint8).reshape(nflows, 4)
+    raw[:, 0] |= 0x0A                                  # distinct local ips (10.x.y.z-ish)
+    return raw
+
+
+def flow_state(keys: np.ndarray, seed: int = SEED) -> np.ndarray:
+    """The flow-state array (FLOWST_SIZE bytes per flow, random other fields)
+    with each flow's key at FLOWST_KEY_OFF."""
+    n = len(keys)
+    fs = random_bytes(seed ^ 0xF57A, n * FLOWST_SIZE).reshape(n, FLOWST_SIZE)
+    fs[:, FLOWST_KEY_OFF:FLOWST_KEY_OFF + 12] = keys
+    return fs.reshape(-1)
+
+
+def flow_table(hashes: np.ndarray, ht_entries: int, fids=None) -> tuple[np.ndarray, np.ndarray]:
+    """flowht for flows with the given hashes: each goes to the first free of
+    its FLOWHT_NBSZ entries (h + d) % ht_entries with d in the POSSHIFT bits,
+    as flow_slot_alloc() places it when no displacement is needed
+    (tas/slow/nicif.c:603-622, :241-244).  Flows whose bucket is full are left
+    out.  Returns (flowht u32[2 * ht_entries], inserted mask)."""
+    ht = np.zeros(2 * ht_entries, np.uint32)
+    fids = np.arange(len(hashes)) if fids is None else np.asarray(fids)
+    ok = np.zeros(len(hashes), bool)
+    for i, (h, fid) in enumerate(zip(np.asarray(hashes, np.uint64), fids)):
+        for d in range(FLOWHT_NBSZ):
+            k = int((int(h) + d) & 0xFFFFFFFF) % ht_entries
+            if not ht[2 * k] & FLOWHTE_VALID:
+                ht[2 * k] = FLOWHTE_VALID | (d << FLOWHTE_POSSHIFT) | int(fid)
+                ht[2 * k + 1] = int(h)
+                ok[i] = True
+                break
+    return ht, ok
+
+
+def rx_frames(keys: np.ndarray, stride: int = MBUF_ROOM, seed: int = SEED) -> np.ndarray:
+    """One received TCP frame per key, as the peer sends it: ip.src = the
+    flow's remote ip, ip.dst = local ip, tcp.src = remote port, tcp.dst =
+    local port (the key fast_flows_packet_fss builds, :1097-1101).  Only the
+    first 64 bytes of each frame are filled (headers); the rest is random."""
+    n = len(keys)
+    f = tcp4_frames(n, payload=0, stride=stride, seed=seed).reshape(n, stride)
+    ip, t = ETH_LEN, ETH_LEN + IP_LEN
+    f[:, ip + 16: ip + 20] = keys[:, 0:4]
+    f[:, ip + 12: ip + 16] = keys[:, 4:8]
+    f[:, t + 2: t + 4] = keys[:, 8:10]
+    f[:, t: t + 2] = keys[:, 10:12]
+    return f.reshape(-1)
+
+
 def kat_frame() -> bytearray:
     """The window-update segment built by the reference unit test
     test_rxbump_fc_reopen_notx (tests/tas_unit/fastpath.c:18-22,68-89,187-207

@@ -46,6 +46,8 @@ SIGNATURES = {
     "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                 _c_u32, _vp]),
     "tasx_tcp4_verify_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
+    "tasx_flow_lookup_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32,
+                                            _c_u32, _c_u32, _vp, _vp, _vp]),
     "tasx_tx_segment_batch_dev": (_c_int, [_vp, _c_u64, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
     "tasx_ctx_destroy": (_c_int, [_uns]),
@@ -194,6 +196,24 @@ def tcp4_verify_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | N
     _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
                                             _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
     return out
+
+
+FLOW_NONE = 0xFFFFFFFF
+
+
+def flow_lookup_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst: torch.Tensor, fs_num: int, *,
+                      offsets: torch.Tensor | None = None, stride: int = 0, ip_off: int = TAS_IP_OFF,
+                      l4_off: int = TAS_L4_OFF, fs_stride: int = 128, fs_key_off: int = 32,
+                      want_hash: bool = True, stream=None):
+    """RX flow lookup (fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163):
+    returns (hashes int32 or None, flow ids int32; FLOW_NONE = no flow)."""
+    fid = torch.empty(n, dtype=torch.int32, device=frames.device)
+    h = torch.empty(n, dtype=torch.int32, device=frames.device) if want_hash else None
+    ent = flowht.numel() * flowht.element_size() // 8
+    _check(lib().tasx_flow_lookup_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off, _ptr(flowht),
+                                            ent, _ptr(flowst), fs_num, fs_stride, fs_key_off, _ptr(h), _ptr(fid),
+                                            _stream(stream)), "tasx_flow_lookup_batch_dev")
+    return h, fid
 
 
 def tx_segment_batch(shm: torch.Tensor, frames: torch.Tensor, segs: torch.Tensor, n: int, *,

@@ -180,6 +180,39 @@ def txseg_fixture():
                 frames_out=frames_out, expected=exp)
 
 
+def flow_fixture():
+    """RX flow lookup (fast_flows_packet_fss + CRC32C flow_hash, SURVEY.md
+    section 8f row 4): a small, crowded table (61 entries, not a power of two,
+    so probes wrap and buckets fill), frames for inserted flows, for flows whose
+    bucket was full, for unknown keys, and planted entries that must be
+    skipped: same hash but another flow's key, invalid bit clear, flow id past
+    the flow-state array."""
+    nflows, ent, stride = 48, 61, 128
+    keys = pktgen.flow_keys(nflows, seed=SEED)
+    fs = pktgen.flow_state(keys, seed=SEED)
+    hashes = np.asarray([R.crc32c(bytes(k), 0) for k in keys], np.uint64)
+    ht, ok = pktgen.flow_table(hashes, ent)
+    unknown = pktgen.flow_keys(8, seed=SEED ^ 0x5555)
+    unknown[:, 0] ^= 0x80
+    fkeys = np.concatenate([keys, unknown])
+    frames = pktgen.rx_frames(fkeys, stride=stride, seed=SEED).reshape(len(fkeys), stride)
+    # planted entries: for three unknown keys, fill their whole bucket with
+    # entries carrying their hash -- flow 0 (wrong key), invalid, past the array
+    for u, kind in zip(range(3), ("wrong_key", "invalid", "past_end")):
+        h = R.crc32c(bytes(unknown[u]), 0)
+        for d in range(4):
+            k = ((h + d) & 0xFFFFFFFF) % ent
+            fid = {"wrong_key": 0, "invalid": 1, "past_end": nflows + 5}[kind]
+            ht[2 * k] = (0 if kind == "invalid" else pktgen.FLOWHTE_VALID) | fid
+            ht[2 * k + 1] = h
+    exp_h = np.empty(len(fkeys), np.uint32)
+    exp_f = np.empty(len(fkeys), np.uint32)
+    for i in range(len(fkeys)):
+        exp_h[i], exp_f[i] = R.flow_lookup(frames[i].tobytes(), ht, fs.tobytes(), nflows)
+    return dict(frames=frames.reshape(-1), stride=np.uint64(stride), flowht=ht, flowst=fs,
+                fs_num=np.uint32(nflows), expected_hash=exp_h, expected_fid=exp_f)
+
+
 def main():
     raw = raw_fixture()
     np.savez_compressed(HERE / "raw_vectors.npz", **raw)
@@ -189,6 +222,12 @@ def main():
         "rfc1071_sec3": {"bytes": "0001f203f4f5f6f7", "raw_cksum_be": "ddf2",
                          "raw_cksum_native_le": 0xF2DD,
                          "source": "RFC 1071 section 3 numerical example"},
+        "crc32c_rfc3720_b4": {
+            "note": "standard CRC32C (init 0xffffffff, final xor 0xffffffff); TAS's flow_hash uses the "
+                    "same polynomial with init 0 and no final xor",
+            "zeros32": "8a9136aa", "ones32": "62a8ab43", "inc32": "46dd794e", "dec32": "113fdb5c",
+            "check_123456789": "e3069283",
+            "source": "RFC 3720 appendix B.4 (iSCSI CRC32C examples) and the CRC catalogue check value"},
         "tas_unit_window_update": {
             "frame_hex": bytes(pktgen.kat_frame()).hex(),
             "ip_chksum_bytes": "a3bb", "tcp_chksum_bytes": "cfd7",
@@ -196,11 +235,13 @@ def main():
                       "flow_tx_segment, tas/fast/fast_flows.c:886-928); values hand-derived "
                       "in SURVEY.md section 8c"},
     }
+    fl = flow_fixture()
+    np.savez_compressed(HERE / "flow_vectors.npz", **fl)
     tx = txseg_fixture()
     np.savez_compressed(HERE / "txseg_vectors.npz", **tx)
     (HERE / "kat.json").write_text(json.dumps(kat, indent=2) + "\n")
     print("raw:", len(raw["lengths"]), "vectors;", "tcp4:", len(tcp["offsets"]), "frames;",
-          "txseg:", len(tx["expected"]), "segments")
+          "txseg:", len(tx["expected"]), "segments;", "flow:", len(fl["expected_fid"]), "frames")
 
 
 if __name__ == "__main__":
