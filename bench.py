@@ -69,6 +69,7 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--no-txseg", action="store_true")
+    ap.add_argument("--no-flow", action="store_true")
     ap.add_argument("--pmc", action="store_true", help="collect HBM traffic via rocprofv3 child runs")
     ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -293,6 +294,74 @@ class TxSegWorkload:
                 "sample": f"rotation 0's {self.n} segments, oracle flow_tx_read + tcp_checksums per segment, "
                           f"median of {reps} passes",
                 "parity_vs_gpu": "bit-exact" if np.array_equal(frames, gpu_frames) else "MISMATCH"}
+
+
+class FlowLookupWorkload:
+    """RX flow lookup (fast_flows_packet_fss,
+    tas/fast/fast_flows.c:1084-1163): per received frame the CRC32C flow hash,
+    the 4-entry bucket probe and the flow-state key check.  TAS-sized table:
+    FLEXNIC_PL_FLOWST_NUM = 131072 flows, 2x hash entries; 90% of the frames
+    hit a random flow, 10% carry unknown keys.  Frames one per 2 KiB mbuf.
+    Bytes per frame: 12 key + 32 bucket + 12 flow key read, 8 written."""
+    NFLOWS, ENTRIES, N = 131072, 262144, 262144
+    desc = (f"{N} RX frames (2 KiB mbufs) looked up in a {NFLOWS}-flow / {ENTRIES}-entry flow table "
+            "(CRC32C hash, 4-entry bucket, flow-state key check), 10% unknown keys")
+
+    def __init__(self, rotate: int, seed: int):
+        keys = pktgen.flow_keys(self.NFLOWS, seed=seed)
+        self.fs_np = pktgen.flow_state(keys, seed=seed)
+        self.fs = torch.from_numpy(self.fs_np).cuda()
+        # hashes of the flows' own keys through the kernel (one-entry dummy table)
+        fr = torch.from_numpy(pktgen.rx_frames(keys, stride=128, seed=seed)).cuda()
+        dummy = torch.zeros(2, dtype=torch.int32, device="cuda")
+        h, _ = xsum.flow_lookup_batch(fr, self.NFLOWS, dummy, self.fs, self.NFLOWS, stride=128)
+        ht, ok = pktgen.flow_table(h.cpu().numpy().view(np.uint32), self.ENTRIES)
+        self.ht_np = ht
+        self.ht = torch.from_numpy(ht).cuda()
+        rng = np.random.default_rng(seed)
+        fkeys = keys[rng.integers(0, self.NFLOWS, self.N)].copy()
+        miss = rng.random(self.N) < 0.1
+        fkeys[miss, 4] ^= 0x5A
+        self.frames_np = pktgen.rx_frames(fkeys, stride=STRIDE, seed=seed + 1)
+        first = torch.from_numpy(self.frames_np).cuda()
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.fids = [torch.empty(self.N, dtype=torch.int32, device="cuda") for _ in range(rotate)]
+        self.hashes = [torch.empty(self.N, dtype=torch.int32, device="cuda") for _ in range(rotate)]
+        self.n = self.N
+        self.bytes_per_step = self.N * (12 + 32 + 12 + 8)
+        self.inserted = float(ok.mean())
+
+    def launcher(self):
+        fn = xsum.lib().tasx_flow_lookup_batch_dev
+        stream = torch.cuda.current_stream().cuda_stream
+        args = [(b.data_ptr(), None, STRIDE, self.N, pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN,
+                 self.ht.data_ptr(), self.ENTRIES, self.fs.data_ptr(), self.NFLOWS, pktgen.FLOWST_SIZE,
+                 pktgen.FLOWST_KEY_OFF, h.data_ptr(), f.data_ptr(), stream)
+                for b, h, f in zip(self.bufs, self.hashes, self.fids)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_flow_lookup_batch_dev")
+        return launch
+
+    def cpu_check(self, budget_s: float) -> dict:
+        from oracle import oracle_lib
+        orc = oracle_lib.Oracle()
+        torch.cuda.synchronize()
+        gpu_fid = self.fids[0].cpu().numpy().view(np.uint32)
+        _, exp = orc.flow_lookup_batch(self.frames_np, self.N, self.ht_np, self.fs_np, fs_num=self.NFLOWS,
+                                       stride=STRIDE)
+        threads = min(16, len(os.sched_getaffinity(0)))
+        kw = dict(fs_num=self.NFLOWS, stride=STRIDE)
+        t = orc.bench_flow_lookup(self.frames_np, self.N, self.ht_np, self.fs_np, threads=threads, reps=1, **kw)
+        reps = max(3, min(500, int(budget_s / max(t, 1e-6))))
+        t = orc.bench_flow_lookup(self.frames_np, self.N, self.ht_np, self.fs_np, threads=threads, reps=reps, **kw)
+        return {"value": self.N / t / 1e6, "unit": "Mpps", "cores": threads, "kind": "port",
+                "sample": f"rotation 0's {self.N} frames, oracle fast_flows_packet_fss restatement, "
+                          f"median of {reps} passes",
+                "parity_vs_gpu": "bit-exact" if np.array_equal(exp, gpu_fid) else "MISMATCH"}
 
 
 def prewarm(launch, seconds: float = 0.25):
@@ -587,6 +656,18 @@ def main():
         del tw
         torch.cuda.empty_cache()
 
+    flow = None
+    if not args.no_flow:
+        fw = FlowLookupWorkload(min(rot, 4), pktgen.SEED + 3000 + rank)
+        flow = leg(fw, args, ws, FlowLookupWorkload.desc)
+        flow["mpps"] = fw.N * args.steps / (flow["ms_per_step"] * 1e-3 * args.steps) / 1e6
+        flow["flows_inserted_frac"] = fw.inserted
+        flow["bytes_per_frame"] = 64
+        if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+            flow["cpu_baseline"] = fw.cpu_check(3.0)
+        del fw
+        torch.cuda.empty_cache()
+
     extra = {}
     if rank == 0 and ws == 1:
         torch.cuda.synchronize()
@@ -626,6 +707,8 @@ def main():
             line["raw"] = raw
         if txseg is not None:
             line["tx_segment"] = txseg
+        if flow is not None:
+            line["flow_lookup"] = flow
         if "e2e" in extra:
             line["e2e"] = extra["e2e"]
         if "pmc" in extra:
