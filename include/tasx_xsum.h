@@ -226,7 +226,9 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
  *   1 first-generation group-per-packet kernels (A/B baseline)
  *   2 raw_group_kernel / tcp4_frame_kernel (any layout)
  *   3 tcp4_tas_kernel (TAS layout, stride mode; falls back to 2)
- *   4 tcp4_tas_kernel with wave-timeline stamps into the diag buffer */
+ *   4 tcp4_tas_kernel with wave-timeline stamps into the diag buffer
+ *   5 tcp4_tas_kernel with 32 lanes x 3 chunks per frame (TCP4 only; RAW
+ *     uses 2) */
 int tasx_set_kernel_variant(int variant);
 /* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
  * wave.  NULL disables. */

@@ -163,6 +163,19 @@ __device__ __forceinline__ uint32_t row_sum16(uint32_t v)
   return v;
 }
 
+// G-lane group total (G = 16, 32, 64; groups aligned in the wave) in the
+// group's last lane: DPP row scan, then row_bcast15 / row_bcast31 across rows
+template <int G>
+__device__ __forceinline__ uint32_t group_total(uint32_t v)
+{
+  v = row_sum16(v);
+  if constexpr (G >= 32) // rows 1, 3 += lane 15 of rows 0, 2
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x142, 0xa, 0xf, false);
+  if constexpr (G == 64) // rows 2, 3 += lane 31
+    v += (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 // sum of the dwords of chunk v restricted to bytes [0, h) (0 <= h <= 16)
 __device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
 {
@@ -202,29 +215,29 @@ __device__ __forceinline__ Chunks<U> chunk_range(const uint8_t *start, uint32_t 
   return r;
 }
 
-// this lane's exact partial over the group's chunks gl, gl+16, ...
-template <int U>
+// this lane's exact partial over the group's chunks gl, gl+G, ... (G lanes)
+template <int U, int G = 16>
 __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
 {
   uint64_t acc = 0;
   if (r.nch == 0)
     return 0;
-  for (uint32_t c = (uint32_t) gl; c < r.nch; c += 16u * U) {
+  for (uint32_t c = (uint32_t) gl; c < r.nch; c += (uint32_t) G * U) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(r.c0p, min(c + 16u * u, r.nch - 1));
+      v[u] = ld16nt(r.c0p, min(c + (uint32_t) G * u, r.nch - 1));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool keep = c + 16u * u < r.nch;
+      const bool keep = c + (uint32_t) G * u < r.nch;
       acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
     }
     // boundary fix-ups: drop bytes [0, head) of chunk 0, [tail, 16) of chunk nch-1
     if (c == 0 && r.head)
       acc -= chunk_prefix_sum(v[0], r.head);
     const uint32_t last = r.nch - 1;
-    if (last >= c && last < c + 16u * U && ((last - c) & 15u) == 0 && r.tail < 16) {
-      const uint32_t ut = (last - c) >> 4;
+    if (last >= c && last < c + (uint32_t) G * U && ((last - c) % G) == 0 && r.tail < 16) {
+      const uint32_t ut = (last - c) / G;
       u32x4 t = v[0];
 #pragma unroll
       for (int u = 1; u < U; ++u)

@@ -352,14 +352,14 @@ __device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
   return __builtin_nontemporal_load((gcu4 *) (base + off));
 }
 
-template <int U, int DIAG = 0>
+template <int U, int DIAG = 0, int G = 16>
 __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 {
   if constexpr (DIAG)
     diag_stamp<kBlock>(p, 0);
-  const int gl = threadIdx.x & 15;
-  const int gbase = (threadIdx.x & 63) & ~15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  const int gl = threadIdx.x & (G - 1);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
   if (i >= p.n)
     return;
   const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
   u32x4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + 16u * u, nld - 1));
+    v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + (uint32_t) G * u, nld - 1));
   const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
   const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
   const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
@@ -385,12 +385,12 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const int E = 20 + (int) len;
   const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
-  const uint32_t need = min(nch, 16u * U);
+  const uint32_t need = min(nch, (uint32_t) G * U);
   if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
     const uint32_t top = max(need, nld);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + 16u * u, top - 1));
+      v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + (uint32_t) G * u, top - 1));
   }
   const uint32_t last = nch - 1;
   const int tail = (int) ((ipo + (uint32_t) E) - ((ipo + (uint32_t) E - 1) & ~15u));
@@ -413,11 +413,11 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
   }
 #pragma unroll
   for (int u = 1; u < U; ++u) {
-    const uint32_t c = (uint32_t) gl + 16u * u;
+    const uint32_t c = (uint32_t) gl + (uint32_t) G * u;
     acc += c < nch ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
   }
-  if (last >= 4u && last < 16u * U && (last & 15u) == (uint32_t) gl && tail < 16) {
-    const uint32_t ut = last >> 4;
+  if (last >= 4u && last < (uint32_t) G * U && (last % G) == (uint32_t) gl && tail < 16) {
+    const uint32_t ut = last / G;
     u32x4 t = v[0];
 #pragma unroll
     for (int u = 1; u < U; ++u)
@@ -426,22 +426,22 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
     acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
   }
   uint32_t part = fold64_to_18(acc);
-  if (nch > 16u * U) {
+  if (nch > (uint32_t) G * U) {
     Chunks<U> rest;
-    rest.c0p = (const u32x4 *) (base + a0) + 16u * U;
-    rest.nch = nch - 16u * U;
+    rest.c0p = (const u32x4 *) (base + a0) + (uint32_t) G * U;
+    rest.nch = nch - (uint32_t) G * U;
     rest.head = 0;
     rest.tail = tail;
-    part += group_lane_sum<U>(rest, gl);
+    part += group_lane_sum<U, G>(rest, gl);
   }
   uint32_t c_ip = fold64_to_18(acc_ip);
   uint32_t c_ph = fold64_to_18(acc_ph);
   if constexpr (DIAG)
     diag_stamp<kBlock>(p, 2);
-  part = row_sum16(part);
-  c_ip = row_sum16(c_ip);
-  c_ph = row_sum16(c_ph);
-  if (gl == 15) {
+  part = group_total<G>(part);
+  c_ip = group_total<G>(c_ip);
+  c_ph = group_total<G>(c_ph);
+  if (gl == G - 1) {
     uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
     if (hb & 1) {
       ri = bswap16(ri);
@@ -466,13 +466,13 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
     diag_stamp<kBlock>(p, 3);
 }
 
-template <typename K, typename Prm>
+template <int G = 16, typename K, typename Prm>
 int launch_groups(K kern, const Prm &p, hipStream_t s)
 {
-  // one 16-lane group per packet, 16 groups per 256-thread block: the grid
-  // covers the batch once (measured faster than persistent grids at these
-  // batch sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
-  constexpr uint64_t fpb = kBlock / 16;
+  // one G-lane group per packet, kBlock / G groups per block: the grid covers
+  // the batch once (measured faster than persistent grids at these batch
+  // sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
+  constexpr uint64_t fpb = kBlock / G;
   const uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
   if (blocks == 0)
     return 0;
@@ -533,7 +533,7 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   const bool tas_ok = tas_kernel_ok(*p);
   if (variant == 0) // TAS layout + frame-length hints -> tcp4_tas_kernel
     variant = (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
-  if ((variant == 3 || variant == 4) && !tas_ok)
+  if (variant >= 3 && !tas_ok)
     variant = 2;
   switch (variant) {
   case 1:
@@ -544,6 +544,8 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
     return launch_groups(tcp4_tas_kernel<6>, *p, s);
   case 4:
     return p->diag ? launch_groups(tcp4_tas_kernel<6, 1>, *p, s) : -2;
+  case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
+    return launch_groups<32>(tcp4_tas_kernel<3, 0, 32>, *p, s);
   default:
     return -2;
   }

@@ -242,7 +242,7 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5])
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
@@ -284,14 +284,19 @@ def test_raw_all_variants(oracle, variant):
         xsum.set_kernel_variant(0)
 
 
-def test_tso_with_hints(oracle):
+@pytest.mark.parametrize("variant", [0, 5])
+def test_tso_with_hints(oracle, variant):
     n, stride = 512, 65552
     frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=58,
                                 ip_total_len=np.where(np.arange(n) % 3 == 0, 65535, 30000))
     exp = oracle.tcp4_batch(frames.copy(), n, stride=stride)
     d = to_dev(frames)
-    for hint in (None, 65549, 1514, stride):
-        np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride, frame_len=hint)), exp)
+    xsum.set_kernel_variant(variant)
+    try:
+        for hint in (None, 65549, 1514, stride):
+            np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride, frame_len=hint)), exp)
+    finally:
+        xsum.set_kernel_variant(0)
 
 
 def test_deterministic_and_n0():
