@@ -10,8 +10,9 @@
 // load of a phase is issued before any is used (the four bucket entries
 // together, then the four candidates' keys together, clamped to flow 0 when
 // not a candidate), and the kernel keeps few registers so many frames are in
-// flight per CU.  CRC32C is computed bitwise on the VALU (96 steps, no table
-// lookups in the chain).
+// flight per CU.  CRC32C is computed bit by bit on the VALU by default (a
+// slice-by-4 variant from LDS tables built at compile time measured the same:
+// the CRC is not on the critical path).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,10 +23,36 @@ namespace {
 
 constexpr uint32_t kPoly = 0x82f63b78u; // CRC32C (Castagnoli), reflected
 
-// SSE4.2 crc32 on one 32-bit little-endian word: crc32c_sse42_u32(w, crc)
-__device__ __forceinline__ uint32_t crc32c_word(uint32_t crc, uint32_t w)
+// slice-by-4 tables: t[k][x] = CRC of byte x followed by k zero bytes (init 0)
+struct CrcTables {
+  uint32_t t[4][256];
+};
+
+constexpr CrcTables make_crc_tables()
+{
+  CrcTables T{};
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k)
+      c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
+    T.t[0][i] = c;
+  }
+  for (int k = 1; k < 4; ++k)
+    for (uint32_t i = 0; i < 256; ++i)
+      T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xffu];
+  return T;
+}
+
+__constant__ CrcTables kCrc = make_crc_tables();
+
+// SSE4.2 crc32 on one 32-bit little-endian word (crc32c_sse42_u32(w, crc)):
+// slice-by-4 from the LDS copy of the tables, or bit by bit on the VALU
+template <bool TAB>
+__device__ __forceinline__ uint32_t crc32c_word(const uint32_t (*t)[256], uint32_t crc, uint32_t w)
 {
   crc ^= w;
+  if constexpr (TAB)
+    return t[3][crc & 0xffu] ^ t[2][(crc >> 8) & 0xffu] ^ t[1][(crc >> 16) & 0xffu] ^ t[0][crc >> 24];
 #pragma unroll
   for (int k = 0; k < 32; ++k)
     crc = (crc >> 1) ^ (kPoly & (0u - (crc & 1u)));
@@ -37,44 +64,73 @@ __device__ __forceinline__ uint32_t ld32b(const uint8_t *p)
   return ld8(p) | (ld8(p + 1) << 8) | (ld8(p + 2) << 16) | (ld8(p + 3) << 24);
 }
 
+// the 16 bytes starting at address x, from the one or two aligned chunks that
+// hold its first n (<= 16) bytes (a second chunk is loaded only if needed)
+__device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
+{
+  const uintptr_t a = (uintptr_t) x;
+  const u32x4 *c0 = (const u32x4 *) (a & ~(uintptr_t) 15);
+  const u32x4 *c1 = (const u32x4 *) ((a + (uintptr_t) n - 1) & ~(uintptr_t) 15);
+  return funnel16(ld16(c0, 0), ld16(c1, 0), (int) (a & 15));
+}
+
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+// TAB: slice-by-4 CRC from LDS (else bitwise); CHUNK: key fields from 16-byte
+// chunk loads (else byte loads)
+template <bool TAB, bool CHUNK>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
+  __shared__ uint32_t lt[TAB ? 4 : 1][256];
+  if constexpr (TAB) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lt[k][threadIdx.x] = kCrc.t[k][threadIdx.x];
+    __syncthreads();
+  }
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= p.n)
     return;
   const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  const uint8_t *ip = f + p.ip_off, *l4 = f + p.l4_off;
-  // key = (local = destination, remote = source), network byte order
-  const uint32_t lip = ld32b(ip + 16), rip = ld32b(ip + 12);
-  const uint32_t ports = (ld8(l4 + 2) | (ld8(l4 + 3) << 8)) | ((ld8(l4) | (ld8(l4 + 1) << 8)) << 16);
-  // flow_hash: crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0))
-  const uint32_t h = crc32c_word(crc32c_word(crc32c_word(0u, lip), rip), ports);
-  // bucket: entries (h + j) % ht_entries, j < NBSZ
-  uint32_t fid[TASX_FLOWHT_NBSZ], ehash[TASX_FLOWHT_NBSZ];
-#pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-    const uint32_t k = (h + j) % p.ht_entries;
-    fid[j] = ldg(p.flowht, 2 * k);
-    ehash[j] = ldg(p.flowht, 2 * k + 1);
+  // key = (local = destination, remote = source), network byte order:
+  // ip.src/ip.dst are bytes [12, 20) of the IPv4 header, the ports bytes
+  // [0, 4) of the TCP header
+  uint32_t rip, lip, l4x;
+  if constexpr (CHUNK) {
+    const u32x4 ipw = load_window(f + p.ip_off + 12, 8), l4w = load_window(f + p.l4_off, 4);
+    rip = ipw.x;
+    lip = ipw.y;
+    l4x = l4w.x;
+  } else {
+    rip = ld32b(f + p.ip_off + 12);
+    lip = ld32b(f + p.ip_off + 16);
+    l4x = ld32b(f + p.l4_off);
   }
-  // candidates' keys, all loads issued together
+  const uint32_t ports = (l4x >> 16) | (l4x << 16); // tcp.dest | tcp.src << 16
+  // flow_hash: crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0))
+  const uint32_t h = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip), rip), ports);
+  // bucket: entries (h + j) % ht_entries, j < NBSZ, loaded together
+  uint64_t e[TASX_FLOWHT_NBSZ];
+#pragma unroll
+  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+    e[j] = ldg((const uint64_t *) p.flowht, (h + j) % p.ht_entries);
+  // candidates' keys, loaded together (non-candidates read flow 0)
   bool cand[TASX_FLOWHT_NBSZ];
-  uint32_t klip[TASX_FLOWHT_NBSZ], krip[TASX_FLOWHT_NBSZ], kport[TASX_FLOWHT_NBSZ];
+  uint32_t fid[TASX_FLOWHT_NBSZ];
+  u32x3 key[TASX_FLOWHT_NBSZ];
 #pragma unroll
   for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-    const uint32_t id = fid[j] & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-    cand[j] = (fid[j] & TASX_FLOWHTE_VALID) && ehash[j] == h && id < p.fs_num;
-    fid[j] = id;
-    const uint32_t *key = (const uint32_t *) (p.flowst + (uint64_t) (cand[j] ? id : 0u) * p.fs_stride +
-                                              p.fs_key_off);
-    klip[j] = ldg(key, 0);
-    krip[j] = ldg(key, 1);
-    kport[j] = ldg(key, 2);
+    const uint32_t ffid = (uint32_t) e[j], eh = (uint32_t) (e[j] >> 32);
+    fid[j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
+    cand[j] = (ffid & TASX_FLOWHTE_VALID) && eh == h && fid[j] < p.fs_num;
+    key[j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
+                                                                 (uint64_t) (cand[j] ? fid[j] : 0u) * p.fs_stride +
+                                                                 p.fs_key_off);
   }
   uint32_t res = TASX_FLOW_NONE;
 #pragma unroll
   for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j) // first match wins
-    if (cand[j] && klip[j] == lip && krip[j] == rip && kport[j] == ports)
+    if (cand[j] && key[j].x == lip && key[j].y == rip && key[j].z == ports)
       res = fid[j];
   stg(p.fid_out, i, res);
   if (p.hash_out)
@@ -83,11 +139,22 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 
 } // namespace
 
-extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, void *stream)
+extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream)
 {
   const uint64_t blocks = ((uint64_t) p->n + 255) / 256;
   if (blocks == 0)
     return 0;
-  hipLaunchKernelGGL(flow_lookup_kernel, dim3((uint32_t) blocks), dim3(256), 0, (hipStream_t) stream, *p);
+  const dim3 g((uint32_t) blocks), b(256);
+  hipStream_t s = (hipStream_t) stream;
+  // A/B (tasx_set_kernel_variant; tools/flow_probe.py, profiles/r01_flow_variants.jsonl):
+  // bitwise CRC + byte loads (the default, 0/1) 12.7 us, LDS slice-by-4 13.0 us,
+  // 16-byte chunk key loads +1.7 us either way: the lookup is bound by its
+  // dependent load chain, not by the CRC arithmetic
+  switch (variant) {
+  case 2: hipLaunchKernelGGL((flow_lookup_kernel<false, true>), g, b, 0, s, *p); break;
+  case 3: hipLaunchKernelGGL((flow_lookup_kernel<true, false>), g, b, 0, s, *p); break;
+  case 4: hipLaunchKernelGGL((flow_lookup_kernel<true, true>), g, b, 0, s, *p); break;
+  default: hipLaunchKernelGGL((flow_lookup_kernel<false, false>), g, b, 0, s, *p); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -236,7 +236,7 @@ int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
   p.fs_num = fs_num;
   p.fs_stride = fs_stride;
   p.fs_key_off = fs_key_off;
-  if (tasx_launch_flow_lookup(&p, stream) != 0)
+  if (tasx_launch_flow_lookup(&p, g_variant, stream) != 0)
     return hip_err(hipGetLastError(), "flow lookup kernel launch");
   return 0;
 }

@@ -189,6 +189,23 @@ __device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
   return s;
 }
 
+// 16 bytes starting at byte s (0..15) of the 32-byte pair (a, b)
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, int s)
+{
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const int q = s >> 2;
+  const uint32_t r = (uint32_t) (s & 3);
+  uint32_t o[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const uint32_t w0 = w[t], w1 = w[t + 1], w2 = w[t + 2];
+    const uint32_t w3 = (t + 3 < 8) ? w[t + 3] : 0u;
+    o[t] = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+  }
+  return u32x4{__builtin_amdgcn_alignbyte(o[1], o[0], r), __builtin_amdgcn_alignbyte(o[2], o[1], r),
+               __builtin_amdgcn_alignbyte(o[3], o[2], r), __builtin_amdgcn_alignbyte(o[4], o[3], r)};
+}
+
 // byte b (0..15) of a 16-byte chunk
 __device__ __forceinline__ uint32_t chunk_byte(u32x4 v, int b)
 {
