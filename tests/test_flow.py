@@ -102,10 +102,18 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-def test_gpu_flow_golden(flow_golden):
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+def test_gpu_flow_golden(flow_golden, variant):
+    """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
+    chunks) on the fixture."""
+    from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
-    h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
+    xsum.set_kernel_variant(variant)
+    try:
+        h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
+    finally:
+        xsum.set_kernel_variant(0)
     np.testing.assert_array_equal(h, g["expected_hash"])
     np.testing.assert_array_equal(fid, g["expected_fid"])
 
