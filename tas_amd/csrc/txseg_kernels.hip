@@ -109,7 +109,8 @@ __device__ __forceinline__ void window_pair(uintptr_t S, int lo, int hi, const u
 // loads of a round are issued before any is consumed, so a segment costs one
 // memory latency after its descriptor (plus one per extra 96-chunk round).
 // MODE (diagnostics, TASX_TXSEG_DEBUG): bit 0 = no full-chunk payload stores,
-// bit 1 = temporal instead of non-temporal stores.
+// bit 1 = temporal instead of non-temporal stores, bit 3 = no header
+// write-back, bit 4 = no partial-chunk stores.
 template <int U, int MODE = 0>
 __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
 {
@@ -182,7 +183,14 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   const u32x4 *const f0p = (const u32x4 *) ((uintptr_t) f & ~(uintptr_t) 15);
   const uint32_t nhc = (uint32_t) ((fh + (int) hl + 15) >> 4);
   u32x4 hv = ld16nt(f0p, min((uint32_t) gl, nhc - 1));
-  const bool own_ce = ce != 0xffffffffu && ((ce - cp0) & 15u) == (uint32_t) gl;
+  // lanes map to chunks by ADDRESS (lane = absolute chunk index % 16), so each
+  // slot's 16 stores cover whole 256-byte blocks: the frame's payload lines are
+  // written whole by one instruction, not merged across instructions in L2
+  // (chunk indices below cp0 are idle lanes; signed, as base0 may be < 0)
+  const int aoff = (int) (((uintptr_t) c0p >> 4) & 15u);
+  const int base0 = (int) cp0 - (((int) cp0 + aoff) & 15);
+  auto lane_of = [&](uint32_t c) -> uint32_t { return (uint32_t) ((int) c - base0) & 15u; };
+  const bool own_ce = ce != 0xffffffffu && lane_of(ce) == (uint32_t) gl;
   uint32_t o1 = 0, oa = 0, ob = 0; // exception chunks (offset 0 on other lanes)
   {
     const int j0 = 16 * (int) ce - head - dlo;
@@ -203,19 +211,20 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   // ---- payload chunks: gather, store, sum
   uint64_t acc = 0;
   u32x4 vfirst = u32x4{0, 0, 0, 0}, vlast = vfirst;
-  for (uint32_t base = cp0; base < nend; base += 16u * U) {
+  for (int base = base0; base < (int) nend; base += 16 * U) {
     u32x4 a[U];
     int sh;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      a[u] = shm_chunk(window(base + (uint32_t) gl + 16u * u, sh));
-    const u32x4 ext = shm_chunk(window(base + 16u * U, sh)); // lane 15's last neighbour
+      a[u] = shm_chunk(window((uint32_t) max(base + gl + 16 * u, (int) cp0), sh));
+    const u32x4 ext = shm_chunk(window((uint32_t) max(base + 16 * U, (int) cp0), sh)); // lane 15's last neighbour
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t c = base + (uint32_t) gl + 16u * u;
-      const bool valid = c < nend;
+      const int ci = base + gl + 16 * u;
+      const bool valid = ci >= (int) cp0 && ci < (int) nend;
+      const uint32_t c = valid ? (uint32_t) ci : cp0 - 1; // idle lanes: a chunk holding no payload
       const int o = 16 * (int) c - head, j0 = o - dlo;
-      const int blo = max(-j0, 0), bhi = min(dhi - o, 16);
+      const int blo = min(max(-j0, 0), 16), bhi = min(dhi - o, 16);
       // second chunk: a[u] of lane (gl + 1) % 16 (lane 15: slot u + 1 of lane 0)
       const u32x4 nx = (u + 1 < U) ? a[u + 1 < U ? u + 1 : u] : ext;
       const u32x4 t0 = u32x4{ror15(a[u].x), ror15(a[u].y), ror15(a[u].z), ror15(a[u].w)};
@@ -246,21 +255,14 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
     }
   }
   if (!(MODE & 16) && nend > cp0) {
-    // partial first / last payload chunks (lanes 0 and (nend - 1 - cp0) % 16)
-    if (gl == 0) {
+    // partial first / last payload chunks, on the lanes that own them
+    if (lane_of(cp0) == (uint32_t) gl) {
       const int o = 16 * (int) cp0 - head;
       store_range((uint8_t *) (c0p + cp0), vfirst, max(dlo - o, 0), min(dhi - o, 16));
     }
-    if (((nend - 1 - cp0) & 15u) == (uint32_t) gl && nend - 1 > cp0) {
+    if (lane_of(nend - 1) == (uint32_t) gl && nend - 1 > cp0) {
       const int o = 16 * (int) (nend - 1) - head;
-      if (MODE & 4) { // diagnostic: pad the frame's last cache line (needs room)
-        uint8_t *e = (uint8_t *) (c0p + (nend - 1));
-        store_range(e, vlast, 0, 16);
-        for (e += 16; ((uintptr_t) e & 127) != 0; e += 16)
-          store_range(e, u32x4{0, 0, 0, 0}, 0, 16);
-      } else {
-        store_range((uint8_t *) (c0p + (nend - 1)), vlast, 0, min(dhi - o, 16));
-      }
+      store_range((uint8_t *) (c0p + (nend - 1)), vlast, 0, min(dhi - o, 16));
     }
   }
   // ---- header chunks: L4 bytes [0, min(dlo, send)) summed, tcp.chksum as zero
@@ -321,18 +323,11 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
     return 0;
   const dim3 grid((uint32_t) blocks), block(kBlock);
   hipStream_t s = (hipStream_t) stream;
-  switch (p->dbg) {
-  case 1: hipLaunchKernelGGL((tx_segment_kernel<3, 1>), grid, block, 0, s, *p); break;
-  case 2: hipLaunchKernelGGL((tx_segment_kernel<3, 2>), grid, block, 0, s, *p); break;
-  case 3: hipLaunchKernelGGL((tx_segment_kernel<2, 0>), grid, block, 0, s, *p); break;
-  case 4: hipLaunchKernelGGL((tx_segment_kernel<4, 0>), grid, block, 0, s, *p); break;
-  case 5: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;
-  case 6: hipLaunchKernelGGL((tx_segment_kernel<1, 0>), grid, block, 0, s, *p); break;
-  case 7: hipLaunchKernelGGL((tx_segment_kernel<6, 4>), grid, block, 0, s, *p); break;
-  case 8: hipLaunchKernelGGL((tx_segment_kernel<3, 8>), grid, block, 0, s, *p); break;
-  case 9: hipLaunchKernelGGL((tx_segment_kernel<3, 16>), grid, block, 0, s, *p); break;
-  case 10: hipLaunchKernelGGL((tx_segment_kernel<3, 25>), grid, block, 0, s, *p); break;
-  default: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;
+  switch (p->dbg) { // diagnostics (TASX_TXSEG_DEBUG, tools/txseg_probe.py)
+  case 1: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;  // 3 slots per round
+  case 2: hipLaunchKernelGGL((tx_segment_kernel<6, 1>), grid, block, 0, s, *p); break;  // no full-chunk stores
+  case 3: hipLaunchKernelGGL((tx_segment_kernel<6, 25>), grid, block, 0, s, *p); break; // no stores at all
+  default: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
