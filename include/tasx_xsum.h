@@ -221,14 +221,18 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for A/B tests (process-wide; set it before launching).
- *   0 automatic: RAW -> 2; TCP4 -> 3 for the TAS layout in stride mode with a
- *     frame-length hint, else 2
+ *   0 automatic: RAW -> 2; TCP4 -> 6 when it applies, else 3 for the TAS
+ *     layout in stride mode with a frame-length hint, else 2
  *   1 first-generation group-per-packet kernels (A/B baseline)
  *   2 raw_group_kernel / tcp4_frame_kernel (any layout)
  *   3 tcp4_tas_kernel (TAS layout, stride mode; falls back to 2)
  *   4 tcp4_tas_kernel with wave-timeline stamps into the diag buffer
  *   5 tcp4_tas_kernel with 32 lanes x 3 chunks per frame (TCP4 only; RAW
- *     uses 2) */
+ *     uses 2)
+ *   6 tcp4_tas14_kernel: TAS layout with the IPv4 header at 14 mod 16 (16-byte
+ *     aligned base and stride), stride mode, one uniform hint flen0 with
+ *     ip_off + 64 <= flen0 and the datagram within 96 chunks (uniform-MTU
+ *     batches up to ip.len 1522); otherwise as 0 */
 int tasx_set_kernel_variant(int variant);
 /* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
  * wave.  NULL disables. */

@@ -176,6 +176,30 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v)
   return v;
 }
 
+// acc + both LE 16-bit words of w (v_sad_u16 against 0): the address-aligned
+// 16-bit word sum in one VALU op per dword, exact in 32 bits
+__device__ __forceinline__ uint32_t sadw(uint32_t w, uint32_t acc)
+{
+  return __builtin_amdgcn_sad_u16(w, 0u, acc);
+}
+
+__device__ __forceinline__ uint32_t sad4(u32x4 v, uint32_t acc)
+{
+  return sadw(v.w, sadw(v.z, sadw(v.y, sadw(v.x, acc))));
+}
+
+// DPP lane moves inside 16-lane rows (lanes without a source get 0)
+template <int K>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x110 + K, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ uint32_t row_shl(uint32_t v)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x100 + K, 0xf, 0xf, false);
+}
+
 // sum of the dwords of chunk v restricted to bytes [0, h) (0 <= h <= 16)
 __device__ __forceinline__ uint64_t chunk_prefix_sum(u32x4 v, int h)
 {

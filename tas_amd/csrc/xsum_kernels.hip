@@ -28,9 +28,11 @@
 //     bytes modulo 0xffff.
 //
 // Kernels (tasx_set_kernel_variant): 2 = raw_group_kernel / tcp4_frame_kernel
-// (any layout), 3 = tcp4_tas_kernel (TAS frame layout, stride mode), 1 = the
-// first-generation group-per-packet kernels (kept as the A/B baseline),
-// 4 = tcp4_tas_kernel with wave-timeline stamps (diagnostic).
+// (any layout), 3 = tcp4_tas_kernel (TAS frame layout, stride mode), 6 =
+// tcp4_tas14_kernel (the headline: TAS frames in 16-byte aligned rooms, one
+// uniform frame-length hint), 1 = the first-generation group-per-packet
+// kernels (kept as the A/B baseline), 4 = tcp4_tas_kernel with wave-timeline
+// stamps (diagnostic), 5 = tcp4_tas_kernel with 32-lane groups (A/B).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -352,16 +354,10 @@ __device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
   return __builtin_nontemporal_load((gcu4 *) (base + off));
 }
 
+// one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave
 template <int U, int DIAG = 0, int G = 16>
-__global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
+__device__ __forceinline__ void tcp4_tas_frame(const tasx_tcp4_params &p, uint32_t i, int gl, int gbase)
 {
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 0);
-  const int gl = threadIdx.x & (G - 1);
-  const int gbase = (threadIdx.x & 63) & ~(G - 1);
-  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-  if (i >= p.n)
-    return;
   const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
   const uint32_t fo = (uint32_t) pkt_offset(p.off, p.stride, i);
   const uint32_t ipo = fo + p.ip_off;
@@ -466,6 +462,107 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
     diag_stamp<kBlock>(p, 3);
 }
 
+template <int U, int DIAG = 0, int G = 16>
+__global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
+{
+  if constexpr (DIAG)
+    diag_stamp<kBlock>(p, 0);
+  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  if (i >= p.n)
+    return;
+  tcp4_tas_frame<U, DIAG, G>(p, i, threadIdx.x & (G - 1), (threadIdx.x & 63) & ~(G - 1));
+}
+
+// TCP4 headline kernel: TAS frames in 16-byte aligned mbuf rooms (IPv4 header
+// at 14 mod 16, TCP at +20), stride mode, one uniform frame-length hint
+// (flen0, the mbuf data_len of a uniform-MTU batch) that the host has checked
+// spans 5..16U chunks.  The chunk geometry is then compile-time or uniform,
+// and the per-lane work is the fold itself: one v_sad_u16 per dword (both LE
+// 16-bit words of the dword added into a 32-bit accumulator: the
+// address-aligned word sum, exact), U loads, U selects, and a fixed header
+// split.  Chunk map (chunk c = frame bytes [16c, 16c+16), dN = its dword N):
+//   chunk 0 = eth[0,14) + ip[0,2)   IP: d3.hi
+//   chunk 1 = ip[2,18)              IP: d0, d1, d2.hi, d3 (ip.chksum = d2.lo left out)
+//                                   PH: d1 byte 3 (proto), d2.hi, d3 (src, dst)
+//   chunk 2 = ip[18,20) + tcp[0,14) IP, PH: d0.lo;  L4: d0.hi, d1..d3
+//   chunk 3 = tcp[14,30)            L4: d0.lo, d1..d3 (tcp.chksum = d0.hi left out)
+//   chunks 4.. = the segment        L4 (bytes past ip + total_length subtracted
+//                                   on lane 15, whose last load is the last chunk)
+// Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved
+// in by DPP.  A group whose ip.total_length differs from the hint is redone
+// by the general body (tcp4_tas_frame): results always follow total_length.
+template <int U>
+__global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  // uniform: the hinted datagram [ip, ip + hend) and its last chunk
+  const uint32_t hend = p.flen0 - p.ip_off;
+  const uint32_t last = (14u + hend - 1u) >> 4;
+  const uint32_t tail = 14u + hend - 16u * last; // bytes of the last chunk inside, 1..16
+  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * last;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
+
+  // chunks 0..3: the L4 part of chunk gl (none for 0, 1), whole chunks elsewhere
+  const u32x4 h = v[0];
+  const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 ? 0x0000ffffu : 0xffffffffu);
+  uint32_t acc = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
+  acc = (gl < 2 || (uint32_t) gl > last) ? 0u : acc;
+  // IP and PH channels on lane 1
+  const uint32_t c0d3 = row_shr<1>(h.w), c2d0 = row_shl<1>(h.x);
+  const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u))); // src, dst
+  const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
+  const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
+  const uint32_t tlw = h.x & 0xffffu; // ip[2,4): total_length, network order
+#pragma unroll
+  for (int u = 1; u < U; ++u) {
+    const uint32_t s = sad4(v[u], acc);
+    acc = ((uint32_t) gl + 16u * u <= last) ? s : acc;
+  }
+  // bytes [tail, 16) of the last chunk lie past the datagram.  Lane 15's last
+  // load was clamped to that chunk (15 + 16(U-1) >= last), so lane 15 takes them
+  // off (its own partial may wrap; the group total is exact mod 2^32)
+  {
+    uint32_t gm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = tail > 4u * j ? min(tail - 4u * j, 4u) : 0u;
+      gm[j] = (uint32_t) (~0ull << (8u * k));
+    }
+    const u32x4 t = v[U - 1];
+    const uint32_t g = sad4(u32x4{t.x & gm[0], t.y & gm[1], t.z & gm[2], t.w & gm[3]}, 0u);
+    acc -= gl == 15 ? g : 0u;
+  }
+  acc = row_sum16(acc);
+  const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
+  const bool bad = tl15 != hend; // meaningful on lane 15
+  if (gl == 15 && !bad) {
+    const uint32_t ipc = inv_result(residue(fold32_to_16(ip15)));
+    const uint32_t r = fold32_to_16(acc) + fold32_to_16(ph15) + bswap16(hend - 20u);
+    const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
+    if (p.out)
+      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+    if (p.flags & TASX_F_INPLACE) {
+      uint8_t *ip = p.base + a0 + 14u;
+      st8(ip + 10, ipc);
+      st8(ip + 11, ipc >> 8);
+      st8(ip + 36, tcpc);
+      st8(ip + 37, tcpc >> 8);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
+    const int gbase = (threadIdx.x & 63) & ~15;
+    if (__shfl((int) bad, gbase + 15, 64))
+      tcp4_tas_frame<U>(p, i, gl, gbase);
+  }
+}
+
 template <int G = 16, typename K, typename Prm>
 int launch_groups(K kern, const Prm &p, hipStream_t s)
 {
@@ -507,6 +604,17 @@ static bool tas_kernel_ok(const tasx_tcp4_params &p)
          (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
 }
 
+// tcp4_tas14_kernel, in addition: IPv4 header at 14 mod 16 in every frame, a
+// uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
+static bool tas14_ok(const tasx_tcp4_params &p)
+{
+  if (!tas_kernel_ok(p) || (p.ip_off & 15u) != 14u || (p.stride & 15u) != 0 || p.flen || !p.flen0)
+    return false;
+  if (p.flen0 < p.ip_off + 64u || p.flen0 - p.ip_off > 65535u)
+    return false;
+  return ((14u + (p.flen0 - p.ip_off) + 15u) >> 4) <= 16u * 6u;
+}
+
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
@@ -531,8 +639,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 {
   hipStream_t s = (hipStream_t) stream;
   const bool tas_ok = tas_kernel_ok(*p);
-  if (variant == 0) // TAS layout + frame-length hints -> tcp4_tas_kernel
-    variant = (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
+  if (variant == 6 && !tas14_ok(*p)) // headline kernel not applicable: automatic choice
+    variant = 0;
+  if (variant == 0) // uniform-MTU TAS batch -> tcp4_tas14_kernel; TAS layout + hints -> tcp4_tas_kernel
+    variant = tas14_ok(*p) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
   if (variant >= 3 && !tas_ok)
     variant = 2;
   switch (variant) {
@@ -546,6 +656,8 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
     return p->diag ? launch_groups(tcp4_tas_kernel<6, 1>, *p, s) : -2;
   case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
     return launch_groups<32>(tcp4_tas_kernel<3, 0, 32>, *p, s);
+  case 6:
+    return launch_groups(tcp4_tas14_kernel<6>, *p, s);
   default:
     return -2;
   }

@@ -242,7 +242,7 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6])
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
@@ -295,6 +295,40 @@ def test_tso_with_hints(oracle, variant):
     try:
         for hint in (None, 65549, 1514, stride):
             np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride, frame_len=hint)), exp)
+    finally:
+        xsum.set_kernel_variant(0)
+
+
+@pytest.mark.parametrize("variant", [0, 6])
+def test_tcp4_uniform_hint_every_size(oracle, variant):
+    """Uniform-MTU batches (one frame-length hint for the batch, as bench.py
+    passes it): every datagram size the headline kernel takes (ip.len 64..1522)
+    and the sizes around it, in place and to the result array; then the same
+    hint over frames whose total_length disagrees with it (the general body
+    redoes those groups)."""
+    xsum.set_kernel_variant(variant)
+    try:
+        for tl in list(range(40, 1540, 7)) + [63, 64, 65, 1500, 1521, 1522, 1523]:
+            n = 48
+            frames = pktgen.tcp4_frames(n, payload=0, stride=1536 + 64, seed=tl, ip_total_len=tl)
+            exp = oracle.tcp4_batch(frames.copy(), n, stride=1600)
+            d = to_dev(frames)
+            got = u16(xsum.tcp4_cksum_batch(d, n, stride=1600, frame_len=14 + tl))
+            np.testing.assert_array_equal(got, exp, err_msg=f"ip.len {tl}")
+            xsum.tcp4_cksum_batch(d, n, stride=1600, frame_len=14 + tl, inplace=True, want_out=False)
+            f = d.cpu().numpy().reshape(n, 1600)
+            ipc = f[:, 24].astype(np.uint16) | (f[:, 25].astype(np.uint16) << 8)
+            tcpc = f[:, 50].astype(np.uint16) | (f[:, 51].astype(np.uint16) << 8)
+            np.testing.assert_array_equal(ipc, exp[0::2], err_msg=f"in place ip.len {tl}")
+            np.testing.assert_array_equal(tcpc, exp[1::2], err_msg=f"in place ip.len {tl}")
+        # one hint, mixed total_length: every 5th frame disagrees with it
+        n = 4096
+        tl = np.full(n, 1500)
+        tl[::5] = (pktgen.splitmix64(3, n)[::5] % np.uint64(1600)).astype(np.int64)
+        frames = pktgen.tcp4_frames(n, payload=1448, stride=2048, seed=4, ip_total_len=tl)
+        exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
+        got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=2048, frame_len=1514))
+        np.testing.assert_array_equal(got, exp)
     finally:
         xsum.set_kernel_variant(0)
 
