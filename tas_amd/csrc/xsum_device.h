@@ -28,6 +28,12 @@ __device__ __forceinline__ u32x4 ld16nt(const u32x4 *p, uint32_t i)
 {
   return __builtin_nontemporal_load(&((gcu4 *) p)[i]);
 }
+// the same at a 32-bit byte offset from a uniform base: global_load_dwordx4
+// v, v_off, s[base] (one VGPR per address)
+__device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
+{
+  return __builtin_nontemporal_load((gcu4 *) (base + off));
+}
 __device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8 *) p; }
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t v) { *(gu8 *) p = (uint8_t) v; }
 template <typename T>
@@ -198,6 +204,30 @@ template <int K>
 __device__ __forceinline__ uint32_t row_shl(uint32_t v)
 {
   return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x100 + K, 0xf, 0xf, false);
+}
+
+// byte mask of [0, h) over a 16-byte chunk as two qwords (0 <= h <= 16)
+__device__ __forceinline__ void below_mask(uint32_t h, uint64_t &lo, uint64_t &hi)
+{
+  const uint64_t a = ~(~0ull << (8u * (h & 7u))); // bytes [0, h mod 8)
+  lo = h >= 8u ? ~0ull : a;
+  hi = h >= 16u ? ~0ull : (h >= 8u ? a : 0ull);
+}
+
+// word sum (sad) of the bytes [0, h) / [h, 16) of a 16-byte chunk (0 <= h <= 16)
+__device__ __forceinline__ uint32_t sad_below(u32x4 v, uint32_t h)
+{
+  uint64_t lo, hi;
+  below_mask(h, lo, hi);
+  return sad4(u32x4{v.x & (uint32_t) lo, v.y & (uint32_t) (lo >> 32), v.z & (uint32_t) hi,
+                    v.w & (uint32_t) (hi >> 32)}, 0u);
+}
+__device__ __forceinline__ uint32_t sad_from(u32x4 v, uint32_t h)
+{
+  uint64_t lo, hi;
+  below_mask(h, lo, hi);
+  return sad4(u32x4{v.x & ~(uint32_t) lo, v.y & ~(uint32_t) (lo >> 32), v.z & ~(uint32_t) hi,
+                    v.w & ~(uint32_t) (hi >> 32)}, 0u);
 }
 
 // sum of the dwords of chunk v restricted to bytes [0, h) (0 <= h <= 16)

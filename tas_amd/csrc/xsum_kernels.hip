@@ -174,6 +174,72 @@ __global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
     }
   }
 }
+// RAW, any layout, word sums by v_sad_u16 into exact 32-bit accumulators
+// (variant 6).  Rounds of U chunk loads per lane, clamped to the packet's last
+// chunk and issued back to back; chunk-index selects keep the clamped
+// re-reads out.  Bytes before the packet in chunk 0 come off on lane 0; bytes
+// past it in the last chunk on lane 15, whose last load of the final round is
+// always that chunk (its partial may wrap: the group total, < 2^32 for
+// TASX_RAW_MAX_LEN, is exact mod 2^32).
+// S32: stride mode from a 16-byte aligned base with the whole batch within
+// 4 GiB of it (host-checked): 32-bit byte offsets from the SGPR base, so each
+// load is global_load_dwordx4 v, v_off, s[base] (one VGPR per address).
+template <int U, bool S32 = false>
+__global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
+  const uint8_t *s = nullptr;
+  uint32_t o0 = 0, head, last;
+  if constexpr (S32) {
+    const uint32_t so = i * (uint32_t) p.stride;
+    o0 = so & ~15u;
+    head = so & 15u;
+    last = (head + len - 1u) >> 4; // valid when len > 0
+  } else {
+    s = p.base + pkt_offset(p.off, p.stride, i);
+    head = (uint32_t) ((uintptr_t) s & 15u);
+    last = (head + len - 1u) >> 4;
+  }
+  const u32x4 *c0p = (const u32x4 *) ((uintptr_t) s & ~(uintptr_t) 15);
+  uint32_t acc = 0;
+  if (len) {
+    u32x4 t;
+    for (uint32_t cb = 0; cb <= last; cb += 16u * U) {
+      u32x4 v[U];
+      if constexpr (S32) {
+        const uint32_t lb = o0 + 16u * (cb + (uint32_t) gl), lastoff = o0 + 16u * last;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] = ld16nt_off(p.base, min(lb + 256u * u, lastoff));
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] = ld16nt(c0p, min(cb + (uint32_t) gl + 16u * u, last));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t a = sad4(v[u], acc);
+        acc = cb + (uint32_t) gl + 16u * u <= last ? a : acc;
+      }
+      if (cb == 0)
+        acc -= gl == 0 ? sad_below(v[0], head) : 0u;
+      t = v[U - 1];
+    }
+    acc -= gl == 15 ? sad_from(t, head + len - 16u * last) : 0u;
+  }
+  acc = row_sum16(acc);
+  if (gl == 15) {
+    uint32_t f = fold32_to_16(acc);
+    if (head & 1)
+      f = bswap16(f);
+    stg(p.out, i, (uint16_t) f);
+  }
+}
+
 // TCP4, any frame layout: header words and the checksum-field bytes by byte
 // loads, then the segment chunks.  With a frame-length hint (the mbuf
 // data_len tx_send() sets before tx_flush) the chunk loads are issued together
@@ -349,10 +415,6 @@ __device__ __forceinline__ uint32_t pat_bits(uint64_t pat, int s)
   return s < 64 ? (uint32_t) (pat >> s) & 0xfu : 0u;
 }
 
-__device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
-{
-  return __builtin_nontemporal_load((gcu4 *) (base + off));
-}
 
 // one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave
 template <int U, int DIAG = 0, int G = 16>
@@ -619,12 +681,19 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
 {
   hipStream_t s = (hipStream_t) stream;
   switch (variant) {
-  case 0:
   case 2:
   case 3:
+  case 4:
+  case 5:
     return launch_groups(raw_group_kernel<6>, *p, s);
   case 1:
     return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+  case 0:
+  case 6:
+    if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
+        (uint64_t) p->n * p->stride + p->len0 + 16u < (1ull << 32) && p->len == nullptr)
+      return launch_groups(raw_sad_kernel<6, true>, *p, s);
+    return launch_groups(raw_sad_kernel<6>, *p, s);
   default:
     return -2;
   }

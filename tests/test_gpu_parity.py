@@ -270,7 +270,7 @@ def test_tcp4_all_variants_and_hints(oracle, variant):
         xsum.set_kernel_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6])
 def test_raw_all_variants(oracle, variant):
     buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
     n = len(lens)
