@@ -185,17 +185,18 @@ class RxVerifyWorkload:
         self.bytes_per_step = wl.n * (wl.ip_total + 1)
 
     def launcher(self):
-        fn = xsum.lib().tasx_tcp4_verify_batch_dev
+        # the received frames' length (mbuf data_len) as the prefetch hint
+        fn = xsum.lib().tasx_tcp4_verify_batch_dev_hint
         stream = torch.cuda.current_stream().cuda_stream
         wl = self.wl
-        args = [(b.data_ptr(), None, wl.stride, wl.n, pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN,
-                 f.data_ptr(), stream) for b, f in zip(wl.bufs, wl.rx_flags)]
+        args = [(b.data_ptr(), None, wl.stride, None, wl.hint, wl.n, pktgen.ETH_LEN,
+                 pktgen.ETH_LEN + pktgen.IP_LEN, f.data_ptr(), stream) for b, f in zip(wl.bufs, wl.rx_flags)]
         R = len(args)
 
         def launch(k):
             rc = fn(*args[k % R])
             if rc:
-                raise xsum.TasxError(rc, "tasx_tcp4_verify_batch_dev")
+                raise xsum.TasxError(rc, "tasx_tcp4_verify_batch_dev_hint")
         return launch
 
 
@@ -629,7 +630,8 @@ def main():
     xsum.tcp4_cksum_batch(wl.bufs[0], wl.n, stride=wl.stride, inplace=True, want_out=False)
     for b in wl.bufs[1:]:
         b.copy_(wl.bufs[0])
-    rx = leg(RxVerifyWorkload(wl), args, ws, "same frames after TX checksums, tasx_tcp4_verify_batch_dev")
+    rx = leg(RxVerifyWorkload(wl), args, ws, "same frames after TX checksums, tasx_tcp4_verify_batch_dev_hint "
+             "(received frame length as the hint)")
     torch.cuda.synchronize()
     rx["all_frames_verified"] = bool((wl.rx_flags[0] == 3).all().item())
     src = torch.from_numpy(wl.host).cuda()

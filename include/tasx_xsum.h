@@ -110,6 +110,12 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
 int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream);
+/* Same, with frame-length hints (the received mbuf's data_len, flen[i], or
+ * flen0 for the whole batch when flen == NULL; 0 = none), as for
+ * tasx_tcp4_cksum_batch_dev_hint: the flags always follow ip.total_length. */
+int tasx_tcp4_verify_batch_dev_hint(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream);
 
 /* Fused TX segment build: the payload copy of
  * flow_tx_segment() -- flow_tx_read() from the flow's circular transmit buffer

@@ -149,6 +149,14 @@ int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream)
 {
+  return tasx_tcp4_verify_batch_dev_hint(base, off, stride, NULL, 0, n, ip_off,
+      l4_off, flags, stream);
+}
+
+int tasx_tcp4_verify_batch_dev_hint(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream)
+{
   tasx_tcp4_params p;
   if (n == 0)
     return 0;
@@ -162,7 +170,9 @@ int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
   p.n = n;
   p.ip_off = ip_off;
   p.l4_off = l4_off;
-  if (tasx_launch_tcp4_verify(&p, stream) != 0)
+  p.flen = flen;
+  p.flen0 = flen0;
+  if (tasx_launch_tcp4_verify(&p, g_variant, stream) != 0)
     return hip_err(hipGetLastError(), "tcp4 verify kernel launch");
   return 0;
 }

@@ -70,7 +70,7 @@ typedef struct tasx_flow_params {
 int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 /* receive-side verification; p->out points to n flag bytes */
-int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream);
+int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream);
 /* RX flow lookup (flow_kernels.hip) */
 int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */

@@ -404,6 +404,9 @@ __device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
 constexpr uint64_t kPatIP = (((1ull << 10) - 1) << 16) | (((1ull << 8) - 1) << 28);  // [0,10)+[12,20)
 constexpr uint64_t kPatPH = (1ull << 25) | (((1ull << 8) - 1) << 28);                // {9}+[12,20)
 constexpr uint64_t kPatNL4 = ((1ull << 36) - 1) | (3ull << 52);                     // [-16,20)+{36,37}
+// receive-side check: the checksum fields are summed as received
+constexpr uint64_t kPatIPV = ((1ull << 20) - 1) << 16;                               // [0,20)
+constexpr uint64_t kPatNL4V = (1ull << 36) - 1;                                      // [-16,20)
 
 __device__ __forceinline__ uint32_t expand4(uint32_t bits)
 {
@@ -416,10 +419,12 @@ __device__ __forceinline__ uint32_t pat_bits(uint64_t pat, int s)
 }
 
 
-// one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave
-template <int U, int DIAG = 0, int G = 16>
-__device__ __forceinline__ void tcp4_tas_frame(const tasx_tcp4_params &p, uint32_t i, int gl, int gbase)
+// one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave.
+// VERIFY: the receive-side flags of tcp4_frame_kernel<U, true> instead.
+template <int U, int DIAG = 0, int G = 16, bool VERIFY = false>
+__device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, int gl, int gbase)
 {
+  constexpr uint64_t pat_ip = VERIFY ? kPatIPV : kPatIP, pat_nl4 = VERIFY ? kPatNL4V : kPatNL4;
   const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
   const uint32_t fo = (uint32_t) pkt_offset(p.off, p.stride, i);
   const uint32_t ipo = fo + p.ip_off;
@@ -459,9 +464,9 @@ __device__ __forceinline__ void tcp4_tas_frame(const tasx_tcp4_params &p, uint32
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int sft = 16 * gl + 4 * j - hb + 16;
-      acc_ip += w[j] & expand4(pat_bits(kPatIP, sft));
+      acc_ip += w[j] & expand4(pat_bits(pat_ip, sft));
       acc_ph += w[j] & expand4(pat_bits(kPatPH, sft));
-      uint32_t ml4 = ~expand4(pat_bits(kPatNL4, sft));
+      uint32_t ml4 = ~expand4(pat_bits(pat_nl4, sft));
       if ((uint32_t) gl == last) // a short segment ends in this chunk: bytes < tail only
         ml4 &= in_range(4 * j, 0, tail);
       acc += l4ok ? (w[j] & ml4) : 0u;
@@ -499,7 +504,28 @@ __device__ __forceinline__ void tcp4_tas_frame(const tasx_tcp4_params &p, uint32
   part = group_total<G>(part);
   c_ip = group_total<G>(c_ip);
   c_ph = group_total<G>(c_ph);
-  if (gl == G - 1) {
+  if constexpr (VERIFY) {
+    const uint32_t vihl = (uint32_t) __shfl((int) chunk_byte(v[0], hb & 15), gbase + (hb >> 4), 64);
+    if (gl == G - 1) {
+      // every sum above is exact, so the folds are rte_raw_cksum's values
+      uint32_t ri = fold32_to_16(c_ip);
+      if (hb & 1)
+        ri = bswap16(ri);
+      uint32_t flags = ri == 0xffffu ? TASX_RX_IP_OK : 0u;
+      if (tl >= 20) {
+        uint32_t r4 = fold32_to_16(part), rp = fold32_to_16(c_ph);
+        if (hb & 1) {
+          r4 = bswap16(r4);
+          rp = bswap16(rp);
+        }
+        uint32_t c = r4 + fold32_to_16(rp + bswap16(len)); // + rte_ipv4_phdr_cksum
+        c = (c >> 16) + (c & 0xffffu);
+        flags |= c == 0xffffu ? TASX_RX_L4_OK : 0u;
+      }
+      flags |= (vihl & 0xfu) != 5u ? TASX_RX_IHL_NOT5 : 0u;
+      stg((uint8_t *) p.out, i, (uint8_t) flags);
+    }
+  } else if (gl == G - 1) {
     uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
     if (hb & 1) {
       ri = bswap16(ri);
@@ -553,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved
 // in by DPP.  A group whose ip.total_length differs from the hint is redone
 // by the general body (tcp4_tas_frame): results always follow total_length.
-template <int U>
+template <int U, bool VERIFY = false>
 __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -573,14 +599,16 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
 
   // chunks 0..3: the L4 part of chunk gl (none for 0, 1), whole chunks elsewhere
   const u32x4 h = v[0];
-  const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 ? 0x0000ffffu : 0xffffffffu);
+  const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 && !VERIFY ? 0x0000ffffu : 0xffffffffu);
   uint32_t acc = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
   acc = (gl < 2 || (uint32_t) gl > last) ? 0u : acc;
   // IP and PH channels on lane 1
   const uint32_t c0d3 = row_shr<1>(h.w), c2d0 = row_shl<1>(h.x);
   const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u))); // src, dst
   const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
-  const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
+  uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
+  if constexpr (VERIFY) // the received ip.chksum is part of the check
+    ipsum = sadw(h.z & 0xffffu, ipsum);
   const uint32_t tlw = h.x & 0xffffu; // ip[2,4): total_length, network order
 #pragma unroll
   for (int u = 1; u < U; ++u) {
@@ -604,7 +632,18 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
   const bool bad = tl15 != hend; // meaningful on lane 15
-  if (gl == 15 && !bad) {
+  if constexpr (VERIFY) {
+    const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
+    if (gl == 15 && !bad) {
+      // exact rte_raw_cksum values (every sum above is exact)
+      uint32_t flags = fold32_to_16(ip15) == 0xffffu ? TASX_RX_IP_OK : 0u;
+      uint32_t c = fold32_to_16(acc) + fold32_to_16(ph15 + bswap16(hend - 20u)); // + rte_ipv4_phdr_cksum
+      c = (c >> 16) + (c & 0xffffu);
+      flags |= c == 0xffffu ? TASX_RX_L4_OK : 0u;
+      flags |= (vihl & 0xfu) != 5u ? TASX_RX_IHL_NOT5 : 0u;
+      stg((uint8_t *) p.out, i, (uint8_t) flags);
+    }
+  } else if (gl == 15 && !bad) {
     const uint32_t ipc = inv_result(residue(fold32_to_16(ip15)));
     const uint32_t r = fold32_to_16(acc) + fold32_to_16(ph15) + bswap16(hend - 20u);
     const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
@@ -620,8 +659,9 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
   }
   if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
-    if (__shfl((int) bad, gbase + 15, 64))
-      tcp4_tas_frame<U>(p, i, gl, gbase);
+    if (__shfl((int) bad, gbase + 15, 64)) {
+      tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
+    }
   }
 }
 
@@ -699,8 +739,10 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
   }
 }
 
-extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, void *stream)
+extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
+  if ((variant == 0 || variant == 6) && tas14_ok(*p))
+    return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream);
   return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 

@@ -46,6 +46,8 @@ SIGNATURES = {
     "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                 _c_u32, _vp]),
     "tasx_tcp4_verify_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
+    "tasx_tcp4_verify_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
+                                                 _vp]),
     "tasx_flow_lookup_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32,
                                             _c_u32, _c_u32, _vp, _vp, _vp]),
     "tasx_tx_segment_batch_dev": (_c_int, [_vp, _c_u64, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _vp]),
@@ -186,15 +188,27 @@ RX_IP_OK, RX_L4_OK, RX_IHL_NOT5 = 0x1, 0x2, 0x4
 
 def tcp4_verify_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
                       stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
-                      out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                      out: torch.Tensor | None = None, frame_len: torch.Tensor | int | None = None,
+                      stream=None) -> torch.Tensor:
     """Receive-side checksum verification of n frames: uint8 flags per frame
-    (RX_IP_OK | RX_L4_OK | RX_IHL_NOT5)."""
+    (RX_IP_OK | RX_L4_OK | RX_IHL_NOT5).  frame_len: optional received frame
+    lengths (int32 tensor, or one int for all frames) -- prefetch only."""
     if out is None:
         out = torch.empty(n, dtype=torch.uint8, device=frames.device)
     if offsets is not None:
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
-    _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
-                                            _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
+    if frame_len is None:
+        _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
+                                                _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
+    else:
+        if isinstance(frame_len, int):
+            flen, flen0 = None, frame_len
+        else:
+            assert frame_len.dtype == torch.int32 and frame_len.numel() >= n
+            flen, flen0 = frame_len, 0
+        _check(lib().tasx_tcp4_verify_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0, n,
+                                                     ip_off, l4_off, _ptr(out), _stream(stream)),
+               "tasx_tcp4_verify_batch_dev_hint")
     return out
 
 

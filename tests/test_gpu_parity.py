@@ -526,3 +526,41 @@ def test_verify_edges(oracle, tcp4_golden, shift):
     buf[shift:shift + mixed.size] = to_dev(mixed)
     got = xsum.tcp4_verify_batch(buf[shift:], 2 * n, stride=stride).cpu().numpy()
     np.testing.assert_array_equal(got, oracle.tcp4_verify_batch(mixed, 2 * n, stride=stride))
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_verify_uniform_hint(oracle, variant):
+    """Received uniform-MTU batches with one frame-length hint (the headline
+    kernel's verify mode): good frames, single-bit corruption anywhere in the
+    datagram (checksum fields included), IHL 6, and total_length disagreeing
+    with the hint (general body); then every datagram size it takes."""
+    xsum.set_kernel_variant(variant)
+    try:
+        n = 8192
+        frames = pktgen.tcp4_frames(n, payload=1448, stride=2048, seed=91)
+        d = to_dev(frames)
+        xsum.tcp4_cksum_batch(d, n, stride=2048, inplace=True, want_out=False)
+        h = d.cpu().numpy()
+        rng = pktgen.splitmix64(92, n)
+        pos = 14 + (rng % np.uint64(1500)).astype(np.int64)
+        bit = (rng >> np.uint64(61)).astype(np.int64)
+        sel = np.arange(0, n, 3)
+        h[sel * 2048 + pos[sel]] ^= (1 << bit[sel]).astype(np.uint8)
+        f = h.reshape(n, 2048)
+        f[1::11, 14] = 0x46                         # IHL 6
+        f[2::13, 16:18] = [0x05, 0x00]              # total_length 1280 (hint disagrees)
+        f[4::17, 24:26] ^= 0xFF                     # ip.chksum flipped
+        f[5::19, 50:52] = 0                         # tcp.chksum zeroed
+        exp = oracle.tcp4_verify_batch(h, n, stride=2048)
+        got = xsum.tcp4_verify_batch(to_dev(h), n, stride=2048, frame_len=1514).cpu().numpy()
+        np.testing.assert_array_equal(got, exp)
+        for tl in list(range(40, 1540, 11)) + [64, 1500, 1522, 1523]:
+            m = 32
+            fr = pktgen.tcp4_frames(m, payload=0, stride=1600, seed=tl, ip_total_len=tl)
+            oracle.tcp4_batch(fr, m, stride=1600, inplace=True)
+            fr.reshape(m, 1600)[::4, 40] ^= 0x10        # corrupt a quarter (a tcp header byte)
+            exp = oracle.tcp4_verify_batch(fr, m, stride=1600)
+            got = xsum.tcp4_verify_batch(to_dev(fr), m, stride=1600, frame_len=14 + tl).cpu().numpy()
+            np.testing.assert_array_equal(got, exp, err_msg=f"ip.len {tl}")
+    finally:
+        xsum.set_kernel_variant(0)
