@@ -125,21 +125,15 @@ int main(int argc, char **argv)
   printf("65536 frames, %d rotating buffers of %zu B, %d launches x 5 reps\n", R, B, K);
   for (int rep = 0; rep < 2; ++rep) {
     fcase<16, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);    // the headline pattern
-    fcase<16, 1, 95, 256, 64>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 256, 128>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 256, 256>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 256, 512>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s, 21 * 1024); // 7 blocks/CU
-    fcase<16, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s, 26 * 1024); // 6 blocks/CU
-    fcase<64, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s, 21 * 1024);
-    fcase<16, 1, 95, 256>("packed", buf, n, 1520, out, R, K, s);  // same bytes, contiguous
-    fcase<16, 1, 96, 256>("packed1536", buf, n, 1536, out, R, K, s);
-    fcase<16, 1, 128, 256>("full2048", buf, n, 2048, out, R, K, s); // whole mbuf rooms
-    fcase<16, 2, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 512>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<16, 1, 95, 128>("mbuf", buf, n, 2048, out, R, K, s);
-    fcase<32, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);
     fcase<64, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 1, 95, 128>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 1, 95, 512>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 1, 95, 1024>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 2, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 1, 95, 256, 32>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<64, 1, 95, 256, 64>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<32, 1, 95, 256>("mbuf", buf, n, 2048, out, R, K, s);
+    fcase<16, 1, 95, 256, 64>("mbuf", buf, n, 2048, out, R, K, s);
   }
   return 0;
 }
