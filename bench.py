@@ -244,11 +244,14 @@ class TxSegWorkload:
     written + the 20 B IP header and hdrs_len - l4_off L4 header bytes read +
     4 B of checksums written."""
     desc = (f"{N_FRAMES} TAS TX segments of {pktgen.TCP_MSS} B payload from 8192 flows' 16 KiB circular TX "
-            f"buffers (wraps included) into 1514 B frames at {STRIDE} B stride, checksums in place")
+            f"buffers (wraps included) into 1514 B frames at {STRIDE} B stride (descriptor room = the {STRIDE} B "
+            "mbuf data room), checksums in place")
 
     def __init__(self, rotate: int, seed: int, n: int = N_FRAMES):
         self.n = n
-        _, _, segs, shm_len = pktgen.tx_segments(n, seed=seed, nflows=8192, tx_len=16384, make_shm=False)
+        # room = the mbuf data room (TAS: BUFFER_SIZE, tas/fast/internal.h:34)
+        _, _, segs, shm_len = pktgen.tx_segments(n, seed=seed, nflows=8192, tx_len=16384, make_shm=False,
+                                                 room=STRIDE)
         self.segs_np, self.shm_len = segs, shm_len
         self.segs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
         self.shms = [device_random(shm_len, seed + 7 + r) for r in range(rotate)]

@@ -131,7 +131,10 @@ typedef struct tasx_tx_seg {
   uint32_t pos;       /* payload_pos, the read position in the TX buffer */
   uint16_t payload;   /* payload bytes */
   uint16_t hdrs_len;  /* payload offset in the frame (66 in TAS data segments) */
-  uint32_t reserved;  /* 0 */
+  uint32_t room;      /* bytes from the frame start the build may rewrite (with
+                       * their own values past the frame): the mbuf data room,
+                       * BUFFER_SIZE in TAS (tas/fast/internal.h:34); 0 = only
+                       * [0, hdrs_len + payload) */
 } tasx_tx_seg;
 /* For each segment: copy `payload` bytes from shm + tx_base at circular
  * position pos into frame + hdrs_len, then store ip.chksum / tcp.chksum into
@@ -145,7 +148,9 @@ typedef struct tasx_tx_seg {
  * shm_len < 4 GiB (TAS's shared region is far smaller); l4_off >= ip_off + 20.
  * Frames must not overlap.  Besides the payload and the two checksum fields,
  * the header bytes [0, hdrs_len) are rewritten with their own values (whole
- * cache lines avoid HBM read-modify-write).  Asynchronous on `stream`. */
+ * cache lines avoid HBM read-modify-write), and so are the bytes between the
+ * frame's end and the end of its last 16-byte chunk when `room` covers them.
+ * Asynchronous on `stream`. */
 int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
     const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint32_t *out, void *stream);

@@ -69,7 +69,7 @@ struct oracle_tx_seg {
   uint64_t frame_off, tx_base;
   uint32_t tx_len, pos;
   uint16_t payload, hdrs_len;
-  uint32_t reserved;
+  uint32_t room;     /* ignored: the oracle writes exactly the frame's bytes */
 };
 void oracle_tx_segment_batch(const uint8_t *shm, uint64_t shm_len,
     uint8_t *frames, const struct oracle_tx_seg *segs, size_t n,

@@ -6,7 +6,12 @@
 // then the checksum loop); here each payload byte is read once from the TX
 // buffer, written once into the frame, and summed from registers.
 //
-// Layout: one 16-lane group (a DPP row) per segment, as in the checksum
+// Kernels (tasx_launch_txseg): tx_segment_tas_kernel (the default for TAS's
+// layout: one unaligned window load per frame chunk, fixed header geometry),
+// tx_segment_u_kernel (any layout, same load scheme: txseg_row), and the
+// first-generation aligned-gather kernel below (TASX_TXSEG_DEBUG=4, A/B).
+//
+// Aligned-gather kernel layout: one 16-lane group (a DPP row) per segment, as in the checksum
 // kernels.  The group walks the frame's address-aligned 16-byte chunks
 // covering [l4_off, hdrs_len + payload).  For a chunk that holds payload bytes
 // the lane loads the two aligned source chunks spanning the payload bytes'
@@ -313,6 +318,400 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
   }
 }
 
+// ---------------------------------------------------------------------------
+// tx_segment_u_kernel: the same segment build with ONE UNALIGNED 16-byte load
+// per destination chunk (gfx950 global loads take any byte address; measured
+// as fast as aligned loads for this copy, tools/copy_unaligned.hip), so there
+// is no funnel shift, no neighbour exchange and no exception chunk: the lane
+// that owns frame chunk k loads the payload window that lands in it straight
+// from the TX buffer, stores it and sums it from the registers.
+//   frame chunk k = frame bytes [16k - fh, +16) (fh = frame start mod 16);
+//   payload index j at s1 + j before the buffer wraps (j < wrap), s2 + j after;
+//   the window of chunk k starts at payload index j0 = 16k - fh - hdrs_len.
+// Window loads are clamped to [0, shm_len - 16]; a window that had to be
+// clamped (a flow buffer within 16 bytes of the region's ends) is gathered
+// byte by byte instead.  The chunk holding the wrap takes its bytes from
+// index `wrap` on from a piece-2 window loaded up front.  Header chunks (frame
+// bytes [0, hdrs_len), at most 16 of them: the host checks that the checksum
+// fields lie in the first 256 bytes) are loaded up front, get their payload
+// bytes spliced in, and are written back at the end with both checksums
+// inserted; payload chunks are stored as they are built (byte-exact stores at
+// the frame's last partial chunk, nothing outside [0, hdrs_len + payload)).
+// Lanes own chunks by ADDRESS (lane = absolute chunk index mod 16), so each
+// store instruction covers whole 256-byte blocks.  Sums are exact 32-bit word
+// sums (v_sad_u16) over frame bytes [l4_off, l4_off + len), tcp.chksum as 0.
+
+// bytes [lo, hi) of ins, the rest of base (lo, hi in [0, 16])
+__device__ __forceinline__ u32x4 splice(u32x4 base, u32x4 ins, int lo, int hi)
+{
+  uint64_t l0, l1, h0, h1;
+  below_mask((uint32_t) min(max(lo, 0), 16), l0, l1);
+  below_mask((uint32_t) min(max(hi, 0), 16), h0, h1);
+  const uint64_t m0 = h0 & ~l0, m1 = h1 & ~l1;
+  const uint32_t m[4] = {(uint32_t) m0, (uint32_t) (m0 >> 32), (uint32_t) m1, (uint32_t) (m1 >> 32)};
+  return u32x4{(ins.x & m[0]) | (base.x & ~m[0]), (ins.y & m[1]) | (base.y & ~m[1]),
+               (ins.z & m[2]) | (base.z & ~m[2]), (ins.w & m[3]) | (base.w & ~m[3])};
+}
+
+// word sum of bytes [lo, hi) of v (lo, hi in [0, 16])
+__device__ __forceinline__ uint32_t sad_range(u32x4 v, int lo, int hi)
+{
+  uint64_t l0, l1, h0, h1;
+  below_mask((uint32_t) min(max(lo, 0), 16), l0, l1);
+  below_mask((uint32_t) min(max(hi, 0), 16), h0, h1);
+  const uint64_t m0 = h0 & ~l0, m1 = h1 & ~l1;
+  return sad4(u32x4{v.x & (uint32_t) m0, v.y & (uint32_t) (m0 >> 32), v.z & (uint32_t) m1,
+                    v.w & (uint32_t) (m1 >> 32)}, 0u);
+}
+
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4u gcu4u;
+
+// 16 bytes at any byte offset (global_load_dwordx4 at an unaligned address)
+__device__ __forceinline__ u32x4 ld16u(const uint8_t *base, uint32_t off)
+{
+  const u32x4u v = *(gcu4u *) (base + off);
+  return u32x4{v.x, v.y, v.z, v.w};
+}
+
+// the window at shm offset `off` byte by byte; bytes outside [0, shm_len) as 0
+__device__ __noinline__ u32x4 gather16(const uint8_t *shm, uint32_t off, uint64_t shm_len)
+{
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  for (int b = 0; b < 16; ++b) {
+    const uint32_t a = off + (uint32_t) b;
+    if (a < shm_len)
+      w[b >> 2] |= ld8(shm + a) << (8 * (b & 3));
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+// segment i on the 16 lanes of one DPP row (lane gl); any frame layout
+template <int U, bool NTS>
+__device__ __forceinline__ void txseg_row(const tasx_txseg_params &p, uint32_t i, int gl)
+{
+  const u32x4 d0 = ld16((const u32x4 *) p.segs, 2 * i), d1 = ld16((const u32x4 *) p.segs, 2 * i + 1);
+  const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
+  const uint64_t tx_base = d0.z | ((uint64_t) d0.w << 32);
+  const uint32_t tx_len = d1.x, pos = d1.y, pay_ = d1.z & 0xffffu, hl_ = d1.z >> 16;
+  const bool ok = (pay_ == 0 || pos < tx_len) && pay_ <= tx_len && tx_base <= p.shm_len &&
+                  tx_len <= p.shm_len - tx_base && hl_ >= p.l4_off + 20;
+  if (!ok) {
+    if (gl == 15 && p.out)
+      stg(p.out, i, 0u);
+    return;
+  }
+  uint8_t *const f = p.frames + frame_off;
+  uint8_t *const ip = f + p.ip_off;
+  const int fh = (int) ((uintptr_t) f & 15);
+  uint8_t *const c0 = f - fh;
+  const int hl = (int) hl_, pay = (int) pay_, fend = hl + pay;
+  // chunks: [0, nhc) hold header bytes, [nhc, kpay) are whole payload chunks,
+  // [kpay, K) the partial last one
+  const int K = (fh + fend + 15) >> 4, nhc = (fh + hl + 15) >> 4, kpay = max((fh + fend) >> 4, nhc);
+  // TX buffer pieces (32-bit shm offsets, modular)
+  const uint8_t *const shm = p.shm;
+  const uint32_t s1 = (uint32_t) (tx_base + pos), s2 = s1 - tx_len;
+  const int wrap = (int) tx_len - (int) pos;
+  const bool wraps = pay > 0 && wrap < pay;
+  const uint32_t smax = (uint32_t) (p.shm_len - 16u);
+  auto woff = [&](int j0) -> uint32_t { return (wraps && j0 >= wrap ? s2 : s1) + (uint32_t) j0; };
+  // the chunk holding payload index `wrap` (not on a chunk boundary) and its piece-2 window
+  const bool straddle = wraps && ((fh + hl + wrap) & 15);
+  const int ks = straddle ? (fh + hl + wrap) >> 4 : -1;
+  const uint32_t xoff = straddle ? s2 + (uint32_t) (16 * ks - fh - hl) : woff(16 * nhc - fh - hl);
+
+  // ---- up-front loads: IPv4 header words, total_length, this lane's header
+  // chunk, its boundary chunk's window, the straddle chunk's piece-2 window
+  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  const int wl = min(gl, 9);
+  const uint32_t w_ = ld8(ip + 2 * wl) | (ld8(ip + 2 * wl + 1) << 8);
+  const uint32_t w = gl < 10 ? w_ : 0u;
+  const u32x4 hv = ld16((const u32x4 *) c0, (uint32_t) min(gl, nhc - 1));
+  // boundary entries: b < nhc header chunk b, b == nhc the straddle chunk,
+  // b == nhc + 1 the partial last chunk
+  const int bk0 = gl < nhc ? gl : gl == nhc ? ks : kpay;
+  // (nothing below uses total_length before the whole-chunk loads are issued:
+  // the loads above and the loop's loads share one memory latency)
+  const int bkc = min(max(bk0, 0), K - 1);
+  const uint32_t boff = woff(16 * bkc - fh - hl);
+  const u32x4 bw = ld16u(shm, min(boff, smax));
+  const u32x4 xw = ld16u(shm, min(xoff, smax));
+
+  // ---- whole payload chunks [nhc, kpay) but the straddle chunk: U unaligned
+  // window loads per lane, then stores and sums from the registers.  Lanes own
+  // chunks by address, so each store instruction covers whole 256-byte blocks.
+  uint32_t acc = 0;
+  const int aoff = (int) (((uintptr_t) c0 >> 4) & 15u);
+  for (int base = nhc - ((nhc + aoff) & 15); base < kpay; base += 16 * U) {
+    u32x4 a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = min(max(base + gl + 16 * u, nhc), kpay - 1);
+      a[u] = ld16u(shm, min(woff(16 * k - fh - hl), smax));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = base + gl + 16 * u;
+      const bool in = k >= nhc && k < kpay && k != ks;
+      if (in) {
+        uint8_t *const cp = c0 + 16 * k;
+        if (NTS)
+          __builtin_nontemporal_store(a[u], (__attribute__((address_space(1))) u32x4 *) cp);
+        else
+          *(__attribute__((address_space(1))) u32x4 *) cp = a[u];
+      }
+      const uint32_t t = sad4(a[u], acc);
+      acc = in ? t : acc;
+    }
+  }
+  const uint32_t len = tl >= 20 ? tl - 20 : 0;
+  const int sum_lo = (int) p.l4_off, sum_end = sum_lo + (int) len, sum_hi = min(sum_end, fend);
+  const int ck = (int) p.l4_off + 16 + fh; // tcp.chksum's chunk-grid position
+  // total_length ends inside the whole payload chunks (never for flow_tx_segment's
+  // frames, :897): take their bytes from sum_hi on back off
+  for (int k = max((fh + sum_hi) >> 4, nhc) + gl; k < kpay; k += 16) {
+    if (k == ks)
+      continue;
+    const int o = 16 * k - fh;
+    acc -= sad_range(ld16u(shm, woff(o - hl)), sum_hi - o, 16);
+  }
+
+  // ---- boundary chunks (generic; one entry per lane in the common case)
+  u32x4 vh = hv;
+  for (int b = gl; b < nhc + 2; b += 16) {
+    int k;
+    if (b < nhc)
+      k = b;
+    else if (b == nhc)
+      k = (straddle && ks >= nhc && ks < kpay) ? ks : -1;
+    else
+      k = kpay < K ? kpay : -1;
+    if (k < 0)
+      continue;
+    const int o = 16 * k - fh, j0 = o - hl;
+    u32x4 v;
+    if (pay > 0 && o + 16 > hl && o < fend) { // payload bytes [hl - o, fend - o) of this chunk
+      const uint32_t off = woff(j0);
+      u32x4 win = (b == gl && k == bk0 && off <= smax) ? bw : (off <= smax ? ld16u(shm, off) : gather16(shm, off, p.shm_len));
+      if (k == ks)
+        win = splice(win, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap - j0, 16);
+      v = win;
+      if (k < nhc)
+        v = splice(b < 16 ? hv : ld16((const u32x4 *) c0, (uint32_t) k), win, hl - o, fend - o);
+    } else {
+      v = b < 16 ? hv : ld16((const u32x4 *) c0, (uint32_t) k);
+    }
+    u32x4 sv = v;
+    if (k < nhc) { // tcp.chksum taken as zero
+      sv = put_byte(sv, ck - 16 * k, 0u);
+      sv = put_byte(sv, ck + 1 - 16 * k, 0u);
+    }
+    acc += sad_range(sv, sum_lo - o, sum_hi - o);
+    if (b < 16 && k < nhc)
+      vh = v; // written back with the checksums at the end
+    else
+      store_range(c0 + 16 * k, v, max(-o, 0), min(fend - o, 16), false);
+  }
+  uint32_t part = acc;
+  if (sum_end > fend) { // total_length reaches past the frame's written bytes
+    const Chunks<U> t = chunk_range<U>(f + fend, (uint32_t) (sum_end - fend));
+    part += group_lane_sum<U>(t, gl);
+  }
+  const uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0u;
+  const uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
+  part = row_sum16(part);
+  const uint32_t s_ip = row_sum16(c_ip), s_ph = row_sum16(c_ph);
+  const uint32_t ipc = inv_result(residue(fold32_to_16(s_ip)));
+  uint32_t tcpc = 0;
+  if (tl >= 20) {
+    uint32_t r4 = fold32_to_16(part);
+    if ((fh + (int) p.l4_off) & 1)
+      r4 = bswap16(r4);
+    tcpc = inv_result(residue(fold32_to_16(r4 + s_ph + bswap16(len))));
+  }
+  const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
+  if (gl == 15 && p.out)
+    stg(p.out, i, res);
+  // header write-back: frame bytes [0, min(hdrs_len, frame end)) of chunk gl, checksums inserted
+  if (gl < nhc) {
+    const int b0 = 16 * gl, fi = (int) p.ip_off + 10 + fh;
+    u32x4 v = put_byte(vh, fi - b0, res);
+    v = put_byte(v, fi + 1 - b0, res >> 8);
+    v = put_byte(v, ck - b0, res >> 16);
+    v = put_byte(v, ck + 1 - b0, res >> 24);
+    store_range(c0 + b0, v, max(fh - b0, 0), min(fh + fend - b0, 16), false);
+  }
+}
+
+template <int U, bool NTS>
+__global__ __launch_bounds__(kBlock) void tx_segment_u_kernel(tasx_txseg_params p)
+{
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group leaves together
+  txseg_row<U, NTS>(p, i, threadIdx.x & 15);
+}
+
+// DPP row rotate: lane k of each 16-lane row gets lane (k - N) % 16's value
+template <int N>
+__device__ __forceinline__ uint32_t row_ror(uint32_t x)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x120 + N, 0xf, 0xf, false);
+}
+
+// ---------------------------------------------------------------------------
+// tx_segment_tas_kernel: TAS data segments as flow_tx_segment() builds them
+// (fast_flows.c:877-955): IPv4 at frame + 14, TCP at + 34 (host-checked for
+// the batch), hdrs_len 66 (TCP header + 12-byte timestamp option, :887-888),
+// frames 16-byte aligned (the mbuf data room).  The header geometry is then
+// fixed and the per-chunk work is the copy itself: frame chunk k >= 5 holds
+// payload [16k - 66, 16k - 50), one unaligned window load, one store, four
+// v_sad_u16.  Chunks 0..4 (ethernet + IPv4 + TCP + option, and chunk 4's
+// first 14 payload bytes) are read from the frame and written back whole at
+// the end with both checksums inserted; the IPv4 / pseudo-header channels
+// come from chunks 0..2 as in tcp4_tas14_kernel (xsum_kernels.hip).  A
+// segment with another hdrs_len or frame alignment, or whose ip.total_length
+// is not 52 + payload (:897), is done by the general body (txseg_row), which
+// rewrites the same payload bytes and then the checksums.  When the
+// descriptor's room (the mbuf data room) covers the frame's last 16-byte
+// chunk, that chunk is written whole, its bytes past the frame with their own
+// values, instead of by dword and byte stores.
+template <int U, bool NTS>
+__global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group leaves together
+  const u32x4 d0 = ld16((const u32x4 *) p.segs, 2 * i), d1 = ld16((const u32x4 *) p.segs, 2 * i + 1);
+  const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
+  const uint64_t tx_base = d0.z | ((uint64_t) d0.w << 32);
+  const uint32_t tx_len = d1.x, pos = d1.y, pay_ = d1.z & 0xffffu, hl_ = d1.z >> 16;
+  const bool ok = (pay_ == 0 || pos < tx_len) && pay_ <= tx_len && tx_base <= p.shm_len &&
+                  tx_len <= p.shm_len - tx_base && hl_ >= p.l4_off + 20;
+  uint8_t *const f = p.frames + frame_off;
+  bool fast = ok && hl_ == 66u && ((uintptr_t) f & 15u) == 0;
+  if (fast) {
+    const int pay = (int) pay_, fend = 66 + pay;
+    const int K = (fend + 15) >> 4;
+    // the descriptor's room covers the last chunk: write it whole, the bytes
+    // past the frame with their own values (sub-dword stores cost ~10% here)
+    const bool whole = d1.w >= 16u * (uint32_t) K;
+    const int aoff = (int) (((uintptr_t) f >> 4) & 15u);
+    const int kh = (gl - aoff) & 15; // this lane's chunk in the frame's first 256-byte block
+    const uint8_t *const shm = p.shm;
+    const uint32_t s1 = (uint32_t) (tx_base + pos);
+    const int wrap = (int) tx_len - (int) pos;
+    const int wrapc = (pay > 0 && wrap < pay) ? wrap : 0x7fffffff; // payload index where piece 2 starts
+    const uint32_t smax = (uint32_t) (p.shm_len - 16u);
+    auto woff = [&](int j0) -> uint32_t { return s1 + (uint32_t) j0 - (j0 >= wrapc ? tx_len : 0u); };
+    const bool straddle = wrapc < pay && ((66 + wrap) & 15);
+    const int ks = straddle ? (66 + wrap) >> 4 : -1;
+    const uint32_t xoff = straddle ? s1 - tx_len + (uint32_t) (16 * ks - 66) : s1;
+    // up front: the header chunk, chunk 4's window (payload [-2, 14)), the piece-2 window
+    const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4));
+    const uint32_t o4 = s1 - 2u;
+    const u32x4 w4 = ld16u(shm, min(o4, smax));
+    const u32x4 xw = ld16u(shm, min(xoff, smax));
+    const u32x4 tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
+
+    // whole payload chunks 5..K-1; each store instruction covers whole 256-byte
+    // blocks.  The payload chunks of the frame's first block (k < fbe) are kept
+    // in vfb and stored at the end together with the header chunks, so the
+    // block's lines are written whole by one instruction (a line written in two
+    // parts at different times costs an HBM read-modify-write).
+    const int fbe = aoff <= 10 ? 16 - aoff : 0;
+    u32x4 vfb = hv;
+    uint32_t acc = 0;
+    for (int base = 5 - ((5 + aoff) & 15); base < K; base += 16 * U) {
+      u32x4 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = min(max(base + gl + 16 * u, 5), K - 1);
+        a[u] = ld16u(shm, min(woff(16 * k - 66), smax));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = base + gl + 16 * u, j0 = 16 * k - 66;
+        if (k < 5 || k >= K)
+          continue;
+        u32x4 v = a[u];
+        const uint32_t off = woff(j0);
+        if (off > smax) // a window reaching past the region's end: byte by byte
+          v = gather16(shm, off, p.shm_len);
+        if (k == ks)
+          v = splice(v, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap - j0, 16);
+        uint8_t *const cp = f + 16 * k;
+        const int hi = fend - 16 * k;
+        if (u == 0 && k < fbe && hi >= 16) {
+          vfb = v;
+          acc = sad4(v, acc);
+        } else if (hi >= 16) {
+          if (NTS)
+            __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
+          else
+            *(__attribute__((address_space(1))) u32x4 *) cp = v;
+          acc = sad4(v, acc);
+        } else {
+          acc += sad_below(v, (uint32_t) hi);
+          if (whole)
+            *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
+          else
+            store_range(cp, v, 0, hi, false);
+        }
+      }
+    }
+
+    // chunks 0..4 (tcp4_tas14_kernel's map for 0..3; chunk 4 = option pad + payload [0, 14))
+    u32x4 h = hv;
+    if (kh == 4) {
+      u32x4 win = o4 <= smax ? w4 : gather16(shm, o4, p.shm_len);
+      if (ks == 4)
+        win = splice(win, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap + 2, 16);
+      h = splice(hv, win, 2, fend - 64);
+    }
+    const uint32_t m0 = kh == 2 ? 0xffff0000u : (kh == 3 ? 0x0000ffffu : 0xffffffffu);
+    uint32_t l4 = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
+    if (kh == 4 && fend < 80)
+      l4 = sad_below(h, (uint32_t) (fend - 64));
+    acc += (kh >= 2 && kh <= 4) ? l4 : 0u;
+    const uint32_t c0d3 = row_ror<1>(h.w), c2d0 = row_ror<15>(h.x);
+    const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u)));
+    const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
+    const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
+    acc = row_sum16(acc);
+    const int l1 = (int) ((threadIdx.x & 63u) & ~15u) + ((1 + aoff) & 15); // lane holding chunk 1
+    const uint32_t ip1 = (uint32_t) __shfl((int) ipsum, l1, 64), ph1 = (uint32_t) __shfl((int) ph, l1, 64);
+    const uint32_t tl = bswap16((uint32_t) __shfl((int) (h.x & 0xffffu), l1, 64));
+    fast = tl == 52u + (uint32_t) pay; // otherwise the general body redoes the segment
+    const uint32_t ipc = inv_result(residue(fold32_to_16(ip1)));
+    const uint32_t len = 32u + (uint32_t) pay;
+    const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph1) + bswap16(len))));
+    const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
+    if (fast) {
+      if (gl == 15 && p.out)
+        stg(p.out, i, res);
+      // the first block: header chunks with the checksums inserted (ip.chksum:
+      // chunk 1 bytes 8-9, tcp.chksum: chunk 3 bytes 2-3) and the kept payload chunks
+      if (kh == 1)
+        h.z = (h.z & 0xffff0000u) | (res & 0xffffu);
+      if (kh == 3)
+        h.x = (h.x & 0x0000ffffu) | (res & 0xffff0000u);
+      uint8_t *const cp = f + 16 * kh;
+      const int hi = fend - 16 * kh;
+      if ((kh < 5 || kh < fbe) && hi >= 16)
+        *(__attribute__((address_space(1))) u32x4 *) cp = kh < 5 ? h : vfb;
+      else if (kh < 5 && whole && kh < K) // h holds the frame's own bytes past its end
+        *(__attribute__((address_space(1))) u32x4 *) cp = h;
+      else if (kh < 5)
+        store_range(cp, h, 0, hi, false);
+    }
+  }
+  if (!fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
+    txseg_row<3, NTS>(p, i, gl);
+}
+
 } // namespace
 
 extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
@@ -323,11 +722,24 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
     return 0;
   const dim3 grid((uint32_t) blocks), block(kBlock);
   hipStream_t s = (hipStream_t) stream;
-  switch (p->dbg) { // diagnostics (TASX_TXSEG_DEBUG, tools/txseg_probe.py)
+  // the unaligned-load kernel needs both checksum fields within the frame's first
+  // 16 chunks (any frame alignment) and shm_len >= 16
+  const bool u_ok = p->l4_off + 18u + 15u <= 256u && p->ip_off + 12u + 15u <= 256u && p->shm_len >= 16u;
+  // the TAS kernel: IPv4 at 14, TCP at 34 (its other segments go to the general body)
+  const bool tas = p->ip_off == 14u && p->l4_off == 34u;
+  switch (u_ok ? p->dbg : 4u) { // diagnostics (TASX_TXSEG_DEBUG, tools/txseg_probe.py)
   case 1: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;  // 3 slots per round
   case 2: hipLaunchKernelGGL((tx_segment_kernel<6, 1>), grid, block, 0, s, *p); break;  // no full-chunk stores
   case 3: hipLaunchKernelGGL((tx_segment_kernel<6, 25>), grid, block, 0, s, *p); break; // no stores at all
-  default: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;
+  case 4: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;  // aligned-gather kernel
+  case 5: hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p); break; // general layout
+  case 6: hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); break; // plain stores
+  default:
+    if (tas)
+      hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 0, s, *p);
+    else
+      hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p);
+    break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -115,18 +115,19 @@ def tcp4_frames(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SE
 
 # struct tasx_tx_seg (include/tasx_xsum.h), 32 bytes
 TX_SEG_DTYPE = np.dtype([("frame_off", "<u8"), ("tx_base", "<u8"), ("tx_len", "<u4"), ("pos", "<u4"),
-                         ("payload", "<u2"), ("hdrs_len", "<u2"), ("reserved", "<u4")])
+                         ("payload", "<u2"), ("hdrs_len", "<u2"), ("room", "<u4")])
 
 
 def tx_segments(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SEED,
                 nflows: int | None = None, tx_len: int = 16384, odd: bool = False,
-                make_shm: bool = True):
+                make_shm: bool = True, room: int = 0):
     """n TX data segments the way fast_flows_qman -> flow_tx_segment() builds
     them (/root/reference/tas/fast/fast_flows.c:877-955): headers filled (as
     tcp4_frames), payload still to be read from the flow's circular TX buffer.
     Segment i belongs to flow i % nflows; a flow's segments read consecutive
     payload from a random start position, wrapping at tx_len.  odd=True gives
-    odd buffer lengths and odd, unaligned buffer bases.
+    odd buffer lengths and odd, unaligned buffer bases.  room: the
+    descriptors' room field (TAS passes its mbuf data room, e.g. the stride).
     Returns (shm u8, frames u8, segs TX_SEG_DTYPE, shm_bytes)."""
     payload = np.broadcast_to(np.asarray(payload, dtype=np.int64), (n,)).copy()
     nflows = nflows or max(1, n // 8)
@@ -157,6 +158,7 @@ def tx_segments(n: int, payload=TCP_MSS, stride: int = MBUF_ROOM, seed: int = SE
     segs["pos"] = (start[flow] + before) % tlen[flow]
     segs["payload"] = payload
     segs["hdrs_len"] = HDRS_LEN
+    segs["room"] = room  # the mbuf data room the build may rewrite (0: frame bytes only)
     frames = tcp4_frames(n, payload, stride, seed)
     shm = random_bytes(seed ^ 0x7E5B, shm_bytes) if make_shm else None
     return shm, frames, segs, shm_bytes

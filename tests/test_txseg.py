@@ -98,14 +98,15 @@ def test_gpu_txseg_golden(txseg_golden, shift):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("room", [0, pktgen.MBUF_ROOM])
 @pytest.mark.parametrize("odd,tx_len,nflows", [(False, 16384, 512), (True, 16384, 512), (True, 1500, 7),
                                                (False, 1448, 3)])
-def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows):
+def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows, room):
     n = 4096
     pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 131) % 1449, pktgen.TCP_MSS)
     pay = np.minimum(pay, tx_len - (7 if odd else 0))
     shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=tx_len, nflows=nflows, odd=odd,
-                                           seed=0xC0FFEE + tx_len)
+                                           seed=0xC0FFEE + tx_len, room=room)
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
     out, got = _gpu_run(shm, sl, fr, segs)
@@ -142,6 +143,11 @@ def test_gpu_txseg_tso(oracle):
     out, got = _gpu_run(shm, sl, fr, segs)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
+    # with the mbuf room given, the same frames (tail chunks written whole)
+    segs["room"] = 65536 + 64
+    out, got = _gpu_run(shm, sl, fr, segs)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(got, exp_fr)
 
 
 @pytest.mark.gpu
@@ -164,6 +170,45 @@ def test_gpu_txseg_other_layouts(oracle):
         out, got = _gpu_run(shm, sl, fr, segs, ip_off=ip_off, l4_off=l4_off)
         np.testing.assert_array_equal(out, exp)
         np.testing.assert_array_equal(got, exp_fr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("room", [0, 2048])
+def test_gpu_txseg_wrap_positions_and_region_edges(oracle, room):
+    """Every buffer wrap after 1..60 payload bytes (inside the frame's chunk 4,
+    on chunk boundaries, in the first whole payload chunks) and payloads at the
+    very start and the very end of the shared region (windows that would reach
+    outside it are gathered byte by byte), for TAS segments and for segments
+    with other header lengths (general body)."""
+    tx_len, nfl = 1600, 64
+    shm_len = tx_len * nfl
+    shm = pktgen.random_bytes(77, shm_len)
+    rows = [(w % nfl, tx_len - w, 1448, 66) for w in range(1, 61)]
+    rows += [(0, 0, 1448, 66), (0, 0, 5, 66), (0, 1, 13, 66),              # region start
+             (nfl - 1, tx_len - 1448, 1448, 66), (nfl - 1, tx_len - 3, 3, 66),  # region end
+             (nfl - 1, tx_len - 10, 1448, 66), (nfl - 1, tx_len - 1, 1448, 66),
+             (0, 0, 1448, 54), (nfl - 1, tx_len - 7, 1448, 80), (5, tx_len - 20, 700, 67)]
+    n = len(rows)
+    pay = np.array([r[2] for r in rows])
+    hl = np.array([r[3] for r in rows])
+    fr = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=78)
+    f = fr.reshape(n, 2048)
+    tl = hl - 14 + pay                       # ip.total_length for each header length
+    f[:, 16] = (tl >> 8) & 0xFF
+    f[:, 17] = tl & 0xFF
+    segs = np.zeros(n, pktgen.TX_SEG_DTYPE)
+    segs["frame_off"] = np.arange(n, dtype=np.uint64) * np.uint64(2048)
+    segs["tx_base"] = [r[0] * tx_len for r in rows]
+    segs["tx_len"] = tx_len
+    segs["pos"] = [r[1] for r in rows]
+    segs["payload"] = pay
+    segs["hdrs_len"] = hl
+    segs["room"] = room
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, shm_len, exp_fr, segs)
+    out, got = _gpu_run(shm, shm_len, fr, segs)
+    np.testing.assert_array_equal(out, exp)
+    np.testing.assert_array_equal(got, exp_fr)
 
 
 @pytest.mark.gpu

@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--only-kernel", action="store_true")
     ap.add_argument("--tag", default="")
     ap.add_argument("--case", default="", help="only cases whose name contains this")
+    ap.add_argument("--room", type=int, default=STRIDE, help="descriptor room (0: frame bytes only)")
     a = ap.parse_args()
     R = a.rotate
     frames = [torch.zeros(N * STRIDE, dtype=torch.uint8, device="cuda") for _ in range(R)]
@@ -92,7 +93,7 @@ def kernel_cases(a, R, frames):
     for name, kw in cases:
         if a.case not in name:
             continue
-        _, _, segs, shm_len = pktgen.tx_segments(N, seed=9, make_shm=False, **kw)
+        _, _, segs, shm_len = pktgen.tx_segments(N, seed=9, make_shm=False, room=a.room, **kw)
         if "flows64" in name:  # sequential: flow-major order, consecutive segments read consecutive bytes
             order = np.argsort(np.arange(N) % 64, kind="stable")
             segs = segs.copy()
