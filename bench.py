@@ -21,8 +21,9 @@ prints one JSON line.
 
 Extra legs (rank 0, N == 1): the same frames without the hint, the RAW payload
 fold (rte_raw_cksum over 64K x 1500 B), the end-to-end host-memory rate through
-pinned hipMemcpyAsync, the CPU oracle baseline, and (--pmc) HBM traffic from
-rocprofv3 counters.  --workload {shard8m,mixed,tso} measures the other
+pinned hipMemcpyAsync, the CPU oracle baseline, and HBM traffic from
+rocprofv3 counters (two short child runs; --no-pmc skips them).
+--workload {shard8m,mixed,tso} measures the other
 BASELINE.json configs instead (one JSON line each).
 """
 from __future__ import annotations
@@ -70,7 +71,8 @@ def parse(argv=None):
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--no-txseg", action="store_true")
     ap.add_argument("--no-flow", action="store_true")
-    ap.add_argument("--pmc", action="store_true", help="collect HBM traffic via rocprofv3 child runs")
+    ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
+    ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
     ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
@@ -681,7 +683,7 @@ def main():
             extra["cpu_baseline"] = cpu_baseline_leg(wl, gpu_out, args.cpu_seconds)
         if not args.no_e2e:
             extra["e2e"] = e2e_leg()
-        if args.pmc:
+        if not args.no_pmc:
             del wl
             torch.cuda.empty_cache()
             p = pmc_leg("tcp4", "tcp4", 64)

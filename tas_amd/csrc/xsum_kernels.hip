@@ -181,9 +181,10 @@ __global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
 // past it in the last chunk on lane 15, whose last load of the final round is
 // always that chunk (its partial may wrap: the group total, < 2^32 for
 // TASX_RAW_MAX_LEN, is exact mod 2^32).
-// S32: stride mode from a 16-byte aligned base with the whole batch within
-// 4 GiB of it (host-checked): 32-bit byte offsets from the SGPR base, so each
-// load is global_load_dwordx4 v, v_off, s[base] (one VGPR per address).
+// S32: stride mode from a 16-byte aligned base (host-checked): 32-bit byte
+// offsets from the block's first packet (a uniform 64-bit base: 16 strides
+// from a 16-byte aligned base stay 16-byte aligned), so each load is
+// global_load_dwordx4 v, v_off, s[base] (one VGPR per address) at any batch size.
 template <int U, bool S32 = false>
 __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
 {
@@ -193,9 +194,10 @@ __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
     return;
   const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
   const uint8_t *s = nullptr;
+  const uint8_t *const bb = p.base + (uint64_t) (blockIdx.x * (kBlock / 16)) * p.stride;
   uint32_t o0 = 0, head, last;
   if constexpr (S32) {
-    const uint32_t so = i * (uint32_t) p.stride;
+    const uint32_t so = (threadIdx.x / 16) * (uint32_t) p.stride;
     o0 = so & ~15u;
     head = so & 15u;
     last = (head + len - 1u) >> 4; // valid when len > 0
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
         const uint32_t lb = o0 + 16u * (cb + (uint32_t) gl), lastoff = o0 + 16u * last;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          v[u] = ld16nt_off(p.base, min(lb + 256u * u, lastoff));
+          v[u] = ld16nt_off(bb, min(lb + 256u * u, lastoff));
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -665,8 +667,15 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
   }
 }
 
+// Dynamic LDS reserved (never used) by the v_sad_u16 kernels to cap residency
+// at 5 blocks = 20 waves per CU: with ~100 VALU per wave they would otherwise
+// run 8 waves per SIMD, and the extra bytes in flight only lengthen the queue
+// (interleaved sweeps: 64K TAS frames -0.4%, 64K x 1500 B RAW -1%, 8M x 1500 B
+// RAW -1.5%; profiles/r01_sweeps_s2.jsonl).
+constexpr uint32_t kOccLds = 30u * 1024u;
+
 template <int G = 16, typename K, typename Prm>
-int launch_groups(K kern, const Prm &p, hipStream_t s)
+int launch_groups(K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
   // one G-lane group per packet, kBlock / G groups per block: the grid covers
   // the batch once (measured faster than persistent grids at these batch
@@ -677,7 +686,7 @@ int launch_groups(K kern, const Prm &p, hipStream_t s)
     return 0;
   if (blocks > 0x7fffffffull)
     return -2;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -731,9 +740,9 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
   case 0:
   case 6:
     if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
-        (uint64_t) p->n * p->stride + p->len0 + 16u < (1ull << 32) && p->len == nullptr)
-      return launch_groups(raw_sad_kernel<6, true>, *p, s);
-    return launch_groups(raw_sad_kernel<6>, *p, s);
+        (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32))
+      return launch_groups(raw_sad_kernel<6, true>, *p, s, kOccLds);
+    return launch_groups(raw_sad_kernel<6>, *p, s, kOccLds);
   default:
     return -2;
   }
@@ -742,7 +751,7 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
   if ((variant == 0 || variant == 6) && tas14_ok(*p))
-    return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream);
+    return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
   return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 
@@ -768,7 +777,7 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
     return launch_groups<32>(tcp4_tas_kernel<3, 0, 32>, *p, s);
   case 6:
-    return launch_groups(tcp4_tas14_kernel<6>, *p, s);
+    return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
   default:
     return -2;
   }

@@ -1,10 +1,10 @@
 #!/bin/bash
-# One GPU-box pass: smoke, GPU parity tests, bench, rocprofv3 kernel stats.
-# Every GPU step has its own time limit; a crash / timeout / abort ends the
-# script (rc not in {0,1}); a plain test failure (rc 1) still lets the
-# measurement run.  Usage: bash tools/gpu_check.sh [tag] [bench args...]
+# Round-end measurement pass on the GPU box: smoke, GPU tests, the default
+# bench line (with PMC traffic), the other BASELINE configs, and the rocprofv3
+# kernel-trace summary of the bench.  Each step has its own time limit; a
+# crash / timeout / abort ends the script.  Usage: bash tools/gpu_round.sh TAG
 set -u
-TAG=${1:-r01}; shift || true
+TAG=${1:-r01}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -13,13 +13,16 @@ step() {  # name timeout cmd...
   echo "== $name: $*"
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 5 "$OUT/$name.log"
+  echo "== $name rc=$rc"; tail -n 3 "$OUT/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
 step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()'
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
-step bench 300 python bench.py "$@"
+step bench 400 python bench.py
+for w in mixed shard8m tso; do
+  step bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3
+done
 export TMPDIR=/tmp
 step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --steps 100 --warmup 10
 echo done
