@@ -581,18 +581,32 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved
 // in by DPP.  A group whose ip.total_length differs from the hint is redone
 // by the general body (tcp4_tas_frame): results always follow total_length.
-template <int U, bool VERIFY = false>
+// NOHINT: no frame-length hint; the row first reads the frame's chunk 1 (all
+// 16 lanes, one line) for ip.total_length and then proceeds as with a hint of
+// exactly that length -- two dependent memory latencies per frame instead of
+// one, no bytes read past ip.total_length (DPDK's own trust in the header).
+// Rows with total_length outside [64, 1522] take the general body.
+template <int U, bool VERIFY = false, bool NOHINT = false>
 __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
-  // uniform: the hinted datagram [ip, ip + hend) and its last chunk
-  const uint32_t hend = p.flen0 - p.ip_off;
+  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  // the datagram [ip, ip + hend) and its last chunk: uniform from the hint, or
+  // per row from the frame's own total_length
+  uint32_t hend;
+  bool in_range = true;
+  if constexpr (NOHINT) {
+    const uint32_t tl0 = bswap16(ld16nt_off(p.base, a0 + 16u).x & 0xffffu);
+    in_range = tl0 >= 64u && tl0 <= 1522u;
+    hend = in_range ? tl0 : 20u; // out of range: the header only, then the general body
+  } else {
+    hend = p.flen0 - p.ip_off;
+  }
   const uint32_t last = (14u + hend - 1u) >> 4;
   const uint32_t tail = 14u + hend - 16u * last; // bytes of the last chunk inside, 1..16
-  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
   const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * last;
   u32x4 v[U];
 #pragma unroll
@@ -633,7 +647,7 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  const bool bad = tl15 != hend; // meaningful on lane 15
+  const bool bad = NOHINT ? !in_range : tl15 != hend; // meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
     if (gl == 15 && !bad) {
@@ -715,6 +729,12 @@ static bool tas_kernel_ok(const tasx_tcp4_params &p)
          (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
 }
 
+// tcp4_tas14_kernel without a hint: IPv4 header at 14 mod 16 in every frame
+static bool tas14_nohint_ok(const tasx_tcp4_params &p)
+{
+  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0 && !p.flen && !p.flen0;
+}
+
 // tcp4_tas14_kernel, in addition: IPv4 header at 14 mod 16 in every frame, a
 // uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
 static bool tas14_ok(const tasx_tcp4_params &p)
@@ -752,6 +772,8 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
 {
   if ((variant == 0 || variant == 6) && tas14_ok(*p))
     return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
+  if ((variant == 0 || variant == 6) && tas14_nohint_ok(*p))
+    return launch_groups(tcp4_tas14_kernel<6, true, true>, *p, (hipStream_t) stream, kOccLds);
   return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 
@@ -759,10 +781,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 {
   hipStream_t s = (hipStream_t) stream;
   const bool tas_ok = tas_kernel_ok(*p);
-  if (variant == 6 && !tas14_ok(*p)) // headline kernel not applicable: automatic choice
+  if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p)) // headline kernel not applicable
     variant = 0;
-  if (variant == 0) // uniform-MTU TAS batch -> tcp4_tas14_kernel; TAS layout + hints -> tcp4_tas_kernel
-    variant = tas14_ok(*p) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
+  if (variant == 0) // TAS frames, uniform hint or none -> tcp4_tas14_kernel; TAS layout + per-frame hints -> 3
+    variant = (tas14_ok(*p) || tas14_nohint_ok(*p)) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
   if (variant >= 3 && !tas_ok)
     variant = 2;
   switch (variant) {
@@ -777,7 +799,9 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
     return launch_groups<32>(tcp4_tas_kernel<3, 0, 32>, *p, s);
   case 6:
-    return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
+    if (tas14_ok(*p))
+      return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
+    return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, kOccLds);
   default:
     return -2;
   }
