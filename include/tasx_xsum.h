@@ -91,7 +91,10 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
  * frame's length from its start -- the mbuf data_len that tx_send() sets
  * (tas/fast/fastemu.h:81-95) before tx_flush().  Hints only let the kernel
  * issue a frame's data loads together with its header loads; results always
- * follow ip.total_length, whatever the hint (0 = no hint). */
+ * follow ip.total_length, whatever the hint (0 = no hint).  The kernel may read
+ * the 16-byte aligned chunks covering [frame, frame + hint), so a hint must
+ * not exceed the frame's buffer.  One uniform hint for a uniform-MTU batch of
+ * TAS frames (IPv4 at 14 mod 16) selects the fastest kernel. */
 int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
     uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
     uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
