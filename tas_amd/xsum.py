@@ -24,7 +24,8 @@ from pathlib import Path
 
 import torch  # noqa: F401  -- must be imported first: libtasx then binds torch's HIP runtime
 
-_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libtasx.so"
+# TASX_LIB: another in-tree build of the library (A/B of kernel revisions, tools/ab_lib.sh)
+_LIB_PATH = Path(os.environ.get("TASX_LIB") or Path(__file__).resolve().parent / "_lib" / "libtasx.so")
 _lib = None
 
 TASX_F_INPLACE = 0x1
