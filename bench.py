@@ -19,12 +19,14 @@ data-path collective: the path shards); the timed region i
 barrier + synchronize on both sides and the MAX over ranks is taken.  Rank 0
 prints one JSON line.
 
-Extra legs (rank 0, N == 1): the same frames without the hint, the RAW payload
-fold (rte_raw_cksum over 64K x 1500 B), the end-to-end host-memory rate through
-pinned hipMemcpyAsync, the CPU oracle baseline, and HBM traffic from
-rocprofv3 counters (two short child runs; --no-pmc skips them).
---workload {shard8m,mixed,tso} measures the other
-BASELINE.json configs instead (one JSON line each).
+Extra legs (rank 0, N == 1): the same frames without the hint, the same
+batches over two streams (two fast-path contexts), RX verification, the RAW
+payload fold (rte_raw_cksum over 64K x 1500 B), the TX segment build, the flow
+lookup, the end-to-end host-memory rate through pinned memory, the CPU oracle
+baseline, and HBM traffic from rocprofv3 counters (two short child runs;
+--no-pmc skips them).  --workload {shard8m,mixed,tso} measures the other
+BASELINE.json configs instead (one JSON line each, with the oracle timed on a
+bounded sample of the same packets at N == 1).
 """
 from __future__ import annotations
 
@@ -525,18 +527,24 @@ def e2e_leg(reps: int = 5) -> dict:
     return res
 
 
-def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> dict:
-    """The oracle (C restatement of the reference path, per-frame calls) timed on
-    this box's host cores, on a bounded sample of the same workload."""
+def host_oracle():
+    """The C oracle built with the reference's own flags (-O3 -march=native) for
+    THIS host, in a temp dir the caller removes; the prebuilt one otherwise."""
     from oracle import oracle_lib
     tmp = Path(tempfile.mkdtemp(prefix="tasx_oracle_"))
-    try:  # the reference's own flags: -O3 -march=native, built for THIS host
+    try:
         lib_path = oracle_lib.build(out_dir=tmp, march="native")
         kind_note = "-O3 -march=native (built on this host)"
     except Exception:
         lib_path = None
         kind_note = "-O3 -march=x86-64-v3 (prebuilt)"
-    orc = oracle_lib.Oracle(lib_path)
+    return oracle_lib.Oracle(lib_path), kind_note, tmp
+
+
+def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> dict:
+    """The oracle (C restatement of the reference path, per-frame calls) timed on
+    this box's host cores, on a bounded sample of the same workload."""
+    orc, kind_note, tmp = host_oracle()
     frames = wl.host.copy()
     n = wl.n
     exp = orc.tcp4_batch(frames.copy(), n, stride=STRIDE)
@@ -637,13 +645,61 @@ def other_workload(args, ws, rank):
         desc = "16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B), tcp_checksums() flag-off, hinted"
         scaling = "weak"
     r = leg(wl, args, ws, desc)
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        torch.cuda.synchronize()
+        cpu = other_cpu_baseline(name, wl, args.cpu_seconds / 2)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(r["value"], 2), "unit": "GiB/s", "n_gpus": ws,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
                           "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
                           "data": "synthetic (device-generated random bytes)",
                           "config": {"workload": desc, "parallelism": f"shard{ws}"},
-                          "roofline": r["roofline"]}), flush=True)
+                          "roofline": r["roofline"], "cpu_baseline": cpu}), flush=True)
+
+
+def other_cpu_baseline(name: str, wl, budget_s: float) -> dict:
+    """The oracle on a bounded sample of the other configs (BASELINE.md's CPU
+    plan: the same generator, per-packet calls, 1 and 16 host threads), checked
+    against the GPU's results for the same packets."""
+    orc, kind_note, tmp = host_oracle()
+    threads = min(16, len(os.sched_getaffinity(0)))
+    if name == "tso":
+        m, stride = 4096, wl.stride  # 268 MB: beyond the 16 threads' share of L3
+        host = wl.bufs[0][:m * stride].cpu().numpy().copy()
+        gpu = wl.outs[0][:2 * m].cpu().numpy().view(np.uint16)
+        parity = np.array_equal(orc.tcp4_batch(host.copy(), m, stride=stride), gpu)
+        kw = dict(stride=stride)
+        mode, alg = 1, m * (wl.ip_total + 4)
+        sample = f"the first {m} TSO segments (ip.len {wl.ip_total}), per-segment oracle_tcp_checksums in place"
+    else:
+        m = 65536
+        gpu = wl.outs[0][:m].cpu().numpy().view(np.uint16)
+        if wl.off is None:
+            host = wl.bufs[0][:m * wl.len0].cpu().numpy()
+            kw = dict(stride=wl.len0, len0=wl.len0)
+            alg = m * (wl.len0 + 2)
+        else:
+            offs = wl.off[:m].cpu().numpy().astype(np.uint64)
+            lens = wl.lens[:m].cpu().numpy().astype(np.uint32)
+            host = wl.bufs[0][:int(offs[-1]) + int(lens[-1])].cpu().numpy()
+            kw = dict(offsets=offs, lengths=lens)
+            alg = int(lens.astype(np.int64).sum()) + 2 * m
+        parity = np.array_equal(orc.raw_batch(host, m, **kw), gpu)
+        mode = 0
+        sample = f"the first {m} packets of the batch, per-packet oracle_raw_cksum (rte_raw_cksum restatement)"
+    t1 = orc.bench(mode, host, m, threads=1, reps=1, **kw)
+    reps1 = max(3, min(200, int(budget_s * 0.4 / max(t1, 1e-6))))
+    t1 = orc.bench(mode, host, m, threads=1, reps=reps1, **kw)
+    tn = orc.bench(mode, host, m, threads=threads, reps=1, **kw)
+    repsn = max(3, min(2000, int(budget_s * 0.4 / max(tn, 1e-6))))
+    tn = orc.bench(mode, host, m, threads=threads, reps=repsn, **kw)
+    shutil.rmtree(tmp, ignore_errors=True)
+    return {"value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{sample} ({alg / 1e6:.1f} MB algorithmic), median of {repsn} passes on {threads} "
+                      f"pinned threads; 1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}",
+            "single_core_value": alg / t1 / GIB,
+            "parity_vs_gpu": "bit-exact" if parity else "MISMATCH"}
 
 
 def main():

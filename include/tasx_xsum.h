@@ -212,7 +212,12 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
  * calls tx_flush(), outside any flow lock -- checksums every recorded frame
  * on the GPU and stores ip.chksum / tcp.chksum into the frames before it
  * returns.  Frames must stay valid and unmodified until then.
- * Recorded frames are read up to ip_off + ip.total_length. */
+ * Recorded frames are read up to ip_off + ip.total_length.  tasx_flush
+ * gathers the frames into pinned staging, which the kernel reads directly;
+ * results land in pinned memory.  It then waits by spinning on a completion
+ * word that a one-lane kernel posts after the checksum launch, not in
+ * hipStreamSynchronize.  The spin polls the stream now and then, so a failed
+ * stream returns -EIO. */
 int tasx_tcp_checksums(unsigned ctx_id, void *nbh, void *p, uint32_t ip_s,
     uint32_t ip_d, uint16_t l3_paylen);
 int tasx_fast_flows_kernelxsums(unsigned ctx_id, void *nbh, void *p);

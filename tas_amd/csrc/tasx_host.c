@@ -279,6 +279,13 @@ struct tasx_ctx {
   uint32_t *h_flen;  /* pinned frame-length hints, and its device view */
   uint32_t *d_hflen;
   uint32_t n_zerocopy_flushes, n_staged_flushes;
+  /* flush completion: a word in coherent pinned memory that a one-lane kernel
+   * sets after the flush's work (tasx_launch_post_done); the caller spins on
+   * it instead of hipStreamSynchronize (~3.5 us less per flush) */
+  uint32_t *h_done, *d_done;
+  uint32_t done_seq;
+  uint8_t *d_hstage; /* device views of h_stage[0] / h_out[0] */
+  uint16_t *d_hout;
 };
 
 static struct tasx_ctx g_ctx[TASX_MAX_CTX];
@@ -311,6 +318,8 @@ static void ctx_release(struct tasx_ctx *c)
   }
   if (c->h_flen)
     hipHostFree(c->h_flen);
+  if (c->h_done)
+    hipHostFree(c->h_done);
   if (c->zc_registered)
     hipHostUnregister(c->zc_host);
   free(c->pend_ip);
@@ -355,7 +364,11 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
   }
   if ((e = hipHostMalloc((void **) &c->h_flen, (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
       (e = hipHostGetDevicePointer((void **) &c->d_hoff, c->h_off[0], 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_hflen, c->h_flen, 0)) != hipSuccess) {
+      (e = hipHostGetDevicePointer((void **) &c->d_hflen, c->h_flen, 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &c->d_hstage, c->h_stage[0], 0)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &c->d_hout, c->h_out[0], 0)) != hipSuccess ||
+      (e = hipHostMalloc((void **) &c->h_done, 64, hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &c->d_done, c->h_done, 0)) != hipSuccess) {
     ctx_release(c);
     return hip_err(e, "tasx_ctx_init pinned descriptors");
   }
@@ -600,11 +613,35 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
   return 0;
 }
 
+/* Wait for everything enqueued on c->st[0]: a one-lane kernel posts the next
+ * sequence number into the context's completion word and the caller spins on
+ * it.  Every 4096 polls (a few microseconds) the stream is queried, so an
+ * error or a lost word ends the wait instead of spinning on. */
+static int wait_done(struct tasx_ctx *c)
+{
+  volatile uint32_t *w = c->h_done;
+  const uint32_t seq = ++c->done_seq;
+  uint32_t k = 0;
+  if (tasx_launch_post_done(c->d_done, seq, c->st[0]) != 0)
+    return hip_err(hipGetLastError(), "completion-word launch");
+  while (*w != seq) {
+    if ((++k & 4095u) == 0) {
+      hipError_t e = hipStreamQuery(c->st[0]);
+      if (e == hipSuccess && *w != seq)
+        return set_err(-EIO, "flush: stream idle but completion word %u != %u", *w, seq);
+      if (e != hipSuccess && e != hipErrorNotReady)
+        return hip_err(e, "flush: hipStreamQuery");
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return 0;
+}
+
 /* Zero-copy flush: every pending frame lies in the registered region and has
  * the TAS layout (tcp = ip + 20).  The kernel reads the frames straight from
  * host memory over PCIe (only the bytes it sums), writes both checksum fields
  * in place, and the descriptors (offset, frame-length hint) are read from
- * pinned memory: one launch + one synchronize, no copies. */
+ * pinned memory: one launch + the completion-word wait, no copies. */
 static int flush_zerocopy(struct tasx_ctx *c)
 {
   tasx_tcp4_params p;
@@ -626,7 +663,9 @@ static int flush_zerocopy(struct tasx_ctx *c)
   p.flen = c->d_hflen;
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-  HIPCHK(hipStreamSynchronize(c->st[0]));
+  int rc = wait_done(c);
+  if (rc != 0)
+    return rc;
   c->n_zerocopy_flushes++;
   c->npend = 0;
   return 0;
@@ -690,12 +729,12 @@ int tasx_flush(unsigned ctx_id)
       offs[cnt++] = pos;
       pos += rec;
     }
-    HIPCHK(hipMemcpyAsync(c->d_buf[s], stage, pos, hipMemcpyHostToDevice, c->st[s]));
-    HIPCHK(hipMemcpyAsync(c->d_off[s], offs, (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
+    /* the kernel reads the pinned records and offsets and writes the results
+     * into pinned memory directly: no copy-engine work on the flush path */
     memset(&p, 0, sizeof(p));
-    p.base = c->d_buf[s];
-    p.off = c->d_off[s];
-    p.out = c->d_out[s];
+    p.base = c->d_hstage;
+    p.off = c->d_hoff;
+    p.out = c->d_hout;
     p.stride = 0;
     p.n = cnt;
     p.ip_off = 0;
@@ -703,9 +742,9 @@ int tasx_flush(unsigned ctx_id)
     p.flags = 0;
     if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4,
-        hipMemcpyDeviceToHost, c->st[s]));
-    HIPCHK(hipStreamSynchronize(c->st[s]));
+    int rc = wait_done(c);
+    if (rc != 0)
+      return rc;
     for (i = 0; i < cnt; i++) {
       memcpy(c->pend_ip[start + i] + 10, &c->h_out[s][2 * i], 2);
       memcpy(c->pend_l4[start + i] + 16, &c->h_out[s][2 * i + 1], 2);

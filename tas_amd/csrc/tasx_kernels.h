@@ -73,6 +73,9 @@ int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream);
 /* RX flow lookup (flow_kernels.hip) */
 int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream);
+/* one-lane kernel storing seq into *word (pinned host memory, device view)
+ * with system-scope release, after everything before it on the stream */
+int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 

@@ -746,6 +746,21 @@ static bool tas14_ok(const tasx_tcp4_params &p)
   return ((14u + (p.flen0 - p.ip_off) + 15u) >> 4) <= 16u * 6u;
 }
 
+// completion word: stream-ordered after the work before it, one lane stores
+// seq into pinned host memory with system-scope release, so a host spinning on
+// the word sees every earlier result (tasx_flush's wait, tasx_host.c)
+__global__ __launch_bounds__(64) void post_done_kernel(uint32_t *word, uint32_t seq)
+{
+  if (threadIdx.x == 0)
+    __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
+{
+  hipLaunchKernelGGL(post_done_kernel, dim3(1), dim3(64), 0, (hipStream_t) stream, word, seq);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
