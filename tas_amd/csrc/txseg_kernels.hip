@@ -367,10 +367,11 @@ __device__ __forceinline__ uint32_t sad_range(u32x4 v, int lo, int hi)
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4u gcu4u;
 
-// 16 bytes at any byte offset (global_load_dwordx4 at an unaligned address)
+// 16 bytes at any byte offset (global_load_dwordx4 at an unaligned address),
+// non-temporal: payload windows are read once (-2% on the TX build)
 __device__ __forceinline__ u32x4 ld16u(const uint8_t *base, uint32_t off)
 {
-  const u32x4u v = *(gcu4u *) (base + off);
+  const u32x4u v = __builtin_nontemporal_load((gcu4u *) (base + off)); // read once
   return u32x4{v.x, v.y, v.z, v.w};
 }
 
