@@ -75,6 +75,7 @@ __device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
 }
 
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x3u __attribute__((ext_vector_type(3), aligned(1)));
 
 // TAB: slice-by-4 CRC from LDS (else bitwise); CHUNK: key fields from 16-byte
 // chunk loads (else byte loads)
@@ -101,6 +102,13 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
     rip = ipw.x;
     lip = ipw.y;
     l4x = l4w.x;
+  } else if (p.l4_off == p.ip_off + 20u) {
+    // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
+    // unaligned dwordx3 load (gfx950 global loads take any byte address)
+    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (f + p.ip_off + 12);
+    rip = k.x;
+    lip = k.y;
+    l4x = k.z;
   } else {
     rip = ld32b(f + p.ip_off + 12);
     lip = ld32b(f + p.ip_off + 16);
