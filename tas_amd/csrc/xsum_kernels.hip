@@ -242,6 +242,131 @@ __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
   }
 }
 
+// RAW with per-packet lengths (variant 7; the automatic choice when lengths
+// are given).  The 16-lane-group kernels keep a wave for as many rounds as its
+// longest packet needs while the other groups' lanes idle: on the
+// {64,576,1500,9000} B mix two waves in three hold a 9000 B packet and keep
+// ~30% of their lanes loading.  Here a wave's 4 packets form ONE chunk
+// sequence (packet k owns flattened chunks [P_k, P_k+1)) and all 64 lanes load
+// consecutive flattened chunks, U per lane per round: ceil(total / 64U) rounds.
+// Whole chunks go into cumulative accumulators A_j = sum over the chunks of
+// packets >= j, so packet k's sum is A_k - A_{k+1}, exact mod 2^32 (every
+// packet sum is < 2^32 for len <= TASX_RAW_MAX_LEN).  The bytes outside
+// packet k in its first / last chunk come off on lane k / 4 + k, whose loads
+// of those two chunks are issued before round 0 (their addresses come from
+// the descriptors: no dependent load phase).
+template <int U, bool S32>
+__device__ __forceinline__ void wave_chunk_sums(uint64_t lo, const uint64_t (&B)[4], const uint32_t (&P)[4],
+                                                uint32_t T, uint32_t lane, uint32_t (&A)[4])
+{
+  // B[k] = chunk-aligned start of packet k - 16 P_k (mod 2^64): flattened
+  // chunk f of packet k is at B[k] + 16 f.  S32: every chunk lies within
+  // 4 GiB above lo, so the address is lo + 32-bit offset (one VGPR).
+  uint32_t d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    d[k] = (uint32_t) (B[k] - lo);
+  const uint8_t *sb = (const uint8_t *) (uintptr_t) lo;
+  for (uint32_t f0 = 0; f0 < T; f0 += 64u * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t fc = min(f0 + 64u * u + lane, T - 1u);
+      if constexpr (S32) {
+        const uint32_t dk = fc >= P[3] ? d[3] : fc >= P[2] ? d[2] : fc >= P[1] ? d[1] : d[0];
+        v[u] = ld16nt_off(sb, dk + 16u * fc);
+      } else {
+        const uint64_t bk = fc >= P[3] ? B[3] : fc >= P[2] ? B[2] : fc >= P[1] ? B[1] : B[0];
+        v[u] = __builtin_nontemporal_load((gcu4 *) (uintptr_t) (bk + 16ull * fc));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t f = f0 + 64u * u + lane;
+      const uint32_t s = f < T ? sad4(v[u], 0u) : 0u;
+      A[0] += s;
+      A[1] += f >= P[1] ? s : 0u;
+      A[2] += f >= P[2] ? s : 0u;
+      A[3] += f >= P[3] ? s : 0u;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
+{
+  const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) x, l);
+  const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (x >> 32), l);
+  return ((uint64_t) hi << 32) | lo;
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
+  if (i0 >= p.n) // wave-uniform
+    return;
+  const uint32_t k = lane & 3u;
+  const uint32_t i = i0 + k;
+  // lanes k and 4 + k hold packet k's descriptor
+  uint64_t a = 0;
+  uint32_t len = 0;
+  if (lane < 8u && i < p.n) {
+    a = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i);
+    len = p.len ? ldg(p.len, i) : p.len0;
+  }
+  const uint32_t head = (uint32_t) a & 15u;
+  const uint32_t nch = len ? (head + len + 15u) >> 4 : 0u;
+  const uint64_t c0 = a & ~15ull;
+  // packet k's first (lane k) and last (lane 4 + k) chunk, in flight with round 0
+  u32x4 bv = {0u, 0u, 0u, 0u};
+  if (lane < 8u && nch)
+    bv = ld16nt((const u32x4 *) (uintptr_t) c0, lane < 4u ? 0u : nch - 1u);
+
+  uint64_t B[4];
+  uint32_t P[4];
+  uint32_t T = 0;
+  uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const uint32_t nk = (uint32_t) __builtin_amdgcn_readlane((int) nch, kk);
+    const uint64_t ck = readlane64(c0, kk);
+    P[kk] = T;
+    B[kk] = ck - 16ull * T;
+    if (nk) {
+      lo = min(lo, ck);
+      hi = max(hi, ck + 16ull * nk);
+    }
+    T += nk;
+  }
+  uint32_t A[4] = {0u, 0u, 0u, 0u};
+  if (T) {
+    if (hi - lo <= 0xffffffffull)
+      wave_chunk_sums<U, true>(lo, B, P, T, lane, A);
+    else
+      wave_chunk_sums<U, false>(lo, B, P, T, lane, A);
+  }
+  // boundary bytes of packet k off A_0..A_k (packet k's sum is A_k - A_{k+1})
+  uint32_t corr = 0;
+  if (lane < 8u && nch)
+    corr = lane < 4u ? sad_below(bv, head) : sad_from(bv, head + len - 16u * (nch - 1u));
+  A[0] -= corr;
+  A[1] -= k >= 1u ? corr : 0u;
+  A[2] -= k >= 2u ? corr : 0u;
+  A[3] -= k == 3u ? corr : 0u;
+  uint32_t t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    t[j] = (uint32_t) __builtin_amdgcn_readlane((int) group_total<64>(A[j]), 63);
+  if (lane < 4u && i < p.n) {
+    const uint32_t s = k == 0u ? t[0] - t[1] : k == 1u ? t[1] - t[2] : k == 2u ? t[2] - t[3] : t[3];
+    uint32_t f = fold32_to_16(s);
+    if (head & 1u)
+      f = bswap16(f);
+    stg(p.out, i, (uint16_t) f);
+  }
+}
+
 // TCP4, any frame layout: header words and the checksum-field bytes by byte
 // loads, then the segment chunks.  With a frame-length hint (the mbuf
 // data_len tx_send() sets before tx_flush) the chunk loads are issued together
@@ -688,6 +813,14 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
 // RAW -1.5%; profiles/r01_sweeps_s2.jsonl).
 constexpr uint32_t kOccLds = 30u * 1024u;
 
+// raw_wave_kernel: chunks per lane per round and the LDS reservation (A/B knobs)
+#ifndef TASX_WAVE_U
+#define TASX_WAVE_U 6
+#endif
+#ifndef TASX_WAVE_LDS
+#define TASX_WAVE_LDS kOccLds
+#endif
+
 template <int G = 16, typename K, typename Prm>
 int launch_groups(K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
@@ -772,8 +905,12 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
     return launch_groups(raw_group_kernel<6>, *p, s);
   case 1:
     return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+  case 7:
+    return launch_groups(raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
   case 0:
   case 6:
+    if (variant == 0 && p->len)
+      return launch_groups(raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
     if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
         (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32))
       return launch_groups(raw_sad_kernel<6, true>, *p, s, kOccLds);

@@ -202,6 +202,50 @@ def test_config3_mixed_mtu_1M(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 4099])
+def test_raw_wave_descriptor_orders(oracle, n):
+    """raw_wave_kernel (a wave's 4 packets as one chunk sequence): packets in
+    descending, repeated and interleaved order, empty and maximum-length
+    (TASX_RAW_MAX_LEN) packets, batch sizes that leave a wave partly empty."""
+    rng = np.random.default_rng(n)
+    total = 3 << 20
+    d = dev_random(total, 70 + n)
+    h = d.cpu().numpy()
+    lens = rng.choice([0, 1, 2, 15, 16, 17, 1500, 9000, 65535, 131073], n).astype(np.int64)  # 131073 = TASX_RAW_MAX_LEN
+    offs = rng.integers(0, total - 131073, n).astype(np.int64)
+    if n > 3:
+        offs[1::4] = offs[0::4][:len(offs[1::4])]           # repeated packet
+        offs[2::4] = np.sort(offs[2::4])[::-1]               # descending
+    exp = oracle.raw_batch(h, n, offsets=offs, lengths=lens)
+    for v in (0, 7):
+        xsum.set_kernel_variant(v)
+        try:
+            got = u16(xsum.raw_cksum_batch(d, n, offsets=to_dev(offs), lengths=to_dev(lens.astype(np.int32))))
+        finally:
+            xsum.set_kernel_variant(0)
+        np.testing.assert_array_equal(got, exp, err_msg=f"variant {v}")
+
+
+def test_raw_wave_span_beyond_4gib(oracle):
+    """A wave whose packets lie more than 4 GiB apart takes raw_wave_kernel's
+    64-bit addressing path (the 32-bit-offset path covers spans below 4 GiB)."""
+    far = (4 << 30) + 4093                                   # odd: misaligned far packets
+    big = torch.empty(far + 20000, dtype=torch.uint8, device=DEV)
+    near = dev_random(20000, 81)
+    big[:20000] = near
+    big[far:far + 20000] = dev_random(20000, 82)
+    lens = np.array([1500, 9000, 17, 9001, 64, 0, 1, 576], np.int64)
+    offs = np.array([0, far, 3, far + 7, far + 10001, 5, 19999, 11], np.int64)
+    hn = near.cpu().numpy()
+    hf = big[far:far + 20000].cpu().numpy()
+    exp = np.array([oracle.raw_batch(hf if o >= far else hn, 1, offsets=np.array([o - far if o >= far else o]),
+                                     lengths=np.array([ln]))[0] for o, ln in zip(offs, lens)], np.uint16)
+    got = u16(xsum.raw_cksum_batch(big, len(lens), offsets=to_dev(offs), lengths=to_dev(lens.astype(np.int32))))
+    del big
+    torch.cuda.empty_cache()
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_config4_shard_1M_1500(oracle):
     """One GPU's shard of the 8M x 1500 B 8-GPU config (1,048,576 packets)."""
     n, L = 1 << 20, 1500
@@ -291,7 +335,7 @@ def test_tcp4_all_variants_and_hints(oracle, variant):
         xsum.set_kernel_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 7])
 def test_raw_all_variants(oracle, variant):
     buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
     n = len(lens)

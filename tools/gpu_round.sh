@@ -24,5 +24,5 @@ for w in mixed shard8m tso; do
   step bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3
 done
 export TMPDIR=/tmp
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --steps 100 --warmup 10
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --steps 100 --warmup 10
 echo done
