@@ -240,7 +240,8 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for A/B tests (process-wide; set it before launching).
- *   0 automatic: RAW -> 6; TCP4 -> 6 when it applies, else 3 for the TAS
+ *   0 automatic: RAW -> 7 with per-packet lengths, else 6; TCP4 -> 6 when
+ *     it applies, else 3 for the TAS
  *     layout in stride mode with a frame-length hint, else 2
  *   1 first-generation group-per-packet kernels (A/B baseline)
  *   2 raw_group_kernel / tcp4_frame_kernel (any layout)
@@ -252,7 +253,9 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
  *     aligned base and stride), stride mode, one uniform hint flen0 with
  *     ip_off + 64 <= flen0 and the datagram within 96 chunks (uniform-MTU
  *     batches up to ip.len 1522); otherwise as 0.  RAW: raw_sad_kernel
- *     (32-bit offsets from the base in stride mode within 4 GiB) */
+ *     (32-bit offsets from the base in stride mode within 4 GiB)
+ *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk
+ *     sequence: mixed lengths keep every lane loading); TCP4 as 0 */
 int tasx_set_kernel_variant(int variant);
 /* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
  * wave.  NULL disables. */

@@ -32,7 +32,9 @@
 // tcp4_tas14_kernel (the headline: TAS frames in 16-byte aligned rooms, one
 // uniform frame-length hint), 1 = the first-generation group-per-packet
 // kernels (kept as the A/B baseline), 4 = tcp4_tas_kernel with wave-timeline
-// stamps (diagnostic), 5 = tcp4_tas_kernel with 32-lane groups (A/B).
+// stamps (diagnostic), 5 = tcp4_tas_kernel with 32-lane groups (A/B), 7 =
+// raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
+// chunk sequence).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -922,6 +924,8 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
+  if (variant == 7) // RAW-only variant
+    variant = 0;
   if ((variant == 0 || variant == 6) && tas14_ok(*p))
     return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
   if ((variant == 0 || variant == 6) && tas14_nohint_ok(*p))
@@ -933,6 +937,8 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 {
   hipStream_t s = (hipStream_t) stream;
   const bool tas_ok = tas_kernel_ok(*p);
+  if (variant == 7) // RAW-only variant
+    variant = 0;
   if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p)) // headline kernel not applicable
     variant = 0;
   if (variant == 0) // TAS frames, uniform hint or none -> tcp4_tas14_kernel; TAS layout + per-frame hints -> 3

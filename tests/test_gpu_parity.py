@@ -307,7 +307,7 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6, 7])
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
