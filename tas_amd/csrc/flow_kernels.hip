@@ -45,6 +45,28 @@ constexpr CrcTables make_crc_tables()
 
 __constant__ CrcTables kCrc = make_crc_tables();
 
+// byte-position tables for the whole 12-byte key: CRC32C from state 0 is
+// linear, so flow_hash = XOR over key byte positions p of b[p][key[p]], with
+// b[p][x] = CRC of byte x followed by 11 - p zero bytes: 12 independent LDS
+// reads instead of a 96-step dependent chain
+struct CrcKeyTables {
+  uint32_t t[12][256];
+};
+
+constexpr CrcKeyTables make_crc_key_tables()
+{
+  CrcKeyTables T{};
+  const CrcTables S = make_crc_tables();
+  for (uint32_t i = 0; i < 256; ++i)
+    T.t[11][i] = S.t[0][i];
+  for (int p = 10; p >= 0; --p)
+    for (uint32_t i = 0; i < 256; ++i)
+      T.t[p][i] = (T.t[p + 1][i] >> 8) ^ S.t[0][T.t[p + 1][i] & 0xffu];
+  return T;
+}
+
+__constant__ CrcKeyTables kCrcKey = make_crc_key_tables();
+
 // SSE4.2 crc32 on one 32-bit little-endian word (crc32c_sse42_u32(w, crc)):
 // slice-by-4 from the LDS copy of the tables, or bit by bit on the VALU
 template <bool TAB>
@@ -77,21 +99,19 @@ __device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 typedef uint32_t u32x3u __attribute__((ext_vector_type(3), aligned(1)));
 
-// TAB: slice-by-4 CRC from LDS (else bitwise); CHUNK: key fields from 16-byte
-// chunk loads (else byte loads)
-template <bool TAB, bool CHUNK>
+// CRC: 0 bitwise on the VALU, 1 slice-by-4 from LDS, 2 byte-position tables
+// from LDS (3: no CRC, a diagnostic build only -- wrong flow ids); CHUNK: key
+// fields from 16-byte chunk loads (else byte loads)
+enum { kCrcBitwise = 0, kCrcSlice4 = 1, kCrcKeyTab = 2, kCrcNone = 3 };
+
+template <int CRC, bool CHUNK>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
+  constexpr bool TAB = CRC == kCrcSlice4;
   __shared__ uint32_t lt[TAB ? 4 : 1][256];
-  if constexpr (TAB) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      lt[k][threadIdx.x] = kCrc.t[k][threadIdx.x];
-    __syncthreads();
-  }
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i >= p.n)
-    return;
+  __shared__ uint32_t kt[CRC == kCrcKeyTab ? 12 : 1][256];
+  const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t i = min(i0, p.n - 1u); // lanes past the batch repeat the last frame (no store)
   const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
   // key = (local = destination, remote = source), network byte order:
   // ip.src/ip.dst are bytes [12, 20) of the IPv4 header, the ports bytes
@@ -115,8 +135,32 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
     l4x = ld32b(f + p.l4_off);
   }
   const uint32_t ports = (l4x >> 16) | (l4x << 16); // tcp.dest | tcp.src << 16
+  // tables into LDS while the key loads are in flight
+  if constexpr (TAB) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      lt[k][threadIdx.x] = kCrc.t[k][threadIdx.x];
+  }
+  if constexpr (CRC == kCrcKeyTab) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      kt[k][threadIdx.x] = kCrcKey.t[k][threadIdx.x];
+  }
+  if constexpr (TAB || CRC == kCrcKeyTab)
+    __syncthreads();
   // flow_hash: crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0))
-  const uint32_t h = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip), rip), ports);
+  uint32_t h;
+  if constexpr (CRC == kCrcKeyTab) {
+    h = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      h ^= kt[b][(lip >> (8 * b)) & 0xffu] ^ kt[4 + b][(rip >> (8 * b)) & 0xffu] ^
+           kt[8 + b][(ports >> (8 * b)) & 0xffu];
+  } else if constexpr (CRC == kCrcNone) {
+    h = lip ^ rip ^ ports;
+  } else {
+    h = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip), rip), ports);
+  }
   // bucket: entries (h + j) % ht_entries, j < NBSZ, loaded together
   uint64_t e[TASX_FLOWHT_NBSZ];
 #pragma unroll
@@ -140,6 +184,8 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
   for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j) // first match wins
     if (cand[j] && key[j].x == lip && key[j].y == rip && key[j].z == ports)
       res = fid[j];
+  if (i0 >= p.n)
+    return;
   stg(p.fid_out, i, res);
   if (p.hash_out)
     stg(p.hash_out, i, h);
@@ -155,14 +201,20 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   const dim3 g((uint32_t) blocks), b(256);
   hipStream_t s = (hipStream_t) stream;
   // A/B (tasx_set_kernel_variant; tools/flow_probe.py, profiles/r01_flow_variants.jsonl):
-  // bitwise CRC + byte loads (the default, 0/1) 12.7 us, LDS slice-by-4 13.0 us,
-  // 16-byte chunk key loads +1.7 us either way: the lookup is bound by its
-  // dependent load chain, not by the CRC arithmetic
+  // bitwise CRC + byte loads (the default, 0/1) 12.6-12.7 us, LDS slice-by-4
+  // 12.4-13.0 us, LDS byte-position tables (5) 12.6 us, 16-byte chunk key loads
+  // +1.7 us: the lookup is bound by its dependent load chain (frame header ->
+  // bucket -> flow state), not by the CRC arithmetic
   switch (variant) {
-  case 2: hipLaunchKernelGGL((flow_lookup_kernel<false, true>), g, b, 0, s, *p); break;
-  case 3: hipLaunchKernelGGL((flow_lookup_kernel<true, false>), g, b, 0, s, *p); break;
-  case 4: hipLaunchKernelGGL((flow_lookup_kernel<true, true>), g, b, 0, s, *p); break;
-  default: hipLaunchKernelGGL((flow_lookup_kernel<false, false>), g, b, 0, s, *p); break;
+  case 2: hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, true>), g, b, 0, s, *p); break;
+  case 3: hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, false>), g, b, 0, s, *p); break;
+  case 4: hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, true>), g, b, 0, s, *p); break;
+#ifdef TASX_FLOW_NOCRC_DIAG
+  case 5: hipLaunchKernelGGL((flow_lookup_kernel<kCrcNone, false>), g, b, 0, s, *p); break;
+#else
+  case 5: hipLaunchKernelGGL((flow_lookup_kernel<kCrcKeyTab, false>), g, b, 0, s, *p); break;
+#endif
+  default: hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false>), g, b, 0, s, *p); break;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

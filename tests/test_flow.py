@@ -102,7 +102,7 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5])
 def test_gpu_flow_golden(flow_golden, variant):
     """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
     chunks) on the fixture."""
