@@ -228,6 +228,10 @@ def main():
             "zeros32": "8a9136aa", "ones32": "62a8ab43", "inc32": "46dd794e", "dec32": "113fdb5c",
             "check_123456789": "e3069283",
             "source": "RFC 3720 appendix B.4 (iSCSI CRC32C examples) and the CRC catalogue check value"},
+        "ipv4_header_public": {
+            "header_hex": "450000730000400040110000c0a80001c0a800c7", "ip_chksum_bytes": "b861",
+            "source": "the widely published IPv4 header checksum example (192.168.0.1 -> "
+                      "192.168.0.199, UDP, total length 115): checksum field b8 61"},
         "tas_unit_window_update": {
             "frame_hex": bytes(pktgen.kat_frame()).hex(),
             "ip_chksum_bytes": "a3bb", "tcp_chksum_bytes": "cfd7",

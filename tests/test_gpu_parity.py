@@ -55,6 +55,27 @@ def test_golden_raw(raw_golden):
     np.testing.assert_array_equal(u16(out), g["expected"])
 
 
+def test_kat_ipv4_header_public(oracle):
+    """The published IPv4 header example inside a frame (ip at 14): ip.chksum
+    bytes b8 61 from the GPU, every kernel variant, with and without a hint."""
+    import json
+    from pathlib import Path
+    kat = json.loads((Path(__file__).parent / "golden" / "kat.json").read_text())["ipv4_header_public"]
+    frame = np.zeros(2048, np.uint8)
+    frame[14:34] = np.frombuffer(bytes.fromhex(kat["header_hex"]), np.uint8)
+    frame[34:14 + 115] = np.arange(95, dtype=np.uint8) * 7
+    exp = oracle.tcp4_batch(frame.copy(), 1, stride=2048)
+    for v in (0, 1, 2, 3, 6):
+        xsum.set_kernel_variant(v)
+        try:
+            for hint in (None, 14 + 115):
+                got = u16(xsum.tcp4_cksum_batch(to_dev(frame), 1, stride=2048, frame_len=hint))
+                assert int(got[0]).to_bytes(2, "little").hex() == kat["ip_chksum_bytes"]
+                np.testing.assert_array_equal(got, exp)
+        finally:
+            xsum.set_kernel_variant(0)
+
+
 @pytest.mark.parametrize("shift", [0, 1, 2, 3, 15])
 def test_golden_tcp4(tcp4_golden, shift):
     g = tcp4_golden

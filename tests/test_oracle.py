@@ -23,6 +23,14 @@ def test_rfc1071_section3(oracle):
     assert oracle.raw_cksum(b).to_bytes(2, "little").hex() == kat["raw_cksum_be"]
 
 
+def test_ipv4_header_public_kat(oracle):
+    """rte_ipv4_cksum on the widely published IPv4 header example: b8 61."""
+    kat = json.loads((GOLDEN / "kat.json").read_text())["ipv4_header_public"]
+    h = bytes.fromhex(kat["header_hex"])
+    assert oracle.ipv4_cksum(h).to_bytes(2, "little").hex() == kat["ip_chksum_bytes"] == "b861"
+    assert R.ipv4_cksum(h) == oracle.ipv4_cksum(h)
+
+
 def test_unit_test_frame_kat(oracle):
     kat = json.loads((GOLDEN / "kat.json").read_text())["tas_unit_window_update"]
     f = bytearray(bytes.fromhex(kat["frame_hex"]))
