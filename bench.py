@@ -76,7 +76,7 @@ def parse(argv=None):
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
-    ap.add_argument("--pmc-child", choices=["tcp4", "raw"], help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed"], help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
 
@@ -612,7 +612,14 @@ def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
 def pmc_child(mode: str, steps: int):
     torch.cuda.set_device(0)
     xsum.lib()
-    wl = Tcp4Workload(16, pktgen.SEED) if mode == "tcp4" else RawWorkload(16, pktgen.SEED)
+    if mode == "tcp4":
+        wl = Tcp4Workload(16, pktgen.SEED)
+    elif mode == "raw":
+        wl = RawWorkload(16, pktgen.SEED)
+    elif mode == "txseg":
+        wl = TxSegWorkload(16, pktgen.SEED + 2000)
+    else:
+        wl = mixed_workload(0)
     launch = wl.launcher()
     for k in range(steps):
         launch(k)
@@ -621,6 +628,18 @@ def pmc_child(mode: str, steps: int):
 
 # ---------------------------------------------------------------------------
 # other BASELINE.json configs (--workload)
+
+def mixed_workload(rank: int) -> "RawWorkload":
+    """Config 3: 1,048,576 RAW packets, sizes uniform over {64,576,1500,9000} B in
+    random order, packed at 16-byte aligned offsets."""
+    n = 1 << 20
+    lens = pktgen.mixed_lengths(n, seed=pktgen.SEED + rank).astype(np.int64)
+    slot = (lens + 15) // 16 * 16
+    offs = np.zeros(n, np.int64)
+    np.cumsum(slot[:-1], out=offs[1:])
+    return RawWorkload(1, pktgen.SEED + rank, n=n, offsets=offs, lengths=lens,
+                       total_bytes=int(offs[-1] + slot[-1]))
+
 
 def other_workload(args, ws, rank):
     name = args.workload
@@ -631,13 +650,7 @@ def other_workload(args, ws, rank):
         desc = f"8,388,608 x 1500 B payloads sharded over {ws} GPU(s): {b - a} packets on this rank"
         scaling = "strong"
     elif name == "mixed":
-        n = 1 << 20
-        lens = pktgen.mixed_lengths(n, seed=pktgen.SEED + rank).astype(np.int64)
-        slot = (lens + 15) // 16 * 16
-        offs = np.zeros(n, np.int64)
-        np.cumsum(slot[:-1], out=offs[1:])
-        wl = RawWorkload(1, pktgen.SEED + rank, n=n, offsets=offs, lengths=lens,
-                         total_bytes=int(offs[-1] + slot[-1]))
+        wl = mixed_workload(rank)
         desc = "1,048,576 RAW packets per GPU, sizes uniform over {64,576,1500,9000} B in random order"
         scaling = "weak"
     else:  # tso
@@ -649,13 +662,19 @@ def other_workload(args, ws, rank):
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize()
         cpu = other_cpu_baseline(name, wl, args.cpu_seconds / 2)
+    pmc = None
+    if rank == 0 and ws == 1 and not args.no_pmc and name == "mixed":
+        pmc = pmc_leg("mixed", "raw_wave_kernel", 8)
+        if pmc and "hbm_bytes_per_launch" in pmc:
+            r["roofline"]["traffic"] = int(pmc["hbm_bytes_per_launch"])
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(r["value"], 2), "unit": "GiB/s", "n_gpus": ws,
                           "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
                           "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
                           "data": "synthetic (device-generated random bytes)",
                           "config": {"workload": desc, "parallelism": f"shard{ws}"},
-                          "roofline": r["roofline"], "cpu_baseline": cpu}), flush=True)
+                          "roofline": r["roofline"], "cpu_baseline": cpu,
+                          **({"pmc": pmc} if pmc else {})}), flush=True)
 
 
 def other_cpu_baseline(name: str, wl, budget_s: float) -> dict:
@@ -797,6 +816,11 @@ def main():
                 if pr and "hbm_bytes_per_launch" in pr:
                     raw["roofline"]["traffic"] = int(pr["hbm_bytes_per_launch"])
                 raw["pmc"] = pr
+            if txseg is not None:
+                pt = pmc_leg("txseg", "tx_segment", 32)
+                if pt and "hbm_bytes_per_launch" in pt:
+                    txseg["roofline"]["traffic"] = int(pt["hbm_bytes_per_launch"])
+                txseg["pmc"] = pt
 
     if rank == 0:
         line = {
