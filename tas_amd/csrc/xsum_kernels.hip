@@ -382,13 +382,11 @@ __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
 // = rte_ipv4_udptcp_cksum_verify passes (DPDK >= 21.11: fold1(raw(L4) +
 // phdr) == 0xffff; total_length < 20 fails), bit 2 = IHL != 5 (TAS drops
 // such frames, fast_flows.c:247; bits 0/1 then describe a 20-byte header).
+// One frame (i) per 16-lane DPP row, lane gl (the body of tcp4_frame_kernel,
+// also run by the persistent flush kernel).
 template <int U, bool VERIFY = false>
-__global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
+__device__ __forceinline__ void tcp4_frame_row(const tasx_tcp4_params &p, uint32_t i, int gl)
 {
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return; // whole 16-lane group (one DPP row) leaves together
   uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
   uint8_t *ip = f + p.ip_off;
   uint8_t *l4 = f + p.l4_off;
@@ -493,6 +491,15 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
       st8(l4 + 17, tcpc >> 8);
     }
   }
+}
+
+template <int U, bool VERIFY = false>
+__global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
+{
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group (one DPP row) leaves together
+  tcp4_frame_row<U, VERIFY>(p, i, threadIdx.x & 15);
 }
 
 // mask of the bytes of a dword (first byte at ip-relative offset `base`) that
@@ -888,6 +895,69 @@ __global__ __launch_bounds__(64) void post_done_kernel(uint32_t *word, uint32_t 
 {
   if (threadIdx.x == 0)
     __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Persistent flush kernel (tasx_ctx_set_persistent): one 1024-thread block
+// stays resident and polls a doorbell word in coherent pinned host memory, so a
+// tx_flush costs the PCIe round trips and no kernel launch.  Thread 0 polls
+// (system-scope acquire loads, s_sleep between polls); on a new sequence
+// number the block runs tcp4_frame_row over the published frames (64 per
+// pass, frames and descriptors read over PCIe, both checksum fields written in
+// place), makes its stores visible system-wide and posts the sequence number
+// to the completion word.  Exit conditions every wave reaches: the stop word,
+// or the lifetime cap (s_memrealtime, 100 MHz), after which the host launches
+// it again; the exit reason is posted to the mailbox.  A relaunched kernel
+// takes the completion word as its last sequence, so a doorbell rung while it
+// was exiting is served by its successor.
+__global__ __launch_bounds__(1024) void flush_persist_kernel(tasx_persist_params q)
+{
+  __shared__ uint32_t s_seq, s_n, s_quit;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t last = 0;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_load(&q.mbox[TASX_MB_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t quit = 0, seq = last;
+      for (;;) {
+        seq = __hip_atomic_load(&q.mbox[TASX_MB_BELL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (seq != last)
+          break;
+        if (__hip_atomic_load(&q.mbox[TASX_MB_STOP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          quit = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > q.max_ticks) {
+          quit = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_seq = seq;
+      s_quit = quit;
+      s_n = quit ? 0u : __hip_atomic_load(&q.mbox[TASX_MB_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    if (s_quit)
+      break;
+    const uint32_t seq = s_seq, n = min(s_n, q.cap);
+    for (uint32_t i = threadIdx.x / 16; i < n; i += 1024 / 16)
+      tcp4_frame_row<6>(q.frames, i, (int) (threadIdx.x & 15));
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      last = seq;
+      __hip_atomic_store(&q.mbox[TASX_MB_DONE], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&q.mbox[TASX_MB_EXIT], s_quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int tasx_launch_flush_persist(const tasx_persist_params *q, void *stream)
+{
+  hipLaunchKernelGGL(flush_persist_kernel, dim3(1), dim3(1024), 0, (hipStream_t) stream, *q);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
