@@ -237,20 +237,6 @@ int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes);
 /* counts of zero-copy and staged flushes since tasx_ctx_init */
 int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
     uint32_t *staged_flushes);
-/* Persistent flush kernel for zero-copy flushes (needs
- * tasx_ctx_register_frames): one resident 1024-thread block polls a doorbell
- * in coherent pinned memory, so a tasx_flush() of up to `cap` frames costs
- * PCIe round trips instead of a kernel launch (larger flushes launch as
- * before).  The kernel exits by itself after TASX_PERSIST_LIFETIME_MS and is
- * launched again by the next flush; enable = 0 (or tasx_ctx_destroy) stops
- * it and waits for it.  Replaces the launch in tx_flush's checksum work
- * (fastemu.c:544-566) for a core whose mbufs are registered.  The kernel runs
- * on a non-blocking high-priority stream; hipDeviceSynchronize() in the
- * process waits for it (at most TASX_PERSIST_LIFETIME_MS). */
-#define TASX_PERSIST_LIFETIME_MS 100u
-int tasx_ctx_set_persistent(unsigned ctx_id, int enable, uint32_t cap);
-/* flushes served by the persistent kernel, and its launches */
-int tasx_ctx_persist_stats(unsigned ctx_id, uint32_t *flushes, uint32_t *launches);
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for A/B tests (process-wide; set it before launching).

@@ -14,7 +14,6 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -287,14 +286,6 @@ struct tasx_ctx {
   uint32_t done_seq;
   uint8_t *d_hstage; /* device views of h_stage[0] / h_out[0] */
   uint16_t *d_hout;
-  /* persistent flush kernel (tasx_ctx_set_persistent) */
-  int persist, persist_running;
-  uint32_t persist_cap, bell;
-  hipStream_t pst;
-  uint32_t *h_mb, *d_mb;     /* mailbox, coherent pinned */
-  uint64_t *h_poff, *d_poff; /* descriptors, coherent pinned */
-  uint32_t *h_pflen, *d_pflen;
-  uint32_t n_persist_flushes, n_persist_launches;
 };
 
 static struct tasx_ctx g_ctx[TASX_MAX_CTX];
@@ -306,12 +297,9 @@ static struct tasx_ctx *get_ctx(unsigned id)
   return &g_ctx[id];
 }
 
-static void persist_release(struct tasx_ctx *c);
-
 static void ctx_release(struct tasx_ctx *c)
 {
   int s;
-  persist_release(c);
   for (s = 0; s < NSLOT; s++) {
     if (c->st[s])
       hipStreamDestroy(c->st[s]);
@@ -649,170 +637,6 @@ static int wait_done(struct tasx_ctx *c)
   return 0;
 }
 
-/* ---------------------------------------------------------------------- */
-/* persistent flush kernel */
-
-static double now_s(void)
-{
-  struct timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
-}
-
-/* stop a resident kernel and wait for it (it polls the stop word) */
-static void persist_stop(struct tasx_ctx *c)
-{
-  if (!c->persist_running)
-    return;
-  __atomic_store_n(&c->h_mb[TASX_MB_STOP], 1u, __ATOMIC_RELEASE);
-  hipStreamSynchronize(c->pst);
-  c->persist_running = 0;
-}
-
-static void persist_release(struct tasx_ctx *c)
-{
-  persist_stop(c);
-  if (c->pst)
-    hipStreamDestroy(c->pst);
-  if (c->h_mb)
-    hipHostFree(c->h_mb);
-  if (c->h_poff)
-    hipHostFree(c->h_poff);
-  if (c->h_pflen)
-    hipHostFree(c->h_pflen);
-  c->pst = NULL;
-  c->h_mb = c->d_mb = c->h_pflen = c->d_pflen = NULL;
-  c->h_poff = c->d_poff = NULL;
-  c->persist = 0;
-}
-
-static int persist_launch(struct tasx_ctx *c)
-{
-  tasx_persist_params q;
-  if (c->persist_running) { /* a previous instance exited (lifetime cap) */
-    HIPCHK(hipStreamSynchronize(c->pst));
-    c->persist_running = 0;
-  }
-  memset(&q, 0, sizeof(q));
-  q.frames.base = c->zc_dev;
-  q.frames.off = c->d_poff;
-  q.frames.ip_off = 0;
-  q.frames.l4_off = 20;
-  q.frames.flags = TASX_F_INPLACE;
-  q.frames.flen = c->d_pflen;
-  q.mbox = c->d_mb;
-  q.cap = c->persist_cap;
-  q.max_ticks = (uint64_t) TASX_PERSIST_LIFETIME_MS * 100000u; /* s_memrealtime: 100 MHz */
-  __atomic_store_n(&c->h_mb[TASX_MB_STOP], 0u, __ATOMIC_RELEASE);
-  __atomic_store_n(&c->h_mb[TASX_MB_EXIT], 0u, __ATOMIC_RELEASE);
-  if (tasx_launch_flush_persist(&q, c->pst) != 0)
-    return hip_err(hipGetLastError(), "persistent flush kernel launch");
-  c->persist_running = 1;
-  c->n_persist_launches++;
-  return 0;
-}
-
-int tasx_ctx_set_persistent(unsigned ctx_id, int enable, uint32_t cap)
-{
-  struct tasx_ctx *c = get_ctx(ctx_id);
-  hipError_t e;
-  if (!c)
-    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
-  HIPCHK(hipSetDevice(c->device));
-  if (!enable) {
-    persist_release(c);
-    return 0;
-  }
-  if (!c->zc_host)
-    return set_err(-EINVAL, "persistent flush: ctx %u has no registered frame region", ctx_id);
-  if (cap == 0 || cap > (1u << 20))
-    return set_err(-EINVAL, "persistent flush: cap %u out of range", cap);
-  persist_release(c);
-  /* non-blocking (the legacy null stream must not wait for the resident
-   * kernel: a blocking CU-masked stream held the default stream's next op for
-   * the kernel's whole lifetime) and high priority, so the kernel does not sit
-   * in a hardware queue shared with the ordinary streams
-   * (tools/persist_stream_probe.py) */
-  int prio_lo = 0, prio_hi = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if ((e = hipStreamCreateWithPriority(&c->pst, hipStreamNonBlocking, prio_hi)) != hipSuccess ||
-      (e = hipHostMalloc((void **) &c->h_mb, TASX_MB_WORDS * 4, hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_mb, c->h_mb, 0)) != hipSuccess ||
-      (e = hipHostMalloc((void **) &c->h_poff, (size_t) cap * 8, hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_poff, c->h_poff, 0)) != hipSuccess ||
-      (e = hipHostMalloc((void **) &c->h_pflen, (size_t) cap * 4, hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_pflen, c->h_pflen, 0)) != hipSuccess) {
-    persist_release(c);
-    return hip_err(e, "persistent flush: allocation");
-  }
-  memset(c->h_mb, 0, TASX_MB_WORDS * 4);
-  c->bell = 0;
-  c->persist_cap = cap;
-  c->persist = 1;
-  return 0;
-}
-
-int tasx_ctx_persist_stats(unsigned ctx_id, uint32_t *flushes, uint32_t *launches)
-{
-  struct tasx_ctx *c = get_ctx(ctx_id);
-  if (!c)
-    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
-  if (flushes)
-    *flushes = c->n_persist_flushes;
-  if (launches)
-    *launches = c->n_persist_launches;
-  return 0;
-}
-
-/* Ring the resident kernel for the pending frames (all in the registered
- * region, TAS layout) and spin on the completion word.  A kernel that reached
- * its lifetime cap (exit word set, or no answer for 20 ms while its stream is
- * idle) is launched again; its successor serves the doorbell. */
-static int flush_persistent(struct tasx_ctx *c)
-{
-  const uint32_t n = c->npend;
-  uint32_t i, k = 0;
-  double t0 = 0.0;
-  if (!c->persist_running || __atomic_load_n(&c->h_mb[TASX_MB_EXIT], __ATOMIC_ACQUIRE) != 0) {
-    int rc = persist_launch(c);
-    if (rc)
-      return rc;
-  }
-  for (i = 0; i < n; i++) {
-    const uint8_t *ip = c->pend_ip[i];
-    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-    c->h_poff[i] = (uint64_t) (ip - c->zc_host);
-    c->h_pflen[i] = (tl < 20 ? 20 : tl);
-  }
-  __atomic_store_n(&c->h_mb[TASX_MB_N], n, __ATOMIC_RELAXED);
-  const uint32_t seq = ++c->bell;
-  __atomic_store_n(&c->h_mb[TASX_MB_BELL], seq, __ATOMIC_RELEASE);
-  while (__atomic_load_n(&c->h_mb[TASX_MB_DONE], __ATOMIC_ACQUIRE) != seq) {
-    if ((++k & 1023u) != 0)
-      continue;
-    if (t0 == 0.0)
-      t0 = now_s();
-    else if (now_s() - t0 > 0.02) {
-      hipError_t e = hipStreamQuery(c->pst);
-      if (e == hipSuccess) { /* the kernel exited before it saw the doorbell */
-        int rc = persist_launch(c);
-        if (rc)
-          return rc;
-        t0 = now_s();
-      } else if (e != hipErrorNotReady) {
-        c->persist_running = 0;
-        return hip_err(e, "persistent flush kernel");
-      } else if (now_s() - t0 > 2.0) {
-        return set_err(-EIO, "persistent flush: no completion for seq %u", seq);
-      }
-    }
-  }
-  c->n_persist_flushes++;
-  c->n_zerocopy_flushes++;
-  c->npend = 0;
-  return 0;
-}
-
 /* Zero-copy flush: every pending frame lies in the registered region and has
  * the TAS layout (tcp = ip + 20).  The kernel reads the frames straight from
  * host memory over PCIe (only the bytes it sums), writes both checksum fields
@@ -879,7 +703,7 @@ int tasx_flush(unsigned ctx_id)
     return 0;
   HIPCHK(hipSetDevice(c->device));
   if (zerocopy_ok(c))
-    return (c->persist && c->npend <= c->persist_cap) ? flush_persistent(c) : flush_zerocopy(c);
+    return flush_zerocopy(c);
   c->n_staged_flushes++;
   while (start < c->npend) {
     const int s = 0;

@@ -66,19 +66,6 @@ typedef struct tasx_flow_params {
   uint32_t fs_key_off;
 } tasx_flow_params;
 
-/* persistent flush kernel (tasx_ctx_set_persistent): mailbox words, each on
- * its own 64-byte line of coherent pinned host memory */
-enum { TASX_MB_BELL = 0, TASX_MB_N = 1, TASX_MB_DONE = 16, TASX_MB_STOP = 32, TASX_MB_EXIT = 48,
-       TASX_MB_WORDS = 64 };
-
-typedef struct tasx_persist_params {
-  tasx_tcp4_params frames;  /* base = registered frame region, off / flen =
-                             * coherent pinned descriptors; n set per flush */
-  uint32_t *mbox;           /* device view of the mailbox */
-  uint32_t cap;             /* descriptor capacity (frames per flush) */
-  uint64_t max_ticks;       /* lifetime cap, s_memrealtime ticks (100 MHz) */
-} tasx_persist_params;
-
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
@@ -89,8 +76,6 @@ int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream
 /* one-lane kernel storing seq into *word (pinned host memory, device view)
  * with system-scope release, after everything before it on the stream */
 int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
-/* the persistent flush kernel: one 1024-thread block polling the mailbox */
-int tasx_launch_flush_persist(const tasx_persist_params *q, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 

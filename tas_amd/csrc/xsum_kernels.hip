@@ -897,69 +897,6 @@ __global__ __launch_bounds__(64) void post_done_kernel(uint32_t *word, uint32_t 
     __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Persistent flush kernel (tasx_ctx_set_persistent): one 1024-thread block
-// stays resident and polls a doorbell word in coherent pinned host memory, so a
-// tx_flush costs the PCIe round trips and no kernel launch.  Thread 0 polls
-// (system-scope acquire loads, s_sleep between polls); on a new sequence
-// number the block runs tcp4_frame_row over the published frames (64 per
-// pass, frames and descriptors read over PCIe, both checksum fields written in
-// place), makes its stores visible system-wide and posts the sequence number
-// to the completion word.  Exit conditions every wave reaches: the stop word,
-// or the lifetime cap (s_memrealtime, 100 MHz), after which the host launches
-// it again; the exit reason is posted to the mailbox.  A relaunched kernel
-// takes the completion word as its last sequence, so a doorbell rung while it
-// was exiting is served by its successor.
-__global__ __launch_bounds__(1024) void flush_persist_kernel(tasx_persist_params q)
-{
-  __shared__ uint32_t s_seq, s_n, s_quit;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t last = 0;
-  if (threadIdx.x == 0)
-    last = __hip_atomic_load(&q.mbox[TASX_MB_DONE], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-  for (;;) {
-    if (threadIdx.x == 0) {
-      uint32_t quit = 0, seq = last;
-      for (;;) {
-        seq = __hip_atomic_load(&q.mbox[TASX_MB_BELL], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (seq != last)
-          break;
-        if (__hip_atomic_load(&q.mbox[TASX_MB_STOP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-          quit = 1;
-          break;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > q.max_ticks) {
-          quit = 2;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      s_seq = seq;
-      s_quit = quit;
-      s_n = quit ? 0u : __hip_atomic_load(&q.mbox[TASX_MB_N], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();
-    if (s_quit)
-      break;
-    const uint32_t seq = s_seq, n = min(s_n, q.cap);
-    for (uint32_t i = threadIdx.x / 16; i < n; i += 1024 / 16)
-      tcp4_frame_row<6>(q.frames, i, (int) (threadIdx.x & 15));
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      last = seq;
-      __hip_atomic_store(&q.mbox[TASX_MB_DONE], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&q.mbox[TASX_MB_EXIT], s_quit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-extern "C" int tasx_launch_flush_persist(const tasx_persist_params *q, void *stream)
-{
-  hipLaunchKernelGGL(flush_persist_kernel, dim3(1), dim3(1024), 0, (hipStream_t) stream, *q);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
 {
   hipLaunchKernelGGL(post_done_kernel, dim3(1), dim3(64), 0, (hipStream_t) stream, word, seq);

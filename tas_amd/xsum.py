@@ -63,8 +63,6 @@ SIGNATURES = {
     "tasx_flush": (_c_int, [_uns]),
     "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
     "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
-    "tasx_ctx_set_persistent": (_c_int, [_uns, _c_int, _c_u32]),
-    "tasx_ctx_persist_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_set_diag_buffer": (_c_int, [_vp]),
     "tasx_host_alloc": (_vp, [_sz]),
@@ -286,18 +284,6 @@ def tx_flush(ctx_id: int) -> None:
 def register_frames(ctx_id: int, base_addr: int, nbytes: int) -> None:
     """Zero-copy region for the context's frames (tasx_ctx_register_frames)."""
     _check(lib().tasx_ctx_register_frames(ctx_id, base_addr, nbytes), "tasx_ctx_register_frames")
-
-
-def set_persistent(ctx_id: int, enable: bool = True, cap: int = 1024) -> None:
-    """Serve zero-copy flushes of up to `cap` frames from a resident kernel
-    (tasx_ctx_set_persistent)."""
-    _check(lib().tasx_ctx_set_persistent(ctx_id, 1 if enable else 0, cap), "tasx_ctx_set_persistent")
-
-
-def persist_stats(ctx_id: int) -> tuple[int, int]:
-    f, la = ctypes.c_uint32(), ctypes.c_uint32()
-    _check(lib().tasx_ctx_persist_stats(ctx_id, ctypes.byref(f), ctypes.byref(la)), "tasx_ctx_persist_stats")
-    return f.value, la.value
 
 
 def ctx_stats(ctx_id: int) -> tuple[int, int]:

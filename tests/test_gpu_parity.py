@@ -524,62 +524,6 @@ def test_zero_copy_flush(oracle):
         xsum.ctx_destroy(3)
 
 
-def test_persistent_flush(oracle):
-    """tasx_ctx_set_persistent: zero-copy flushes served by the resident kernel.
-    The same frame slots get new contents every round (stale-cache check),
-    lengths vary, a flush above the cap launches as before, other streams keep
-    running while the kernel is resident, the kernel is relaunched after its
-    lifetime cap and after disable / enable."""
-    import time
-    xsum.ctx_init(5, 0, 1 << 20)
-    pin = xsum.PinnedBuffer(64 * 2048)
-    try:
-        xsum.register_frames(5, pin.addr, pin.nbytes)
-        xsum.set_persistent(5, True, cap=48)
-
-        def flush_round(cnt, seed):
-            pay = (np.arange(cnt) * 47 + seed * 13) % 1449
-            frames = pktgen.tcp4_frames(cnt, payload=pay, stride=2048, seed=seed)
-            ref = frames.copy()
-            oracle.tcp4_batch(ref, cnt, stride=2048, inplace=True)
-            pin.array[:frames.size] = frames
-            for i in range(cnt):
-                xsum.tcp_checksums(5, pin.addr + i * 2048)
-            xsum.tx_flush(5)
-            np.testing.assert_array_equal(pin.array[:frames.size], ref, err_msg=f"{cnt} frames, seed {seed}")
-
-        for rnd in range(40):
-            flush_round([1, 7, 32, 48][rnd % 4], 100 + rnd)
-        f, la = xsum.persist_stats(5)
-        assert f == 40 and la >= 1
-        z0, _ = xsum.ctx_stats(5)
-        flush_round(64, 200)  # above the cap: an ordinary zero-copy launch
-        assert xsum.persist_stats(5)[0] == 40 and xsum.ctx_stats(5)[0] == z0 + 1
-        # the default stream's kernels run while the flush kernel is resident
-        # (a fresh instance: it stays for TASX_PERSIST_LIFETIME_MS = 100 ms)
-        torch.ones(1 << 20, device=DEV).sum().item()  # kernels loaded before timing
-        xsum.set_persistent(5, False)
-        xsum.set_persistent(5, True, cap=48)
-        flush_round(32, 201)
-        t0 = time.perf_counter()
-        torch.ones(1 << 20, device=DEV).sum().item()
-        assert time.perf_counter() - t0 < 0.03
-        # lifetime cap: the next flush relaunches
-        la = xsum.persist_stats(5)[1]
-        time.sleep(0.15)
-        flush_round(32, 202)
-        assert xsum.persist_stats(5) == (42, la + 1)
-        xsum.set_persistent(5, False)
-        flush_round(8, 203)  # ordinary zero-copy again
-        assert xsum.persist_stats(5)[0] == 42
-        xsum.set_persistent(5, True, cap=48)
-        flush_round(8, 204)
-        assert xsum.persist_stats(5) == (43, la + 2)
-    finally:
-        xsum.ctx_destroy(5)
-        pin.free()
-
-
 def test_zero_copy_pageable_region(oracle):
     """hipHostRegister of ordinary (numpy) memory as the frame region."""
     xsum.ctx_init(4, 0, 1 << 20)

@@ -69,8 +69,7 @@ int main(int argc, char **argv)
   int r;
 
   if (!pool || !plain || !ref || tasx_ctx_init(0, 0, 32u << 20) || tasx_ctx_init(1, 0, 32u << 20) ||
-      tasx_ctx_register_frames(1, pool, (size_t) maxn * STRIDE) || tasx_ctx_init(2, 0, 32u << 20) ||
-      tasx_ctx_register_frames(2, pool, (size_t) maxn * STRIDE) || tasx_ctx_set_persistent(2, 1, maxn)) {
+      tasx_ctx_register_frames(1, pool, (size_t) maxn * STRIDE)) {
     fprintf(stderr, "setup: %s\n", tasx_last_error());
     return 1;
   }
@@ -83,7 +82,7 @@ int main(int argc, char **argv)
 
   for (s = 0; s < sizeof(sizes) / sizeof(sizes[0]); s++) {
     const unsigned n = sizes[s];
-    double staged, zc, pers, cpu;
+    double staged, zc, cpu;
     /* staged flush (frames in ordinary memory) */
     for (r = 0; r < reps; r++) {
       double t0 = now_us();
@@ -108,18 +107,6 @@ int main(int argc, char **argv)
       t[r] = now_us() - t0;
     }
     zc = median(t, reps);
-    /* zero-copy flush served by the resident kernel (tasx_ctx_set_persistent) */
-    for (r = 0; r < reps; r++) {
-      double t0 = now_us();
-      for (i = 0; i < n; i++)
-        tasx_tcp_checksums(2, NULL, pool + (size_t) i * STRIDE, 0, 0, 0);
-      if (tasx_flush(2)) {
-        fprintf(stderr, "flush: %s\n", tasx_last_error());
-        return 1;
-      }
-      t[r] = now_us() - t0;
-    }
-    pers = median(t, reps);
     /* the reference path on one core: tcp_checksums per frame */
     for (r = 0; r < reps; r++) {
       double t0 = now_us();
@@ -133,8 +120,7 @@ int main(int argc, char **argv)
       return 2;
     }
     printf("{\"frames\": %u, \"staged_flush_us\": %.2f, \"zero_copy_flush_us\": %.2f, "
-           "\"persistent_flush_us\": %.2f, \"cpu_1core_us\": %.2f, \"bytes_per_frame\": 1504}\n",
-           n, staged, zc, pers, cpu);
+           "\"cpu_1core_us\": %.2f, \"bytes_per_frame\": 1504}\n", n, staged, zc, cpu);
     fflush(stdout);
   }
   {
@@ -142,14 +128,8 @@ int main(int argc, char **argv)
     tasx_ctx_stats(1, &z, &st);
     fprintf(stderr, "zero-copy flushes %u, staged %u\n", z, st);
   }
-  {
-    uint32_t f = 0, la = 0;
-    tasx_ctx_persist_stats(2, &f, &la);
-    fprintf(stderr, "persistent flushes %u, kernel launches %u\n", f, la);
-  }
   tasx_ctx_destroy(0);
   tasx_ctx_destroy(1);
-  tasx_ctx_destroy(2);
   tasx_host_free(pool);
   return 0;
 }
