@@ -255,7 +255,12 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
  *     batches up to ip.len 1522); otherwise as 0.  RAW: raw_sad_kernel
  *     (32-bit offsets from the base in stride mode within 4 GiB)
  *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk
- *     sequence: mixed lengths keep every lane loading); TCP4 as 0 */
+ *     sequence: mixed lengths keep every lane loading); TCP4 as 0
+ *   8 TCP4: tcp4_wave_kernel (the same flattening over each frame's hinted
+ *     datagram, header words taken off per frame; frames whose
+ *     ip.total_length differs from the hint are redone by 2's row body);
+ *     needs l4_off == ip_off + 20, else as 0.  A/B only: slower than 3 on
+ *     data/ACK mixes.  RAW and verification as 0 */
 int tasx_set_kernel_variant(int variant);
 /* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
  * wave.  NULL disables. */

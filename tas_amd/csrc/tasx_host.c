@@ -73,7 +73,7 @@ int tasx_set_diag_buffer(void *dev_buf)
 
 int tasx_set_kernel_variant(int variant)
 {
-  if (variant < 0 || variant > 7)
+  if (variant < 0 || variant > 8)
     return set_err(-EINVAL, "kernel variant %d out of range", variant);
   g_variant = variant;
   return 0;

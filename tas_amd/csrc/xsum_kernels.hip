@@ -34,9 +34,11 @@
 // kernels (kept as the A/B baseline), 4 = tcp4_tas_kernel with wave-timeline
 // stamps (diagnostic), 5 = tcp4_tas_kernel with 32-lane groups (A/B), 7 =
 // raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
-// chunk sequence).
+// chunk sequence), 8 = tcp4_wave_kernel (TCP4 with per-frame hints: the same
+// flattening over each frame's datagram).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "tasx_kernels.h"
 
@@ -301,22 +303,14 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
   return ((uint64_t) hi << 32) | lo;
 }
 
+// The flattened sum of a wave's 4 packets (raw_wave_kernel, tcp4_wave_kernel):
+// lanes k and 4 + k hold packet k's start address a and length len (len 0 =
+// nothing to sum); returns on lane k < 4 the exact 32-bit sum of packet k's
+// little-endian 16-bit words counted in the address frame (from even addresses).
 template <int U>
-__global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
+__device__ __forceinline__ uint32_t wave4_sums(uint32_t lane, uint64_t a, uint32_t len)
 {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
-  if (i0 >= p.n) // wave-uniform
-    return;
   const uint32_t k = lane & 3u;
-  const uint32_t i = i0 + k;
-  // lanes k and 4 + k hold packet k's descriptor
-  uint64_t a = 0;
-  uint32_t len = 0;
-  if (lane < 8u && i < p.n) {
-    a = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i);
-    len = p.len ? ldg(p.len, i) : p.len0;
-  }
   const uint32_t head = (uint32_t) a & 15u;
   const uint32_t nch = len ? (head + len + 15u) >> 4 : 0u;
   const uint64_t c0 = a & ~15ull;
@@ -360,10 +354,28 @@ __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     t[j] = (uint32_t) __builtin_amdgcn_readlane((int) group_total<64>(A[j]), 63);
+  return k == 0u ? t[0] - t[1] : k == 1u ? t[1] - t[2] : k == 2u ? t[2] - t[3] : t[3];
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
+  if (i0 >= p.n) // wave-uniform
+    return;
+  const uint32_t i = i0 + (lane & 3u);
+  // lanes k and 4 + k hold packet k's descriptor
+  uint64_t a = 0;
+  uint32_t len = 0;
+  if (lane < 8u && i < p.n) {
+    a = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i);
+    len = p.len ? ldg(p.len, i) : p.len0;
+  }
+  const uint32_t s = wave4_sums<U>(lane, a, len);
   if (lane < 4u && i < p.n) {
-    const uint32_t s = k == 0u ? t[0] - t[1] : k == 1u ? t[1] - t[2] : k == 2u ? t[2] - t[3] : t[3];
     uint32_t f = fold32_to_16(s);
-    if (head & 1u)
+    if (a & 1u)
       f = bswap16(f);
     stg(p.out, i, (uint16_t) f);
   }
@@ -500,6 +512,90 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
   if (i >= p.n)
     return; // whole 16-lane group (one DPP row) leaves together
   tcp4_frame_row<U, VERIFY>(p, i, threadIdx.x & 15);
+}
+
+// TCP4 batches of mixed frame lengths with per-frame hints (a tx_flush batch:
+// flow_tx_segment data frames among flow_tx_ack / inject_tcp_ts frames,
+// fast_flows.c:877-1030).  One row per frame leaves the rows of short frames
+// idle while the wave's longest frame is read; here a wave's 4 frames are one
+// flattened chunk sequence, as in raw_wave_kernel: each datagram [ip, ip +
+// hint - ip_off) is summed whole (exact 32-bit word sum; the IPv4 header is at
+// an even address), then lane k takes frame k's header words off it:
+//   L4 sum  = datagram sum - the 10 IPv4 header words - tcp.chksum as stored
+//   IP sum  = the IPv4 header words - ip.chksum as stored
+// (exact subtractions of words the datagram sum holds; tcp.chksum lies inside
+// it because the hint covers ip + 40).  The header words are loaded up front,
+// in flight with round 0.  A frame whose ip.total_length is not the hinted
+// datagram length, whose hint does not cover ip + 40, or whose header sits at
+// an odd address is redone by one 16-lane row (tcp4_frame_row): the results
+// always follow ip.total_length, the hint only decides the reads.
+// Measured (tools/ackmix_probe.py, profiles/r01_ackmix.jsonl): slower than
+// tcp4_tas_kernel's row per frame at every ACK fraction (0 / 25 / 50 / 75 %:
+// 18.0 / 15.9 / 14.9 / 14.0 us against 17.2 / 15.0 / 13.8 / 12.7 us for 64K
+// frames).  These batches are bound by per-wave dependent latency (hint ->
+// data -> store) over ~2.7 generations of resident waves, not by bytes, and
+// the flattened pass adds VALU and registers (70 VGPRs against 55 for
+// raw_wave_kernel) without removing a dependent step.  Kept as variant 8 (A/B).
+template <int U>
+__global__ __launch_bounds__(kBlock) void tcp4_wave_kernel(tasx_tcp4_params p)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
+  if (i0 >= p.n) // wave-uniform
+    return;
+  const uint32_t i = i0 + (lane & 3u);
+  uint64_t a = 0;
+  uint32_t len = 0;
+  if (lane < 8u && i < p.n) {
+    const uint32_t h = p.flen ? ldg(p.flen, i) : p.flen0;
+    const uint64_t ipa = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i) + p.ip_off;
+    if (h >= p.ip_off + 40u && !(ipa & 1u)) {
+      a = ipa;
+      len = min(h - p.ip_off, 65535u);
+    }
+  }
+  uint32_t w[10], wt = 0;
+#pragma unroll
+  for (int j = 0; j < 10; ++j)
+    w[j] = 0;
+  if (lane < 4u && len) {
+    const uint16_t *ip16 = (const uint16_t *) (uintptr_t) a;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      w[j] = ldg(ip16, (uint32_t) j);
+    wt = ldg(ip16, 18u); // tcp.chksum: ip + 20 + 16 (l4_off == ip_off + 20)
+  }
+  const uint32_t s = wave4_sums<U>(lane, a, len);
+  bool redo = false;
+  if (lane < 4u && i < p.n) {
+    const uint32_t tl = bswap16(w[1]);
+    redo = len == 0u || tl != len;
+    if (!redo) {
+      uint32_t ipall = 0;
+#pragma unroll
+      for (int j = 0; j < 10; ++j)
+        ipall += w[j];
+      const uint32_t ph = w[6] + w[7] + w[8] + w[9] + (w[4] & 0xff00u); // src, dst, {0, proto}
+      const uint32_t ipc = inv_result(residue(fold32_to_16(ipall - w[5])));
+      const uint32_t r = fold32_to_16(s - ipall - wt) + fold32_to_16(ph) + bswap16(tl - 20u);
+      const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
+      if (p.out)
+        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+      if (p.flags & TASX_F_INPLACE) {
+        uint8_t *ip = (uint8_t *) (uintptr_t) a;
+        st8(ip + 10, ipc);
+        st8(ip + 11, ipc >> 8);
+        st8(ip + 36, tcpc);
+        st8(ip + 37, tcpc >> 8);
+      }
+    }
+  }
+  const uint64_t rb = __builtin_amdgcn_ballot_w64(redo);
+  if (rb) { // row r (lanes 16r..16r+15) redoes frame i0 + r
+    const uint32_t r = lane >> 4;
+    if ((rb >> r) & 1ull)
+      tcp4_frame_row<3>(p, i0 + r, (int) (lane & 15u)); // (3 per round: keeps the rare redo below the flattened pass's registers)
+  }
 }
 
 // mask of the bytes of a dword (first byte at ip-relative offset `base`) that
@@ -863,6 +959,18 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
+// tcp4_wave_kernel's LDS reservation (residency cap), bytes; A/B knob
+// TASX_WAVE_TCP4_LDS (KiB), read once; default none
+static uint32_t tasx_wave_lds_tcp4()
+{
+  static int v = -1;
+  if (v < 0) {
+    const char *e = getenv("TASX_WAVE_TCP4_LDS");
+    v = e ? atoi(e) * 1024 : 0;
+  }
+  return (uint32_t) v;
+}
+
 // tcp4_tas_kernel preconditions: TAS layout, 16-byte aligned base, stride mode,
 // every frame within 4 GiB of the base (32-bit offsets)
 static bool tas_kernel_ok(const tasx_tcp4_params &p)
@@ -906,6 +1014,8 @@ extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
+  if (variant == 8) // TCP4-only variant
+    variant = 0;
   switch (variant) {
   case 2:
   case 3:
@@ -931,7 +1041,7 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
-  if (variant == 7) // RAW-only variant
+  if (variant == 7 || variant == 8) // RAW-only / TX-only variants
     variant = 0;
   if ((variant == 0 || variant == 6) && tas14_ok(*p))
     return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
@@ -948,8 +1058,12 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
     variant = 0;
   if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p)) // headline kernel not applicable
     variant = 0;
+  if (variant == 8 && p->l4_off != p->ip_off + 20u) // tcp4_wave_kernel needs TCP right after a 20-byte IPv4 header
+    variant = 0;
   if (variant == 0) // TAS frames, uniform hint or none -> tcp4_tas14_kernel; TAS layout + per-frame hints -> 3
     variant = (tas14_ok(*p) || tas14_nohint_ok(*p)) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
+  if (variant == 8)
+    return launch_groups(tcp4_wave_kernel<TASX_WAVE_U>, *p, s, tasx_wave_lds_tcp4());
   if (variant >= 3 && !tas_ok)
     variant = 2;
   switch (variant) {

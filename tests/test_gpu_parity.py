@@ -328,7 +328,62 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 8])
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 4099])
+@pytest.mark.parametrize("ack_frac", [0.0, 0.5, 0.9])
+def test_tcp4_flush_mix_per_frame_hints(oracle, n, ack_frac, variant):
+    """tx_flush-shaped batches with per-frame hints (automatic: tcp4_tas_kernel;
+    8: tcp4_wave_kernel): data segments among pure ACKs (ip.len 52), ragged batch
+    ends, a few hints that disagree with ip.total_length or do not cover ip + 40,
+    in place and to the output array."""
+    xsum.set_kernel_variant(variant)
+    try:
+        _flush_mix(oracle, n, ack_frac)
+    finally:
+        xsum.set_kernel_variant(0)
+
+
+def _flush_mix(oracle, n, ack_frac):
+    rng = np.random.default_rng(n * 7 + int(ack_frac * 10))
+    pay = np.where(rng.random(n) < ack_frac, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=n + 3)
+    hint = (14 + 52 + pay).astype(np.int32)
+    hint[5::37] -= 1           # short hint: the row body redoes the frame
+    hint[6::37] += 7           # long hint
+    hint[7::37] = 40           # does not cover tcp.chksum
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
+    d = to_dev(frames)
+    got = u16(xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=to_dev(hint)))
+    np.testing.assert_array_equal(got, exp)
+    xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=to_dev(hint), inplace=True, want_out=False)
+    f = d.cpu().numpy().reshape(n, 2048)
+    np.testing.assert_array_equal(f[:, 24:26].copy().view(np.uint16).ravel(), exp[0::2])
+    np.testing.assert_array_equal(f[:, 50:52].copy().view(np.uint16).ravel(), exp[1::2])
+
+
+def test_tcp4_wave_odd_offsets(oracle):
+    """Per-frame hints with frames at odd and even offsets (odd IPv4 headers go
+    to the row body, even ones are flattened)."""
+    n = 2048
+    pay = np.where(np.arange(n) % 3 == 0, 0, 1448 - (np.arange(n) % 200)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=81)
+    shift = (pktgen.splitmix64(82, n) % np.uint64(100)).astype(np.int64)
+    offs = np.arange(n, dtype=np.int64) * 2176 + shift
+    big = np.zeros(n * 2176 + 2048, np.uint8)
+    for i in range(n):
+        big[offs[i]:offs[i] + 2048] = frames[i * 2048:(i + 1) * 2048]
+    exp = oracle.tcp4_batch(big, n, offsets=offs)
+    hint = (14 + 52 + pay).astype(np.int32)
+    for v in (0, 8):
+        xsum.set_kernel_variant(v)
+        try:
+            got = u16(xsum.tcp4_cksum_batch(to_dev(big), n, offsets=to_dev(offs), frame_len=to_dev(hint)))
+        finally:
+            xsum.set_kernel_variant(0)
+        np.testing.assert_array_equal(got, exp, err_msg=f"variant {v}")
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6, 7, 8])
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
@@ -356,7 +411,7 @@ def test_tcp4_all_variants_and_hints(oracle, variant):
         xsum.set_kernel_variant(0)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 7, 8])
 def test_raw_all_variants(oracle, variant):
     buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
     n = len(lens)
