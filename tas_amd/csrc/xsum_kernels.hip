@@ -830,7 +830,10 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
   bool in_range = true;
   if constexpr (NOHINT) {
     const uint32_t tl0 = bswap16(ld16nt_off(p.base, a0 + 16u).x & 0xffffu);
-    in_range = tl0 >= 64u && tl0 <= 1522u;
+    // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
+    // the end never include the masked field; pure ACKs, ip.len 52, qualify)
+    // to 1522 (96 chunks)
+    in_range = tl0 >= 38u && tl0 <= 1522u;
     hend = in_range ? tl0 : 20u; // out of range: the header only, then the general body
   } else {
     hend = p.flen0 - p.ip_off;
@@ -979,10 +982,15 @@ static bool tas_kernel_ok(const tasx_tcp4_params &p)
          (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
 }
 
-// tcp4_tas14_kernel without a hint: IPv4 header at 14 mod 16 in every frame
+// tcp4_tas14_kernel without a hint: IPv4 header at 14 mod 16 in every frame.
+// Per-frame hints are ignored here (hints only steer reads): each row reads its
+// own total_length first, which on data/ACK mixes beats tcp4_tas_kernel's
+// hint-first rows at every ACK fraction (64K frames, 0 / 25 / 50 / 75 % ACKs:
+// 17.0 / 14.1 / 11.9 / 10.2 us against 17.5 / 15.2 / 14.0 / 12.8 us;
+// profiles/r01_ackmix_nohint.jsonl)
 static bool tas14_nohint_ok(const tasx_tcp4_params &p)
 {
-  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0 && !p.flen && !p.flen0;
+  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0 && !p.flen0;
 }
 
 // tcp4_tas14_kernel, in addition: IPv4 header at 14 mod 16 in every frame, a
@@ -1060,7 +1068,8 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
     variant = 0;
   if (variant == 8 && p->l4_off != p->ip_off + 20u) // tcp4_wave_kernel needs TCP right after a 20-byte IPv4 header
     variant = 0;
-  if (variant == 0) // TAS frames, uniform hint or none -> tcp4_tas14_kernel; TAS layout + per-frame hints -> 3
+  if (variant == 0) // TAS frames in 16-byte rooms: uniform hint, per-frame hints or none -> tcp4_tas14_kernel;
+                    // other TAS-layout batches with a hint -> 3
     variant = (tas14_ok(*p) || tas14_nohint_ok(*p)) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
   if (variant == 8)
     return launch_groups(tcp4_wave_kernel<TASX_WAVE_U>, *p, s, tasx_wave_lds_tcp4());

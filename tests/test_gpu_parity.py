@@ -669,6 +669,40 @@ def test_verify_edges(oracle, tcp4_golden, shift):
     np.testing.assert_array_equal(got, oracle.tcp4_verify_batch(mixed, 2 * n, stride=stride))
 
 
+@pytest.mark.parametrize("stride", [80, 128, 2048])
+def test_tcp4_and_verify_short_frames_no_hint(oracle, stride):
+    """Frames with total_length 0..90 (ACK and SYN sizes among them) without a
+    hint: tcp4_tas14_kernel takes 38..1522 itself, the rest goes to the general
+    body; TX checksums, then verification of the checksummed frames and of
+    frames with random checksum fields."""
+    tl = np.tile(np.arange(91), 9)
+    n = len(tl)
+    frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=stride, ip_total_len=np.minimum(tl, stride - 14))
+    f = frames.reshape(n, stride)
+    f[:, 16] = (tl >> 8) & 0xFF
+    f[:, 17] = tl & 0xFF       # total_length may exceed the room: the bytes past it are the next frame's
+    big = np.concatenate([frames, np.zeros(128, np.uint8)])
+    exp = oracle.tcp4_batch(big.copy(), n, stride=stride)
+    d = to_dev(big)
+    np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride)), exp)
+    vexp = oracle.tcp4_verify_batch(big.copy(), n, stride=stride)
+    np.testing.assert_array_equal(xsum.tcp4_verify_batch(d, n, stride=stride).cpu().numpy(), vexp)
+    xsum.tcp4_cksum_batch(d, n, stride=stride, inplace=True, want_out=False)
+    good = d.cpu().numpy()
+    np.testing.assert_array_equal(xsum.tcp4_verify_batch(d, n, stride=stride).cpu().numpy(),
+                                  oracle.tcp4_verify_batch(good, n, stride=stride))
+
+
+def test_tcp4_flush_mix_no_hint(oracle):
+    """Data segments among pure ACKs, no hint (each row reads its own total_length)."""
+    n = 8192
+    rng = np.random.default_rng(5)
+    pay = np.where(rng.random(n) < 0.5, 0, pktgen.TCP_MSS).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=5)
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
+    np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=2048)), exp)
+
+
 @pytest.mark.parametrize("variant", [0, 2])
 def test_verify_uniform_hint(oracle, variant):
     """Received uniform-MTU batches with one frame-length hint (the headline
