@@ -962,16 +962,27 @@ int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStr
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-// tcp4_wave_kernel's LDS reservation (residency cap), bytes; A/B knob
-// TASX_WAVE_TCP4_LDS (KiB), read once; default none
+// LDS reservations (residency caps) as A/B knobs, KiB in the environment
+static uint32_t env_lds(const char *name, uint32_t dflt)
+{
+  const char *e = getenv(name);
+  return e ? (uint32_t) atoi(e) * 1024u : dflt;
+}
+// tcp4_wave_kernel: TASX_WAVE_TCP4_LDS, default none
 static uint32_t tasx_wave_lds_tcp4()
 {
-  static int v = -1;
-  if (v < 0) {
-    const char *e = getenv("TASX_WAVE_TCP4_LDS");
-    v = e ? atoi(e) * 1024 : 0;
-  }
-  return (uint32_t) v;
+  static const uint32_t v = env_lds("TASX_WAVE_TCP4_LDS", 0u);
+  return v;
+}
+// tcp4_tas14_kernel without a uniform hint (TX): TASX_TAS14_NOHINT_LDS, default
+// none.  The batches this path sees mix lengths (per-frame hints or none) and
+// ACK-heavy ones are latency-bound, so the 6 waves/SIMD its 74 VGPRs allow pay
+// (64K frames at 50 / 75 % ACKs: 11.8 -> 11.25, 10.1 -> 9.3 us) where the
+// uniform batch loses 0.7 % (16.88 -> 17.0 us; profiles/r01_ackmix_lds_ab.txt)
+static uint32_t tas14_nohint_lds()
+{
+  static const uint32_t v = env_lds("TASX_TAS14_NOHINT_LDS", 0u);
+  return v;
 }
 
 // tcp4_tas_kernel preconditions: TAS layout, 16-byte aligned base, stride mode,
@@ -1089,7 +1100,7 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   case 6:
     if (tas14_ok(*p))
       return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
-    return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, kOccLds);
+    return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, tas14_nohint_lds());
   default:
     return -2;
   }
