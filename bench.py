@@ -73,6 +73,7 @@ def parse(argv=None):
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--no-txseg", action="store_true")
     ap.add_argument("--no-flow", action="store_true")
+    ap.add_argument("--no-flushmix", action="store_true")
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
@@ -179,6 +180,39 @@ class Tcp4Workload:
 
         def launch(k):
             rc = fn(*args[k % R], ss[k % S])
+            if rc:
+                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev_hint")
+        return launch
+
+
+class FlushMixWorkload:
+    """A tx_flush-shaped TCP4 batch: flow_tx_segment data frames (1514 B) and
+    flow_tx_ack frames (66 B, ip.len 52; fast_flows.c:877-1030) half and half in
+    random order, 2048 B mbuf rooms, each frame's length (mbuf data_len) as its
+    hint; automatic kernel selection."""
+    desc = (f"{N_FRAMES} TAS TX frames in {STRIDE} B rooms, 50% data segments (ip.len {IP_TOTAL}) and 50% "
+            "pure ACKs (ip.len 52) in random order, per-frame hints (mbuf data_len)")
+
+    def __init__(self, rotate: int, seed: int, n: int = N_FRAMES, stride: int = STRIDE):
+        rng = np.random.default_rng(seed)
+        pay = np.where(rng.random(n) < 0.5, 0, IP_TOTAL - 52).astype(np.int64)
+        self.n, self.stride = n, stride
+        self.host = pktgen.tcp4_frames(n, payload=pay, stride=stride, seed=seed)
+        first = torch.from_numpy(self.host).cuda()
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.flen = torch.from_numpy((pktgen.ETH_LEN + 52 + pay).astype(np.int32)).cuda()
+        self.outs = [torch.empty(2 * n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
+        self.bytes_per_step = int((52 + pay + 4).sum())
+
+    def launcher(self):
+        fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
+        s = torch.cuda.current_stream().cuda_stream
+        args = [(b.data_ptr(), None, self.stride, self.flen.data_ptr(), 0, self.n, pktgen.ETH_LEN,
+                 pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), 0, s) for b, o in zip(self.bufs, self.outs)]
+        R = len(args)
+
+        def launch(k):
+            rc = fn(*args[k % R])
             if rc:
                 raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev_hint")
         return launch
@@ -764,6 +798,13 @@ def main():
     for b in wl.bufs:  # restore the un-checksummed frames for the legs below
         b.copy_(src)
     del src
+    mix = None
+    if not args.no_flushmix:
+        mw = FlushMixWorkload(min(rot, 12), pktgen.SEED + 500 + rank)
+        mix = leg(mw, args, ws, FlushMixWorkload.desc)
+        mix["parity"] = "tests/test_gpu_parity.py::test_tcp4_flush_mix_per_frame_hints"
+        del mw
+        torch.cuda.empty_cache()
     raw = None
     if not args.no_raw:
         rw = RawWorkload(rot, pktgen.SEED + 1000 + rank)
@@ -836,6 +877,7 @@ def main():
             "tcp4_nohint": nohint,
             "two_contexts": ctx2,
             "rx_verify": rx,
+            "flush_mix": mix,
         }
         if raw is not None:
             line["raw"] = raw

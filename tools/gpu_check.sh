@@ -21,5 +21,5 @@ step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()'
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step bench 300 python bench.py "$@"
 export TMPDIR=/tmp
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --steps 100 --warmup 10
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --no-flushmix --steps 100 --warmup 10
 echo done

@@ -25,7 +25,7 @@ for w in mixed shard8m tso; do
 done
 # the N>1 code path (2 ranks on this one GPU; gloo carries the barrier and the
 # two scalar reductions, as TASX_DIST_BACKEND allows)
-step bench_n2 300 env TASX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts
+step bench_n2 300 env TASX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts --no-flushmix
 export TMPDIR=/tmp
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --steps 100 --warmup 10
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --no-flushmix --steps 100 --warmup 10
 echo done
