@@ -816,8 +816,8 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // exactly that length -- two dependent memory latencies per frame instead of
 // one, no bytes read past ip.total_length (DPDK's own trust in the header).
 // Rows with total_length outside [64, 1522] take the general body.
-template <int U, bool VERIFY = false, bool NOHINT = false>
-__global__ __launch_bounds__(kBlock) void tcp4_tas14_kernel(tasx_tcp4_params p)
+template <int U, bool VERIFY = false, bool NOHINT = false, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
@@ -974,6 +974,13 @@ static uint32_t tasx_wave_lds_tcp4()
   static const uint32_t v = env_lds("TASX_WAVE_TCP4_LDS", 0u);
   return v;
 }
+// tcp4_tas14_kernel without a uniform hint (TX): register budget (waves per
+// SIMD) as an A/B knob, TASX_TAS14_WPE, default 8
+static int tas14_nohint_wpe()
+{
+  static const int v = getenv("TASX_TAS14_WPE") ? atoi(getenv("TASX_TAS14_WPE")) : 8;
+  return v;
+}
 // tcp4_tas14_kernel without a uniform hint (TX): TASX_TAS14_NOHINT_LDS, default
 // none.  The batches this path sees mix lengths (per-frame hints or none) and
 // ACK-heavy ones are latency-bound, so the 6 waves/SIMD its 74 VGPRs allow pay
@@ -1100,7 +1107,19 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   case 6:
     if (tas14_ok(*p))
       return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
-    return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, tas14_nohint_lds());
+    // built for 8 waves per SIMD (64 VGPRs; the spills are confined to the
+    // general-body fallback after the fast path's stores): ACK-heavy mixes are
+    // latency-bound and gain from the residency (64K frames at 50 / 75 / 100 %
+    // ACKs: 11.2 / 9.3-9.9 / 7.38 -> 10.8 / 8.6 / 6.97 us; uniform MTU 17.05 ->
+    // 17.0; profiles/r01_ackmix_wpe_ab.txt).  TASX_TAS14_WPE=6 or 7 for A/B.
+    switch (tas14_nohint_wpe()) {
+    case 6:
+      return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, tas14_nohint_lds());
+    case 7:
+      return launch_groups(tcp4_tas14_kernel<6, false, true, 7>, *p, s, tas14_nohint_lds());
+    default:
+      return launch_groups(tcp4_tas14_kernel<6, false, true, 8>, *p, s, tas14_nohint_lds());
+    }
   default:
     return -2;
   }
