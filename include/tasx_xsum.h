@@ -253,7 +253,10 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
  *     aligned base and stride), stride mode, one uniform hint flen0 with
  *     ip_off + 64 <= flen0 and the datagram within 96 chunks (uniform-MTU
  *     batches up to ip.len 1522), or no uniform hint (per-frame hints are
- *     then ignored: each row reads its total_length first); otherwise as 0.
+ *     then ignored: each row reads its total_length first), and the same
+ *     without a uniform hint for frames by an offsets array with the IPv4
+ *     header at 14 mod 16 from the frame start (frames not 16-byte aligned
+ *     go to 2's row body); otherwise as 0.
  *     RAW: raw_sad_kernel
  *     (32-bit offsets from the base in stride mode within 4 GiB)
  *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk

@@ -816,25 +816,40 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // exactly that length -- two dependent memory latencies per frame instead of
 // one, no bytes read past ip.total_length (DPDK's own trust in the header).
 // Rows with total_length outside [64, 1522] take the general body.
-template <int U, bool VERIFY = false, bool NOHINT = false, int WPE = 1>
+// OFFS (with NOHINT, TX): frames at base + off[i] instead of i * stride; a row
+// whose frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned
+// loads only the aligned chunk holding the IPv4 header start and is redone by
+// the general row body (tcp4_frame_row).
+template <int U, bool VERIFY = false, bool NOHINT = false, int WPE = 1, bool OFFS = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
-  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
+  uint32_t a0;
+  bool row_ok = true;
+  if constexpr (OFFS) {
+    const uint64_t fo = (uint64_t) (uintptr_t) p.base + ldg(p.off, i) + (p.ip_off & ~15u);
+    row_ok = (fo & 15u) == 0u;
+    fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
+    a0 = 0;
+  } else {
+    a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  }
   // the datagram [ip, ip + hend) and its last chunk: uniform from the hint, or
   // per row from the frame's own total_length
   uint32_t hend;
   bool in_range = true;
   if constexpr (NOHINT) {
-    const uint32_t tl0 = bswap16(ld16nt_off(p.base, a0 + 16u).x & 0xffffu);
+    const uint32_t tl0 = bswap16(ld16nt_off(fb, a0 + (row_ok ? 16u : 0u)).x & 0xffffu);
     // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
     // the end never include the masked field; pure ACKs, ip.len 52, qualify)
     // to 1522 (96 chunks)
-    in_range = tl0 >= 38u && tl0 <= 1522u;
-    hend = in_range ? tl0 : 20u; // out of range: the header only, then the general body
+    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u;
+    // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   } else {
     hend = p.flen0 - p.ip_off;
   }
@@ -844,7 +859,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   u32x4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
+    v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
 
   // chunks 0..3: the L4 part of chunk gl (none for 0, 1), whole chunks elsewhere
   const u32x4 h = v[0];
@@ -899,7 +914,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     if (p.out)
       stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
     if (p.flags & TASX_F_INPLACE) {
-      uint8_t *ip = p.base + a0 + 14u;
+      uint8_t *ip = (uint8_t *) fb + a0 + 14u;
       st8(ip + 10, ipc);
       st8(ip + 11, ipc >> 8);
       st8(ip + 36, tcpc);
@@ -909,7 +924,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
     if (__shfl((int) bad, gbase + 15, 64)) {
-      tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
+      if constexpr (OFFS)
+        tcp4_frame_row<3, VERIFY>(p, i, gl);
+      else
+        tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
     }
   }
 }
@@ -1011,6 +1029,14 @@ static bool tas14_nohint_ok(const tasx_tcp4_params &p)
   return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0 && !p.flen0;
 }
 
+// tcp4_tas14_kernel<OFFS> (no uniform hint, offsets array): TCP right after a
+// 20-byte IPv4 header at 14 mod 16 from the frame start; frames whose start is
+// not 16-byte aligned are checked per row and go to the general body
+static bool tas14_offs_ok(const tasx_tcp4_params &p)
+{
+  return p.off != nullptr && p.l4_off == p.ip_off + 20 && (p.ip_off & 15u) == 14u && !p.flen0;
+}
+
 // tcp4_tas14_kernel, in addition: IPv4 header at 14 mod 16 in every frame, a
 // uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
 static bool tas14_ok(const tasx_tcp4_params &p)
@@ -1082,8 +1108,15 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   const bool tas_ok = tas_kernel_ok(*p);
   if (variant == 7) // RAW-only variant
     variant = 0;
-  if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p)) // headline kernel not applicable
+  if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p) && !tas14_offs_ok(*p)) // headline kernel not applicable
     variant = 0;
+  if ((variant == 0 || variant == 6) && tas14_offs_ok(*p)) {
+    // frames by offsets (the INTEGRATION.md section 5 call, the flush paths): as
+    // tas14_nohint_ok below, one extra descriptor load per row
+    if (tas14_nohint_wpe() == 6)
+      return launch_groups(tcp4_tas14_kernel<6, false, true, 1, true>, *p, s, tas14_nohint_lds());
+    return launch_groups(tcp4_tas14_kernel<6, false, true, 8, true>, *p, s, tas14_nohint_lds());
+  }
   if (variant == 8 && p->l4_off != p->ip_off + 20u) // tcp4_wave_kernel needs TCP right after a 20-byte IPv4 header
     variant = 0;
   if (variant == 0) // TAS frames in 16-byte rooms: uniform hint, per-frame hints or none -> tcp4_tas14_kernel;

@@ -693,6 +693,38 @@ def test_tcp4_and_verify_short_frames_no_hint(oracle, stride):
                                   oracle.tcp4_verify_batch(good, n, stride=stride))
 
 
+@pytest.mark.parametrize("hinted", [False, True])
+def test_tcp4_offsets_aligned_rooms_mix(oracle, hinted):
+    """Frames by an offsets array over 16-byte aligned rooms in shuffled order
+    (tcp4_tas14_kernel<OFFS>): data segments, ACKs and total_length 0..90, a few
+    rooms shifted off alignment (general body), in place and to the output."""
+    n = 6000
+    rng = np.random.default_rng(11)
+    pay = np.where(rng.random(n) < 0.5, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=11)
+    tl = 52 + pay
+    tl[::13] = np.arange(len(tl[::13])) % 91
+    f = frames.reshape(n, 2048)
+    f[:, 16] = (tl >> 8) & 0xFF
+    f[:, 17] = tl & 0xFF
+    perm = rng.permutation(n)
+    big = np.zeros((n + 1) * 2048, np.uint8)
+    offs = perm.astype(np.int64) * 2048
+    offs[::17] += (np.arange(len(offs[::17])) % 15) + 1       # misaligned frames
+    for i in range(n):
+        big[offs[i]:offs[i] + 2048] = f[i]
+    exp = oracle.tcp4_batch(big.copy(), n, offsets=offs)
+    d = to_dev(big)
+    hint = to_dev(np.minimum(14 + tl, 2048).astype(np.int32)) if hinted else None
+    np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, offsets=to_dev(offs), frame_len=hint)), exp)
+    xsum.tcp4_cksum_batch(d, n, offsets=to_dev(offs), frame_len=hint, inplace=True, want_out=False)
+    got = d.cpu().numpy()
+    ipc = np.array([int(got[o + 24]) | (int(got[o + 25]) << 8) for o in offs], np.uint16)
+    tcpc = np.array([int(got[o + 50]) | (int(got[o + 51]) << 8) for o in offs], np.uint16)
+    np.testing.assert_array_equal(ipc, exp[0::2])
+    np.testing.assert_array_equal(tcpc, exp[1::2])
+
+
 def test_tcp4_flush_mix_no_hint(oracle):
     """Data segments among pure ACKs, no hint (each row reads its own total_length)."""
     n = 8192
