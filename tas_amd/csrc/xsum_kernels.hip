@@ -1097,8 +1097,15 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
     variant = 0;
   if ((variant == 0 || variant == 6) && tas14_ok(*p))
     return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
-  if ((variant == 0 || variant == 6) && tas14_nohint_ok(*p))
-    return launch_groups(tcp4_tas14_kernel<6, true, true>, *p, (hipStream_t) stream, kOccLds);
+  if ((variant == 0 || variant == 6) && tas14_nohint_ok(*p)) {
+    // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
+    // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
+    // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt)
+    static const uint32_t lds = env_lds("TASX_TAS14_VERIFY_LDS", 0u);
+    if (tas14_nohint_wpe() == 6)
+      return launch_groups(tcp4_tas14_kernel<6, true, true>, *p, (hipStream_t) stream, lds);
+    return launch_groups(tcp4_tas14_kernel<6, true, true, 8>, *p, (hipStream_t) stream, lds);
+  }
   return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--fracs", default="0,0.25,0.5,0.75")
     ap.add_argument("--variants", default="0,3,8")
     ap.add_argument("--hints", default="per,none,max")
+    ap.add_argument("--verify", action="store_true", help="RX verification of checksummed frames instead of TX")
     ap.add_argument("--offsets", action="store_true", help="frames by an offsets array (i * 2048) instead of stride mode")
     a = ap.parse_args()
     n, stride = a.n, pktgen.MBUF_ROOM
@@ -40,6 +41,9 @@ def main():
         pay = np.where(rng.random(n) < frac, 0, pktgen.TCP_MSS).astype(np.int64)
         host = pktgen.tcp4_frames(n, payload=pay, stride=stride)
         exp = orc.tcp4_batch(host.copy(), n, stride=stride)
+        if a.verify:  # received frames: checksummed in place, flags expected from the oracle
+            orc.tcp4_batch(host, n, stride=stride, inplace=True)
+            exp = orc.tcp4_verify_batch(host.copy(), n, stride=stride)
         tl = pay + 52
         flen = torch.from_numpy((tl + pktgen.ETH_LEN).astype(np.int32)).cuda()
         alg = int((tl + 4).sum())
@@ -53,14 +57,23 @@ def main():
                 fl0 = pktgen.ETH_LEN + 1500 if hint == "max" else 0  # uniform MTU hint (rooms are 2048 B)
                 offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride if a.offsets else None
                 out.zero_()
-                xsum.tcp4_cksum_batch(bufs[0], n, stride=0 if a.offsets else stride, offsets=offs, out=out, frame_len=fl if fl is not None else (fl0 or None))
-                torch.cuda.synchronize()
-                ok = np.array_equal(out.cpu().numpy().view(np.uint16), exp)
+                if a.verify:
+                    got = xsum.tcp4_verify_batch(bufs[0], n, stride=0 if a.offsets else stride, offsets=offs,
+                                                 frame_len=fl if fl is not None else (fl0 or None))
+                    torch.cuda.synchronize()
+                    ok = np.array_equal(got.cpu().numpy(), exp)
+                    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+                else:
+                    xsum.tcp4_cksum_batch(bufs[0], n, stride=0 if a.offsets else stride, offsets=offs, out=out,
+                                          frame_len=fl if fl is not None else (fl0 or None))
+                    torch.cuda.synchronize()
+                    ok = np.array_equal(out.cpu().numpy().view(np.uint16), exp)
                 # direct C-ABI calls with prebuilt arguments (no wrapper overhead in the loop)
-                fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
+                fn = xsum.lib().tasx_tcp4_verify_batch_dev_hint if a.verify else xsum.lib().tasx_tcp4_cksum_batch_dev_hint
                 s = torch.cuda.current_stream().cuda_stream
                 args = [(b.data_ptr(), offs.data_ptr() if a.offsets else None, 0 if a.offsets else stride, fl.data_ptr() if fl is not None else None, fl0, n,
-                         pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN, out.data_ptr(), 0, s) for b in bufs]
+                         pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN, out.data_ptr(), *(() if a.verify else (0,)), s)
+                        for b in bufs]
                 for k in range(20):
                     assert fn(*args[k % a.rotate]) == 0
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -71,7 +84,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.steps
-                print(json.dumps({"ack_frac": frac, "variant": v, "hint": hint, "offsets": a.offsets, "bit_exact": ok,
+                print(json.dumps({"ack_frac": frac, "variant": v, "hint": hint, "offsets": a.offsets, "verify": a.verify, "bit_exact": ok,
                                   "us": round(us, 3), "alg_bytes": alg,
                                   "GBps": round(alg / us / 1e3, 1), "frac_8TBps": round(alg / us / 8e6, 4)}),
                       flush=True)
