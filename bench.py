@@ -4,29 +4,35 @@
 Headline step = one launch of the TCP4 checksum kernel (tcp_checksums()
 flag-off branch: rte_ipv4_cksum + rte_ipv4_udptcp_cksum per frame) over one
 batch of 65,536 TAS TX data segments (1514 B frames, ip.len 1500, one per
-2048 B mbuf data room: BASELINE.json configs[1] / BASELINE.md), with the frame
-length (the mbuf data_len tx_send() sets before tx_flush) as the prefetch hint.
-Inputs are resident in HBM before the timed region; steps rotate over R
-distinct batches (R x 134 MB >> the 256 MiB Infinity Cache) so every step
-reads HBM, not the MALL.
+2048 B mbuf data room: BASELINE.json configs[1] / BASELINE.md), through
+tasx_tcp4_cksum_batch_dev_hint with the frame length (the mbuf data_len
+tx_send() sets before tx_flush) as the uniform hint.  Inputs are resident in
+HBM before the timed region; steps rotate over R distinct batches (R x 134 MB
+>> the 256 MiB Infinity Cache) so every step reads HBM, not the MALL.  The K
+timed steps are K calls of that C entry point made from C
+(tas_amd/benchsrc/bench_loop.c), so no Python runs between launches.
 
 Algorithmic bytes per frame = ip.total_length (1500, the bytes summed) + 4
 (results written) -- SURVEY.md section 8d.  value = GiB/s = bytes / s / 2^30.
 
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
-One process per GPU, each with its own batches and stream (weak scaling, no
-data-path collective: the path shards); the timed region is
-barrier + synchronize on both sides and the MAX over ranks is taken.  Rank 0
-prints one JSON line.
+Multi-GPU (the path shards, no data-path collective):
+`python bench.py --gpus N` starts N ranks itself (one process per GPU, before
+anything touches a GPU) and refuses when fewer than N GPUs are visible unless
+--rehearse (ranks share the visible GPUs, gloo control plane).  Under
+torch.distributed.run the ranks come from the launcher (WORLD_SIZE must equal
+--gpus).  Each rank pins itself to its GPU's NUMA node, checksums its own
+batches on its own stream (weak scaling); the timed region is barrier +
+synchronize on both sides, the MAX over ranks is taken, and rank 0 prints one
+JSON line with the aggregate and per-rank rates.
 
-Extra legs (rank 0, N == 1): the same frames without the hint, the same
-batches over two streams (two fast-path contexts), RX verification, the RAW
-payload fold (rte_raw_cksum over 64K x 1500 B), the TX segment build, the flow
-lookup, the end-to-end host-memory rate through pinned memory, the CPU oracle
-baseline, and HBM traffic from rocprofv3 counters (two short child runs;
---no-pmc skips them).  --workload {shard8m,mixed,tso} measures the other
-BASELINE.json configs instead (one JSON line each, with the oracle timed on a
-bounded sample of the same packets at N == 1).
+Extra legs (all ranks unless noted): the same frames with no hint and a room
+(the mbuf data room: the TAS drop-in form) and with neither, the same batches
+over two streams, RX verification, a data/ACK flush mix, the RAW payload fold,
+the TX segment build, the flow lookup, the end-to-end host-memory rate (one
+NUMA-local host thread per GPU), and on rank 0 at N == 1 the CPU oracle
+baseline, tx_flush latencies and HBM traffic from rocprofv3 counters (child
+runs; --no-pmc skips them).  --workload {shard8m,mixed,tso} measures the other
+BASELINE.json configs instead.
 """
 from __future__ import annotations
 
@@ -35,6 +41,7 @@ import csv
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -48,17 +55,19 @@ import torch.distributed as dist
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from tas_amd import pktgen, shard, xsum  # noqa: E402
+from tas_amd import benchloop, pktgen, shard, xsum  # noqa: E402
+from tas_amd.benchloop import DEV, HINT, ROOM, VERIFY  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 METRIC = "TCP/IP checksum GiB/s (device-resident), 1500B MTU batch, 1/2/4/8 GPU"
 
 N_FRAMES = 65536
-STRIDE = pktgen.MBUF_ROOM              # 2048
+STRIDE = pktgen.MBUF_ROOM              # 2048, BUFFER_SIZE (tas/fast/internal.h:34)
 IP_TOTAL = 1500
 FRAME_LEN = pktgen.ETH_LEN + IP_TOTAL  # 1514, the mbuf data_len tx_send() sets
 RAW_LEN = 1500
+IP_OFF, L4_OFF = pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN
 
 
 def parse(argv=None):
@@ -68,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rotate", type=int, default=16, help="distinct device batches cycled through")
     ap.add_argument("--workload", default="tcp4", choices=["tcp4", "shard8m", "mixed", "tso"])
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N ranks may share the visible GPUs (gloo control plane): a rehearsal, not a scaling run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-raw", action="store_true")
@@ -78,31 +89,124 @@ def parse(argv=None):
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
     ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed"], help=argparse.SUPPRESS)
+    ap.add_argument("--control-selftest", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank plumbing
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
 
 
 # ---------------------------------------------------------------------------
-# distributed plumbing (one process per GPU; control only, never data)
+# ranks: one process per GPU (control plane only, never data)
 
-def dist_setup():
-    """One process per GPU.  The process group carries only the barrier and two
-    scalar reductions (RCCL as "nccl"; TASX_DIST_BACKEND=gloo runs the same
-    control plane on the CPU, e.g. to rehearse N ranks on a one-GPU box)."""
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (this
+    process never touches a GPU: torch.cuda.device_count() does not initialise
+    HIP on this image) and return their combined exit status.  Fewer visible
+    GPUs than N is an error unless --rehearse."""
+    n = args.gpus
+    ndev = 0 if args.control_selftest else torch.cuda.device_count()
+    if ndev < n and not (args.rehearse or args.control_selftest):
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {ndev} visible "
+              f"(--rehearse runs {n} ranks sharing the visible GPUs over gloo: not a scaling measurement)",
+              file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    # a rank that fails leaves the others waiting in a barrier: end them
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            time.sleep(5)
+            for i, p in enumerate(procs):
+                if p.poll() is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
+
+
+def pci_bus_id(dev: int) -> str:
+    """The GPU's PCI address as sysfs spells it (domain:bus:device.function)."""
+    pr = torch.cuda.get_device_properties(dev)
+    return f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+
+
+def _cpulist(text: str) -> set[int]:
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def numa_pin(bus_id: str) -> dict:
+    """Pin this rank to the CPUs of its GPU's NUMA node (intersected with the
+    CPUs it may use) before any host buffer is touched, so pinned staging and
+    the host thread feeding the GPU are NUMA-local."""
+    info = {"pci_bus_id": bus_id, "numa_node": None, "cpus": len(os.sched_getaffinity(0))}
+    try:
+        node = int(Path(f"/sys/bus/pci/devices/{bus_id}/numa_node").read_text())
+        info["numa_node"] = node
+        if node >= 0:
+            local = _cpulist(Path(f"/sys/devices/system/node/node{node}/cpulist").read_text())
+            use = local & os.sched_getaffinity(0)
+            if use:
+                os.sched_setaffinity(0, use)
+                info["cpus"] = len(use)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def dist_setup(args):
+    """Rank setup.  WORLD_SIZE (from the launcher or spawn_ranks) must equal
+    --gpus; each rank takes GPU LOCAL_RANK (distinct devices are checked), or
+    shares the visible GPUs under --rehearse (gloo)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
-        dev = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev)
-        backend = os.environ.get("TASX_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend)
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+    rehearse = args.rehearse or os.environ.get("TASX_DIST_BACKEND") == "gloo"
+    info = {}
+    if args.control_selftest:
+        dev = None
     else:
-        torch.cuda.set_device(0)
-    return ws, rank, local
+        ndev = torch.cuda.device_count()
+        if not rehearse and local >= ndev:
+            raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, {ndev} visible (--rehearse to share)")
+        dev = local % max(1, ndev)
+        torch.cuda.set_device(dev)
+        info = numa_pin(pci_bus_id(dev))
+    if ws > 1:
+        if rehearse or args.control_selftest:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        ids = [None] * ws
+        dist.all_gather_object(ids, info.get("pci_bus_id", f"cpu{rank}"))
+        if not rehearse and not args.control_selftest and len(set(ids)) != ws:
+            raise SystemExit(f"bench.py: ranks share GPUs {ids}; one GPU per rank is required (or --rehearse)")
+        info["all_bus_ids"] = ids
+    info["rehearse"] = bool(rehearse)
+    return ws, rank, local, info
 
 
 def _red_device():
@@ -130,8 +234,21 @@ def sum_over_ranks(x: float, ws: int) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(x: float, ws: int) -> list[float]:
+    if ws == 1:
+        return [x]
+    t = torch.tensor([x], dtype=torch.float64, device=_red_device())
+    out = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 # ---------------------------------------------------------------------------
-# workloads: device-resident batches + a zero-overhead launcher
+# workloads: device-resident batches + C launch loops
+
+def _stream_ptrs(streams):
+    return [s.cuda_stream for s in streams] if streams else [torch.cuda.current_stream().cuda_stream]
+
 
 def device_random(nbytes: int, seed: int) -> torch.Tensor:
     g = torch.Generator(device="cuda")
@@ -152,7 +269,8 @@ def device_tcp4_frames(n: int, stride: int, ip_total: int, seed: int) -> torch.T
 
 class Tcp4Workload:
     desc = (f"{N_FRAMES} TAS TX segments (1514 B frames, ip.len {IP_TOTAL}, {STRIDE} B mbuf stride), "
-            "tcp_checksums() flag-off per frame, frame length (mbuf data_len) as the prefetch hint")
+            "tcp_checksums() flag-off per frame, frame length (mbuf data_len) as the uniform hint "
+            "(tasx_tcp4_cksum_batch_dev_hint)")
 
     def __init__(self, rotate: int, seed: int, n: int = N_FRAMES, stride: int = STRIDE,
                  ip_total: int = IP_TOTAL, hint: int | None = None, host: bool = True):
@@ -168,30 +286,26 @@ class Tcp4Workload:
         self.outs = [torch.empty(2 * n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
         self.bytes_per_step = n * (ip_total + 4)
 
-    def launcher(self, streams=None):
-        """streams: launch batch k on streams[k % S] (independent batches of S
-        fast-path contexts, each with its own stream); default: the current stream."""
-        fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
-        ss = [s.cuda_stream for s in streams] if streams else [torch.cuda.current_stream().cuda_stream]
-        S = len(ss)
-        args = [(b.data_ptr(), None, self.stride, None, self.hint, self.n, pktgen.ETH_LEN,
-                 pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), 0) for b, o in zip(self.bufs, self.outs)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R], ss[k % S])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev_hint")
-        return launch
+    def loop(self, which: int = HINT, *, flen0: int | None = None, room: int = 0, streams=None,
+             outs=None, inplace: bool = False) -> benchloop.Loop:
+        """The timed call: `which` entry point (HINT: the uniform hint flen0,
+        default the frame length; ROOM: no hint, `room` bytes readable per frame;
+        DEV: frames only; VERIFY: RX flags into `outs`)."""
+        flen0 = self.hint if flen0 is None else flen0
+        outs = self.outs if outs is None else outs
+        args = [benchloop.Tcp4Args(b.data_ptr(), None, self.stride, None, flen0, room, self.n, IP_OFF, L4_OFF,
+                                   xsum.TASX_F_INPLACE if inplace else 0, o.data_ptr())
+                for b, o in zip(self.bufs, outs)]
+        return benchloop.Loop("tcp4", args, _stream_ptrs(streams), which, "tcp4 batch")
 
 
 class FlushMixWorkload:
     """A tx_flush-shaped TCP4 batch: flow_tx_segment data frames (1514 B) and
     flow_tx_ack frames (66 B, ip.len 52; fast_flows.c:877-1030) half and half in
     random order, 2048 B mbuf rooms, each frame's length (mbuf data_len) as its
-    hint; automatic kernel selection."""
+    hint and the mbuf data room as the room (tasx_tcp4_cksum_batch_dev_room)."""
     desc = (f"{N_FRAMES} TAS TX frames in {STRIDE} B rooms, 50% data segments (ip.len {IP_TOTAL}) and 50% "
-            "pure ACKs (ip.len 52) in random order, per-frame hints (mbuf data_len)")
+            "pure ACKs (ip.len 52) in random order, per-frame hints (mbuf data_len), room = the mbuf data room")
 
     def __init__(self, rotate: int, seed: int, n: int = N_FRAMES, stride: int = STRIDE):
         rng = np.random.default_rng(seed)
@@ -204,42 +318,26 @@ class FlushMixWorkload:
         self.outs = [torch.empty(2 * n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
         self.bytes_per_step = int((52 + pay + 4).sum())
 
-    def launcher(self):
-        fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
-        s = torch.cuda.current_stream().cuda_stream
-        args = [(b.data_ptr(), None, self.stride, self.flen.data_ptr(), 0, self.n, pktgen.ETH_LEN,
-                 pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), 0, s) for b, o in zip(self.bufs, self.outs)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_tcp4_cksum_batch_dev_hint")
-        return launch
+    def loop(self, room: int = STRIDE, streams=None) -> benchloop.Loop:
+        args = [benchloop.Tcp4Args(b.data_ptr(), None, self.stride, self.flen.data_ptr(), 0, room, self.n, IP_OFF,
+                                   L4_OFF, 0, o.data_ptr()) for b, o in zip(self.bufs, self.outs)]
+        return benchloop.Loop("tcp4", args, _stream_ptrs(streams), ROOM, "tasx_tcp4_cksum_batch_dev_room")
 
 
 class RxVerifyWorkload:
-    """Receive-side verification over a Tcp4Workload's (checksummed) frames."""
+    """Receive-side verification over a Tcp4Workload's (checksummed) frames,
+    the received frame length as the uniform hint (the read bound)."""
 
     def __init__(self, wl: Tcp4Workload):
         self.wl = wl
         wl.rx_flags = [torch.empty(wl.n, dtype=torch.uint8, device="cuda") for _ in wl.bufs]
         self.bytes_per_step = wl.n * (wl.ip_total + 1)
 
-    def launcher(self):
-        # the received frames' length (mbuf data_len) as the prefetch hint
-        fn = xsum.lib().tasx_tcp4_verify_batch_dev_hint
-        stream = torch.cuda.current_stream().cuda_stream
+    def loop(self, streams=None) -> benchloop.Loop:
         wl = self.wl
-        args = [(b.data_ptr(), None, wl.stride, None, wl.hint, wl.n, pktgen.ETH_LEN,
-                 pktgen.ETH_LEN + pktgen.IP_LEN, f.data_ptr(), stream) for b, f in zip(wl.bufs, wl.rx_flags)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_tcp4_verify_batch_dev_hint")
-        return launch
+        args = [benchloop.Tcp4Args(b.data_ptr(), None, wl.stride, None, wl.hint, 0, wl.n, IP_OFF, L4_OFF, 0,
+                                   f.data_ptr()) for b, f in zip(wl.bufs, wl.rx_flags)]
+        return benchloop.Loop("tcp4", args, _stream_ptrs(streams), VERIFY, "tasx_tcp4_verify_batch_dev_room")
 
 
 class RawWorkload:
@@ -261,20 +359,12 @@ class RawWorkload:
         self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
         self.outs = [torch.empty(n, dtype=torch.int16, device="cuda") for _ in range(rotate)]
 
-    def launcher(self):
-        fn = xsum.lib().tasx_raw_cksum_batch_dev
-        stream = torch.cuda.current_stream().cuda_stream
+    def loop(self, streams=None) -> benchloop.Loop:
         op = self.off.data_ptr() if self.off is not None else None
         lp = self.lens.data_ptr() if self.lens is not None else None
-        args = [(b.data_ptr(), op, self.len0 if op is None else 0, lp, self.len0, self.n, o.data_ptr(), stream)
-                for b, o in zip(self.bufs, self.outs)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_raw_cksum_batch_dev")
-        return launch
+        args = [benchloop.RawArgs(b.data_ptr(), op, self.len0 if op is None else 0, lp, self.len0, self.n,
+                                  o.data_ptr()) for b, o in zip(self.bufs, self.outs)]
+        return benchloop.Loop("raw", args, _stream_ptrs(streams), what="tasx_raw_cksum_batch_dev")
 
 
 class TxSegWorkload:
@@ -304,19 +394,10 @@ class TxSegWorkload:
         self.bytes_per_seg = 2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4
         self.bytes_per_step = n * self.bytes_per_seg
 
-    def launcher(self):
-        fn = xsum.lib().tasx_tx_segment_batch_dev
-        stream = torch.cuda.current_stream().cuda_stream
-        args = [(sh.data_ptr(), self.shm_len, b.data_ptr(), self.segs.data_ptr(), self.n, pktgen.ETH_LEN,
-                 pktgen.ETH_LEN + pktgen.IP_LEN, o.data_ptr(), stream)
-                for sh, b, o in zip(self.shms, self.bufs, self.outs)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_tx_segment_batch_dev")
-        return launch
+    def loop(self, streams=None) -> benchloop.Loop:
+        args = [benchloop.TxSegArgs(sh.data_ptr(), self.shm_len, b.data_ptr(), self.segs.data_ptr(), self.n, IP_OFF,
+                                    L4_OFF, o.data_ptr()) for sh, b, o in zip(self.shms, self.bufs, self.outs)]
+        return benchloop.Loop("txseg", args, _stream_ptrs(streams), what="tasx_tx_segment_batch_dev")
 
     def cpu_check(self, budget_s: float) -> dict:
         """The oracle's copy + tcp_checksums per segment on this box's cores, on
@@ -377,20 +458,12 @@ class FlowLookupWorkload:
         self.bytes_per_step = self.N * (12 + 32 + 12 + 8)
         self.inserted = float(ok.mean())
 
-    def launcher(self):
-        fn = xsum.lib().tasx_flow_lookup_batch_dev
-        stream = torch.cuda.current_stream().cuda_stream
-        args = [(b.data_ptr(), None, STRIDE, self.N, pktgen.ETH_LEN, pktgen.ETH_LEN + pktgen.IP_LEN,
-                 self.ht.data_ptr(), self.ENTRIES, self.fs.data_ptr(), self.NFLOWS, pktgen.FLOWST_SIZE,
-                 pktgen.FLOWST_KEY_OFF, h.data_ptr(), f.data_ptr(), stream)
+    def loop(self, streams=None) -> benchloop.Loop:
+        args = [benchloop.FlowArgs(b.data_ptr(), None, STRIDE, self.N, IP_OFF, L4_OFF, self.ht.data_ptr(),
+                                   self.ENTRIES, self.fs.data_ptr(), self.NFLOWS, pktgen.FLOWST_SIZE,
+                                   pktgen.FLOWST_KEY_OFF, h.data_ptr(), f.data_ptr())
                 for b, h, f in zip(self.bufs, self.hashes, self.fids)]
-        R = len(args)
-
-        def launch(k):
-            rc = fn(*args[k % R])
-            if rc:
-                raise xsum.TasxError(rc, "tasx_flow_lookup_batch_dev")
-        return launch
+        return benchloop.Loop("flow", args, _stream_ptrs(streams), what="tasx_flow_lookup_batch_dev")
 
     def cpu_check(self, budget_s: float) -> dict:
         from oracle import oracle_lib
@@ -410,52 +483,47 @@ class FlowLookupWorkload:
                 "parity_vs_gpu": "bit-exact" if np.array_equal(exp, gpu_fid) else "MISMATCH"}
 
 
-def prewarm(launch, seconds: float = 0.25):
+# flow lookup latency roofline: three dependent memory
+# accesses per frame -- the frame header (HBM miss), the 4-entry bucket (2 MB
+# flowht: L2) and the candidate flow keys (16 MB flowst: Infinity Cache) -- at
+# the guide's idle-chip latencies (MI355X_MICROARCH.md cycle constants: HBM
+# miss ~900 cyc, MALL hit ~545 cyc, L2 hit ~200 cyc at 2.4 GHz), for as many
+# generations of resident frames (64 per wave, 8 waves per SIMD) as the batch needs
+FLOW_CHAIN_NS = {"hbm": 900 / 2.4, "l2": 200 / 2.4, "mall": 545 / 2.4}
+
+
+def flow_latency_roofline(n_frames: int, avg_us: float, waves_per_simd: int = 8) -> dict:
+    frames_in_flight = 256 * 4 * waves_per_simd * 64
+    gens = -(-n_frames // frames_in_flight)
+    chain_ns = FLOW_CHAIN_NS["hbm"] + FLOW_CHAIN_NS["l2"] + FLOW_CHAIN_NS["mall"]
+    bound_us = gens * chain_ns / 1e3
+    return {"bound": "latency", "achieved": round(n_frames / avg_us, 1), "unit": "lookups/us",
+            "peak": round(n_frames / bound_us, 1), "frac": round(bound_us / avg_us, 4),
+            "chain": "frame header (HBM) -> flowht bucket (L2) -> flow-state key (MALL)",
+            "chain_ns": round(chain_ns, 1), "generations": gens, "frames_in_flight": frames_in_flight,
+            "launch_avg_us": round(avg_us, 3)}
+
+
+def prewarm(run, seconds: float = 0.25):
     """Bring the GPU out of idle clocks before any measured step (not part of
     W or K)."""
     t0 = time.perf_counter()
     k = 0
     while time.perf_counter() - t0 < seconds:
-        for _ in range(32):
-            launch(k)
-            k += 1
+        run(k, 32)
+        k += 32
         torch.cuda.synchronize()
 
 
-def timed_run(wl, steps: int, warmup: int, ws: int):
-    """W untimed steps, then exactly K timed steps between barrier+sync pairs.
-    A HIP event pair on the launch stream around the K back-to-back launches
-    gives the average launch duration (no per-launch events, which would add
-    gaps of their own)."""
-    launch = wl.launcher()
-    prewarm(launch)
-    for k in range(warmup):
-        launch(k)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(ws)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record()
-    for k in range(steps):
-        launch(warmup + k)
-    e1.record()
-    torch.cuda.synchronize()
-    barrier(ws)
-    t1 = time.perf_counter()
-    return t1 - t0, e0.elapsed_time(e1) / steps
-
-
-def timed_run_contexts(wl, steps: int, warmup: int, ws: int, n_ctx: int):
-    """As timed_run, with batch k launched on stream k % n_ctx: n_ctx fast-path
-    contexts submitting independent batches, so one batch's ramp-up overlaps
-    another's drain.  The event pair brackets all streams (they wait on the
-    start event; the current stream waits on each one's end)."""
-    streams = [torch.cuda.Stream() for _ in range(n_ctx)]
-    launch = wl.launcher(streams)
-    prewarm(launch)
-    for k in range(warmup):
-        launch(k)
+def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
+    """W untimed steps, then exactly K timed steps between barrier+sync pairs,
+    issued by one C loop.  A HIP event pair on the launch stream around the K
+    launches gives the average launch duration (no per-launch events, which
+    would add gaps of their own).  With several streams the event pair brackets
+    all of them (they wait on the start event; the current stream waits on each
+    one's end)."""
+    prewarm(run)
+    run(0, warmup)
     torch.cuda.synchronize()
     cur = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -463,11 +531,10 @@ def timed_run_contexts(wl, steps: int, warmup: int, ws: int, n_ctx: int):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(cur)
-    for s in streams:
+    for s in streams or []:
         s.wait_event(e0)
-    for k in range(steps):
-        launch(warmup + k)
-    for s in streams:
+    run(warmup, steps)
+    for s in streams or []:
         cur.wait_stream(s)
     e1.record(cur)
     torch.cuda.synchronize()
@@ -484,27 +551,34 @@ def roofline(bytes_per_launch: int, avg_ms: float, traffic):
             "launch_avg_us": round(avg_s * 1e6, 3), "algorithmic_bytes_per_launch": bytes_per_launch}
 
 
-def leg(wl, args, ws, desc):
-    dt, avg_ms = timed_run(wl, args.steps, args.warmup, ws)
-    dt = max_over_ranks(dt, ws)
-    total = sum_over_ranks(float(wl.bytes_per_step * args.steps), ws)
-    return {"value": total / dt / GIB, "unit": "GiB/s", "ms_per_step": dt / args.steps * 1e3,
-            "workload": desc, "roofline": roofline(wl.bytes_per_step, avg_ms, None)}
+def leg(run, bytes_per_step: int, args, ws, desc, kernel: str = "", streams=None):
+    dt, avg_ms = timed_run(run, args.steps, args.warmup, ws, streams)
+    per_rank = gather_over_ranks(bytes_per_step * args.steps / dt / GIB, ws)
+    dtm = max_over_ranks(dt, ws)
+    total = sum_over_ranks(float(bytes_per_step * args.steps), ws)
+    r = {"value": total / dtm / GIB, "unit": "GiB/s", "ms_per_step": dtm / args.steps * 1e3,
+         "workload": desc, "roofline": roofline(bytes_per_step, avg_ms, None)}
+    if kernel:
+        r["kernel"] = kernel
+    if ws > 1:
+        r["per_rank_value"] = [round(v, 2) for v in per_rank]
+    return r
 
 
 # ---------------------------------------------------------------------------
-# rank-0 extra legs
+# end to end (PCIe-inclusive; never the headline)
 
-def e2e_leg(reps: int = 5) -> dict:
-    """PCIe-inclusive rates (never the headline):
+def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
+    """Every rank at once, each from its own NUMA-local host thread (this
+    process, pinned by numa_pin before these buffers were touched):
     * staged: host frames -> chunked pinned H2D of whole mbuf rooms -> kernel ->
       D2H of the results (tasx_tcp4_cksum_batch_host);
     * zero-copy: the kernel reads the frames from pinned host memory over PCIe
       (only the bytes it sums) and writes the results to device memory;
-    * tx_flush at TAS's batch size (32 frames): deferred tcp_checksums() calls +
-      tasx_flush, staged and zero-copy (frames in a registered region)."""
+    * (rank 0) tx_flush at TAS's batch size (32 frames): deferred tcp_checksums()
+      calls + tasx_flush, staged and zero-copy (frames in a registered region)."""
     n = N_FRAMES
-    frames = pktgen.tcp4_frames(n, payload=IP_TOTAL - 52, stride=STRIDE, seed=41)
+    frames = pktgen.tcp4_frames(n, payload=IP_TOTAL - 52, stride=STRIDE, seed=41 + rank)
     pin = xsum.PinnedBuffer(frames.size)
     pin.array[:] = frames
     out = np.empty(2 * n, np.uint16)
@@ -514,52 +588,59 @@ def e2e_leg(reps: int = 5) -> dict:
     xsum.ctx_init(0, torch.cuda.current_device(), 32 << 20)
     try:
         xsum.tcp4_cksum_batch_host(0, pin.addr, STRIDE, n, out.ctypes.data)  # warm
-        ts = []
+        barrier(ws)
+        t0 = time.perf_counter()
         for _ in range(reps):
-            t0 = time.perf_counter()
             xsum.tcp4_cksum_batch_host(0, pin.addr, STRIDE, n, out.ctypes.data)
-            ts.append(time.perf_counter() - t0)
-        t = float(np.median(ts))
-        res["staged"] = {"value": alg / t / GIB, "unit": "GiB/s", "ms_per_batch": t * 1e3,
-                         "pcie_h2d_bytes": n * STRIDE, "pcie_d2h_bytes": n * 4}
-        zc = []
-        for r in range(reps + 1):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
+        t = time.perf_counter() - t0
+        tm = max_over_ranks(t, ws)
+        res["staged"] = {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s",
+                         "ms_per_batch": tm / reps * 1e3, "pcie_h2d_bytes_per_rank": n * STRIDE,
+                         "pcie_d2h_bytes_per_rank": n * 4}
+        xsum.tcp4_cksum_batch(pin.dev_addr, n, stride=STRIDE, out=dout, frame_len=FRAME_LEN)
+        torch.cuda.synchronize()
+        barrier(ws)
+        t0 = time.perf_counter()
+        for _ in range(reps):
             xsum.tcp4_cksum_batch(pin.dev_addr, n, stride=STRIDE, out=dout, frame_len=FRAME_LEN)
-            torch.cuda.synchronize()
-            if r:
-                zc.append(time.perf_counter() - t0)
-        t = float(np.median(zc))
-        res["zero_copy"] = {"value": alg / t / GIB, "unit": "GiB/s", "ms_per_batch": t * 1e3,
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        tm = max_over_ranks(t, ws)
+        res["zero_copy"] = {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s",
+                            "ms_per_batch": tm / reps * 1e3,
                             "note": "frames stay in pinned host memory; results land in HBM"}
-        # tx_flush at TXBUF_SIZE = 32 frames (tas/include/fastpath.h:38)
-        f32 = xsum.PinnedBuffer(32 * STRIDE)
-        f32.array[:] = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
-        plain = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
+        if rank == 0:
+            # tx_flush at TXBUF_SIZE = 32 frames (tas/include/fastpath.h:38)
+            f32 = xsum.PinnedBuffer(32 * STRIDE)
+            f32.array[:] = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
+            plain = pktgen.tcp4_frames(32, payload=IP_TOTAL - 52, stride=STRIDE, seed=42)
 
-        def flush_lat(base):
-            lat = []
-            for _ in range(60):
-                t0 = time.perf_counter()
-                for i in range(32):
-                    xsum.defer_tcp4(0, base + i * STRIDE)
-                xsum.tx_flush(0)
-                lat.append(time.perf_counter() - t0)
-            return float(np.median(lat[10:])) * 1e6
-        res["flush32_staged_us"] = flush_lat(plain.ctypes.data)
-        xsum.register_frames(0, f32.addr, f32.nbytes)
-        res["flush32_zero_copy_us"] = flush_lat(f32.addr)
-        res["flush32_note"] = ("32 x tasx_defer_tcp4 + tasx_flush via ctypes (Python call overhead "
-                               "included); the CPU oracle needs ~7.5 us for the same 32 frames on one core")
-        f32.free()
+            def flush_lat(base):
+                lat = []
+                for _ in range(60):
+                    t0 = time.perf_counter()
+                    for i in range(32):
+                        xsum.defer_tcp4(0, base + i * STRIDE)
+                    xsum.tx_flush(0)
+                    lat.append(time.perf_counter() - t0)
+                return float(np.median(lat[10:])) * 1e6
+            res["flush32_staged_us"] = flush_lat(plain.ctypes.data)
+            xsum.register_frames(0, f32.addr, f32.nbytes)
+            res["flush32_zero_copy_us"] = flush_lat(f32.addr)
+            res["flush32_note"] = ("32 x tasx_defer_tcp4 + tasx_flush via ctypes (Python call overhead "
+                                   "included); tools/flush_bench.c has the C-side numbers")
+            f32.free()
     finally:
         xsum.ctx_destroy(0)
         pin.free()
     res["value"] = res["staged"]["value"]
     res["unit"] = "GiB/s"
+    res["host_threads"] = f"one per GPU ({ws}), each pinned to its GPU's NUMA node"
     return res
 
+
+# ---------------------------------------------------------------------------
+# CPU baseline (rank 0, N == 1)
 
 def host_oracle():
     """The C oracle built with the reference's own flags (-O3 -march=native) for
@@ -575,16 +656,29 @@ def host_oracle():
     return oracle_lib.Oracle(lib_path), kind_note, tmp
 
 
+def cpu_model() -> str:
+    try:
+        return [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
+    except Exception:
+        return "unknown"
+
+
+# The box's CPU share for one GPU: worker pools stay within it (the machine's
+# other cores serve the other GPUs' jobs)
+CPU_SHARE = 16
+
+
 def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> dict:
     """The oracle (C restatement of the reference path, per-frame calls) timed on
-    this box's host cores, on a bounded sample of the same workload."""
+    this box's host cores, on a bounded sample of the same workload: 1 thread
+    and the GPU's CPU share (threads pinned to the cores this rank may use)."""
     orc, kind_note, tmp = host_oracle()
     frames = wl.host.copy()
     n = wl.n
     exp = orc.tcp4_batch(frames.copy(), n, stride=STRIDE)
     parity = bool(np.array_equal(exp, gpu_out))
-    ncpu = len(os.sched_getaffinity(0))
-    threads = min(16, ncpu)  # the box's CPU share for one GPU
+    allowed = len(os.sched_getaffinity(0))
+    threads = min(CPU_SHARE, allowed)
     t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=1)
     reps1 = max(3, min(200, int(budget_s * 0.4 / max(t1, 1e-6))))
     t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=reps1)
@@ -592,18 +686,16 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
     repsn = max(3, min(2000, int(budget_s * 0.4 / max(tn, 1e-6))))
     tn = orc.bench(1, frames, n, stride=STRIDE, threads=threads, reps=repsn)
     alg = n * (IP_TOTAL + 4)
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
-    except Exception:
-        model = "unknown"
     shutil.rmtree(tmp, ignore_errors=True)
     return {
         "value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
         "sample": f"the 64K-frame TCP4 batch (98.6 MB algorithmic), per-frame oracle_tcp_checksums "
                   f"(DPDK 19.11 restatement), median of {repsn} passes on {threads} pinned threads; "
-                  f"1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}; CPU {model}, "
-                  f"{ncpu} cpus visible",
+                  f"1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}; CPU {cpu_model()}",
         "single_core_value": alg / t1 / GIB,
+        "host_cpus": os.cpu_count(), "cpus_this_rank": allowed,
+        "cores_note": (f"{threads} threads = the box's CPU share for one GPU; the host's other "
+                       f"{(os.cpu_count() or 0) - threads} CPUs serve the other GPUs' jobs and are not used"),
         "parity_vs_gpu": "bit-exact" if parity else "MISMATCH",
     }
 
@@ -647,23 +739,21 @@ def pmc_child(mode: str, steps: int):
     torch.cuda.set_device(0)
     xsum.lib()
     if mode == "tcp4":
-        wl = Tcp4Workload(16, pktgen.SEED)
+        run = Tcp4Workload(16, pktgen.SEED).loop(HINT)
     elif mode == "raw":
-        wl = RawWorkload(16, pktgen.SEED)
+        run = RawWorkload(16, pktgen.SEED).loop()
     elif mode == "txseg":
-        wl = TxSegWorkload(16, pktgen.SEED + 2000)
+        run = TxSegWorkload(16, pktgen.SEED + 2000).loop()
     else:
-        wl = mixed_workload(0)
-    launch = wl.launcher()
-    for k in range(steps):
-        launch(k)
+        run = mixed_workload(0).loop()
+    run(0, steps)
     torch.cuda.synchronize()
 
 
 # ---------------------------------------------------------------------------
 # other BASELINE.json configs (--workload)
 
-def mixed_workload(rank: int) -> "RawWorkload":
+def mixed_workload(rank: int) -> RawWorkload:
     """Config 3: 1,048,576 RAW packets, sizes uniform over {64,576,1500,9000} B in
     random order, packed at 16-byte aligned offsets."""
     n = 1 << 20
@@ -675,23 +765,36 @@ def mixed_workload(rank: int) -> "RawWorkload":
                        total_bytes=int(offs[-1] + slot[-1]))
 
 
-def other_workload(args, ws, rank):
+def shard8m_workload(ws: int, rank: int) -> RawWorkload:
+    """Config 4: 8,388,608 x 1500 B split over the ranks (1,048,576 per GPU at 8)."""
+    a, b = shard.shard_ranges(8 * (1 << 20), ws)[rank]
+    return RawWorkload(1, pktgen.SEED + rank, n=b - a, length=RAW_LEN)
+
+
+def tso_workload(rank: int) -> Tcp4Workload:
+    """Config 5: 16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B) in
+    65,552 B rooms, the frame length as the uniform hint."""
+    return Tcp4Workload(2, pktgen.SEED + rank, n=16384, stride=65552, ip_total=65535, host=False)
+
+
+def other_workload(args, ws, rank, info):
     name = args.workload
     if name == "shard8m":
-        total = 8 * (1 << 20)
-        a, b = shard.shard_ranges(total, ws)[rank]
-        wl = RawWorkload(1, pktgen.SEED + rank, n=b - a, length=RAW_LEN)
-        desc = f"8,388,608 x 1500 B payloads sharded over {ws} GPU(s): {b - a} packets on this rank"
+        wl = shard8m_workload(ws, rank)
+        run, kernel = wl.loop(), "raw_sad_kernel<s32>"
+        desc = f"8,388,608 x 1500 B payloads sharded over {ws} GPU(s): {wl.n} packets on this rank"
         scaling = "strong"
     elif name == "mixed":
         wl = mixed_workload(rank)
+        run, kernel = wl.loop(), "raw_wave_kernel"
         desc = "1,048,576 RAW packets per GPU, sizes uniform over {64,576,1500,9000} B in random order"
         scaling = "weak"
     else:  # tso
-        wl = Tcp4Workload(2, pktgen.SEED + rank, n=16384, stride=65552, ip_total=65535, host=False)
+        wl = tso_workload(rank)
+        run, kernel = wl.loop(HINT), "tcp4_tas_kernel"
         desc = "16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B), tcp_checksums() flag-off, hinted"
         scaling = "weak"
-    r = leg(wl, args, ws, desc)
+    r = leg(run, wl.bytes_per_step, args, ws, desc, kernel)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize()
@@ -707,16 +810,19 @@ def other_workload(args, ws, rank):
                           "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
                           "data": "synthetic (device-generated random bytes)",
                           "config": {"workload": desc, "parallelism": f"shard{ws}"},
-                          "roofline": r["roofline"], "cpu_baseline": cpu,
+                          "roofline": r["roofline"], "kernel": kernel,
+                          "frac_of_n_hbm": round(r["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
+                          **({"per_rank_value": r["per_rank_value"]} if "per_rank_value" in r else {}),
+                          "ranks": info.get("all_bus_ids"), "cpu_baseline": cpu,
                           **({"pmc": pmc} if pmc else {})}), flush=True)
 
 
 def other_cpu_baseline(name: str, wl, budget_s: float) -> dict:
     """The oracle on a bounded sample of the other configs (BASELINE.md's CPU
-    plan: the same generator, per-packet calls, 1 and 16 host threads), checked
-    against the GPU's results for the same packets."""
+    plan: the same generator, per-packet calls, 1 thread and the CPU share),
+    checked against the GPU's results for the same packets."""
     orc, kind_note, tmp = host_oracle()
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = min(CPU_SHARE, len(os.sched_getaffinity(0)))
     if name == "tso":
         m, stride = 4096, wl.stride  # 268 MB: beyond the 16 threads' share of L3
         host = wl.bufs[0][:m * stride].cpu().numpy().copy()
@@ -755,25 +861,53 @@ def other_cpu_baseline(name: str, wl, budget_s: float) -> dict:
             "parity_vs_gpu": "bit-exact" if parity else "MISMATCH"}
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+
+def control_selftest(ws: int, rank: int, info: dict) -> None:
+    """--control-selftest: the rank plumbing without a GPU (gloo): barrier,
+    MAX / SUM / gather over ranks; rank 0 prints what a run would aggregate."""
+    barrier(ws)
+    per = gather_over_ranks(float(rank + 1), ws)
+    tot = sum_over_ranks(float(rank + 1), ws)
+    mx = max_over_ranks(float(rank + 1), ws)
+    barrier(ws)
+    if rank == 0:
+        print(json.dumps({"n_gpus": ws, "per_rank_value": per, "sum": tot, "max": mx,
+                          "ranks": info.get("all_bus_ids")}), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
     if args.pmc_child:
         pmc_child(args.pmc_child, args.steps)
-        return
-    ws, rank, local = dist_setup()
-    xsum.lib()
-    if args.workload != "tcp4":
-        other_workload(args, ws, rank)
+        return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, argv)
+    ws, rank, local, info = dist_setup(args)
+    try:
+        if args.control_selftest:
+            control_selftest(ws, rank, info)
+            return 0
+        xsum.lib()
+        if args.workload != "tcp4":
+            other_workload(args, ws, rank, info)
+        else:
+            run_tcp4(args, ws, rank, info)
+        return 0
+    finally:
         if ws > 1:
             dist.destroy_process_group()
-        return
-    rot = max(1, args.rotate)
 
+
+def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
+    rot = max(1, args.rotate)
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
-    head = leg(wl, args, ws, Tcp4Workload.desc)
+    head = leg(wl.loop(HINT), wl.bytes_per_step, args, ws, Tcp4Workload.desc, "tcp4_tas14_kernel<hint>")
     ctx2 = None
     if not args.no_contexts:
-        dt2, avg2 = timed_run_contexts(wl, args.steps, args.warmup, ws, 2)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        dt2, avg2 = timed_run(wl.loop(HINT, streams=streams), args.steps, args.warmup, ws, streams)
         dt2 = max_over_ranks(dt2, ws)
         total = sum_over_ranks(float(wl.bytes_per_step * args.steps), ws)
         ctx2 = {"value": total / dt2 / GIB, "unit": "GiB/s", "ms_per_step": dt2 / args.steps * 1e3,
@@ -783,15 +917,22 @@ def main():
                 "alg_GBps_per_interval": round(wl.bytes_per_step / (avg2 * 1e-3) / 1e9, 1),
                 "note": "kernels overlap, so a kernel's own duration is longer than the interval; "
                         "the headline roofline uses the single-stream launch"}
-    wl.hint = 0
-    nohint = leg(wl, args, ws, "same frames, tasx_tcp4_cksum_batch_dev (frames only, no hint)")
-    wl.hint = FRAME_LEN
+    # the drop-in forms: no hint with the mbuf data room (what TAS would pass),
+    # and frames only
+    nohint = leg(wl.loop(ROOM, flen0=0, room=STRIDE), wl.bytes_per_step, args, ws,
+                 "same frames, tasx_tcp4_cksum_batch_dev_room (no hint, room = the 2048 B mbuf data room)",
+                 "tcp4_tas14_kernel<room>")
+    frames_only = leg(wl.loop(DEV, flen0=0), wl.bytes_per_step, args, ws,
+                      "same frames, tasx_tcp4_cksum_batch_dev (frames only: no hint, no room)",
+                      "tcp4_tas14_kernel<tl_first>")
     # receive-side verification of the same frames (after in-place TX checksums)
     xsum.tcp4_cksum_batch(wl.bufs[0], wl.n, stride=wl.stride, inplace=True, want_out=False)
     for b in wl.bufs[1:]:
         b.copy_(wl.bufs[0])
-    rx = leg(RxVerifyWorkload(wl), args, ws, "same frames after TX checksums, tasx_tcp4_verify_batch_dev_hint "
-             "(received frame length as the hint)")
+    rv = RxVerifyWorkload(wl)
+    rx = leg(rv.loop(), rv.bytes_per_step, args, ws,
+             "same frames after TX checksums, tasx_tcp4_verify_batch_dev_room (received frame length as the "
+             "uniform hint)", "tcp4_tas14_kernel<hint,verify>")
     torch.cuda.synchronize()
     rx["all_frames_verified"] = bool((wl.rx_flags[0] == 3).all().item())
     src = torch.from_numpy(wl.host).cuda()
@@ -801,14 +942,14 @@ def main():
     mix = None
     if not args.no_flushmix:
         mw = FlushMixWorkload(min(rot, 12), pktgen.SEED + 500 + rank)
-        mix = leg(mw, args, ws, FlushMixWorkload.desc)
-        mix["parity"] = "tests/test_gpu_parity.py::test_tcp4_flush_mix_per_frame_hints"
+        mix = leg(mw.loop(), mw.bytes_per_step, args, ws, FlushMixWorkload.desc, "tcp4_tas14_kernel<head5>")
+        mix["parity"] = "tests/test_bench_configs.py::test_bench_flush_mix"
         del mw
         torch.cuda.empty_cache()
     raw = None
     if not args.no_raw:
         rw = RawWorkload(rot, pktgen.SEED + 1000 + rank)
-        raw = leg(rw, args, ws, RawWorkload.desc)
+        raw = leg(rw.loop(), rw.bytes_per_step, args, ws, RawWorkload.desc, "raw_sad_kernel<s32>")
         raw["algorithmic_bytes_per_packet"] = RAW_LEN + 2
         del rw
         torch.cuda.empty_cache()
@@ -818,7 +959,7 @@ def main():
         del wl.bufs[1:], wl.outs[1:]
         torch.cuda.empty_cache()
         tw = TxSegWorkload(rot, pktgen.SEED + 2000 + rank)
-        txseg = leg(tw, args, ws, TxSegWorkload.desc)
+        txseg = leg(tw.loop(), tw.bytes_per_step, args, ws, TxSegWorkload.desc, "tx_segment_tas_kernel")
         txseg["algorithmic_bytes_per_segment"] = tw.bytes_per_seg
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             txseg["cpu_baseline"] = tw.cpu_check(3.0)
@@ -828,23 +969,24 @@ def main():
     flow = None
     if not args.no_flow:
         fw = FlowLookupWorkload(min(rot, 4), pktgen.SEED + 3000 + rank)
-        flow = leg(fw, args, ws, FlowLookupWorkload.desc)
-        flow["mpps"] = fw.N * args.steps / (flow["ms_per_step"] * 1e-3 * args.steps) / 1e6
+        flow = leg(fw.loop(), fw.bytes_per_step, args, ws, FlowLookupWorkload.desc, "flow_lookup_kernel")
+        flow["mpps"] = fw.N / (flow["roofline"]["launch_avg_us"] * 1e-6) / 1e6
         flow["flows_inserted_frac"] = fw.inserted
         flow["bytes_per_frame"] = 64
+        flow["latency_roofline"] = flow_latency_roofline(fw.N, flow["roofline"]["launch_avg_us"])
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             flow["cpu_baseline"] = fw.cpu_check(3.0)
         del fw
         torch.cuda.empty_cache()
 
     extra = {}
+    if not args.no_e2e:
+        extra["e2e"] = e2e_leg(ws, rank)
     if rank == 0 and ws == 1:
         torch.cuda.synchronize()
         gpu_out = wl.outs[0].cpu().numpy().view(np.uint16).copy()
         if not args.no_cpu_baseline:
             extra["cpu_baseline"] = cpu_baseline_leg(wl, gpu_out, args.cpu_seconds)
-        if not args.no_e2e:
-            extra["e2e"] = e2e_leg()
         if not args.no_pmc:
             del wl
             torch.cuda.empty_cache()
@@ -873,8 +1015,14 @@ def main():
                        "algorithmic_bytes_per_frame": IP_TOTAL + 4, "rotation_batches": rot,
                        "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
             "roofline": head["roofline"],
+            "kernel": head["kernel"],
+            "frac_of_n_hbm": round(head["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
+            "per_rank_value": head.get("per_rank_value", [round(head["value"], 2)]),
+            "ranks": {"bus_ids": info.get("all_bus_ids", [info.get("pci_bus_id")]),
+                      "numa_node_rank0": info.get("numa_node"), "rehearse": info.get("rehearse")},
             "cpu_baseline": extra.get("cpu_baseline"),
             "tcp4_nohint": nohint,
+            "tcp4_frames_only": frames_only,
             "two_contexts": ctx2,
             "rx_verify": rx,
             "flush_mix": mix,
@@ -890,9 +1038,7 @@ def main():
         if "pmc" in extra:
             line["pmc"] = extra["pmc"]
         print(json.dumps(line), flush=True)
-    if ws > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,0 +1,34 @@
+/*
+ * tasx_ab.h -- extra entry points of the A/B build of libtasx
+ * (tas_amd/_lib/libtasx_ab.so, compiled with -DTASX_AB; used by tools/ and the
+ * variant tests, never by the product path).  Everything in tasx_xsum.h is
+ * exported as well, and tasx_set_kernel_variant() also accepts:
+ *   1  the first-generation group-per-packet kernels (raw_cksum_kernel,
+ *      tcp4_cksum_kernel)
+ *   2  RAW: raw_group_kernel (64-bit dword accumulators)
+ *   4  tcp4_tas_kernel with wave-timeline stamps into the diag buffer
+ *   5  tcp4_tas_kernel with 32-lane groups (TCP4 only)
+ *   8  tcp4_wave_kernel: a wave's 4 frames flattened over their hinted
+ *      datagrams (TCP4; needs l4_off == ip_off + 20)
+ *   9, 10, 11  tcp4_tas14_kernel without a uniform hint forced into its
+ *      total_length-first / head-5 / whole-room row mode where the room allows
+ * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
+ * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
+ */
+#ifndef TASX_AB_H_
+#define TASX_AB_H_
+
+#include "tasx_xsum.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
+ * wave.  NULL disables. */
+int tasx_set_diag_buffer(void *dev_buf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 1
+#define TASX_ABI_VERSION 2
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -100,12 +100,33 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
     uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
     void *stream);
 
+/* Same, with a room: `room` bytes from every frame's start are mapped and may
+ * be read (TAS: the mbuf data room, BUFFER_SIZE = 2048,
+ * tas/fast/internal.h:34; 0 = unknown).  room >= l4_off + 18, and in stride
+ * mode room <= stride.  A room lets a row issue its loads before it knows its
+ * ip.total_length: a batch without per-frame hints whose frames have room for
+ * a full MTU (IPv4 at 14 mod 16: room >= 1536 from the 16-byte aligned start)
+ * is read at the uniform-hint speed (rows load the whole MTU at once and mask
+ * by their own total_length); with per-frame hints a room of 80 B lets the
+ * first 80 bytes -- a whole pure ACK -- go out with the total_length read.
+ * Results still follow ip.total_length only. */
+int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
+    uint32_t flags, void *stream);
+
 /* Receive-side verification (new behaviour: TAS never verifies RX checksums,
  * tas/fast/fast_flows.c:242-251, and requests no RX offloads,
  * tas/fast/network.c:174).  flags[i] bit 0: the 20-byte IPv4 header folds to
  * 0xffff; bit 1: DPDK (>= 21.11) rte_ipv4_udptcp_cksum_verify() passes, i.e.
  * fold(rte_raw_cksum(L4) + rte_ipv4_phdr_cksum()) == 0xffff (total_length < 20
  * fails); bit 2: IHL != 5 (TAS drops such frames, fast_flows.c:247).
+ * Received frames are untrusted: the kernel reads a frame's 20-byte IPv4
+ * header and, beyond it, nothing past the frame's bound -- its received length
+ * (the hint, below), else the room, else its stride slot (stride mode); a
+ * datagram whose ip_off + total_length exceeds the bound fails bit 1 without
+ * being read.  Only offsets batches with neither hints nor a room trust
+ * total_length (their buffers must hold ip_off + total_length bytes).
  * Asynchronous on `stream`. */
 #define TASX_RX_IP_OK 0x1u
 #define TASX_RX_L4_OK 0x2u
@@ -113,12 +134,17 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
 int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream);
-/* Same, with frame-length hints (the received mbuf's data_len, flen[i], or
- * flen0 for the whole batch when flen == NULL; 0 = none), as for
- * tasx_tcp4_cksum_batch_dev_hint: the flags always follow ip.total_length. */
+/* Same, with the received frame lengths (the mbuf data_len, flen[i], or flen0
+ * for the whole batch when flen == NULL; 0 = none): the read bound above, and
+ * a prefetch hint; the flags always follow ip.total_length. */
 int tasx_tcp4_verify_batch_dev_hint(const void *base, const uint64_t *off,
     uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
     uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream);
+/* Same, with a room (as tasx_tcp4_cksum_batch_dev_room): the read bound of
+ * frames without a received length. */
+int tasx_tcp4_verify_batch_dev_room(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream);
 
 /* Fused TX segment build: the payload copy of
  * flow_tx_segment() -- flow_tx_read() from the flow's circular transmit buffer
@@ -239,37 +265,30 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
     uint32_t *staged_flushes);
 
 /* ---------------------------------------------------------------------- */
-/* Kernel selection, for A/B tests (process-wide; set it before launching).
- *   0 automatic: RAW -> 7 with per-packet lengths, else 6; TCP4 -> 6 when
- *     it applies, else 3 for the TAS
- *     layout in stride mode with a frame-length hint, else 2
- *   1 first-generation group-per-packet kernels (A/B baseline)
- *   2 raw_group_kernel / tcp4_frame_kernel (any layout)
+/* Kernel selection, for tests and A/B runs.  Per calling thread (TAS runs one
+ * fast-path core, i.e. one context, per thread); set it before launching.
+ *   0 automatic: RAW -> 7 with per-packet lengths, else raw_sad_kernel; TCP4 ->
+ *     6 when it applies, else 3 for the TAS layout in stride mode with a hint,
+ *     else 2
+ *   2 raw_sad_kernel (general form) / tcp4_frame_kernel (any layout)
  *   3 tcp4_tas_kernel (TAS layout, stride mode; falls back to 2)
- *   4 tcp4_tas_kernel with wave-timeline stamps into the diag buffer
- *   5 tcp4_tas_kernel with 32 lanes x 3 chunks per frame (TCP4 only; RAW
- *     uses 2)
- *   6 tcp4_tas14_kernel: TAS layout with the IPv4 header at 14 mod 16 (16-byte
- *     aligned base and stride), stride mode, one uniform hint flen0 with
- *     ip_off + 64 <= flen0 and the datagram within 96 chunks (uniform-MTU
- *     batches up to ip.len 1522), or no uniform hint (per-frame hints are
- *     then ignored: each row reads its total_length first), and the same
- *     without a uniform hint for frames by an offsets array with the IPv4
- *     header at 14 mod 16 from the frame start (frames not 16-byte aligned
- *     go to 2's row body); otherwise as 0.
- *     RAW: raw_sad_kernel
- *     (32-bit offsets from the base in stride mode within 4 GiB)
- *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk
- *     sequence: mixed lengths keep every lane loading); TCP4 as 0
- *   8 TCP4: tcp4_wave_kernel (the same flattening over each frame's hinted
- *     datagram, header words taken off per frame; frames whose
- *     ip.total_length differs from the hint are redone by 2's row body);
- *     needs l4_off == ip_off + 20, else as 0.  A/B only: slower than 3 on
- *     data/ACK mixes.  RAW and verification as 0 */
+ *   6 tcp4_tas14_kernel: TAS layout with the IPv4 header at 14 mod 16 from a
+ *     16-byte aligned frame start.  Stride mode with one uniform hint flen0
+ *     (ip_off + 64 <= flen0, the datagram within 96 chunks: uniform-MTU
+ *     batches up to ip.len 1522) fixes every row's geometry; otherwise (stride
+ *     mode or an offsets array, no uniform hint) each row takes its extent from
+ *     its own ip.total_length, loading ahead as far as the room allows (see
+ *     tasx_tcp4_cksum_batch_dev_room); rows it cannot take go to 2's bodies.
+ *     Otherwise as 0.  RAW: as 0 without lengths.
+ *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk sequence:
+ *     mixed lengths keep every lane loading); TCP4 as 0
+ * Variants 1, 4, 5 and 8-11 exist only in the A/B build (libtasx_ab.so,
+ * include/tasx_ab.h); this library rejects them with -EINVAL. */
 int tasx_set_kernel_variant(int variant);
-/* Device buffer for variant 4: 4 x u64 s_memrealtime (100 MHz) stamps per
- * wave.  NULL disables. */
-int tasx_set_diag_buffer(void *dev_buf);
+/* Name of the kernel the calling thread's last batch call launched (its entry
+ * kernel; rows it cannot take are redone inside it by a general body), "" if
+ * none.  For tests that assert which kernel a call ran. */
+const char *tasx_last_kernel(void);
 
 /* ---------------------------------------------------------------------- */
 /* Memory helpers (plumbing for callers without their own HIP code). */

@@ -48,6 +48,9 @@ class Oracle:
             "oracle_ipv4_udptcp_cksum_verify": (ctypes.c_int, [_u8p, _u8p]),
             "oracle_tcp4_verify_batch": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32,
                                                 ctypes.c_uint32, _u8p]),
+            "oracle_tcp4_verify_batch_bounded": (None, [_u8p, _u8p, ctypes.c_uint64, ctypes.c_size_t,
+                                                        ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32,
+                                                        _u8p]),
             "oracle_tx_segment_batch": (None, [_u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_size_t,
                                                ctypes.c_uint32, ctypes.c_uint32, _u8p]),
             "oracle_bench_tx_segment": (ctypes.c_double, [_u8p, ctypes.c_uint64, _u8p, _u8p, ctypes.c_size_t,
@@ -134,6 +137,21 @@ class Oracle:
         o = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
         self.L.oracle_tcp4_verify_batch(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n,
                                         ip_off, l4_off, out.ctypes.data)
+        return out
+
+    def tcp4_verify_batch_bounded(self, buf: np.ndarray, n: int, bounds, offsets=None, stride: int = 0,
+                                  ip_off: int = 14, l4_off: int = 34) -> np.ndarray:
+        """RX verification with per-frame read bounds (an int for all frames, or
+        an array; bytes from the frame start, 0 = none)."""
+        out = np.empty(n, np.uint8)
+        o = None if offsets is None else np.ascontiguousarray(offsets, np.uint64)
+        if isinstance(bounds, (int, np.integer)):
+            b, b0 = None, int(bounds)
+        else:
+            b, b0 = np.ascontiguousarray(bounds, np.uint32), 0
+        self.L.oracle_tcp4_verify_batch_bounded(buf.ctypes.data, None if o is None else o.ctypes.data, stride, n,
+                                                ip_off, l4_off, None if b is None else b.ctypes.data, b0,
+                                                out.ctypes.data)
         return out
 
     def tx_segment_batch(self, shm: np.ndarray, shm_len: int, frames: np.ndarray, segs: np.ndarray,

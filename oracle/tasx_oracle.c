@@ -223,6 +223,32 @@ void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
   }
 }
 
+/* The same, with a per-frame read bound (bytes from the frame start: the
+ * received length, room or stride slot; bound == NULL -> bound0, 0 = none):
+ * a datagram whose L4 part reaches past the bound fails the L4 check without
+ * being read (libtasx's receive-side contract, include/tasx_xsum.h). */
+void oracle_tcp4_verify_batch_bounded(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *bound, uint32_t bound0, uint8_t *flags)
+{
+  size_t i;
+  for (i = 0; i < n; i++) {
+    const uint8_t *f = base + pkt_off(off, stride, i);
+    const uint32_t b = bound ? bound[i] : bound0;
+    const uint32_t tl = (uint32_t) ((f[ip_off + 2] << 8) | f[ip_off + 3]);
+    const uint32_t len = tl >= 20 ? tl - 20 : 0;
+    const uint32_t have = b > l4_off ? b - l4_off : 0;
+    uint8_t v = 0;
+    if (oracle_ipv4_hdr_verify(f + ip_off))
+      v |= 1;
+    if ((b == 0 || len <= have) && oracle_ipv4_udptcp_cksum_verify(f + ip_off, f + l4_off))
+      v |= 2;
+    if ((f[ip_off] & 0x0f) != 5)
+      v |= 4;
+    flags[i] = v;
+  }
+}
+
 /* ---------------------------------------------------------------------- */
 /* TX segment build. */
 

@@ -59,6 +59,11 @@ int oracle_ipv4_udptcp_cksum_verify(const void *ip_hdr, const void *l4_hdr);
 /* flags[i] = hdr_ok | l4_ok << 1 | (IHL != 5) << 2 */
 void oracle_tcp4_verify_batch(const uint8_t *base, const uint64_t *off,
     uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags);
+/* with a per-frame read bound (bound[i], or bound0; 0 = none): L4 fails when
+ * the datagram's L4 part reaches past it (libtasx's RX contract) */
+void oracle_tcp4_verify_batch_bounded(const uint8_t *base, const uint64_t *off,
+    uint64_t stride, size_t n, uint32_t ip_off, uint32_t l4_off,
+    const uint32_t *bound, uint32_t bound0, uint8_t *flags);
 
 /* TX segment build: flow_tx_segment()'s payload
  * copy, flow_tx_read() (tas/fast/fast_flows.c:833-846, :930-933), then

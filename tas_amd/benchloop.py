@@ -1,0 +1,86 @@
+"""ctypes side of libtasx_bench.so (tas_amd/benchsrc/bench_loop.c): bench.py's
+timed steps are K calls of one libtasx entry point made from C, one call per
+step over R rotating batches, so no Python runs between the launches of a
+timed region.  Measurement plumbing only; the product API is tas_amd.xsum."""
+from __future__ import annotations
+
+import ctypes
+
+from . import xsum
+from .build import LIB_BENCH
+
+_vp, _u32, _u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+
+# tasxb_tcp4_loop entry points
+DEV, HINT, ROOM, VERIFY = 0, 1, 2, 3
+
+
+class Tcp4Args(ctypes.Structure):
+    _fields_ = [("base", _vp), ("off", _vp), ("stride", _u64), ("flen", _vp), ("flen0", _u32),
+                ("room", _u32), ("n", _u32), ("ip_off", _u32), ("l4_off", _u32), ("flags", _u32),
+                ("out", _vp)]
+
+
+class RawArgs(ctypes.Structure):
+    _fields_ = [("base", _vp), ("off", _vp), ("stride", _u64), ("len", _vp), ("len0", _u32), ("n", _u32),
+                ("out", _vp)]
+
+
+class TxSegArgs(ctypes.Structure):
+    _fields_ = [("shm", _vp), ("shm_len", _u64), ("frames", _vp), ("segs", _vp), ("n", _u32),
+                ("ip_off", _u32), ("l4_off", _u32), ("out", _vp)]
+
+
+class FlowArgs(ctypes.Structure):
+    _fields_ = [("base", _vp), ("off", _vp), ("stride", _u64), ("n", _u32), ("ip_off", _u32), ("l4_off", _u32),
+                ("flowht", _vp), ("ht_entries", _u32), ("flowst", _vp), ("fs_num", _u32), ("fs_stride", _u32),
+                ("fs_key_off", _u32), ("hash_out", _vp), ("fid_out", _vp)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        xsum.lib()  # libtasx.so first: the loop library binds to the same instance (by soname)
+        if not LIB_BENCH.exists():
+            raise RuntimeError(f"{LIB_BENCH} not built; run python -c 'import __graft_entry__ as g; g.build()'")
+        L = ctypes.CDLL(str(LIB_BENCH))
+        pp = ctypes.POINTER(_vp)
+        L.tasxb_tcp4_loop.argtypes = [ctypes.c_int, ctypes.POINTER(Tcp4Args), ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, pp, ctypes.c_int]
+        L.tasxb_raw_loop.argtypes = [ctypes.POINTER(RawArgs), ctypes.c_int, ctypes.c_int, ctypes.c_int, pp,
+                                     ctypes.c_int]
+        L.tasxb_txseg_loop.argtypes = [ctypes.POINTER(TxSegArgs), ctypes.c_int, ctypes.c_int, ctypes.c_int, pp,
+                                       ctypes.c_int]
+        L.tasxb_flow_loop.argtypes = [ctypes.POINTER(FlowArgs), ctypes.c_int, ctypes.c_int, ctypes.c_int, pp,
+                                      ctypes.c_int]
+        for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop):
+            f.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+class Loop:
+    """run(first, K): K steps, batch (first + k) % R on stream (first + k) % S."""
+
+    def __init__(self, kind: str, args: list, streams: list[int], which: int = 0, what: str = ""):
+        cls = {"tcp4": Tcp4Args, "raw": RawArgs, "txseg": TxSegArgs, "flow": FlowArgs}[kind]
+        self.arr = (cls * len(args))(*args)
+        self.streams = (_vp * len(streams))(*streams)
+        self.R, self.S, self.which, self.kind = len(args), len(streams), which, kind
+        self.what = what or kind
+        L = lib()
+        self.fn = {"tcp4": L.tasxb_tcp4_loop, "raw": L.tasxb_raw_loop, "txseg": L.tasxb_txseg_loop,
+                   "flow": L.tasxb_flow_loop}[kind]
+
+    def __call__(self, first: int, K: int) -> None:
+        if K <= 0:
+            return
+        if self.kind == "tcp4":
+            rc = self.fn(self.which, self.arr, self.R, first, K, self.streams, self.S)
+        else:
+            rc = self.fn(self.arr, self.R, first, K, self.streams, self.S)
+        if rc:
+            raise xsum.TasxError(rc, self.what)

@@ -1,0 +1,137 @@
+/*
+ * bench_loop.c -- launch loops for bench.py (libtasx_bench.so; measurement
+ * plumbing, not part of the product library).
+ *
+ * bench.py's timed region issues K back-to-back launches of one libtasx entry
+ * point over R rotating batches.  From Python each launch is a ctypes call
+ * (~5-8 us of host time), and the first launch of a timed region then reaches
+ * the GPU late.  These loops make the K calls from C, through libtasx's public
+ * C ABI exactly as a TAS integration would call it: same entry point, same
+ * arguments, one call per step.
+ */
+#include <stdint.h>
+
+#include "tasx_xsum.h"
+
+/* tasx_tcp4_cksum_batch_dev_room / tasx_tcp4_verify_batch_dev_room arguments
+ * of one batch */
+typedef struct tasxb_tcp4 {
+  void *base;
+  const uint64_t *off;
+  uint64_t stride;
+  const uint32_t *flen;
+  uint32_t flen0;
+  uint32_t room;
+  uint32_t n;
+  uint32_t ip_off;
+  uint32_t l4_off;
+  uint32_t flags;
+  void *out; /* uint16_t results (TX) or uint8_t flags (verify) */
+} tasxb_tcp4;
+
+/* entry-point selector for tasxb_tcp4_loop */
+enum { TASXB_DEV = 0, TASXB_HINT = 1, TASXB_ROOM = 2, TASXB_VERIFY = 3 };
+
+static int tcp4_call(int which, const tasxb_tcp4 *a, void *stream)
+{
+  switch (which) {
+  case TASXB_DEV:
+    return tasx_tcp4_cksum_batch_dev(a->base, a->off, a->stride, a->n, a->ip_off, a->l4_off,
+        (uint16_t *) a->out, a->flags, stream);
+  case TASXB_HINT:
+    return tasx_tcp4_cksum_batch_dev_hint(a->base, a->off, a->stride, a->flen, a->flen0, a->n,
+        a->ip_off, a->l4_off, (uint16_t *) a->out, a->flags, stream);
+  case TASXB_ROOM:
+    return tasx_tcp4_cksum_batch_dev_room(a->base, a->off, a->stride, a->flen, a->flen0, a->room,
+        a->n, a->ip_off, a->l4_off, (uint16_t *) a->out, a->flags, stream);
+  default:
+    return tasx_tcp4_verify_batch_dev_room(a->base, a->off, a->stride, a->flen, a->flen0, a->room,
+        a->n, a->ip_off, a->l4_off, (uint8_t *) a->out, stream);
+  }
+}
+
+/* launch batches a[(first + k) % R] for k < K, batch k on streams[(first + k)
+ * % S] (S fast-path contexts with a stream each); 0 or the first error */
+int tasxb_tcp4_loop(int which, const tasxb_tcp4 *a, int R, int first, int K, void *const *streams, int S)
+{
+  for (int k = 0; k < K; k++) {
+    int rc = tcp4_call(which, &a[(first + k) % R], streams[(first + k) % S]);
+    if (rc)
+      return rc;
+  }
+  return 0;
+}
+
+typedef struct tasxb_raw {
+  const void *base;
+  const uint64_t *off;
+  uint64_t stride;
+  const uint32_t *len;
+  uint32_t len0;
+  uint32_t n;
+  uint16_t *out;
+} tasxb_raw;
+
+int tasxb_raw_loop(const tasxb_raw *a, int R, int first, int K, void *const *streams, int S)
+{
+  for (int k = 0; k < K; k++) {
+    const tasxb_raw *b = &a[(first + k) % R];
+    int rc = tasx_raw_cksum_batch_dev(b->base, b->off, b->stride, b->len, b->len0, b->n, b->out, streams[(first + k) % S]);
+    if (rc)
+      return rc;
+  }
+  return 0;
+}
+
+typedef struct tasxb_txseg {
+  const void *shm;
+  uint64_t shm_len;
+  void *frames;
+  const tasx_tx_seg *segs;
+  uint32_t n;
+  uint32_t ip_off;
+  uint32_t l4_off;
+  uint32_t *out;
+} tasxb_txseg;
+
+int tasxb_txseg_loop(const tasxb_txseg *a, int R, int first, int K, void *const *streams, int S)
+{
+  for (int k = 0; k < K; k++) {
+    const tasxb_txseg *b = &a[(first + k) % R];
+    int rc = tasx_tx_segment_batch_dev(b->shm, b->shm_len, b->frames, b->segs, b->n, b->ip_off,
+        b->l4_off, b->out, streams[(first + k) % S]);
+    if (rc)
+      return rc;
+  }
+  return 0;
+}
+
+typedef struct tasxb_flow {
+  const void *base;
+  const uint64_t *off;
+  uint64_t stride;
+  uint32_t n;
+  uint32_t ip_off;
+  uint32_t l4_off;
+  const void *flowht;
+  uint32_t ht_entries;
+  const void *flowst;
+  uint32_t fs_num;
+  uint32_t fs_stride;
+  uint32_t fs_key_off;
+  uint32_t *hash_out;
+  uint32_t *fid_out;
+} tasxb_flow;
+
+int tasxb_flow_loop(const tasxb_flow *a, int R, int first, int K, void *const *streams, int S)
+{
+  for (int k = 0; k < K; k++) {
+    const tasxb_flow *b = &a[(first + k) % R];
+    int rc = tasx_flow_lookup_batch_dev(b->base, b->off, b->stride, b->n, b->ip_off, b->l4_off,
+        b->flowht, b->ht_entries, b->flowst, b->fs_num, b->fs_stride, b->fs_key_off, b->hash_out,
+        b->fid_out, streams[(first + k) % S]);
+    if (rc)
+      return rc;
+  }
+  return 0;
+}

@@ -1,4 +1,4 @@
-"""Build libtasx.so in-tree (tas_amd/_lib/) for gfx950.
+"""Build libtasx.so (and the A/B build libtasx_ab.so) in-tree (tas_amd/_lib/) for gfx950.
 
 hipcc compiles the HIP kernels for --offload-arch=gfx950 only; gcc compiles the
 C host layer (gnu99, the reference's dialect) against the HIP runtime's C API.
@@ -17,6 +17,9 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "tas_amd" / "csrc"
 OUT_DIR = ROOT / "tas_amd" / "_lib"
 LIB = OUT_DIR / "libtasx.so"
+# the A/B build (-DTASX_AB): the product kernels plus the kernels and knobs kept
+# for comparisons (include/tasx_ab.h); used by tools/ and the variant tests only
+LIB_AB = OUT_DIR / "libtasx_ab.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
@@ -29,38 +32,58 @@ def _run(cmd: list[str]) -> None:
     subprocess.run(cmd, check=True)
 
 
-def _stale() -> bool:
-    if not LIB.exists():
+def _stale(lib: Path) -> bool:
+    if not lib.exists():
         return True
-    t = LIB.stat().st_mtime
-    deps = list(CSRC.glob("*")) + [ROOT / "include" / "tasx_xsum.h", Path(__file__)]
+    t = lib.stat().st_mtime
+    deps = list(CSRC.glob("*")) + list((ROOT / "include").glob("*.h")) + [Path(__file__)]
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build(force: bool = False, extra_hip_flags: list[str] | None = None) -> Path:
-    if not force and not _stale():
-        return LIB
+def _build_one(lib: Path, defines: list[str], tag: str, extra_hip_flags: list[str] | None) -> Path:
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     objs = []
     hipcc = str(ROCM / "bin" / "hipcc")
     for s in HIP_SRCS:
-        o = OUT_DIR / (Path(s).stem + ".o")
+        o = OUT_DIR / (Path(s).stem + tag + ".o")
         _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-              "-Wall", "-Werror", "-Wno-unused-function",
+              "-Wall", "-Werror", "-Wno-unused-function", *defines,
               "-I", str(ROOT / "include"), *(extra_hip_flags or []),
               "-c", str(CSRC / s), "-o", str(o)])
         objs.append(o)
     for s in C_SRCS:
-        o = OUT_DIR / (Path(s).stem + ".o")
-        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror",
+        o = OUT_DIR / (Path(s).stem + tag + ".o")
+        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", *defines,
               "-D__HIP_PLATFORM_AMD__", "-I", str(ROCM / "include"),
               "-I", str(ROOT / "include"), "-c", str(CSRC / s), "-o", str(o)])
         objs.append(o)
-    tmp = LIB.with_suffix(".so.tmp")
+    tmp = lib.with_suffix(".so.tmp")
+    # -Bsymbolic: each library's internal calls bind to its own definitions, so
+    # the product and the A/B build can be loaded into one process side by side
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp),
-          *map(str, objs), f"-Wl,-rpath,{ROCM / 'lib'}", "-Wl,--no-undefined",
-          "-Wl,-soname,libtasx.so"])
-    tmp.replace(LIB)
+          *map(str, objs), f"-Wl,-rpath,{ROCM / 'lib'}", "-Wl,--no-undefined", "-Wl,-Bsymbolic",
+          f"-Wl,-soname,{lib.name}"])
+    tmp.replace(lib)
+    return lib
+
+
+# bench.py's launch loops (measurement plumbing over libtasx's public C ABI)
+LIB_BENCH = OUT_DIR / "libtasx_bench.so"
+BENCH_SRC = ROOT / "tas_amd" / "benchsrc" / "bench_loop.c"
+
+
+def build(force: bool = False, extra_hip_flags: list[str] | None = None, ab: bool = True) -> Path:
+    """Build libtasx.so (and, with ab=True, libtasx_ab.so; and the bench loop
+    library) when stale; returns the product library's path."""
+    if force or _stale(LIB):
+        _build_one(LIB, [], "", extra_hip_flags)
+    if ab and (force or _stale(LIB_AB)):
+        _build_one(LIB_AB, ["-DTASX_AB"], "_ab", extra_hip_flags)
+    if force or not LIB_BENCH.exists() or LIB_BENCH.stat().st_mtime < max(
+            BENCH_SRC.stat().st_mtime, LIB.stat().st_mtime, (ROOT / "include" / "tasx_xsum.h").stat().st_mtime):
+        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", "-shared", "-I", str(ROOT / "include"),
+              "-o", str(LIB_BENCH), str(BENCH_SRC), "-L", str(OUT_DIR), "-ltasx",
+              "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
     return LIB
 
 

@@ -200,21 +200,28 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
     return 0;
   const dim3 g((uint32_t) blocks), b(256);
   hipStream_t s = (hipStream_t) stream;
-  // A/B (tasx_set_kernel_variant; tools/flow_probe.py, profiles/r01_flow_variants.jsonl):
-  // bitwise CRC + byte loads (the default, 0/1) 12.6-12.7 us, LDS slice-by-4
-  // 12.4-13.0 us, LDS byte-position tables (5) 12.6 us, 16-byte chunk key loads
-  // +1.7 us: the lookup is bound by its dependent load chain (frame header ->
-  // bucket -> flow state), not by the CRC arithmetic
+  // A/B (TASX_AB builds, tasx_set_kernel_variant; tools/flow_probe.py,
+  // profiles/r01_flow_variants.jsonl): bitwise CRC + byte loads (the product
+  // kernel) 12.6-12.7 us, LDS slice-by-4 12.4-13.0 us, LDS byte-position tables
+  // (5) 12.6 us, 16-byte chunk key loads +1.7 us: the lookup is bound by its
+  // dependent load chain (frame header -> bucket -> flow state), not by the
+  // CRC arithmetic
+#ifdef TASX_AB
   switch (variant) {
-  case 2: hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, true>), g, b, 0, s, *p); break;
-  case 3: hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, false>), g, b, 0, s, *p); break;
-  case 4: hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, true>), g, b, 0, s, *p); break;
+  case 2: tasx_note_kernel("flow_lookup_kernel<bitwise,chunk>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, true>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 3: tasx_note_kernel("flow_lookup_kernel<slice4>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 4: tasx_note_kernel("flow_lookup_kernel<slice4,chunk>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, true>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
 #ifdef TASX_FLOW_NOCRC_DIAG
-  case 5: hipLaunchKernelGGL((flow_lookup_kernel<kCrcNone, false>), g, b, 0, s, *p); break;
+  case 5: tasx_note_kernel("flow_lookup_kernel<nocrc>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcNone, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
 #else
-  case 5: hipLaunchKernelGGL((flow_lookup_kernel<kCrcKeyTab, false>), g, b, 0, s, *p); break;
+  case 5: tasx_note_kernel("flow_lookup_kernel<keytab>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcKeyTab, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
 #endif
-  default: hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false>), g, b, 0, s, *p); break;
+  default: break;
   }
+#else
+  (void) variant;
+#endif
+  tasx_note_kernel("flow_lookup_kernel");
+  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false>), g, b, 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -61,8 +61,12 @@ int tasx_device_count(void)
 /* ---------------------------------------------------------------------- */
 /* device-resident batches */
 
-/* kernel selection (tasx_set_kernel_variant); 0 = automatic */
-static int g_variant = 0;
+/* kernel selection (tasx_set_kernel_variant), per calling thread -- one
+ * fast-path core per thread in TAS, so each context selects independently;
+ * 0 = automatic */
+static __thread int g_variant = 0;
+
+#ifdef TASX_AB
 static uint64_t *g_diag = NULL;
 
 int tasx_set_diag_buffer(void *dev_buf)
@@ -70,11 +74,19 @@ int tasx_set_diag_buffer(void *dev_buf)
   g_diag = (uint64_t *) dev_buf;
   return 0;
 }
+#define TASX_MAX_VARIANT 11
+#else
+#define TASX_MAX_VARIANT 7
+#endif
 
 int tasx_set_kernel_variant(int variant)
 {
-  if (variant < 0 || variant > 8)
+  if (variant < 0 || variant > TASX_MAX_VARIANT)
     return set_err(-EINVAL, "kernel variant %d out of range", variant);
+#ifndef TASX_AB
+  if (variant == 1 || variant == 4 || variant == 5)
+    return set_err(-EINVAL, "kernel variant %d is an A/B build variant (libtasx_ab.so)", variant);
+#endif
   g_variant = variant;
   return 0;
 }
@@ -104,10 +116,25 @@ int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
   return 0;
 }
 
-int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
-    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
-    uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
-    void *stream)
+/* a room must hold the headers a row always reads and may not reach into the
+ * next frame of a stride-mode batch */
+static int check_room(uint32_t room, uint64_t stride, const uint64_t *off, uint32_t ip_off,
+    uint32_t l4_off, const char *what)
+{
+  if (room == 0)
+    return 0;
+  if ((uint64_t) room < (uint64_t) ip_off + 20 || (uint64_t) room < (uint64_t) l4_off + 18)
+    return set_err(-EINVAL, "%s: room %u does not hold the headers", what, room);
+  if (!off && stride && room > stride)
+    return set_err(-EINVAL, "%s: room %u exceeds the stride %llu", what, room,
+        (unsigned long long) stride);
+  return 0;
+}
+
+int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
+    uint32_t flags, void *stream)
 {
   tasx_tcp4_params p;
   int r;
@@ -119,6 +146,8 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
     return set_err(-EINVAL, "tcp4 batch: out must be 4-byte aligned");
   if (flags & ~TASX_F_INPLACE)
     return set_err(-EINVAL, "tcp4 batch: unknown flags 0x%x", flags);
+  if ((r = check_room(room, stride, off, ip_off, l4_off, "tcp4 batch")) != 0)
+    return r;
   memset(&p, 0, sizeof(p));
   p.base = (uint8_t *) base;
   p.off = off;
@@ -130,18 +159,30 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
   p.flags = flags;
   p.flen = flen;
   p.flen0 = flen0;
+  p.room = room;
+#ifdef TASX_AB
   p.diag = g_diag;
+#endif
   r = tasx_launch_tcp4(&p, g_variant, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
   return 0;
 }
 
+int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags,
+    void *stream)
+{
+  return tasx_tcp4_cksum_batch_dev_room(base, off, stride, flen, flen0, 0, n, ip_off,
+      l4_off, out, flags, stream);
+}
+
 int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint16_t *out, uint32_t flags, void *stream)
 {
-  return tasx_tcp4_cksum_batch_dev_hint(base, off, stride, NULL, 0, n, ip_off,
+  return tasx_tcp4_cksum_batch_dev_room(base, off, stride, NULL, 0, 0, n, ip_off,
       l4_off, out, flags, stream);
 }
 
@@ -149,7 +190,7 @@ int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream)
 {
-  return tasx_tcp4_verify_batch_dev_hint(base, off, stride, NULL, 0, n, ip_off,
+  return tasx_tcp4_verify_batch_dev_room(base, off, stride, NULL, 0, 0, n, ip_off,
       l4_off, flags, stream);
 }
 
@@ -157,11 +198,22 @@ int tasx_tcp4_verify_batch_dev_hint(const void *base, const uint64_t *off,
     uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t n,
     uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream)
 {
+  return tasx_tcp4_verify_batch_dev_room(base, off, stride, flen, flen0, 0, n, ip_off,
+      l4_off, flags, stream);
+}
+
+int tasx_tcp4_verify_batch_dev_room(const void *base, const uint64_t *off,
+    uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
+    uint32_t n, uint32_t ip_off, uint32_t l4_off, uint8_t *flags, void *stream)
+{
   tasx_tcp4_params p;
+  int r;
   if (n == 0)
     return 0;
   if ((!base && !off) || !flags)
     return set_err(-EINVAL, "tcp4 verify: NULL base/flags");
+  if ((r = check_room(room, stride, off, ip_off, l4_off, "tcp4 verify")) != 0)
+    return r;
   memset(&p, 0, sizeof(p));
   p.base = (uint8_t *) base;
   p.off = off;
@@ -172,6 +224,7 @@ int tasx_tcp4_verify_batch_dev_hint(const void *base, const uint64_t *off,
   p.l4_off = l4_off;
   p.flen = flen;
   p.flen0 = flen0;
+  p.room = room;
   if (tasx_launch_tcp4_verify(&p, g_variant, stream) != 0)
     return hip_err(hipGetLastError(), "tcp4 verify kernel launch");
   return 0;
@@ -201,14 +254,12 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   p.n = n;
   p.ip_off = ip_off;
   p.l4_off = l4_off;
+#ifdef TASX_AB
   {
-    static int dbg = -1;
-    if (dbg < 0) {
-      const char *e = getenv("TASX_TXSEG_DEBUG");
-      dbg = e ? atoi(e) : 0;
-    }
-    p.dbg = (uint32_t) dbg;
+    const char *e = getenv("TASX_TXSEG_DEBUG");
+    p.dbg = e ? (uint32_t) atoi(e) : 0u;
   }
+#endif
   if (tasx_launch_txseg(&p, stream) != 0)
     return hip_err(hipGetLastError(), "tx segment kernel launch");
   return 0;
@@ -460,6 +511,8 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     p.ip_off = ip_off;
     p.l4_off = l4_off;
     p.flags = 0;
+    /* whole mbuf rooms were copied: each frame's stride slot may be read */
+    p.room = stride <= 0xffffffffull ? (uint32_t) stride : 0u;
 
     if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
       return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");

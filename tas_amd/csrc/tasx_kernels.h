@@ -12,6 +12,9 @@
 extern "C" {
 #endif
 
+/* library-internal: not exported from libtasx.so */
+#define TASX_INTERNAL __attribute__((visibility("hidden")))
+
 typedef struct tasx_raw_params {
   const uint8_t *base;   /* device pointer */
   const uint64_t *off;   /* device, n entries, or NULL -> i * stride */
@@ -34,7 +37,9 @@ typedef struct tasx_tcp4_params {
   const uint32_t *flen;  /* device, n frame-length hints (bytes from the frame
                           * start, the mbuf data_len), or NULL -> flen0 */
   uint32_t flen0;        /* uniform hint; 0 = none */
-  uint64_t *diag;        /* diagnostic timestamp buffer (diag variants only) */
+  uint32_t room;         /* bytes from each frame's start that may be read (the
+                          * mbuf data room); 0 = unknown */
+  uint64_t *diag;        /* diagnostic timestamp buffer (TASX_AB diag variant) */
 } tasx_tcp4_params;
 
 typedef struct tasx_txseg_params {
@@ -46,7 +51,7 @@ typedef struct tasx_txseg_params {
   uint32_t n;
   uint32_t ip_off;
   uint32_t l4_off;
-  uint32_t dbg;            /* diagnostics: TASX_TXSEG_DEBUG (0 = product) */
+  uint32_t dbg;            /* TASX_AB builds: TASX_TXSEG_DEBUG diagnostics (0 = product) */
 } tasx_txseg_params;
 
 typedef struct tasx_flow_params {
@@ -67,17 +72,19 @@ typedef struct tasx_flow_params {
 } tasx_flow_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
-int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
-int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
+TASX_INTERNAL int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
+TASX_INTERNAL int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 /* receive-side verification; p->out points to n flag bytes */
-int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream);
+TASX_INTERNAL int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream);
 /* RX flow lookup (flow_kernels.hip) */
-int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream);
+TASX_INTERNAL int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream);
 /* one-lane kernel storing seq into *word (pinned host memory, device view)
  * with system-scope release, after everything before it on the stream */
-int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
+TASX_INTERNAL int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
-int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
+TASX_INTERNAL int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
+/* record the name of the kernel the calling thread launches (tasx_last_kernel) */
+TASX_INTERNAL void tasx_note_kernel(const char *name);
 
 #ifdef __cplusplus
 }

@@ -728,19 +728,31 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   const bool u_ok = p->l4_off + 18u + 15u <= 256u && p->ip_off + 12u + 15u <= 256u && p->shm_len >= 16u;
   // the TAS kernel: IPv4 at 14, TCP at 34 (its other segments go to the general body)
   const bool tas = p->ip_off == 14u && p->l4_off == 34u;
-  switch (u_ok ? p->dbg : 4u) { // diagnostics (TASX_TXSEG_DEBUG, tools/txseg_probe.py)
-  case 1: hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); break;  // 3 slots per round
-  case 2: hipLaunchKernelGGL((tx_segment_kernel<6, 1>), grid, block, 0, s, *p); break;  // no full-chunk stores
-  case 3: hipLaunchKernelGGL((tx_segment_kernel<6, 25>), grid, block, 0, s, *p); break; // no stores at all
-  case 4: hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); break;  // aligned-gather kernel
-  case 5: hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p); break; // general layout
-  case 6: hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); break; // plain stores
-  default:
-    if (tas)
-      hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 0, s, *p);
-    else
-      hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p);
-    break;
+#ifdef TASX_AB
+  // diagnostics (TASX_TXSEG_DEBUG, tools/txseg_probe.py)
+  switch (u_ok ? p->dbg : 4u) {
+  case 1: tasx_note_kernel("tx_segment_kernel<3>"); hipLaunchKernelGGL((tx_segment_kernel<3, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;  // 3 slots per round
+  case 2: tasx_note_kernel("tx_segment_kernel<nostore_full>"); hipLaunchKernelGGL((tx_segment_kernel<6, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;  // no full-chunk stores
+  case 3: tasx_note_kernel("tx_segment_kernel<nostore>"); hipLaunchKernelGGL((tx_segment_kernel<6, 25>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // no stores at all
+  case 4: tasx_note_kernel("tx_segment_kernel"); hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;  // aligned-gather kernel
+  case 5: tasx_note_kernel("tx_segment_u_kernel"); hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // general layout
+  case 6: tasx_note_kernel("tx_segment_tas_kernel<plain>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // plain stores
+  default: break;
+  }
+#else
+  if (!u_ok) {
+    // checksum fields beyond the frame's first 256 bytes: the aligned-gather build
+    tasx_note_kernel("tx_segment_kernel");
+    hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+#endif
+  if (tas) {
+    tasx_note_kernel("tx_segment_tas_kernel");
+    hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 0, s, *p);
+  } else {
+    tasx_note_kernel("tx_segment_u_kernel");
+    hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -206,6 +206,13 @@ __device__ __forceinline__ uint32_t row_shl(uint32_t v)
   return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x100 + K, 0xf, 0xf, false);
 }
 
+// lane K of each 16-lane row broadcast to the whole row (DPP row_newbcast)
+template <int K>
+__device__ __forceinline__ uint32_t row_newbcast(uint32_t v)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) v, 0x150 + K, 0xf, 0xf, false);
+}
+
 // byte mask of [0, h) over a 16-byte chunk as two qwords (0 <= h <= 16)
 __device__ __forceinline__ void below_mask(uint32_t h, uint64_t &lo, uint64_t &hi)
 {

@@ -27,15 +27,18 @@
 //     zeroed checksum fields are handled by masking or by subtracting their
 //     bytes modulo 0xffff.
 //
-// Kernels (tasx_set_kernel_variant): 2 = raw_group_kernel / tcp4_frame_kernel
-// (any layout), 3 = tcp4_tas_kernel (TAS frame layout, stride mode), 6 =
-// tcp4_tas14_kernel (the headline: TAS frames in 16-byte aligned rooms, one
-// uniform frame-length hint), 1 = the first-generation group-per-packet
-// kernels (kept as the A/B baseline), 4 = tcp4_tas_kernel with wave-timeline
-// stamps (diagnostic), 5 = tcp4_tas_kernel with 32-lane groups (A/B), 7 =
-// raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
-// chunk sequence), 8 = tcp4_wave_kernel (TCP4 with per-frame hints: the same
-// flattening over each frame's datagram).
+// Kernels in the product library (tasx_set_kernel_variant):
+//   2 = raw_sad_kernel (general) / tcp4_frame_kernel (any layout),
+//   3 = tcp4_tas_kernel (TAS frame layout, stride mode),
+//   6 = tcp4_tas14_kernel (TAS frames in 16-byte aligned rooms: the headline with
+//       a uniform frame-length hint; per-row total_length modes otherwise),
+//   7 = raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
+//       chunk sequence).
+// Built only with -DTASX_AB (libtasx_ab.so, tools/ and the A/B tests): 1 = the
+// first-generation group-per-packet kernels, 4 = tcp4_tas_kernel with
+// wave-timeline stamps, 5 = tcp4_tas_kernel with 32-lane groups, 8 =
+// tcp4_wave_kernel, RAW variant 2 = raw_group_kernel, and the environment knobs
+// that steer residency (TASX_*_LDS) and the TX segment diagnostics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -46,6 +49,7 @@
 
 namespace {
 
+#ifdef TASX_AB
 // ---------------------------------------------------------------------------
 // First-generation kernels (variant 1, the A/B baseline): one G-lane group per
 // packet, xor-shuffle reductions, byte loads for the TCP4 header.
@@ -178,6 +182,8 @@ __global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
     }
   }
 }
+#endif // TASX_AB
+
 // RAW, any layout, word sums by v_sad_u16 into exact 32-bit accumulators
 // (variant 6).  Rounds of U chunk loads per lane, clamped to the packet's last
 // chunk and issued back to back; chunk-index selects keep the clamped
@@ -381,6 +387,21 @@ __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
   }
 }
 
+// Receive-side read bound of a frame, in bytes from its start: the received
+// frame length (the hint: the mbuf data_len), else the batch's room, else the
+// stride slot; ~0 when nothing bounds it (offsets without hints or room: the
+// buffer must then hold ip_off + total_length bytes, as DPDK assumes).
+__device__ __forceinline__ uint32_t rx_bound(const tasx_tcp4_params &p, uint32_t hint)
+{
+  if (hint)
+    return hint;
+  if (p.room)
+    return p.room;
+  if (!p.off && p.stride)
+    return p.stride < 0xffffffffull ? (uint32_t) p.stride : 0xffffffffu;
+  return 0xffffffffu;
+}
+
 // TCP4, any frame layout: header words and the checksum-field bytes by byte
 // loads, then the segment chunks.  With a frame-length hint (the mbuf
 // data_len tx_send() sets before tx_flush) the chunk loads are issued together
@@ -394,8 +415,11 @@ __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
 // = rte_ipv4_udptcp_cksum_verify passes (DPDK >= 21.11: fold1(raw(L4) +
 // phdr) == 0xffff; total_length < 20 fails), bit 2 = IHL != 5 (TAS drops
 // such frames, fast_flows.c:247; bits 0/1 then describe a 20-byte header).
-// One frame (i) per 16-lane DPP row, lane gl (the body of tcp4_frame_kernel,
-// also run by the persistent flush kernel).
+// Received frames are untrusted: reads stay below the frame's rx_bound() (the
+// received length, else the room, else the stride slot), and a datagram whose
+// total_length reaches past it fails the L4 check (bit 1 clear) without being
+// read; the 20-byte IPv4 header is always read.
+// One frame (i) per 16-lane DPP row, lane gl (the body of tcp4_frame_kernel).
 template <int U, bool VERIFY = false>
 __device__ __forceinline__ void tcp4_frame_row(const tasx_tcp4_params &p, uint32_t i, int gl)
 {
@@ -417,7 +441,15 @@ __device__ __forceinline__ void tcp4_frame_row(const tasx_tcp4_params &p, uint32
   if (gl < 10)
     w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  const Chunks<U> r = chunk_range<U>(l4, len);
+  bool trunc = false; // RX: the datagram reaches past the frame's bound
+  uint32_t rlen = len;
+  if constexpr (VERIFY) {
+    const uint32_t b = rx_bound(p, hint);
+    const uint32_t have = b > p.l4_off ? b - p.l4_off : 0u;
+    trunc = len > have;
+    rlen = trunc ? have : len;
+  }
+  const Chunks<U> r = chunk_range<U>(l4, rlen);
   // first 16*U chunks: reuse the speculative loads when they cover them
   uint64_t acc = 0;
   if (r.nch) {
@@ -472,7 +504,7 @@ __device__ __forceinline__ void tcp4_frame_row(const tasx_tcp4_params &p, uint32
     // exact rte_raw_cksum values: every sum above is exact and non-negative
     const uint32_t ri = fold32_to_16(c_ip);
     uint32_t flags = (ri == 0xffffu) ? 1u : 0u;
-    if (tl >= 20) {
+    if (tl >= 20 && !trunc) {
       uint32_t r4 = fold32_to_16(part);
       if (r.head & 1)
         r4 = bswap16(r4);
@@ -514,6 +546,7 @@ __global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
   tcp4_frame_row<U, VERIFY>(p, i, threadIdx.x & 15);
 }
 
+#ifdef TASX_AB
 // TCP4 batches of mixed frame lengths with per-frame hints (a tx_flush batch:
 // flow_tx_segment data frames among flow_tx_ack / inject_tcp_ts frames,
 // fast_flows.c:877-1030).  One row per frame leaves the rows of short frames
@@ -598,6 +631,8 @@ __global__ __launch_bounds__(kBlock) void tcp4_wave_kernel(tasx_tcp4_params p)
   }
 }
 
+#endif // TASX_AB
+
 // mask of the bytes of a dword (first byte at ip-relative offset `base`) that
 // fall in [lo, hi)
 __device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
@@ -678,7 +713,14 @@ __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, i
   if constexpr (DIAG)
     diag_stamp<kBlock>(p, 1);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  const int E = 20 + (int) len;
+  int E = 20 + (int) len;
+  bool trunc = false; // RX: the datagram reaches past the frame's bound (rx_bound)
+  if constexpr (VERIFY) {
+    const uint32_t b = rx_bound(p, hint);
+    const uint32_t have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
+    trunc = (uint32_t) E > have;
+    E = trunc ? (int) have : E;
+  }
   const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
   const uint32_t need = min(nch, (uint32_t) G * U);
   if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
@@ -744,7 +786,7 @@ __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, i
       if (hb & 1)
         ri = bswap16(ri);
       uint32_t flags = ri == 0xffffu ? TASX_RX_IP_OK : 0u;
-      if (tl >= 20) {
+      if (tl >= 20 && !trunc) {
         uint32_t r4 = fold32_to_16(part), rp = fold32_to_16(c_ph);
         if (hb & 1) {
           r4 = bswap16(r4);
@@ -794,35 +836,47 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 }
 
 // TCP4 headline kernel: TAS frames in 16-byte aligned mbuf rooms (IPv4 header
-// at 14 mod 16, TCP at +20), stride mode, one uniform frame-length hint
-// (flen0, the mbuf data_len of a uniform-MTU batch) that the host has checked
-// spans 5..16U chunks.  The chunk geometry is then compile-time or uniform,
-// and the per-lane work is the fold itself: one v_sad_u16 per dword (both LE
-// 16-bit words of the dword added into a 32-bit accumulator: the
-// address-aligned word sum, exact), U loads, U selects, and a fixed header
-// split.  Chunk map (chunk c = frame bytes [16c, 16c+16), dN = its dword N):
+// at 14 mod 16, TCP at +20), one frame per 16-lane DPP row, U = 6 chunks per
+// lane (96 chunks: datagrams up to 1522 B in one round).  The per-lane work is
+// the fold itself: one v_sad_u16 per dword (both LE 16-bit words of the dword
+// added into a 32-bit accumulator: the address-aligned word sum, exact), U
+// loads, U selects, and a fixed header split.  Chunk map (chunk c = frame
+// bytes [16c, 16c+16), dN = its dword N):
 //   chunk 0 = eth[0,14) + ip[0,2)   IP: d3.hi
 //   chunk 1 = ip[2,18)              IP: d0, d1, d2.hi, d3 (ip.chksum = d2.lo left out)
 //                                   PH: d1 byte 3 (proto), d2.hi, d3 (src, dst)
 //   chunk 2 = ip[18,20) + tcp[0,14) IP, PH: d0.lo;  L4: d0.hi, d1..d3
 //   chunk 3 = tcp[14,30)            L4: d0.lo, d1..d3 (tcp.chksum = d0.hi left out)
 //   chunks 4.. = the segment        L4 (bytes past ip + total_length subtracted
-//                                   on lane 15, whose last load is the last chunk)
-// Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved
-// in by DPP.  A group whose ip.total_length differs from the hint is redone
-// by the general body (tcp4_tas_frame): results always follow total_length.
-// NOHINT: no frame-length hint; the row first reads the frame's chunk 1 (all
-// 16 lanes, one line) for ip.total_length and then proceeds as with a hint of
-// exactly that length -- two dependent memory latencies per frame instead of
-// one, no bytes read past ip.total_length (DPDK's own trust in the header).
-// Rows with total_length outside [64, 1522] take the general body.
-// OFFS (with NOHINT, TX): frames at base + off[i] instead of i * stride; a row
-// whose frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned
-// loads only the aligned chunk holding the IPv4 header start and is redone by
-// the general row body (tcp4_frame_row).
-template <int U, bool VERIFY = false, bool NOHINT = false, int WPE = 1, bool OFFS = false>
+//                                   on the lane holding the last chunk)
+// Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved in
+// by DPP.  How a row learns its datagram's extent (MODE):
+//   kHint    one uniform frame-length hint (flen0, the mbuf data_len of a
+//            uniform-MTU batch) fixes the geometry for every row; a row whose
+//            ip.total_length differs is redone by the general body.  One
+//            dependent memory latency per frame.
+//   kTlFirst the row reads chunk 1 (ip.total_length; all 16 lanes, one line)
+//            first, then exactly its datagram: two dependent latencies, no
+//            byte read past ip.total_length (DPDK's own trust in the header).
+//   kHead5   chunks 0..4 (a whole pure ACK, ip.len 52) are loaded with the
+//            total_length, the rest after it: ACK rows take one latency, data
+//            rows two.  Needs a room of 80 B (the chunk-4 read).
+//   kRoom    all 96 chunks of the frame's room at once, masked per row by its
+//            total_length after the loads: one latency for every frame, at the
+//            price of reading whole rooms.  Needs a room of 1536 B.
+// Rows with total_length outside [38 (51 for kHead5), 1522], or beyond the RX
+// read bound, take the general body (tcp4_tas_frame; tcp4_frame_row with OFFS).
+// OFFS (not kHint): frames at base + off[i] instead of i * stride; a row whose
+// frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned loads
+// only the aligned chunk holding the IPv4 header start and is redone by the
+// general row body.
+enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3 };
+
+template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
+  static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
+  static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   if (i >= p.n)
@@ -838,28 +892,65 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   } else {
     a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
   }
-  // the datagram [ip, ip + hend) and its last chunk: uniform from the hint, or
-  // per row from the frame's own total_length
+  // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
+  uint32_t have = 65535u;
+  if constexpr (VERIFY && MODE != kHint) {
+    const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
+    have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
+  }
+  // the datagram [ip, ip + hend): uniform from the hint, or per row from the
+  // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
+  const uint32_t lo = a0 + 16u * (uint32_t) gl;
   uint32_t hend;
   bool in_range = true;
-  if constexpr (NOHINT) {
+  u32x4 v[U];
+  if constexpr (MODE == kHint) {
+    hend = p.flen0 - p.ip_off;
+    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  } else if constexpr (MODE == kTlFirst) {
     const uint32_t tl0 = bswap16(ld16nt_off(fb, a0 + (row_ok ? 16u : 0u)).x & 0xffffu);
     // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
     // the end never include the masked field; pure ACKs, ip.len 52, qualify)
     // to 1522 (96 chunks)
-    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u;
+    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-  } else {
-    hend = p.flen0 - p.ip_off;
+    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  } else if constexpr (MODE == kHead5) {
+    v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
+    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
+    // from 51: the last chunk is chunk 4 or later, so lane 15 holds it
+    in_range = row_ok && tl0 >= 51u && tl0 <= 1522u && tl0 <= have;
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
+    const uint32_t last = (14u + hend - 1u) >> 4;
+    if (last > 4u) { // the datagram goes on past chunk 4
+      const uint32_t lastoff = a0 + 16u * last;
+      if (gl > 4)
+        v[0] = ld16nt_off(fb, min(lo, lastoff));
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+    } else {
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = v[0]; // excluded below; lane 15's v[U-1] = chunk 4, the last one
+    }
+  } else { // kRoom
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, row_ok ? lo + 256u * u : a0);
+    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
+    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
   const uint32_t last = (14u + hend - 1u) >> 4;
   const uint32_t tail = 14u + hend - 16u * last; // bytes of the last chunk inside, 1..16
-  const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * last;
-  u32x4 v[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
 
   // chunks 0..3: the L4 part of chunk gl (none for 0, 1), whole chunks elsewhere
   const u32x4 h = v[0];
@@ -879,9 +970,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const uint32_t s = sad4(v[u], acc);
     acc = ((uint32_t) gl + 16u * u <= last) ? s : acc;
   }
-  // bytes [tail, 16) of the last chunk lie past the datagram.  Lane 15's last
-  // load was clamped to that chunk (15 + 16(U-1) >= last), so lane 15 takes them
-  // off (its own partial may wrap; the group total is exact mod 2^32)
+  // bytes [tail, 16) of the last chunk lie past the datagram: the lane holding
+  // that chunk takes them off (its own partial may wrap; the group total is
+  // exact mod 2^32).  Clamped loads leave it in lane 15's last slot; kRoom
+  // picks slot last / 16 on lane last % 16.
   {
     uint32_t gm[4];
 #pragma unroll
@@ -889,13 +981,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       const uint32_t k = tail > 4u * j ? min(tail - 4u * j, 4u) : 0u;
       gm[j] = (uint32_t) (~0ull << (8u * k));
     }
-    const u32x4 t = v[U - 1];
+    u32x4 t = v[U - 1];
+    uint32_t tlane = 15u;
+    if constexpr (MODE == kRoom) {
+      const uint32_t ut = last >> 4;
+      t = v[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        t = ut == (uint32_t) u ? v[u] : t;
+      tlane = last & 15u;
+    }
     const uint32_t g = sad4(u32x4{t.x & gm[0], t.y & gm[1], t.z & gm[2], t.w & gm[3]}, 0u);
-    acc -= gl == 15 ? g : 0u;
+    acc -= (uint32_t) gl == tlane ? g : 0u;
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  const bool bad = NOHINT ? !in_range : tl15 != hend; // meaningful on lane 15
+  const bool bad = MODE == kHint ? tl15 != hend : !in_range; // kHint: meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
     if (gl == 15 && !bad) {
@@ -923,7 +1024,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
   if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
-    if (__shfl((int) bad, gbase + 15, 64)) {
+    const bool rbad = MODE == kHint ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
+    if (rbad) {
       if constexpr (OFFS)
         tcp4_frame_row<3, VERIFY>(p, i, gl);
       else
@@ -939,7 +1041,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 // RAW -1.5%; profiles/r01_sweeps_s2.jsonl).
 constexpr uint32_t kOccLds = 30u * 1024u;
 
-// raw_wave_kernel: chunks per lane per round and the LDS reservation (A/B knobs)
+// raw_wave_kernel: chunks per lane per round and the LDS reservation
 #ifndef TASX_WAVE_U
 #define TASX_WAVE_U 6
 #endif
@@ -947,8 +1049,11 @@ constexpr uint32_t kOccLds = 30u * 1024u;
 #define TASX_WAVE_LDS kOccLds
 #endif
 
+// the launched kernel's name, per calling thread (tasx_last_kernel)
+static thread_local const char *t_last_kernel = "";
+
 template <int G = 16, typename K, typename Prm>
-int launch_groups(K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
+int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
   // one G-lane group per packet, kBlock / G groups per block: the grid covers
   // the batch once (measured faster than persistent grids at these batch
@@ -959,56 +1064,52 @@ int launch_groups(K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
     return 0;
   if (blocks > 0x7fffffffull)
     return -2;
+  t_last_kernel = name;
   hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#ifdef TASX_AB
 template <typename K, typename P>
-int launch(K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStream_t s)
+int launch(const char *name, K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStream_t s)
 {
   uint64_t blocks = ((uint64_t) p.n + groups_per_block - 1) / groups_per_block;
   if (blocks > (uint64_t) max_blocks)
     blocks = (uint64_t) max_blocks;
   if (blocks == 0)
     return 0;
+  t_last_kernel = name;
   hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif
 
 } // namespace
 
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
 
-// LDS reservations (residency caps) as A/B knobs, KiB in the environment
+extern "C" const char *tasx_last_kernel(void)
+{
+  return t_last_kernel;
+}
+
+extern "C" void tasx_note_kernel(const char *name)
+{
+  t_last_kernel = name;
+}
+
+#ifdef TASX_AB
+// residency knobs (KiB of reserved LDS / waves per SIMD) for A/B runs
 static uint32_t env_lds(const char *name, uint32_t dflt)
 {
   const char *e = getenv(name);
   return e ? (uint32_t) atoi(e) * 1024u : dflt;
 }
-// tcp4_wave_kernel: TASX_WAVE_TCP4_LDS, default none
-static uint32_t tasx_wave_lds_tcp4()
-{
-  static const uint32_t v = env_lds("TASX_WAVE_TCP4_LDS", 0u);
-  return v;
-}
-// tcp4_tas14_kernel without a uniform hint (TX): register budget (waves per
-// SIMD) as an A/B knob, TASX_TAS14_WPE, default 8
-static int tas14_nohint_wpe()
-{
-  static const int v = getenv("TASX_TAS14_WPE") ? atoi(getenv("TASX_TAS14_WPE")) : 8;
-  return v;
-}
-// tcp4_tas14_kernel without a uniform hint (TX): TASX_TAS14_NOHINT_LDS, default
-// none.  The batches this path sees mix lengths (per-frame hints or none) and
-// ACK-heavy ones are latency-bound, so the 6 waves/SIMD its 74 VGPRs allow pay
-// (64K frames at 50 / 75 % ACKs: 11.8 -> 11.25, 10.1 -> 9.3 us) where the
-// uniform batch loses 0.7 % (16.88 -> 17.0 us; profiles/r01_ackmix_lds_ab.txt)
-static uint32_t tas14_nohint_lds()
-{
-  static const uint32_t v = env_lds("TASX_TAS14_NOHINT_LDS", 0u);
-  return v;
-}
+#define TASX_LDS(name, dflt) env_lds(name, dflt)
+#else
+#define TASX_LDS(name, dflt) (dflt)
+#endif
 
 // tcp4_tas_kernel preconditions: TAS layout, 16-byte aligned base, stride mode,
 // every frame within 4 GiB of the base (32-bit offsets)
@@ -1018,44 +1119,58 @@ static bool tas_kernel_ok(const tasx_tcp4_params &p)
          (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
 }
 
-// tcp4_tas14_kernel without a hint: IPv4 header at 14 mod 16 in every frame.
-// Per-frame hints are ignored here (hints only steer reads): each row reads its
-// own total_length first, which on data/ACK mixes beats tcp4_tas_kernel's
-// hint-first rows at every ACK fraction (64K frames, 0 / 25 / 50 / 75 % ACKs:
-// 17.0 / 14.1 / 11.9 / 10.2 us against 17.5 / 15.2 / 14.0 / 12.8 us;
-// profiles/r01_ackmix_nohint.jsonl)
-static bool tas14_nohint_ok(const tasx_tcp4_params &p)
+// tcp4_tas14_kernel in stride mode: in addition the IPv4 header at 14 mod 16
+// in every frame (a 16-byte multiple stride)
+static bool tas14_stride_ok(const tasx_tcp4_params &p)
 {
-  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0 && !p.flen0;
+  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0;
 }
 
-// tcp4_tas14_kernel<OFFS> (no uniform hint, offsets array): TCP right after a
-// 20-byte IPv4 header at 14 mod 16 from the frame start; frames whose start is
-// not 16-byte aligned are checked per row and go to the general body
-static bool tas14_offs_ok(const tasx_tcp4_params &p)
-{
-  return p.off != nullptr && p.l4_off == p.ip_off + 20 && (p.ip_off & 15u) == 14u && !p.flen0;
-}
-
-// tcp4_tas14_kernel, in addition: IPv4 header at 14 mod 16 in every frame, a
-// uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
+// ... with one uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
 static bool tas14_ok(const tasx_tcp4_params &p)
 {
-  if (!tas_kernel_ok(p) || (p.ip_off & 15u) != 14u || (p.stride & 15u) != 0 || p.flen || !p.flen0)
+  if (!tas14_stride_ok(p) || p.flen || !p.flen0)
     return false;
   if (p.flen0 < p.ip_off + 64u || p.flen0 - p.ip_off > 65535u)
     return false;
   return ((14u + (p.flen0 - p.ip_off) + 15u) >> 4) <= 16u * 6u;
 }
 
+// ... without a uniform hint (per-frame hints only steer reads: each row reads
+// its own total_length), stride mode or frames by an offsets array (IPv4 at 14
+// mod 16 from the frame start; frames not 16-byte aligned are checked per row)
+static bool tas14_nohint_ok(const tasx_tcp4_params &p)
+{
+  return tas14_stride_ok(p) && !p.flen0;
+}
+static bool tas14_offs_ok(const tasx_tcp4_params &p)
+{
+  return p.off != nullptr && p.l4_off == p.ip_off + 20 && (p.ip_off & 15u) == 14u && !p.flen0;
+}
+
+// Row mode without a uniform hint, from the room (bytes readable from each
+// frame's start).  A room covering a full-MTU frame lets rows of a batch that
+// carries no per-frame lengths load the whole MTU at once (bulk TX batches);
+// with per-frame hints (data/ACK mixes) whole-room reads would cost the ACK
+// rows 1.5 KB each, so only an ACK's 80 bytes go out with the total_length.
+static int tas14_mode(const tasx_tcp4_params &p)
+{
+  const uint32_t from_a0 = p.room > (p.ip_off & ~15u) ? p.room - (p.ip_off & ~15u) : 0u;
+  if (!p.flen && from_a0 >= 1536u)
+    return kRoom;
+  return from_a0 >= 80u ? kHead5 : kTlFirst;
+}
+
 // completion word: stream-ordered after the work before it, one lane stores
 // seq into pinned host memory with system-scope release, so a host spinning on
 // the word sees every earlier result (tasx_flush's wait, tasx_host.c)
+namespace {
 __global__ __launch_bounds__(64) void post_done_kernel(uint32_t *word, uint32_t seq)
 {
   if (threadIdx.x == 0)
     __hip_atomic_store(word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+} // namespace
 
 extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
 {
@@ -1066,101 +1181,121 @@ extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  if (variant == 8) // TCP4-only variant
-    variant = 0;
   switch (variant) {
-  case 2:
-  case 3:
-  case 4:
-  case 5:
-    return launch_groups(raw_group_kernel<6>, *p, s);
+#ifdef TASX_AB
   case 1:
-    return launch(raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+    return launch("raw_cksum_kernel", raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
+  case 2:
+    return launch_groups("raw_group_kernel", raw_group_kernel<6>, *p, s);
+#else
+  case 2: // the general form
+    return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
+#endif
   case 7:
-    return launch_groups(raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
+    return launch_groups("raw_wave_kernel", raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
   case 0:
+  case 3:
   case 6:
     if (variant == 0 && p->len)
-      return launch_groups(raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
+      return launch_groups("raw_wave_kernel", raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
     if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
         (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32))
-      return launch_groups(raw_sad_kernel<6, true>, *p, s, kOccLds);
-    return launch_groups(raw_sad_kernel<6>, *p, s, kOccLds);
-  default:
-    return -2;
+      return launch_groups("raw_sad_kernel<s32>", raw_sad_kernel<6, true>, *p, s, kOccLds);
+    return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
+  default: // TCP4-only variants run the automatic RAW kernel
+    return tasx_launch_raw(p, 0, stream);
   }
 }
 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
-  if (variant == 7 || variant == 8) // RAW-only / TX-only variants
-    variant = 0;
-  if ((variant == 0 || variant == 6) && tas14_ok(*p))
-    return launch_groups(tcp4_tas14_kernel<6, true>, *p, (hipStream_t) stream, kOccLds);
-  if ((variant == 0 || variant == 6) && tas14_nohint_ok(*p)) {
+  hipStream_t s = (hipStream_t) stream;
+  const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
+  if (auto6 && tas14_ok(*p))
+    return launch_groups("tcp4_tas14_kernel<hint,verify>", tcp4_tas14_kernel<6, kHint, true>, *p, s,
+                         TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
+  if (auto6 && tas14_nohint_ok(*p))
     // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
     // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
     // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt)
-    static const uint32_t lds = env_lds("TASX_TAS14_VERIFY_LDS", 0u);
-    if (tas14_nohint_wpe() == 6)
-      return launch_groups(tcp4_tas14_kernel<6, true, true>, *p, (hipStream_t) stream, lds);
-    return launch_groups(tcp4_tas14_kernel<6, true, true, 8>, *p, (hipStream_t) stream, lds);
+    return launch_groups("tcp4_tas14_kernel<tl_first,verify>", tcp4_tas14_kernel<6, kTlFirst, true, 8>, *p, s,
+                         TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
+  return launch_groups("tcp4_frame_kernel<verify>", tcp4_frame_kernel<6, true>, *p, s);
+}
+
+// tcp4_tas14_kernel without a uniform hint, in the mode the room allows (or
+// the one an A/B variant forces).  Built for 8 waves per SIMD (64 VGPRs; the
+// spills are confined to the general-body fallback after the fast path's
+// stores): data/ACK mixes are latency-bound and gain from the residency (64K
+// frames at 50 / 75 / 100 % ACKs: 11.2 / 9.3-9.9 / 7.38 -> 10.8 / 8.6 / 6.97
+// us; uniform MTU 17.05 -> 17.0; profiles/r01_ackmix_wpe_ab.txt).
+template <bool OFFS>
+static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
+{
+  const uint32_t lds = TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u);
+  switch (mode) {
+  case kRoom:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<room,offs>" : "tcp4_tas14_kernel<room>",
+                         tcp4_tas14_kernel<6, kRoom, false, 8, OFFS>, p, s, lds);
+  case kHead5:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<head5,offs>" : "tcp4_tas14_kernel<head5>",
+                         tcp4_tas14_kernel<6, kHead5, false, 8, OFFS>, p, s, lds);
+  default:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,offs>" : "tcp4_tas14_kernel<tl_first>",
+                         tcp4_tas14_kernel<6, kTlFirst, false, 8, OFFS>, p, s, lds);
   }
-  return launch_groups(tcp4_frame_kernel<6, true>, *p, (hipStream_t) stream);
 }
 
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  const bool tas_ok = tas_kernel_ok(*p);
+  int mode = tas14_mode(*p);
   if (variant == 7) // RAW-only variant
     variant = 0;
-  if (variant == 6 && !tas14_ok(*p) && !tas14_nohint_ok(*p) && !tas14_offs_ok(*p)) // headline kernel not applicable
+#ifdef TASX_AB
+  // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
+  // where its room requirement holds (else as 0)
+  if (variant >= 9 && variant <= 11) {
+    const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
+    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : kRoom;
+    if ((m == kTlFirst) || (m == kHead5 && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
+      mode = m;
     variant = 0;
-  if ((variant == 0 || variant == 6) && tas14_offs_ok(*p)) {
-    // frames by offsets (the INTEGRATION.md section 5 call, the flush paths): as
-    // tas14_nohint_ok below, one extra descriptor load per row
-    if (tas14_nohint_wpe() == 6)
-      return launch_groups(tcp4_tas14_kernel<6, false, true, 1, true>, *p, s, tas14_nohint_lds());
-    return launch_groups(tcp4_tas14_kernel<6, false, true, 8, true>, *p, s, tas14_nohint_lds());
   }
-  if (variant == 8 && p->l4_off != p->ip_off + 20u) // tcp4_wave_kernel needs TCP right after a 20-byte IPv4 header
-    variant = 0;
-  if (variant == 0) // TAS frames in 16-byte rooms: uniform hint, per-frame hints or none -> tcp4_tas14_kernel;
-                    // other TAS-layout batches with a hint -> 3
-    variant = (tas14_ok(*p) || tas14_nohint_ok(*p)) ? 6 : (tas_ok && (p->flen || p->flen0)) ? 3 : 2;
-  if (variant == 8)
-    return launch_groups(tcp4_wave_kernel<TASX_WAVE_U>, *p, s, tasx_wave_lds_tcp4());
-  if (variant >= 3 && !tas_ok)
-    variant = 2;
+  if (variant == 8 && p->l4_off == p->ip_off + 20u) {
+    static const uint32_t lds = env_lds("TASX_WAVE_TCP4_LDS", 0u);
+    return launch_groups("tcp4_wave_kernel", tcp4_wave_kernel<TASX_WAVE_U>, *p, s, lds);
+  }
   switch (variant) {
   case 1:
-    return launch(tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
-  case 2:
-    return launch_groups(tcp4_frame_kernel<6>, *p, s);
-  case 3:
-    return launch_groups(tcp4_tas_kernel<6>, *p, s);
+    return launch("tcp4_cksum_kernel", tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
   case 4:
-    return p->diag ? launch_groups(tcp4_tas_kernel<6, 1>, *p, s) : -2;
+    return p->diag && tas_kernel_ok(*p) ? launch_groups("tcp4_tas_kernel<diag>", tcp4_tas_kernel<6, 1>, *p, s)
+                                         : -2;
   case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
-    return launch_groups<32>(tcp4_tas_kernel<3, 0, 32>, *p, s);
-  case 6:
-    if (tas14_ok(*p))
-      return launch_groups(tcp4_tas14_kernel<6>, *p, s, kOccLds);
-    // built for 8 waves per SIMD (64 VGPRs; the spills are confined to the
-    // general-body fallback after the fast path's stores): ACK-heavy mixes are
-    // latency-bound and gain from the residency (64K frames at 50 / 75 / 100 %
-    // ACKs: 11.2 / 9.3-9.9 / 7.38 -> 10.8 / 8.6 / 6.97 us; uniform MTU 17.05 ->
-    // 17.0; profiles/r01_ackmix_wpe_ab.txt).  TASX_TAS14_WPE=6 or 7 for A/B.
-    switch (tas14_nohint_wpe()) {
-    case 6:
-      return launch_groups(tcp4_tas14_kernel<6, false, true>, *p, s, tas14_nohint_lds());
-    case 7:
-      return launch_groups(tcp4_tas14_kernel<6, false, true, 7>, *p, s, tas14_nohint_lds());
-    default:
-      return launch_groups(tcp4_tas14_kernel<6, false, true, 8>, *p, s, tas14_nohint_lds());
-    }
+    if (tas_kernel_ok(*p))
+      return launch_groups<32>("tcp4_tas_kernel<g32>", tcp4_tas_kernel<3, 0, 32>, *p, s);
+    break;
   default:
-    return -2;
+    break;
   }
+  if (variant == 1 || variant >= 4)
+    variant = 0;
+#endif
+  if (variant == 0 || variant == 6) {
+    // TAS frames in 16-byte rooms: a uniform hint, per-frame hints or none ->
+    // tcp4_tas14_kernel; frames by offsets -> its OFFS form
+    if (tas14_ok(*p))
+      return launch_groups("tcp4_tas14_kernel<hint>", tcp4_tas14_kernel<6, kHint>, *p, s,
+                           TASX_LDS("TASX_TAS14_HINT_LDS", kOccLds));
+    if (tas14_nohint_ok(*p))
+      return launch_tas14_rows<false>(*p, mode, s);
+    if (tas14_offs_ok(*p))
+      return launch_tas14_rows<true>(*p, mode, s);
+    // other TAS-layout batches with a hint -> 3, the rest -> 2
+    variant = tas_kernel_ok(*p) && (p->flen || p->flen0) ? 3 : 2;
+  }
+  if (variant == 3 && tas_kernel_ok(*p))
+    return launch_groups("tcp4_tas_kernel", tcp4_tas_kernel<6>, *p, s);
+  return launch_groups("tcp4_frame_kernel", tcp4_frame_kernel<6>, *p, s);
 }

@@ -24,9 +24,13 @@ from pathlib import Path
 
 import torch  # noqa: F401  -- must be imported first: libtasx then binds torch's HIP runtime
 
-# TASX_LIB: another in-tree build of the library (A/B of kernel revisions, tools/ab_lib.sh)
-_LIB_PATH = Path(os.environ.get("TASX_LIB") or Path(__file__).resolve().parent / "_lib" / "libtasx.so")
+_LIB_DIR = Path(__file__).resolve().parent / "_lib"
+# TASX_LIB: another in-tree build of the library (the A/B build
+# tas_amd/_lib/libtasx_ab.so, or a kernel revision from tools/ab_lib.sh)
+_LIB_PATH = Path(os.environ.get("TASX_LIB") or _LIB_DIR / "libtasx.so")
+AB_LIB_PATH = _LIB_DIR / "libtasx_ab.so"
 _lib = None
+_loaded: dict = {}
 
 TASX_F_INPLACE = 0x1
 TAS_IP_OFF = 14
@@ -46,7 +50,11 @@ SIGNATURES = {
     "tasx_tcp4_cksum_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp]),
     "tasx_tcp4_cksum_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                 _c_u32, _vp]),
+    "tasx_tcp4_cksum_batch_dev_room": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _c_u32,
+                                                _vp, _c_u32, _vp]),
     "tasx_tcp4_verify_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
+    "tasx_tcp4_verify_batch_dev_room": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _c_u32,
+                                                 _vp, _vp]),
     "tasx_tcp4_verify_batch_dev_hint": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _vp,
                                                  _vp]),
     "tasx_flow_lookup_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32,
@@ -64,7 +72,7 @@ SIGNATURES = {
     "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
     "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
-    "tasx_set_diag_buffer": (_c_int, [_vp]),
+    "tasx_last_kernel": (ctypes.c_char_p, []),
     "tasx_host_alloc": (_vp, [_sz]),
     "tasx_host_free": (_c_int, [_vp]),
     "tasx_host_register": (_c_int, [_vp, _sz]),
@@ -75,6 +83,12 @@ SIGNATURES = {
     "tasx_memcpy_h2d": (_c_int, [_vp, _vp, _sz]),
     "tasx_memcpy_d2h": (_c_int, [_vp, _vp, _sz]),
     "tasx_stream_sync": (_c_int, [_vp]),
+}
+
+
+# A/B build only (include/tasx_ab.h)
+AB_SIGNATURES = {
+    "tasx_set_diag_buffer": (_c_int, [_vp]),
 }
 
 
@@ -89,20 +103,60 @@ def library_path() -> Path:
     return _LIB_PATH
 
 
+def _load(path: Path) -> ctypes.CDLL:
+    path = Path(path)
+    if path in _loaded:
+        return _loaded[path]
+    if not path.exists():
+        raise RuntimeError(
+            f"{path.name} not built ({path}); run python -c 'import __graft_entry__ as g; g.build()'")
+    L = ctypes.CDLL(str(path), mode=os.RTLD_NOW | ctypes.RTLD_LOCAL)
+    for name, (res, args) in {**SIGNATURES, **AB_SIGNATURES}.items():
+        fn = getattr(L, name, None)
+        if fn is None:
+            if name in SIGNATURES:
+                raise RuntimeError(f"{path} does not export {name}")
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    _loaded[path] = L
+    return L
+
+
 def lib() -> ctypes.CDLL:
     """Load libtasx.so (built in-tree by tas_amd.build / __graft_entry__.build)."""
     global _lib
     if _lib is None:
-        if not _LIB_PATH.exists():
-            raise RuntimeError(
-                f"libtasx.so not built ({_LIB_PATH}); run python -c 'import __graft_entry__ as g; g.build()'")
-        L = ctypes.CDLL(str(_LIB_PATH), mode=os.RTLD_NOW | ctypes.RTLD_GLOBAL)
-        for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.restype = res
-            fn.argtypes = args
-        _lib = L
+        _lib = _load(_LIB_PATH)
     return _lib
+
+
+class using_library:
+    """Route this module's calls through another build of the library for the
+    duration of a with-block (the A/B build for variant tests:
+    ``with xsum.using_library(xsum.AB_LIB_PATH): ...``).  Both builds are
+    linked -Bsymbolic and loaded RTLD_LOCAL, so they coexist in one process."""
+
+    def __init__(self, path):
+        self.path = Path(path)
+
+    def __enter__(self):
+        global _lib
+        lib()
+        self.prev = _lib
+        _lib = _load(self.path)
+        return _lib
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.prev
+        return False
+
+
+def last_kernel() -> str:
+    """Name of the kernel this thread's last batch call launched."""
+    s = lib().tasx_last_kernel()
+    return s.decode() if s else ""
 
 
 def last_error() -> str:
@@ -158,30 +212,41 @@ def tcp4_cksum_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | No
                      stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
                      out: torch.Tensor | None = None, inplace: bool = False,
                      want_out: bool = True, frame_len: torch.Tensor | int | None = None,
-                     stream=None) -> torch.Tensor | None:
+                     room: int = 0, stream=None) -> torch.Tensor | None:
     """tcp_checksums() flag-off branch for n frames on the GPU.  Returns an int16
     tensor of 2n values: [ip.chksum, tcp.chksum] per frame (uint16 bit patterns).
     frame_len: optional frame-length hints (int32 tensor, or one int for all
-    frames) -- prefetch only, results never depend on it."""
+    frames) -- prefetch only, results never depend on it.  room: bytes from
+    each frame's start that may be read (the mbuf data room; 0 = unknown)."""
     if out is None and want_out:
         out = torch.empty(2 * n, dtype=torch.int16, device=frames.device)
     if offsets is not None:
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
     flags = TASX_F_INPLACE if inplace else 0
-    if frame_len is None:
+    if frame_len is None and not room:
         _check(lib().tasx_tcp4_cksum_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
                                                _ptr(out), flags, _stream(stream)),
                "tasx_tcp4_cksum_batch_dev")
     else:
-        if isinstance(frame_len, int):
-            flen, flen0 = None, frame_len
+        flen, flen0 = _hints(frame_len, n)
+        if room:
+            _check(lib().tasx_tcp4_cksum_batch_dev_room(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
+                                                        room, n, ip_off, l4_off, _ptr(out), flags,
+                                                        _stream(stream)), "tasx_tcp4_cksum_batch_dev_room")
         else:
-            assert frame_len.dtype == torch.int32 and frame_len.numel() >= n
-            flen, flen0 = frame_len, 0
-        _check(lib().tasx_tcp4_cksum_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
-                                                    n, ip_off, l4_off, _ptr(out), flags, _stream(stream)),
-               "tasx_tcp4_cksum_batch_dev_hint")
+            _check(lib().tasx_tcp4_cksum_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
+                                                        n, ip_off, l4_off, _ptr(out), flags, _stream(stream)),
+                   "tasx_tcp4_cksum_batch_dev_hint")
     return out
+
+
+def _hints(frame_len, n):
+    if frame_len is None:
+        return None, 0
+    if isinstance(frame_len, int):
+        return None, frame_len
+    assert frame_len.dtype == torch.int32 and frame_len.numel() >= n
+    return frame_len, 0
 
 
 RX_IP_OK, RX_L4_OK, RX_IHL_NOT5 = 0x1, 0x2, 0x4
@@ -190,26 +255,23 @@ RX_IP_OK, RX_L4_OK, RX_IHL_NOT5 = 0x1, 0x2, 0x4
 def tcp4_verify_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None,
                       stride: int = 0, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
                       out: torch.Tensor | None = None, frame_len: torch.Tensor | int | None = None,
-                      stream=None) -> torch.Tensor:
+                      room: int = 0, stream=None) -> torch.Tensor:
     """Receive-side checksum verification of n frames: uint8 flags per frame
     (RX_IP_OK | RX_L4_OK | RX_IHL_NOT5).  frame_len: optional received frame
-    lengths (int32 tensor, or one int for all frames) -- prefetch only."""
+    lengths (int32 tensor, or one int for all frames): the read bound and a
+    prefetch hint.  room: the read bound of frames without a length."""
     if out is None:
         out = torch.empty(n, dtype=torch.uint8, device=frames.device)
     if offsets is not None:
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
-    if frame_len is None:
+    if frame_len is None and not room:
         _check(lib().tasx_tcp4_verify_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off,
                                                 _ptr(out), _stream(stream)), "tasx_tcp4_verify_batch_dev")
     else:
-        if isinstance(frame_len, int):
-            flen, flen0 = None, frame_len
-        else:
-            assert frame_len.dtype == torch.int32 and frame_len.numel() >= n
-            flen, flen0 = frame_len, 0
-        _check(lib().tasx_tcp4_verify_batch_dev_hint(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0, n,
-                                                     ip_off, l4_off, _ptr(out), _stream(stream)),
-               "tasx_tcp4_verify_batch_dev_hint")
+        flen, flen0 = _hints(frame_len, n)
+        _check(lib().tasx_tcp4_verify_batch_dev_room(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0,
+                                                     room, n, ip_off, l4_off, _ptr(out), _stream(stream)),
+               "tasx_tcp4_verify_batch_dev_room")
     return out
 
 

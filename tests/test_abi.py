@@ -12,10 +12,11 @@ import pytest
 from conftest import ROOT
 
 HEADER = ROOT / "include" / "tasx_xsum.h"
+AB_HEADER = ROOT / "include" / "tasx_ab.h"
 
 
-def header_functions():
-    text = HEADER.read_text()
+def header_functions(header=HEADER):
+    text = header.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"^[A-Za-z_][\w \t\*]*?\b(tasx_\w+)\s*\(", text, flags=re.M)))
 
@@ -70,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 1
+    assert L.tasx_abi_version() == 2
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -98,3 +99,55 @@ def test_python_wrapper_raises(L):
         xsum.defer_tcp4(2, 4096)
     with pytest.raises(xsum.TasxError):
         xsum.tx_flush(2)
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True,
+                         text=True, check=True).stdout
+    return set(re.findall(r"\bT (\w+)", out))
+
+
+def test_product_exports_only_the_header(libpath):
+    """libtasx.so exports exactly tasx_xsum.h: no internal launchers, no A/B
+    entry points, no kernel stubs."""
+    assert _exports(libpath) == set(header_functions())
+
+
+def test_ab_build_exports_the_ab_header(libpath):
+    from tas_amd import build
+    ab = _exports(build.LIB_AB)
+    assert set(header_functions()) <= ab
+    assert set(header_functions(AB_HEADER)) <= ab
+    assert not set(header_functions(AB_HEADER)) & _exports(libpath)
+
+
+def test_product_rejects_ab_variants(L):
+    for v in (1, 4, 5, 8, 9, 10, 11, 12, -1):
+        assert L.tasx_set_kernel_variant(v) == -errno.EINVAL, v
+    for v in (0, 2, 3, 6, 7):
+        assert L.tasx_set_kernel_variant(v) == 0
+    assert L.tasx_set_kernel_variant(0) == 0
+    assert L.tasx_last_kernel() == b""
+
+
+def test_room_contract_errors(L):
+    # a room must hold the headers and stay inside a stride-mode frame's slot
+    rc = L.tasx_tcp4_cksum_batch_dev_room(ctypes.c_void_p(4096), None, 2048, None, 0, 40, 4, 14, 34,
+                                          ctypes.c_void_p(4096), 0, None)
+    assert rc == -errno.EINVAL and b"room" in L.tasx_last_error()
+    rc = L.tasx_tcp4_cksum_batch_dev_room(ctypes.c_void_p(4096), None, 2048, None, 0, 4096, 4, 14, 34,
+                                          ctypes.c_void_p(4096), 0, None)
+    assert rc == -errno.EINVAL and b"stride" in L.tasx_last_error()
+    rc = L.tasx_tcp4_verify_batch_dev_room(ctypes.c_void_p(4096), None, 2048, None, 0, 4096, 4, 14, 34,
+                                           ctypes.c_void_p(4096), None)
+    assert rc == -errno.EINVAL
+
+
+def test_both_builds_coexist_in_one_process(L):
+    """The A/B build loads next to the product (-Bsymbolic, RTLD_LOCAL): each
+    keeps its own variant range."""
+    from tas_amd import xsum
+    with xsum.using_library(xsum.AB_LIB_PATH) as ab:
+        assert ab.tasx_set_kernel_variant(8) == 0
+        assert ab.tasx_set_kernel_variant(0) == 0
+    assert L.tasx_set_kernel_variant(8) == -errno.EINVAL

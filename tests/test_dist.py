@@ -86,3 +86,41 @@ def test_bench_cli_defaults():
     assert a.gpus == 1 and a.workload == "tcp4" and a.steps > 0 and a.warmup >= 0
     a = bench.parse(["--gpus", "8", "--steps", "5", "--warmup", "1", "--workload", "shard8m"])
     assert (a.gpus, a.steps, a.warmup, a.workload) == (8, 5, 1, "shard8m")
+
+
+def _bench(*args, timeout=180):
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=str(ROOT))
+
+
+def test_bench_spawns_n_ranks_itself():
+    """`bench.py --gpus 2` with no launcher starts 2 rank processes of its own
+    (here with the GPU-free control self-test: gloo barrier, MAX / SUM /
+    gather over ranks); rank 0 prints the per-rank aggregate."""
+    import json
+    r = _bench("--gpus", "2", "--control-selftest")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["per_rank_value"] == [1.0, 2.0]
+    assert line["sum"] == 3.0 and line["max"] == 2.0 and line["ranks"] == ["cpu0", "cpu1"]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """Fewer visible GPUs than --gpus is an error (no silent rehearsal)."""
+    r = _bench("--gpus", "2", timeout=120)
+    assert r.returncode == 2
+    assert "needs 2 GPUs" in r.stderr and "--rehearse" in r.stderr
+
+
+def test_bench_world_size_must_match_gpus():
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--control-selftest"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

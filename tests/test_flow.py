@@ -109,11 +109,15 @@ def test_gpu_flow_golden(flow_golden, variant):
     from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
-    xsum.set_kernel_variant(variant)
-    try:
-        h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
-    finally:
-        xsum.set_kernel_variant(0)
+    import contextlib
+    # the CRC / key-load variants are A/B-build kernels (include/tasx_ab.h)
+    with (xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()):
+        xsum.set_kernel_variant(variant)
+        try:
+            h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
+            assert xsum.last_kernel().startswith("flow_lookup_kernel")
+        finally:
+            xsum.set_kernel_variant(0)
     np.testing.assert_array_equal(h, g["expected_hash"])
     np.testing.assert_array_equal(fid, g["expected_fid"])
 

@@ -5,6 +5,7 @@ short segments, total_length < 20, the 0 -> 0xffff rules, in-place stores).
 
 Run on the MI355X box:  python -m pytest tests -m gpu -x -q
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -24,6 +25,23 @@ def _lib():
     xsum.lib()
     yield
     torch.cuda.synchronize()
+
+
+# variants that exist only in the A/B build (include/tasx_ab.h)
+AB_VARIANTS = {1, 4, 5, 8, 9, 10, 11}
+
+
+@contextlib.contextmanager
+def kernel_variant(v: int):
+    """Run the block with kernel variant v selected -- through the A/B build
+    (tas_amd/_lib/libtasx_ab.so) for the variants only it carries."""
+    ctx = xsum.using_library(xsum.AB_LIB_PATH) if v in AB_VARIANTS else contextlib.nullcontext()
+    with ctx:
+        xsum.set_kernel_variant(v)
+        try:
+            yield
+        finally:
+            xsum.set_kernel_variant(0)
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
@@ -66,14 +84,11 @@ def test_kat_ipv4_header_public(oracle):
     frame[34:14 + 115] = np.arange(95, dtype=np.uint8) * 7
     exp = oracle.tcp4_batch(frame.copy(), 1, stride=2048)
     for v in (0, 1, 2, 3, 6):
-        xsum.set_kernel_variant(v)
-        try:
+        with kernel_variant(v):
             for hint in (None, 14 + 115):
                 got = u16(xsum.tcp4_cksum_batch(to_dev(frame), 1, stride=2048, frame_len=hint))
                 assert int(got[0]).to_bytes(2, "little").hex() == kat["ip_chksum_bytes"]
                 np.testing.assert_array_equal(got, exp)
-        finally:
-            xsum.set_kernel_variant(0)
 
 
 @pytest.mark.parametrize("shift", [0, 1, 2, 3, 15])
@@ -239,11 +254,8 @@ def test_raw_wave_descriptor_orders(oracle, n):
         offs[2::4] = np.sort(offs[2::4])[::-1]               # descending
     exp = oracle.raw_batch(h, n, offsets=offs, lengths=lens)
     for v in (0, 7):
-        xsum.set_kernel_variant(v)
-        try:
+        with kernel_variant(v):
             got = u16(xsum.raw_cksum_batch(d, n, offsets=to_dev(offs), lengths=to_dev(lens.astype(np.int32))))
-        finally:
-            xsum.set_kernel_variant(0)
         np.testing.assert_array_equal(got, exp, err_msg=f"variant {v}")
 
 
@@ -336,11 +348,8 @@ def test_tcp4_flush_mix_per_frame_hints(oracle, n, ack_frac, variant):
     8: tcp4_wave_kernel): data segments among pure ACKs (ip.len 52), ragged batch
     ends, a few hints that disagree with ip.total_length or do not cover ip + 40,
     in place and to the output array."""
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         _flush_mix(oracle, n, ack_frac)
-    finally:
-        xsum.set_kernel_variant(0)
 
 
 def _flush_mix(oracle, n, ack_frac):
@@ -375,11 +384,8 @@ def test_tcp4_wave_odd_offsets(oracle):
     exp = oracle.tcp4_batch(big, n, offsets=offs)
     hint = (14 + 52 + pay).astype(np.int32)
     for v in (0, 8):
-        xsum.set_kernel_variant(v)
-        try:
+        with kernel_variant(v):
             got = u16(xsum.tcp4_cksum_batch(to_dev(big), n, offsets=to_dev(offs), frame_len=to_dev(hint)))
-        finally:
-            xsum.set_kernel_variant(0)
         np.testing.assert_array_equal(got, exp, err_msg=f"variant {v}")
 
 
@@ -402,13 +408,10 @@ def test_tcp4_all_variants_and_hints(oracle, variant):
     d = to_dev(frames)
     exact = (14 + tl).astype(np.int32)
     noise = (pktgen.splitmix64(56, n) % np.uint64(4000)).astype(np.int32)
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         for hint in (None, 1514, 64, 2048, 0, to_dev(exact), to_dev(noise), to_dev(exact // 2)):
             got = u16(xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=hint))
             np.testing.assert_array_equal(got, exp, err_msg=f"variant {variant} hint {hint if isinstance(hint, (int, type(None))) else 'array'}")
-    finally:
-        xsum.set_kernel_variant(0)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 7, 8])
@@ -416,13 +419,10 @@ def test_raw_all_variants(oracle, variant):
     buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
     n = len(lens)
     exp = oracle.raw_batch(buf, n, offsets=offs, lengths=lens)
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         got = u16(xsum.raw_cksum_batch(to_dev(buf), n, offsets=to_dev(offs.astype(np.int64)),
                                        lengths=to_dev(lens.astype(np.int32))))
         np.testing.assert_array_equal(got, exp)
-    finally:
-        xsum.set_kernel_variant(0)
 
 
 @pytest.mark.parametrize("variant", [0, 5])
@@ -432,12 +432,9 @@ def test_tso_with_hints(oracle, variant):
                                 ip_total_len=np.where(np.arange(n) % 3 == 0, 65535, 30000))
     exp = oracle.tcp4_batch(frames.copy(), n, stride=stride)
     d = to_dev(frames)
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         for hint in (None, 65549, 1514, stride):
             np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride, frame_len=hint)), exp)
-    finally:
-        xsum.set_kernel_variant(0)
 
 
 @pytest.mark.parametrize("variant", [0, 6])
@@ -447,8 +444,7 @@ def test_tcp4_uniform_hint_every_size(oracle, variant):
     and the sizes around it, in place and to the result array; then the same
     hint over frames whose total_length disagrees with it (the general body
     redoes those groups)."""
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         for tl in list(range(40, 1540, 7)) + [63, 64, 65, 1500, 1521, 1522, 1523]:
             n = 48
             frames = pktgen.tcp4_frames(n, payload=0, stride=1536 + 64, seed=tl, ip_total_len=tl)
@@ -470,8 +466,6 @@ def test_tcp4_uniform_hint_every_size(oracle, variant):
         exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
         got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=2048, frame_len=1514))
         np.testing.assert_array_equal(got, exp)
-    finally:
-        xsum.set_kernel_variant(0)
 
 
 def test_deterministic_and_n0():
@@ -648,7 +642,7 @@ def test_verify_roundtrip_64k(oracle):
     h2 = h.copy()
     h2[sel * 2048 + pos[sel]] ^= (1 << bit[sel]).astype(np.uint8)
     got = xsum.tcp4_verify_batch(to_dev(h2), n, stride=2048).cpu().numpy()
-    exp = oracle.tcp4_verify_batch(h2, n, stride=2048)
+    exp = oracle.tcp4_verify_batch_bounded(h2, n, 2048, stride=2048)  # RX bound: the stride slot
     np.testing.assert_array_equal(got, exp)
     assert np.all(got[sel] != 3) and np.all(np.delete(got, sel) == 3)
 
@@ -666,7 +660,7 @@ def test_verify_edges(oracle, tcp4_golden, shift):
     buf = torch.zeros(mixed.size + 64, dtype=torch.uint8, device=DEV)
     buf[shift:shift + mixed.size] = to_dev(mixed)
     got = xsum.tcp4_verify_batch(buf[shift:], 2 * n, stride=stride).cpu().numpy()
-    np.testing.assert_array_equal(got, oracle.tcp4_verify_batch(mixed, 2 * n, stride=stride))
+    np.testing.assert_array_equal(got, oracle.tcp4_verify_batch_bounded(mixed, 2 * n, stride, stride=stride))
 
 
 @pytest.mark.parametrize("stride", [80, 128, 2048])
@@ -685,12 +679,12 @@ def test_tcp4_and_verify_short_frames_no_hint(oracle, stride):
     exp = oracle.tcp4_batch(big.copy(), n, stride=stride)
     d = to_dev(big)
     np.testing.assert_array_equal(u16(xsum.tcp4_cksum_batch(d, n, stride=stride)), exp)
-    vexp = oracle.tcp4_verify_batch(big.copy(), n, stride=stride)
+    vexp = oracle.tcp4_verify_batch_bounded(big.copy(), n, stride, stride=stride)  # RX reads stay in the slot
     np.testing.assert_array_equal(xsum.tcp4_verify_batch(d, n, stride=stride).cpu().numpy(), vexp)
     xsum.tcp4_cksum_batch(d, n, stride=stride, inplace=True, want_out=False)
     good = d.cpu().numpy()
     np.testing.assert_array_equal(xsum.tcp4_verify_batch(d, n, stride=stride).cpu().numpy(),
-                                  oracle.tcp4_verify_batch(good, n, stride=stride))
+                                  oracle.tcp4_verify_batch_bounded(good, n, stride, stride=stride))
 
 
 @pytest.mark.parametrize("hinted", [False, True])
@@ -741,8 +735,7 @@ def test_verify_uniform_hint(oracle, variant):
     kernel's verify mode): good frames, single-bit corruption anywhere in the
     datagram (checksum fields included), IHL 6, and total_length disagreeing
     with the hint (general body); then every datagram size it takes."""
-    xsum.set_kernel_variant(variant)
-    try:
+    with kernel_variant(variant):
         n = 8192
         frames = pktgen.tcp4_frames(n, payload=1448, stride=2048, seed=91)
         d = to_dev(frames)
@@ -758,7 +751,7 @@ def test_verify_uniform_hint(oracle, variant):
         f[2::13, 16:18] = [0x05, 0x00]              # total_length 1280 (hint disagrees)
         f[4::17, 24:26] ^= 0xFF                     # ip.chksum flipped
         f[5::19, 50:52] = 0                         # tcp.chksum zeroed
-        exp = oracle.tcp4_verify_batch(h, n, stride=2048)
+        exp = oracle.tcp4_verify_batch_bounded(h, n, 1514, stride=2048)  # the received length bounds reads
         got = xsum.tcp4_verify_batch(to_dev(h), n, stride=2048, frame_len=1514).cpu().numpy()
         np.testing.assert_array_equal(got, exp)
         for tl in list(range(40, 1540, 11)) + [64, 1500, 1522, 1523]:
@@ -766,8 +759,174 @@ def test_verify_uniform_hint(oracle, variant):
             fr = pktgen.tcp4_frames(m, payload=0, stride=1600, seed=tl, ip_total_len=tl)
             oracle.tcp4_batch(fr, m, stride=1600, inplace=True)
             fr.reshape(m, 1600)[::4, 40] ^= 0x10        # corrupt a quarter (a tcp header byte)
-            exp = oracle.tcp4_verify_batch(fr, m, stride=1600)
+            exp = oracle.tcp4_verify_batch_bounded(fr, m, 14 + tl, stride=1600)
             got = xsum.tcp4_verify_batch(to_dev(fr), m, stride=1600, frame_len=14 + tl).cpu().numpy()
             np.testing.assert_array_equal(got, exp, err_msg=f"ip.len {tl}")
-    finally:
-        xsum.set_kernel_variant(0)
+
+
+# ---------------------------------------------------------------------------
+# rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
+
+@pytest.mark.parametrize("room", [80, 1536, 2048])
+@pytest.mark.parametrize("variant", [0, 9, 10, 11])
+def test_tcp4_rooms_every_row_mode(oracle, room, variant):
+    """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
+    selection and every forced row mode (9 total_length first, 10 head-5, 11
+    whole room) over data segments, ACKs, total_length 0..90 and 1523..2034
+    (rows the fast path hands to the general body), with no hint, per-frame
+    hints (exact, short, long) and a uniform hint; out of place and in place."""
+    n = 5000
+    rng = np.random.default_rng(room + variant)
+    pay = np.where(rng.random(n) < 0.4, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=room)
+    tl = 52 + pay
+    tl[::11] = np.arange(len(tl[::11])) % 91
+    tl[5::97] = 1523 + np.arange(len(tl[5::97])) % 500
+    f = frames.reshape(n, 2048)
+    f[:, 16] = (tl >> 8) & 0xFF
+    f[:, 17] = tl & 0xFF
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=2048)
+    exact = (14 + tl).astype(np.int32)
+    noise = (14 + tl + rng.integers(-30, 30, n)).clip(0, 2048).astype(np.int32)
+    with kernel_variant(variant):
+        for hint in (None, to_dev(exact), to_dev(noise), 1514):
+            d = to_dev(frames)
+            got = u16(xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=hint, room=room))
+            tag = f"room {room} variant {variant} hint {'array' if isinstance(hint, torch.Tensor) else hint}"
+            np.testing.assert_array_equal(got, exp, err_msg=tag)
+            xsum.tcp4_cksum_batch(d, n, stride=2048, frame_len=hint, room=room, inplace=True, want_out=False)
+            h = d.cpu().numpy().reshape(n, 2048)
+            np.testing.assert_array_equal(h[:, 24:26].copy().view(np.uint16).ravel(), exp[0::2], err_msg=tag)
+            np.testing.assert_array_equal(h[:, 50:52].copy().view(np.uint16).ravel(), exp[1::2], err_msg=tag)
+
+
+def test_tcp4_room_selects_row_mode():
+    """Which tcp4_tas14_kernel mode a call takes (tasx_last_kernel): a full-MTU
+    room and no per-frame hints -> whole-room rows; per-frame hints with a room
+    of 80 B or more -> head-5 rows; no room -> total_length first; a uniform
+    hint -> the hinted kernel; an offsets array -> the OFFS forms."""
+    n = 64
+    frames = to_dev(pktgen.tcp4_frames(n, stride=2048))
+    flen = to_dev(np.full(n, 1514, np.int32))
+    offs = to_dev(np.arange(n, dtype=np.int64) * 2048)
+    cases = [
+        (dict(stride=2048), "tcp4_tas14_kernel<tl_first>"),
+        (dict(stride=2048, room=2048), "tcp4_tas14_kernel<room>"),
+        (dict(stride=2048, room=1536), "tcp4_tas14_kernel<room>"),
+        (dict(stride=2048, room=1535), "tcp4_tas14_kernel<head5>"),
+        (dict(stride=2048, room=79), "tcp4_tas14_kernel<tl_first>"),
+        (dict(stride=2048, room=2048, frame_len=flen), "tcp4_tas14_kernel<head5>"),
+        (dict(stride=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first>"),
+        (dict(stride=2048, room=2048, frame_len=1514), "tcp4_tas14_kernel<hint>"),
+        (dict(offsets=offs, room=2048), "tcp4_tas14_kernel<room,offs>"),
+        (dict(offsets=offs, room=2048, frame_len=flen), "tcp4_tas14_kernel<head5,offs>"),
+        (dict(offsets=offs), "tcp4_tas14_kernel<tl_first,offs>"),
+        (dict(stride=2048, ip_off=14, l4_off=38), "tcp4_frame_kernel"),
+    ]
+    for kw, name in cases:
+        xsum.tcp4_cksum_batch(frames, n, **kw)
+        assert xsum.last_kernel() == name, (kw, xsum.last_kernel())
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("ip_off", [14, 30])
+@pytest.mark.parametrize("absolute", [False, True])
+@pytest.mark.parametrize("room", [0, 80, 2048])
+def test_tcp4_offsets_rooms_ipoff_absolute(oracle, ip_off, absolute, room):
+    """Frames by an offsets array (tcp4_tas14_kernel<OFFS>) with the IPv4 header
+    at 14 and at 30 (an (ip_off & ~15) term in the frame start), offsets from a
+    base or absolute device addresses (base NULL), some frames misaligned, with
+    and without a room, per-frame hints."""
+    n = 3000
+    rng = np.random.default_rng(ip_off * 7 + room + int(absolute))
+    pay = np.where(rng.random(n) < 0.5, 0, rng.integers(1, 1400, n)).astype(np.int64)
+    raw = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=ip_off).reshape(n, 2048)
+    frames = np.zeros((n, 2048 + 16), np.uint8)
+    frames[:, ip_off - 14:ip_off - 14 + 2048] = raw     # shift: IPv4 header at ip_off
+    perm = rng.permutation(n)
+    big = np.zeros((n + 2) * 2080, np.uint8)
+    offs = perm.astype(np.int64) * 2080
+    offs[::19] += (np.arange(len(offs[::19])) % 15) + 1       # misaligned frames
+    for i in range(n):
+        big[offs[i]:offs[i] + 2064] = frames[i]
+    exp = oracle.tcp4_batch(big.copy(), n, offsets=offs, ip_off=ip_off, l4_off=ip_off + 20)
+    d = to_dev(big)
+    hint = to_dev((ip_off + 52 + pay).astype(np.int32))
+    if absolute:
+        base, o = None, to_dev(offs + d.data_ptr())
+    else:
+        base, o = d, to_dev(offs)
+    out = torch.empty(2 * n, dtype=torch.int16, device=DEV)
+    rc = xsum.lib().tasx_tcp4_cksum_batch_dev_room(None if base is None else base.data_ptr(), o.data_ptr(), 0,
+                                                   hint.data_ptr(), 0, room, n, ip_off, ip_off + 20,
+                                                   out.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, xsum.last_error()
+    assert xsum.last_kernel().startswith("tcp4_tas14_kernel")
+    np.testing.assert_array_equal(u16(out), exp)
+    rc = xsum.lib().tasx_tcp4_cksum_batch_dev_room(None if base is None else base.data_ptr(), o.data_ptr(), 0,
+                                                   hint.data_ptr(), 0, room, n, ip_off, ip_off + 20,
+                                                   None, xsum.TASX_F_INPLACE, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    got = d.cpu().numpy()
+    ipc = np.array([int(got[x + ip_off + 10]) | (int(got[x + ip_off + 11]) << 8) for x in offs], np.uint16)
+    tcpc = np.array([int(got[x + ip_off + 36]) | (int(got[x + ip_off + 37]) << 8) for x in offs], np.uint16)
+    np.testing.assert_array_equal(ipc, exp[0::2])
+    np.testing.assert_array_equal(tcpc, exp[1::2])
+
+
+def test_tcp4_room_tso_rows(oracle):
+    """Whole-room rows over TSO-sized frames (ip.len 1523..65535 in 65,552 B
+    rooms): every row goes to the general body, results still exact."""
+    n, stride = 256, 65552
+    tl = np.where(np.arange(n) % 2 == 0, 65535, 1523 + np.arange(n) * 17)
+    frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=59, ip_total_len=tl)
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=stride)
+    got = u16(xsum.tcp4_cksum_batch(to_dev(frames), n, stride=stride, room=stride))
+    assert xsum.last_kernel() == "tcp4_tas14_kernel<room>"
+    np.testing.assert_array_equal(got, exp)
+
+
+# ---------------------------------------------------------------------------
+# RX: received frames are untrusted (ADVICE r1: forged total_length)
+
+@pytest.mark.parametrize("form", ["flen", "flen0", "stride", "room_offs"])
+def test_verify_forged_total_length_bounded(oracle, form):
+    """Short received frames whose total_length claims far more than arrived
+    (up to 65535), packed at the END of their allocation: reads stay inside
+    each frame's bound (received length, uniform length, stride slot, room) and
+    L4 fails for them; honest frames still verify.  Bit-exact against the
+    bounded oracle."""
+    n, stride = 4096, 128
+    rng = np.random.default_rng(len(form))
+    frames = pktgen.tcp4_frames(n, payload=rng.integers(0, 60, n), stride=stride, seed=71)
+    oracle.tcp4_batch(frames, n, stride=stride, inplace=True)
+    f = frames.reshape(n, stride)
+    rcv = (66 + (f[:, 17].astype(np.int64) - 52)).clip(66, stride)       # what arrived: the frame's bytes
+    forged = np.arange(n) % 3 == 0
+    forged[-1] = True                                                   # the batch's last frame too
+    fake = np.where(np.arange(n) % 2 == 0, 65535, 1500 + np.arange(n) % 500)
+    f[forged, 16] = (fake[forged] >> 8) & 0xFF
+    f[forged, 17] = fake[forged] & 0xFF
+    host = frames.copy()
+    # the frames end exactly where the allocation ends
+    d = torch.empty(host.size, dtype=torch.uint8, device=DEV)
+    d.copy_(torch.from_numpy(host))
+    if form == "flen":
+        got = xsum.tcp4_verify_batch(d, n, stride=stride, frame_len=to_dev((14 + 52 + rcv - 66).astype(np.int32)))
+        bound = (14 + 52 + rcv - 66).astype(np.uint32)
+    elif form == "flen0":
+        got = xsum.tcp4_verify_batch(d, n, stride=stride, frame_len=100)
+        bound = 100
+    elif form == "stride":
+        got = xsum.tcp4_verify_batch(d, n, stride=stride)
+        bound = stride
+    else:
+        offs = np.arange(n, dtype=np.int64) * stride
+        got = xsum.tcp4_verify_batch(d, n, offsets=to_dev(offs), room=stride)
+        bound = stride
+    got = got.cpu().numpy()
+    exp = oracle.tcp4_verify_batch_bounded(host, n, bound, stride=stride)
+    np.testing.assert_array_equal(got, exp)
+    assert np.all(got[forged] & xsum.RX_L4_OK == 0)
+    honest = ~forged & (rcv >= 66)
+    assert np.all(got[honest] == 3) or form == "flen0"
