@@ -107,9 +107,9 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
  * ip.total_length: a batch without per-frame hints whose frames have room for
  * a full MTU (IPv4 at 14 mod 16: room >= 1536 from the 16-byte aligned start)
  * is read at the uniform-hint speed (rows load the whole MTU at once and mask
- * by their own total_length); with per-frame hints a room of 80 B lets the
- * first 80 bytes -- a whole pure ACK -- go out with the total_length read.
- * Results still follow ip.total_length only. */
+ * by their own total_length).  Per-frame hints mark a data/ACK mix, whose rows
+ * read their own total_length first instead (whole-room reads would cost every
+ * ACK 1.5 KB).  Results still follow ip.total_length only. */
 int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
     uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
     uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
@@ -231,6 +231,17 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     uint32_t flags);
 int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     uint64_t stride, uint32_t len0, uint32_t n, uint16_t *out);
+
+/* The calling thread's context: TAS runs one dataplane_context per fast-path
+ * thread (dataplane_loop, tas/fast/fastemu.c:142), so the thread that will call
+ * tcp_checksums() binds its context once, and the per-frame calls pass
+ * TASX_CTX_SELF instead of a context id (tcp_checksums() and
+ * fast_flows_kernelxsums() have no ctx parameter, fast_flows.c:1058,1071).
+ * Every call that takes a ctx_id accepts TASX_CTX_SELF. */
+#define TASX_CTX_SELF 0xffffffffu
+int tasx_set_thread_ctx(unsigned ctx_id);
+/* the calling thread's context id, or -EINVAL if none is bound */
+int tasx_thread_ctx(void);
 
 /* Deferred per-frame surface.  tasx_tcp_checksums() has the reference's
  * argument list plus the context id; it only records the frame (no device

@@ -7,7 +7,7 @@ from __future__ import annotations
 import ctypes
 
 from . import xsum
-from .build import LIB_BENCH
+from .build import LIB_BENCH, LIB_BENCH_AB
 
 _vp, _u32, _u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
 
@@ -43,10 +43,13 @@ _lib = None
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        xsum.lib()  # libtasx.so first: the loop library binds to the same instance (by soname)
-        if not LIB_BENCH.exists():
-            raise RuntimeError(f"{LIB_BENCH} not built; run python -c 'import __graft_entry__ as g; g.build()'")
-        L = ctypes.CDLL(str(LIB_BENCH))
+        # the loops call the library xsum uses (libtasx.so, or the A/B build under
+        # TASX_LIB): loaded first, it is the instance the loop library binds to by soname
+        path = LIB_BENCH_AB if xsum.library_path().name == "libtasx_ab.so" else LIB_BENCH
+        xsum.lib()
+        if not path.exists():
+            raise RuntimeError(f"{path} not built; run python -c 'import __graft_entry__ as g; g.build()'")
+        L = ctypes.CDLL(str(path))
         pp = ctypes.POINTER(_vp)
         L.tasxb_tcp4_loop.argtypes = [ctypes.c_int, ctypes.POINTER(Tcp4Args), ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, pp, ctypes.c_int]

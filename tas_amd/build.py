@@ -69,6 +69,7 @@ def _build_one(lib: Path, defines: list[str], tag: str, extra_hip_flags: list[st
 
 # bench.py's launch loops (measurement plumbing over libtasx's public C ABI)
 LIB_BENCH = OUT_DIR / "libtasx_bench.so"
+LIB_BENCH_AB = OUT_DIR / "libtasx_bench_ab.so"  # the same loops over the A/B build
 BENCH_SRC = ROOT / "tas_amd" / "benchsrc" / "bench_loop.c"
 
 
@@ -79,12 +80,35 @@ def build(force: bool = False, extra_hip_flags: list[str] | None = None, ab: boo
         _build_one(LIB, [], "", extra_hip_flags)
     if ab and (force or _stale(LIB_AB)):
         _build_one(LIB_AB, ["-DTASX_AB"], "_ab", extra_hip_flags)
-    if force or not LIB_BENCH.exists() or LIB_BENCH.stat().st_mtime < max(
-            BENCH_SRC.stat().st_mtime, LIB.stat().st_mtime, (ROOT / "include" / "tasx_xsum.h").stat().st_mtime):
-        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", "-shared", "-I", str(ROOT / "include"),
-              "-o", str(LIB_BENCH), str(BENCH_SRC), "-L", str(OUT_DIR), "-ltasx",
-              "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
+    for out, dep, name in ((LIB_BENCH, LIB, "tasx"), (LIB_BENCH_AB, LIB_AB, "tasx_ab")):
+        if not dep.exists():
+            continue
+        if force or not out.exists() or out.stat().st_mtime < max(
+                BENCH_SRC.stat().st_mtime, dep.stat().st_mtime, (ROOT / "include" / "tasx_xsum.h").stat().st_mtime):
+            _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", "-shared", "-I", str(ROOT / "include"),
+                  "-o", str(out), str(BENCH_SRC), "-L", str(OUT_DIR), f"-l{name}",
+                  "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
     return LIB
+
+
+# C boundary test (tests/c/boundary_test.c): compiled against the reference's own
+# wire headers, so it is built only where /root/reference exists (this build
+# container); the binary travels with the tree to the GPU box
+REF_INCLUDE = Path("/root/reference/include")
+C_TEST_SRC = ROOT / "tests" / "c" / "boundary_test.c"
+C_TEST_BIN = ROOT / "tests" / "c" / "bin" / "boundary_test"
+
+
+def build_c_tests(force: bool = False) -> Path | None:
+    if not (REF_INCLUDE / "packet_defs.h").exists():
+        return C_TEST_BIN if C_TEST_BIN.exists() else None
+    deps = [C_TEST_SRC, C_TEST_SRC.with_name("tas_glue.h"), ROOT / "include" / "tasx_xsum.h", LIB]
+    if force or not C_TEST_BIN.exists() or C_TEST_BIN.stat().st_mtime < max(d.stat().st_mtime for d in deps):
+        C_TEST_BIN.parent.mkdir(parents=True, exist_ok=True)
+        _run(["gcc", "-std=gnu99", "-O2", "-Wall", "-I", str(REF_INCLUDE), "-I", str(ROOT / "include"),
+              "-o", str(C_TEST_BIN), str(C_TEST_SRC), "-L", str(OUT_DIR), "-ltasx",
+              "-Wl,-rpath,$ORIGIN/../../../tas_amd/_lib", "-Wl,--no-undefined"])
+    return C_TEST_BIN
 
 
 if __name__ == "__main__":

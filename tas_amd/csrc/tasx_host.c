@@ -340,12 +340,31 @@ struct tasx_ctx {
 };
 
 static struct tasx_ctx g_ctx[TASX_MAX_CTX];
+/* the calling thread's context (tasx_set_thread_ctx), for TASX_CTX_SELF */
+static __thread unsigned t_ctx = TASX_CTX_SELF;
 
 static struct tasx_ctx *get_ctx(unsigned id)
 {
+  if (id == TASX_CTX_SELF)
+    id = t_ctx;
   if (id >= TASX_MAX_CTX || !g_ctx[id].in_use)
     return NULL;
   return &g_ctx[id];
+}
+
+int tasx_set_thread_ctx(unsigned ctx_id)
+{
+  if (ctx_id != TASX_CTX_SELF && ctx_id >= TASX_MAX_CTX)
+    return set_err(-EINVAL, "ctx id %u >= %u", ctx_id, TASX_MAX_CTX);
+  t_ctx = ctx_id; /* TASX_CTX_SELF unbinds */
+  return 0;
+}
+
+int tasx_thread_ctx(void)
+{
+  if (t_ctx == TASX_CTX_SELF)
+    return set_err(-EINVAL, "no context bound to this thread");
+  return (int) t_ctx;
 }
 
 static void ctx_release(struct tasx_ctx *c)
@@ -384,6 +403,8 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
   int s, ndev = 0;
   hipError_t e;
 
+  if (ctx_id == TASX_CTX_SELF)
+    ctx_id = t_ctx;
   if (ctx_id >= TASX_MAX_CTX)
     return set_err(-EINVAL, "ctx id %u >= %u", ctx_id, TASX_MAX_CTX);
   c = &g_ctx[ctx_id];

@@ -1148,17 +1148,19 @@ static bool tas14_offs_ok(const tasx_tcp4_params &p)
   return p.off != nullptr && p.l4_off == p.ip_off + 20 && (p.ip_off & 15u) == 14u && !p.flen0;
 }
 
-// Row mode without a uniform hint, from the room (bytes readable from each
-// frame's start).  A room covering a full-MTU frame lets rows of a batch that
-// carries no per-frame lengths load the whole MTU at once (bulk TX batches);
-// with per-frame hints (data/ACK mixes) whole-room reads would cost the ACK
-// rows 1.5 KB each, so only an ACK's 80 bytes go out with the total_length.
+// Row mode without a uniform hint.  A room covering a full-MTU frame lets rows
+// of a batch that carries no per-frame lengths load the whole MTU at once
+// (bulk TX batches: 64K MTU frames 15.9 us against 16.9 us total_length
+// first).  Batches with per-frame hints are data/ACK mixes, where whole-room
+// reads cost every ACK row 1.5 KB (16.0 us at any ACK share) and total_length
+// first wins (25 / 50 / 75 % ACKs: 13.6 / 10.6 / 8.5 us); the head-5 mode
+// (an ACK's 80 bytes with the total_length) lost to it everywhere but all-ACK
+// batches (6.3 against 6.8 us) and is an A/B variant (10).
+// tools/ackmix_probe.py, profiles/r02/r02d_ackmix_modes.jsonl.
 static int tas14_mode(const tasx_tcp4_params &p)
 {
   const uint32_t from_a0 = p.room > (p.ip_off & ~15u) ? p.room - (p.ip_off & ~15u) : 0u;
-  if (!p.flen && from_a0 >= 1536u)
-    return kRoom;
-  return from_a0 >= 80u ? kHead5 : kTlFirst;
+  return !p.flen && from_a0 >= 1536u ? kRoom : kTlFirst;
 }
 
 // completion word: stream-ordered after the work before it, one lane stores

@@ -37,6 +37,7 @@ TAS_IP_OFF = 14
 TAS_L4_OFF = 34
 RAW_MAX_LEN = 131073
 MAX_CTX = 16
+CTX_SELF = 0xFFFFFFFF  # TASX_CTX_SELF: the calling thread's context (tasx_set_thread_ctx)
 
 _c_int, _c_u16, _c_u32, _c_u64 = ctypes.c_int, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint64
 _vp, _sz, _uns = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint
@@ -64,6 +65,8 @@ SIGNATURES = {
     "tasx_ctx_destroy": (_c_int, [_uns]),
     "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
     "tasx_raw_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _vp]),
+    "tasx_set_thread_ctx": (_c_int, [_uns]),
+    "tasx_thread_ctx": (_c_int, []),
     "tasx_tcp_checksums": (_c_int, [_uns, _vp, _vp, _c_u32, _c_u32, _c_u16]),
     "tasx_fast_flows_kernelxsums": (_c_int, [_uns, _vp, _vp]),
     "tasx_defer_tcp4": (_c_int, [_uns, _vp, _c_u16, _c_u16]),
@@ -315,6 +318,11 @@ def tx_segment_batch(shm: torch.Tensor, frames: torch.Tensor, segs: torch.Tensor
 
 def ctx_init(ctx_id: int, device: int = 0, max_batch_bytes: int = 0) -> None:
     _check(lib().tasx_ctx_init(ctx_id, device, max_batch_bytes), "tasx_ctx_init")
+
+
+def set_thread_ctx(ctx_id: int) -> None:
+    """Bind ctx_id to the calling thread (calls may then pass CTX_SELF)."""
+    _check(lib().tasx_set_thread_ctx(ctx_id), "tasx_set_thread_ctx")
 
 
 def ctx_destroy(ctx_id: int) -> None:

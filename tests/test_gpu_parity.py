@@ -802,9 +802,9 @@ def test_tcp4_rooms_every_row_mode(oracle, room, variant):
 
 def test_tcp4_room_selects_row_mode():
     """Which tcp4_tas14_kernel mode a call takes (tasx_last_kernel): a full-MTU
-    room and no per-frame hints -> whole-room rows; per-frame hints with a room
-    of 80 B or more -> head-5 rows; no room -> total_length first; a uniform
-    hint -> the hinted kernel; an offsets array -> the OFFS forms."""
+    room and no per-frame hints -> whole-room rows; per-frame hints or less
+    room -> total_length first; a uniform hint -> the hinted kernel; an offsets
+    array -> the OFFS forms."""
     n = 64
     frames = to_dev(pktgen.tcp4_frames(n, stride=2048))
     flen = to_dev(np.full(n, 1514, np.int32))
@@ -813,13 +813,13 @@ def test_tcp4_room_selects_row_mode():
         (dict(stride=2048), "tcp4_tas14_kernel<tl_first>"),
         (dict(stride=2048, room=2048), "tcp4_tas14_kernel<room>"),
         (dict(stride=2048, room=1536), "tcp4_tas14_kernel<room>"),
-        (dict(stride=2048, room=1535), "tcp4_tas14_kernel<head5>"),
+        (dict(stride=2048, room=1535), "tcp4_tas14_kernel<tl_first>"),
         (dict(stride=2048, room=79), "tcp4_tas14_kernel<tl_first>"),
-        (dict(stride=2048, room=2048, frame_len=flen), "tcp4_tas14_kernel<head5>"),
+        (dict(stride=2048, room=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first>"),
         (dict(stride=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first>"),
         (dict(stride=2048, room=2048, frame_len=1514), "tcp4_tas14_kernel<hint>"),
         (dict(offsets=offs, room=2048), "tcp4_tas14_kernel<room,offs>"),
-        (dict(offsets=offs, room=2048, frame_len=flen), "tcp4_tas14_kernel<head5,offs>"),
+        (dict(offsets=offs, room=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first,offs>"),
         (dict(offsets=offs), "tcp4_tas14_kernel<tl_first,offs>"),
         (dict(stride=2048, ip_off=14, l4_off=38), "tcp4_frame_kernel"),
     ]

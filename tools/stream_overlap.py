@@ -18,7 +18,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 import bench  # noqa: E402
-from tas_amd import pktgen, xsum  # noqa: E402
+from tas_amd import benchloop  # noqa: E402
 
 
 def main():
@@ -28,25 +28,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     wl = bench.Tcp4Workload(16, 0x5EED, host=False)
-    fn = xsum.lib().tasx_tcp4_cksum_batch_dev_hint
-    R = len(wl.bufs)
     streams = [torch.cuda.Stream() for _ in range(8)]
     res = {}
     for _ in range(a.rounds):
         for S in [int(s) for s in a.streams.split(",")]:
-            ss = streams[:S]
-
-            def launch(k):
-                s = ss[k % S].cuda_stream
-                rc = fn(wl.bufs[k % R].data_ptr(), None, wl.stride, None, wl.hint, wl.n, pktgen.ETH_LEN,
-                        pktgen.ETH_LEN + pktgen.IP_LEN, wl.outs[k % R].data_ptr(), 0, s)
-                assert rc == 0
-            for k in range(64):
-                launch(k)
+            run = wl.loop(benchloop.HINT, streams=streams[:S])  # batch k on stream k % S, from C
+            run(0, 64)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for k in range(a.steps):
-                launch(k)
+            run(64, a.steps)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             res.setdefault(S, []).append(dt / a.steps * 1e6)
