@@ -377,13 +377,15 @@ class TxSegWorkload:
     4 B of checksums written."""
     desc = (f"{N_FRAMES} TAS TX segments of {pktgen.TCP_MSS} B payload from 8192 flows' 16 KiB circular TX "
             f"buffers (wraps included) into 1514 B frames at {STRIDE} B stride (descriptor room = the {STRIDE} B "
-            "mbuf data room), checksums in place")
+            "mbuf data room, scratch past the frame), checksums in place")
 
     def __init__(self, rotate: int, seed: int, n: int = N_FRAMES):
         self.n = n
-        # room = the mbuf data room (TAS: BUFFER_SIZE, tas/fast/internal.h:34)
+        # room = the mbuf data room (TAS: BUFFER_SIZE, tas/fast/internal.h:34),
+        # scratch past the frame (an mbuf carries nothing past data_len)
         _, _, segs, shm_len = pktgen.tx_segments(n, seed=seed, nflows=8192, tx_len=16384, make_shm=False,
                                                  room=STRIDE)
+        segs["room"] = np.uint32(STRIDE | xsum.TXSEG_SCRATCH)
         self.segs_np, self.shm_len = segs, shm_len
         self.segs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
         self.shms = [device_random(shm_len, seed + 7 + r) for r in range(rotate)]
@@ -393,6 +395,7 @@ class TxSegWorkload:
         hdr = pktgen.HDRS_LEN - pktgen.ETH_LEN - pktgen.IP_LEN
         self.bytes_per_seg = 2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4
         self.bytes_per_step = n * self.bytes_per_seg
+        self.block_floor = txseg_block_floor(segs)
 
     def loop(self, streams=None) -> benchloop.Loop:
         args = [benchloop.TxSegArgs(sh.data_ptr(), self.shm_len, b.data_ptr(), self.segs.data_ptr(), self.n, IP_OFF,
@@ -421,6 +424,27 @@ class TxSegWorkload:
                 "sample": f"rotation 0's {self.n} segments, oracle flow_tx_read + tcp_checksums per segment, "
                           f"median of {reps} passes",
                 "parity_vs_gpu": "bit-exact" if np.array_equal(frames, gpu_frames) else "MISMATCH"}
+
+
+def txseg_block_floor(segs, block: int = 128) -> dict:
+    """HBM bytes the TX segment build cannot avoid at the memory side's 128-byte
+    request granularity (calibrated: tools/fetch_calib.hip): the blocks each
+    payload piece (two at a wrap) occupies in shm, the frame's header block,
+    the 32-byte descriptor; writes of the frame's whole blocks (scratch room)."""
+    base = segs["tx_base"].astype(np.int64)
+    pos = segs["pos"].astype(np.int64)
+    pay = segs["payload"].astype(np.int64)
+    tlen = segs["tx_len"].astype(np.int64)
+    p1 = np.minimum(pay, tlen - pos)
+    a1, b1 = base + pos, base + pos + p1
+    blocks = np.where(p1 > 0, (b1 + block - 1) // block - a1 // block, 0)
+    p2 = pay - p1
+    blocks += np.where(p2 > 0, (base + p2 + block - 1) // block - base // block, 0)
+    off = segs["frame_off"].astype(np.int64)
+    fend = off + segs["hdrs_len"].astype(np.int64) + pay
+    reads = int(blocks.sum()) * block + len(segs) * (block + 32)
+    writes = int(((fend + block - 1) // block - off // block).sum()) * block
+    return {"read_bytes": reads, "write_bytes": writes, "bytes": reads + writes, "block": block}
 
 
 class FlowLookupWorkload:
@@ -483,25 +507,49 @@ class FlowLookupWorkload:
                 "parity_vs_gpu": "bit-exact" if np.array_equal(exp, gpu_fid) else "MISMATCH"}
 
 
-# flow lookup latency roofline: three dependent memory
-# accesses per frame -- the frame header (HBM miss), the 4-entry bucket (2 MB
-# flowht: L2) and the candidate flow keys (16 MB flowst: Infinity Cache) -- at
-# the guide's idle-chip latencies (MI355X_MICROARCH.md cycle constants: HBM
-# miss ~900 cyc, MALL hit ~545 cyc, L2 hit ~200 cyc at 2.4 GHz), for as many
-# generations of resident frames (64 per wave, 8 waves per SIMD) as the batch needs
-FLOW_CHAIN_NS = {"hbm": 900 / 2.4, "l2": 200 / 2.4, "mall": 545 / 2.4}
+# Flow lookup bounds.  The lookup is a dependent chain
+# per frame: the frame's key (HBM), its 4-entry bucket (flowht, 2 MB), the
+# candidate flows' keys (flowst, 16 MB; both MALL-resident).  Each random
+# access costs a whole 128-byte L2 line, so the HBM roofline counts 128 B per
+# frame header (+ 8 B written), and the ceiling of the chain itself is
+# measured live: the same access pattern with no hashing or key logic
+# (tasx_ab_flow_pattern, the A/B build; tools/flow_ceiling.hip).
+L2_LINE = 128
 
 
-def flow_latency_roofline(n_frames: int, avg_us: float, waves_per_simd: int = 8) -> dict:
-    frames_in_flight = 256 * 4 * waves_per_simd * 64
-    gens = -(-n_frames // frames_in_flight)
-    chain_ns = FLOW_CHAIN_NS["hbm"] + FLOW_CHAIN_NS["l2"] + FLOW_CHAIN_NS["mall"]
-    bound_us = gens * chain_ns / 1e3
-    return {"bound": "latency", "achieved": round(n_frames / avg_us, 1), "unit": "lookups/us",
-            "peak": round(n_frames / bound_us, 1), "frac": round(bound_us / avg_us, 4),
-            "chain": "frame header (HBM) -> flowht bucket (L2) -> flow-state key (MALL)",
-            "chain_ns": round(chain_ns, 1), "generations": gens, "frames_in_flight": frames_in_flight,
-            "launch_avg_us": round(avg_us, 3)}
+def flow_bounds(fw: "FlowLookupWorkload", avg_us: float, launches: int = 100) -> dict:
+    ab = xsum._load(xsum.AB_LIB_PATH)
+    out = torch.empty(fw.N, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    R = len(fw.bufs)
+
+    def pat(k):
+        rc = ab.tasx_ab_flow_pattern(fw.bufs[k % R].data_ptr(), STRIDE, fw.N, IP_OFF, fw.ht.data_ptr(), fw.ENTRIES,
+                                     fw.fs.data_ptr(), fw.NFLOWS, pktgen.FLOWST_SIZE, pktgen.FLOWST_KEY_OFF,
+                                     out.data_ptr(), s)
+        if rc:
+            raise xsum.TasxError(rc, "tasx_ab_flow_pattern")
+    for k in range(20):
+        pat(k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for k in range(launches):
+        pat(k)
+    e1.record()
+    torch.cuda.synchronize()
+    ceil_us = e0.elapsed_time(e1) * 1e3 / launches
+    line_bytes = fw.N * (L2_LINE + 8)
+    return {
+        "line_roofline": {"bound": "hbm", "bytes_per_frame": L2_LINE + 8,
+                          "achieved": round(line_bytes / avg_us / 1e3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(line_bytes / avg_us / 1e3 / HBM_PEAK_GBS, 4),
+                          "note": "one 128-byte L2 line per frame header (the key's 12 bytes cost a whole line)"},
+        "pattern_ceiling": {"bound": "dependent access chain", "us": round(ceil_us, 3),
+                            "frac": round(ceil_us / avg_us, 4),
+                            "chain": "frame key (HBM) -> 4-entry bucket (flowht) -> candidate keys (flowst)",
+                            "kernel": "flow_pattern_kernel (libtasx_ab.so): the same loads, no CRC or compares"},
+    }
 
 
 def prewarm(run, seconds: float = 0.25):
@@ -961,6 +1009,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         tw = TxSegWorkload(rot, pktgen.SEED + 2000 + rank)
         txseg = leg(tw.loop(), tw.bytes_per_step, args, ws, TxSegWorkload.desc, "tx_segment_tas_kernel")
         txseg["algorithmic_bytes_per_segment"] = tw.bytes_per_seg
+        txseg["block_floor"] = dict(tw.block_floor)
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             txseg["cpu_baseline"] = tw.cpu_check(3.0)
         del tw
@@ -973,7 +1022,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         flow["mpps"] = fw.N / (flow["roofline"]["launch_avg_us"] * 1e-6) / 1e6
         flow["flows_inserted_frac"] = fw.inserted
         flow["bytes_per_frame"] = 64
-        flow["latency_roofline"] = flow_latency_roofline(fw.N, flow["roofline"]["launch_avg_us"])
+        flow.update(flow_bounds(fw, flow["roofline"]["launch_avg_us"]))
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             flow["cpu_baseline"] = fw.cpu_check(3.0)
         del fw
@@ -1003,6 +1052,9 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                 pt = pmc_leg("txseg", "tx_segment", 32)
                 if pt and "hbm_bytes_per_launch" in pt:
                     txseg["roofline"]["traffic"] = int(pt["hbm_bytes_per_launch"])
+                    fl = txseg.get("block_floor")
+                    if fl:
+                        fl["traffic_over_floor"] = round(pt["hbm_bytes_per_launch"] / fl["bytes"], 4)
                 txseg["pmc"] = pt
 
     if rank == 0:

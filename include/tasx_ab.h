@@ -28,6 +28,13 @@ extern "C" {
  * wave.  NULL disables. */
 int tasx_set_diag_buffer(void *dev_buf);
 
+/* The RX flow lookup's bare access pattern (tasx_flow_lookup_batch_dev's
+ * frame-header -> bucket -> flow-key chain with no hashing or key compare):
+ * the ceiling that chain allows, timed by bench.py beside the lookup. */
+int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t ip_off,
+    const void *flowht, uint32_t ht_entries, const void *flowst, uint32_t fs_num, uint32_t fs_stride,
+    uint32_t fs_key_off, uint32_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

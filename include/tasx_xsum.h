@@ -163,8 +163,15 @@ typedef struct tasx_tx_seg {
   uint32_t room;      /* bytes from the frame start the build may rewrite (with
                        * their own values past the frame): the mbuf data room,
                        * BUFFER_SIZE in TAS (tas/fast/internal.h:34); 0 = only
-                       * [0, hdrs_len + payload) */
+                       * [0, hdrs_len + payload).  | TASX_TXSEG_SCRATCH: the
+                       * room's bytes past the frame are scratch (an mbuf holds
+                       * nothing past data_len) */
 } tasx_tx_seg;
+/* In tasx_tx_seg.room: the bytes from the frame's end to the end of its
+ * 128-byte block (counted from `frames`, within the room) may be overwritten;
+ * their contents afterwards are unspecified.  Lets the build write whole
+ * blocks: no read of the frame's tail and no partial-line write. */
+#define TASX_TXSEG_SCRATCH 0x80000000u
 /* For each segment: copy `payload` bytes from shm + tx_base at circular
  * position pos into frame + hdrs_len, then store ip.chksum / tcp.chksum into
  * the frame exactly as tcp_checksums() would over the finished frame (lengths

@@ -191,7 +191,73 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
     stg(p.hash_out, i, h);
 }
 
+#ifdef TASX_AB
+// The lookup's access pattern with no hashing or key logic (the ceiling its
+// dependent chain allows, tools/flow_ceiling.hip): the 12-byte key of each
+// frame (HBM), then its 4-entry bucket (flowht), then the candidate flow's key
+// line plus three reads of flow 0 (flowst), each level dependent on the last.
+__device__ __forceinline__ uint32_t mix32(uint32_t x)
+{
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  return x;
+}
+
+__global__ __launch_bounds__(256) void flow_pattern_kernel(tasx_flow_params p)
+{
+  const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t i = min(i0, p.n - 1u);
+  const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+  const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (f + p.ip_off + 12);
+  const uint32_t h = mix32(k.x ^ k.y ^ k.z);
+  uint64_t e[TASX_FLOWHT_NBSZ];
+#pragma unroll
+  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+    e[j] = ldg((const uint64_t *) p.flowht, (h + j) % p.ht_entries);
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+    r += (uint32_t) e[j] ^ (uint32_t) (e[j] >> 32);
+#pragma unroll
+  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
+    const uint32_t fid = j == 0 ? mix32(h ^ r) % p.fs_num : 0u;
+    const u32x3 key = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst + (uint64_t) fid * p.fs_stride +
+                                                                           p.fs_key_off);
+    r ^= key.x ^ key.y ^ key.z;
+  }
+  if (i0 < p.n)
+    stg(p.fid_out, i, r);
+}
+#endif
+
 } // namespace
+
+#ifdef TASX_AB
+// A/B build only (include/tasx_ab.h): the flow lookup's bare access pattern
+extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t ip_off,
+    const void *flowht, uint32_t ht_entries, const void *flowst, uint32_t fs_num, uint32_t fs_stride,
+    uint32_t fs_key_off, uint32_t *out, void *stream)
+{
+  tasx_flow_params p = {};
+  p.base = (const uint8_t *) base;
+  p.stride = stride;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.flowht = (const uint32_t *) flowht;
+  p.ht_entries = ht_entries;
+  p.flowst = (const uint8_t *) flowst;
+  p.fs_num = fs_num;
+  p.fs_stride = fs_stride;
+  p.fs_key_off = fs_key_off;
+  p.fid_out = out;
+  if (n == 0)
+    return 0;
+  tasx_note_kernel("flow_pattern_kernel");
+  hipLaunchKernelGGL(flow_pattern_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t) stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream)
 {

@@ -597,8 +597,18 @@ __global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_param
     const int pay = (int) pay_, fend = 66 + pay;
     const int K = (fend + 15) >> 4;
     // the descriptor's room covers the last chunk: write it whole, the bytes
-    // past the frame with their own values (sub-dword stores cost ~10% here)
-    const bool whole = d1.w >= 16u * (uint32_t) K;
+    // past the frame with their own values (sub-dword stores cost ~10% here).
+    // A scratch room (TASX_TXSEG_SCRATCH) also lets the build write the frame's
+    // last 128-byte block whole, with zeros past the frame: no read of the last
+    // chunk and no partial-line write for the memory side to merge.
+    const uint32_t room = d1.w & ~TASX_TXSEG_SCRATCH;
+    const bool scratch = (d1.w & TASX_TXSEG_SCRATCH) != 0u && room >= 16u * (uint32_t) K;
+    const bool whole = room >= 16u * (uint32_t) K;
+    int kend = K; // chunks [K, kend): scratch zeros up to the block's end
+    if (scratch) {
+      const uint64_t be = (frame_off + (uint64_t) fend + 127u) & ~127ull;
+      kend = max(K, min((int) ((be - frame_off + 15u) >> 4), (int) (room >> 4)));
+    }
     const int aoff = (int) (((uintptr_t) f >> 4) & 15u);
     const int kh = (gl - aoff) & 15; // this lane's chunk in the frame's first 256-byte block
     const uint8_t *const shm = p.shm;
@@ -615,7 +625,9 @@ __global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_param
     const uint32_t o4 = s1 - 2u;
     const u32x4 w4 = ld16u(shm, min(o4, smax));
     const u32x4 xw = ld16u(shm, min(xoff, smax));
-    const u32x4 tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
+    u32x4 tv = {0u, 0u, 0u, 0u};
+    if (!scratch)
+      tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
 
     // whole payload chunks 5..K-1; each store instruction covers whole 256-byte
     // blocks.  The payload chunks of the frame's first block (k < fbe) are kept
@@ -664,6 +676,12 @@ __global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_param
       }
     }
 
+    if (scratch) { // the scratch chunks past the frame outside its first block
+      const int k = K + gl;
+      if (k < kend && k >= fbe)
+        __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
+    }
+
     // chunks 0..4 (tcp4_tas14_kernel's map for 0..3; chunk 4 = option pad + payload [0, 14))
     u32x4 h = hv;
     if (kh == 4) {
@@ -707,6 +725,8 @@ __global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_param
         *(__attribute__((address_space(1))) u32x4 *) cp = h;
       else if (kh < 5)
         store_range(cp, h, 0, hi, false);
+      else if (kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
+        *(__attribute__((address_space(1))) u32x4 *) cp = u32x4{0u, 0u, 0u, 0u};
     }
   }
   if (!fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)

@@ -33,6 +33,7 @@ _lib = None
 _loaded: dict = {}
 
 TASX_F_INPLACE = 0x1
+TXSEG_SCRATCH = 0x80000000  # tasx_tx_seg.room flag: bytes past the frame are scratch
 TAS_IP_OFF = 14
 TAS_L4_OFF = 34
 RAW_MAX_LEN = 131073
@@ -92,6 +93,8 @@ SIGNATURES = {
 # A/B build only (include/tasx_ab.h)
 AB_SIGNATURES = {
     "tasx_set_diag_buffer": (_c_int, [_vp]),
+    "tasx_ab_flow_pattern": (_c_int, [_vp, _c_u64, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32, _c_u32, _c_u32, _vp,
+                                      _vp]),
 }
 
 

@@ -224,3 +224,31 @@ def test_gpu_txseg_errors():
     with pytest.raises(xsum.TasxError):
         xsum.tx_segment_batch(shm, fr, segs[8:], 1)                      # misaligned descriptors
     assert xsum.tx_segment_batch(shm, fr, segs, 0).numel() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 16, 48])
+def test_gpu_txseg_scratch_room(oracle, shift):
+    """room | TASX_TXSEG_SCRATCH (the mbuf holds nothing past data_len): frames
+    bit-exact up to their end, results equal, and only the bytes from each
+    frame's end to the end of its 128-byte block (counted from `frames`, within
+    the room) may differ -- everything else in the buffer is untouched."""
+    import torch
+    from tas_amd import xsum
+    n = 3000
+    pay = np.where(np.arange(n) % 3 == 0, (np.arange(n) * 97) % 1449, pktgen.TCP_MSS)
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=97, seed=0x5C2A + shift,
+                                           room=pktgen.MBUF_ROOM)
+    segs["room"] = np.uint32(pktgen.MBUF_ROOM | xsum.TXSEG_SCRATCH)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=shift)
+    np.testing.assert_array_equal(out, exp)
+    mask = np.ones(fr.size, bool)
+    fend = segs["frame_off"].astype(np.int64) + pktgen.HDRS_LEN + segs["payload"].astype(np.int64)
+    bend = (fend + shift + 127) // 128 * 128 - shift                   # block end, counted from `frames`
+    lim = segs["frame_off"].astype(np.int64) + pktgen.MBUF_ROOM
+    for a, b in zip(fend, np.minimum(bend, lim)):
+        mask[a:b] = False
+    np.testing.assert_array_equal(got[mask], exp_fr[mask])
+    assert (~mask).sum() > 0
