@@ -271,6 +271,26 @@ int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off,
 int tasx_pending(unsigned ctx_id);
 int tasx_flush(unsigned ctx_id);
 
+/* Asynchronous flushes: tasx_flush() is tasx_flush_submit() + tasx_flush_wait().
+ * A GPU round trip (launch + completion) costs ~13 us whatever the batch size,
+ * far more than a core's CPU checksums of one tx_flush batch (DESIGN.md
+ * section 5.1); split, a fast-path core submits a batch, keeps polling its
+ * queues, and hands the batch's frames to the NIC once its ticket completes,
+ * with up to 3 batches in flight per context.
+ *   tasx_flush_submit: launches every recorded frame (one or more flushes) and
+ *     returns in *ticket the ticket of the last one (the last submitted ticket
+ *     when nothing was recorded; 0 before the first flush).  Blocks only when
+ *     3 flushes are already in flight (it completes the oldest).
+ *   tasx_flush_poll: 1 when flush `ticket` and every earlier one are complete
+ *     (both checksum fields stored in their frames), 0 if not yet; never
+ *     blocks.  Completes flushes in ticket order.
+ *   tasx_flush_wait: spins until flush `ticket` is complete.
+ * Frames must stay valid and unmodified until their ticket completes.
+ * Tickets count up from 1 and wrap at 2^32 (comparisons are wrap-safe). */
+int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket);
+int tasx_flush_poll(unsigned ctx_id, uint32_t ticket);
+int tasx_flush_wait(unsigned ctx_id, uint32_t ticket);
+
 /* Zero-copy frames: declare the host region the context's frames live in
  * (TAS: the per-core mbuf mempool, tas/fast/network.c:320-330).  It is pinned
  * with hipHostRegister unless it already is (tasx_host_alloc).  A flush whose

@@ -74,7 +74,7 @@ int tasx_set_diag_buffer(void *dev_buf)
   g_diag = (uint64_t *) dev_buf;
   return 0;
 }
-#define TASX_MAX_VARIANT 11
+#define TASX_MAX_VARIANT 18
 #else
 #define TASX_MAX_VARIANT 7
 #endif
@@ -305,6 +305,21 @@ int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
 /* ---------------------------------------------------------------------- */
 /* contexts */
 
+/* One submitted flush (tasx_flush_submit): its frames (the staged path copies
+ * the results into them when the ticket completes) and the device views of its
+ * pinned descriptors.  Flush t uses slot t % NSLOT: the staging, offsets and
+ * results buffers of that slot and completion word t % NSLOT. */
+struct flush_slot {
+  uint32_t ticket; /* the ticket it carries */
+  uint32_t n;
+  int zerocopy;
+  uint8_t **ip, **l4;          /* the batch's frames (slot_frames entries) */
+  uint32_t *h_flen, *d_flen;   /* per-frame hints (zero-copy path) */
+  uint64_t *d_off;             /* device views of h_off[s], h_stage[s], h_out[s] */
+  uint8_t *d_stage;
+  uint16_t *d_out;
+};
+
 struct tasx_ctx {
   int in_use;
   int device;
@@ -317,27 +332,28 @@ struct tasx_ctx {
   uint64_t *h_off[NSLOT];
   uint16_t *h_out[NSLOT];
   uint32_t slot_frames; /* offsets / results capacity per slot */
-  /* deferred frames */
+  /* the open batch: frames recorded since the last submit */
   uint8_t **pend_ip;
   uint8_t **pend_l4;
   uint32_t npend;
+  /* flushes in flight: tickets done_ticket + 1 .. next_ticket, oldest first,
+   * all on stream st[0] in ticket order */
+  struct flush_slot fl[NSLOT];
+  uint32_t next_ticket, done_ticket;
+  /* completion words in coherent pinned memory, one per slot, 64 B apart: a
+   * one-lane kernel stores the ticket after the flush's work
+   * (tasx_launch_post_done); the caller polls them instead of
+   * hipStreamSynchronize (~3.5 us less per flush) */
+  uint32_t *h_done, *d_done;
   /* zero-copy frame region (tasx_ctx_register_frames) */
   uint8_t *zc_host;
   uint8_t *zc_dev;
   size_t zc_bytes;
   int zc_registered; /* we called hipHostRegister on it */
-  uint64_t *d_hoff;  /* device view of h_off[0] (pinned) */
-  uint32_t *h_flen;  /* pinned frame-length hints, and its device view */
-  uint32_t *d_hflen;
   uint32_t n_zerocopy_flushes, n_staged_flushes;
-  /* flush completion: a word in coherent pinned memory that a one-lane kernel
-   * sets after the flush's work (tasx_launch_post_done); the caller spins on
-   * it instead of hipStreamSynchronize (~3.5 us less per flush) */
-  uint32_t *h_done, *d_done;
-  uint32_t done_seq;
-  uint8_t *d_hstage; /* device views of h_stage[0] / h_out[0] */
-  uint16_t *d_hout;
 };
+
+#define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
 
 static struct tasx_ctx g_ctx[TASX_MAX_CTX];
 /* the calling thread's context (tasx_set_thread_ctx), for TASX_CTX_SELF */
@@ -367,6 +383,12 @@ int tasx_thread_ctx(void)
   return (int) t_ctx;
 }
 
+/* ticket order with wrap-around: a at or before b */
+static int ticket_le(uint32_t a, uint32_t b)
+{
+  return (int32_t) (a - b) <= 0;
+}
+
 static void ctx_release(struct tasx_ctx *c)
 {
   int s;
@@ -385,9 +407,11 @@ static void ctx_release(struct tasx_ctx *c)
       hipHostFree(c->h_off[s]);
     if (c->h_out[s])
       hipHostFree(c->h_out[s]);
+    if (c->fl[s].h_flen)
+      hipHostFree(c->fl[s].h_flen);
+    free(c->fl[s].ip);
+    free(c->fl[s].l4);
   }
-  if (c->h_flen)
-    hipHostFree(c->h_flen);
   if (c->h_done)
     hipHostFree(c->h_done);
   if (c->zc_registered)
@@ -423,27 +447,35 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
   c->slot_frames = (uint32_t) (c->slot_bytes / 64 + 1);
   HIPCHK(hipSetDevice(device));
   for (s = 0; s < NSLOT; s++) {
+    struct flush_slot *f = &c->fl[s];
     if ((e = hipStreamCreateWithFlags(&c->st[s], hipStreamNonBlocking)) != hipSuccess ||
         (e = hipMalloc((void **) &c->d_buf[s], c->slot_bytes)) != hipSuccess ||
         (e = hipMalloc((void **) &c->d_off[s], (size_t) c->slot_frames * 8)) != hipSuccess ||
         (e = hipMalloc((void **) &c->d_out[s], (size_t) c->slot_frames * 4)) != hipSuccess ||
         (e = hipHostMalloc((void **) &c->h_stage[s], c->slot_bytes, 0)) != hipSuccess ||
         (e = hipHostMalloc((void **) &c->h_off[s], (size_t) c->slot_frames * 8, 0)) != hipSuccess ||
-        (e = hipHostMalloc((void **) &c->h_out[s], (size_t) c->slot_frames * 4, 0)) != hipSuccess) {
+        (e = hipHostMalloc((void **) &c->h_out[s], (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void **) &f->h_flen, (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &f->d_flen, f->h_flen, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &f->d_off, c->h_off[s], 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &f->d_stage, c->h_stage[s], 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &f->d_out, c->h_out[s], 0)) != hipSuccess) {
       ctx_release(c);
       return hip_err(e, "tasx_ctx_init allocation");
     }
+    f->ip = calloc(c->slot_frames, sizeof(*f->ip));
+    f->l4 = calloc(c->slot_frames, sizeof(*f->l4));
+    if (!f->ip || !f->l4) {
+      ctx_release(c);
+      return set_err(-ENOMEM, "tasx_ctx_init: out of host memory");
+    }
   }
-  if ((e = hipHostMalloc((void **) &c->h_flen, (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_hoff, c->h_off[0], 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_hflen, c->h_flen, 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_hstage, c->h_stage[0], 0)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &c->d_hout, c->h_out[0], 0)) != hipSuccess ||
-      (e = hipHostMalloc((void **) &c->h_done, 64, hipHostMallocCoherent)) != hipSuccess ||
+  if ((e = hipHostMalloc((void **) &c->h_done, 4u * DONE_STRIDE * NSLOT, hipHostMallocCoherent)) != hipSuccess ||
       (e = hipHostGetDevicePointer((void **) &c->d_done, c->h_done, 0)) != hipSuccess) {
     ctx_release(c);
-    return hip_err(e, "tasx_ctx_init pinned descriptors");
+    return hip_err(e, "tasx_ctx_init completion words");
   }
+  memset(c->h_done, 0, 4u * DONE_STRIDE * NSLOT);
   c->pend_ip = calloc(c->slot_frames, sizeof(*c->pend_ip));
   c->pend_l4 = calloc(c->slot_frames, sizeof(*c->pend_l4));
   if (!c->pend_ip || !c->pend_l4) {
@@ -454,12 +486,15 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
   return 0;
 }
 
+static int flush_wait(struct tasx_ctx *c, uint32_t ticket);
+
 int tasx_ctx_destroy(unsigned ctx_id)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   hipSetDevice(c->device);
+  (void) flush_wait(c, c->next_ticket);
   for (int s = 0; s < NSLOT; s++)
     hipStreamSynchronize(c->st[s]);
   ctx_release(c);
@@ -467,7 +502,9 @@ int tasx_ctx_destroy(unsigned ctx_id)
 }
 
 /* ---------------------------------------------------------------------- */
-/* end-to-end host batches: chunk -> H2D -> kernel -> D2H, NSLOT in flight */
+/* end-to-end host batches: chunk -> H2D -> kernel -> D2H, NSLOT in flight
+ * (they share the slots' pinned buffers with the flushes: in-flight flushes
+ * complete first) */
 
 struct chunk_job {
   uint32_t first, cnt;
@@ -509,6 +546,8 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
   if (flags & ~TASX_F_INPLACE)
     return set_err(-EINVAL, "tcp4 host batch: unknown flags 0x%x", flags);
   HIPCHK(hipSetDevice(c->device));
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
   per = (uint32_t) (c->slot_bytes / stride);
   if (per > c->slot_frames)
     per = c->slot_frames;
@@ -555,6 +594,7 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
   struct tasx_ctx *c = get_ctx(ctx_id);
   struct chunk_job jobs[NSLOT];
   uint32_t per, first, k = 0;
+  int rc;
 
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
@@ -563,6 +603,8 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
   if (!base || !out || len0 > TASX_RAW_MAX_LEN || stride < len0 || stride > c->slot_bytes)
     return set_err(-EINVAL, "raw host batch: bad base/out/stride/len0");
   HIPCHK(hipSetDevice(c->device));
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
   per = (uint32_t) (c->slot_bytes / (stride ? stride : 1));
   if (per > c->slot_frames)
     per = c->slot_frames;
@@ -687,70 +729,54 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
   return 0;
 }
 
-/* Wait for everything enqueued on c->st[0]: a one-lane kernel posts the next
- * sequence number into the context's completion word and the caller spins on
- * it.  Every 4096 polls (a few microseconds) the stream is queried, so an
- * error or a lost word ends the wait instead of spinning on. */
-static int wait_done(struct tasx_ctx *c)
+/* Complete every flush up to `upto` whose completion word has arrived, oldest
+ * first (the staged path copies its results into the frames); returns 1 when
+ * `upto` is complete, 0 if not yet. */
+static int flush_reap(struct tasx_ctx *c, uint32_t upto)
 {
-  volatile uint32_t *w = c->h_done;
-  const uint32_t seq = ++c->done_seq;
+  while (!ticket_le(upto, c->done_ticket)) {
+    const uint32_t t = c->done_ticket + 1;
+    struct flush_slot *f = &c->fl[t % NSLOT];
+    volatile uint32_t *w = c->h_done + DONE_STRIDE * (t % NSLOT);
+    if (*w != t)
+      return 0;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    if (!f->zerocopy) {
+      const uint16_t *r = c->h_out[t % NSLOT];
+      for (uint32_t i = 0; i < f->n; i++) {
+        memcpy(f->ip[i] + 10, &r[2 * i], 2);
+        memcpy(f->l4[i] + 16, &r[2 * i + 1], 2);
+      }
+    }
+    c->done_ticket = t;
+  }
+  return 1;
+}
+
+/* Spin until flush `ticket` (and every earlier one) is complete.  Every 4096
+ * polls (a few microseconds) the stream is queried, so an error or a lost word
+ * ends the wait instead of spinning on. */
+static int flush_wait(struct tasx_ctx *c, uint32_t ticket)
+{
   uint32_t k = 0;
-  if (tasx_launch_post_done(c->d_done, seq, c->st[0]) != 0)
-    return hip_err(hipGetLastError(), "completion-word launch");
-  while (*w != seq) {
+  while (!flush_reap(c, ticket)) {
     if ((++k & 4095u) == 0) {
       hipError_t e = hipStreamQuery(c->st[0]);
-      if (e == hipSuccess && *w != seq)
-        return set_err(-EIO, "flush: stream idle but completion word %u != %u", *w, seq);
+      if (e == hipSuccess && !flush_reap(c, ticket))
+        return set_err(-EIO, "flush: stream idle but flush %u not complete", c->done_ticket + 1);
       if (e != hipSuccess && e != hipErrorNotReady)
         return hip_err(e, "flush: hipStreamQuery");
     }
   }
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   return 0;
 }
 
-/* Zero-copy flush: every pending frame lies in the registered region and has
- * the TAS layout (tcp = ip + 20).  The kernel reads the frames straight from
- * host memory over PCIe (only the bytes it sums), writes both checksum fields
- * in place, and the descriptors (offset, frame-length hint) are read from
- * pinned memory: one launch + the completion-word wait, no copies. */
-static int flush_zerocopy(struct tasx_ctx *c)
-{
-  tasx_tcp4_params p;
-  uint32_t i, n = c->npend;
-  for (i = 0; i < n; i++) {
-    const uint8_t *ip = c->pend_ip[i];
-    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-    c->h_off[0][i] = (uint64_t) (ip - c->zc_host);
-    c->h_flen[i] = (tl < 20 ? 20 : tl);
-  }
-  memset(&p, 0, sizeof(p));
-  p.base = c->zc_dev;
-  p.off = c->d_hoff;
-  p.out = NULL;
-  p.n = n;
-  p.ip_off = 0;
-  p.l4_off = 20;
-  p.flags = TASX_F_INPLACE;
-  p.flen = c->d_hflen;
-  if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
-    return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-  int rc = wait_done(c);
-  if (rc != 0)
-    return rc;
-  c->n_zerocopy_flushes++;
-  c->npend = 0;
-  return 0;
-}
-
-static int zerocopy_ok(const struct tasx_ctx *c)
+static int zerocopy_ok(const struct tasx_ctx *c, uint32_t n)
 {
   uint32_t i;
   if (!c->zc_host)
     return 0;
-  for (i = 0; i < c->npend; i++) {
+  for (i = 0; i < n; i++) {
     const uint8_t *ip = c->pend_ip[i];
     uint32_t tl;
     if (c->pend_l4[i] != ip + 20 || ip < c->zc_host || ip + 20 > c->zc_host + c->zc_bytes)
@@ -762,71 +788,145 @@ static int zerocopy_ok(const struct tasx_ctx *c)
   return 1;
 }
 
-/* Gather every pending frame as [20-byte IPv4 header | L4 segment] into
- * pinned staging (16-byte aligned records: the sum is relative to the header
- * / segment start, so where a record sits does not change it), run the TCP4
- * kernel with ip_off 0 / l4_off 20, and store the two results into the
- * frames. */
-int tasx_flush(unsigned ctx_id)
+/* Submit the first `cnt` pending frames as flush `t` into slot t % NSLOT
+ * (whose previous flush the caller has completed), and drop them from the
+ * open batch.
+ *   zero-copy: every frame in the registered region, TAS layout: the kernel
+ *     reads the frames over PCIe (only the bytes it sums) and stores both
+ *     fields in place; descriptors (offset, frame-length hint) from pinned
+ *     memory.
+ *   staged: [20-byte IPv4 header | L4 segment] of each frame gathered into the
+ *     slot's pinned staging (16-byte aligned records: the sums are relative to
+ *     the header / segment start, so where a record sits does not change
+ *     them); the kernel reads the records and writes the results to pinned
+ *     memory directly (no copy-engine work), and the completion copies them
+ *     into the frames. */
+static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
+{
+  const int s = (int) (t % NSLOT);
+  struct flush_slot *f = &c->fl[s];
+  tasx_tcp4_params p;
+  uint32_t i;
+  memset(&p, 0, sizeof(p));
+  p.n = cnt;
+  p.ip_off = 0;
+  p.l4_off = 20;
+  p.off = f->d_off;
+  if (zc) {
+    for (i = 0; i < cnt; i++) {
+      const uint8_t *ip = c->pend_ip[i];
+      const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+      c->h_off[s][i] = (uint64_t) (ip - c->zc_host);
+      f->h_flen[i] = (tl < 20 ? 20 : tl);
+    }
+    p.base = c->zc_dev;
+    p.flags = TASX_F_INPLACE;
+    p.flen = f->d_flen;
+    c->n_zerocopy_flushes++;
+  } else {
+    size_t pos = 0;
+    for (i = 0; i < cnt; i++) {
+      const uint8_t *ip = c->pend_ip[i];
+      const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+      const uint32_t l4len = tl > 20 ? tl - 20 : 0;
+      /* the kernel reads the checksum field of short segments too */
+      const uint32_t cp = l4len < 18 ? 18 : l4len;
+      memcpy(c->h_stage[s] + pos, ip, 20);
+      memcpy(c->h_stage[s] + pos + 20, c->pend_l4[i], cp);
+      c->h_off[s][i] = pos;
+      pos += (20 + (size_t) cp + 15) & ~(size_t) 15;
+    }
+    p.base = f->d_stage;
+    p.out = f->d_out;
+    c->n_staged_flushes++;
+  }
+  memcpy(f->ip, c->pend_ip, (size_t) cnt * sizeof(*f->ip));
+  memcpy(f->l4, c->pend_l4, (size_t) cnt * sizeof(*f->l4));
+  f->n = cnt;
+  f->zerocopy = zc;
+  f->ticket = t;
+  if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
+    return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+  if (tasx_launch_post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
+    return hip_err(hipGetLastError(), "completion-word launch");
+  c->next_ticket = t;
+  if (cnt < c->npend) {
+    memmove(c->pend_ip, c->pend_ip + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_ip));
+    memmove(c->pend_l4, c->pend_l4 + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_l4));
+  }
+  c->npend -= cnt;
+  return 0;
+}
+
+/* frames of the open batch whose staged records fit one slot */
+static uint32_t staged_fit(const struct tasx_ctx *c, size_t *need)
+{
+  size_t pos = 0;
+  uint32_t i;
+  for (i = 0; i < c->npend; i++) {
+    const uint8_t *ip = c->pend_ip[i];
+    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+    const uint32_t l4len = tl > 20 ? tl - 20 : 0;
+    const size_t rec = (20 + (size_t) (l4len < 18 ? 18 : l4len) + 15) & ~(size_t) 15;
+    if (pos + rec > c->slot_bytes) {
+      *need = rec;
+      break;
+    }
+    pos += rec;
+  }
+  return i;
+}
+
+int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
-  uint32_t i, start = 0;
+  int rc;
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
-  if (c->npend == 0)
-    return 0;
   HIPCHK(hipSetDevice(c->device));
-  if (zerocopy_ok(c))
-    return flush_zerocopy(c);
-  c->n_staged_flushes++;
-  while (start < c->npend) {
-    const int s = 0;
-    uint8_t *stage = c->h_stage[s];
-    uint64_t *offs = c->h_off[s];
-    size_t pos = 0;
-    tasx_tcp4_params p;
-    uint32_t cnt = 0;
-    for (i = start; i < c->npend; i++) {
-      const uint8_t *ip = c->pend_ip[i];
-      uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-      uint32_t l4len = tl > 20 ? tl - 20 : 0;
-      /* the kernel reads the checksum field of short segments too */
-      uint32_t cp = l4len < 18 ? 18 : l4len;
-      size_t rec = (20 + (size_t) cp + 15) & ~(size_t) 15;
-      if (pos + rec > c->slot_bytes) {
-        if (cnt == 0)
-          return set_err(-EINVAL, "flush: frame of %zu B exceeds the staging slot", rec);
-        break;
-      }
-      memcpy(stage + pos, ip, 20);
-      memcpy(stage + pos + 20, c->pend_l4[i], cp);
-      offs[cnt++] = pos;
-      pos += rec;
-    }
-    /* the kernel reads the pinned records and offsets and writes the results
-     * into pinned memory directly: no copy-engine work on the flush path */
-    memset(&p, 0, sizeof(p));
-    p.base = c->d_hstage;
-    p.off = c->d_hoff;
-    p.out = c->d_hout;
-    p.stride = 0;
-    p.n = cnt;
-    p.ip_off = 0;
-    p.l4_off = 20;
-    p.flags = 0;
-    if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
-      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-    int rc = wait_done(c);
-    if (rc != 0)
+  while (c->npend > 0) {
+    const uint32_t t = c->next_ticket + 1;
+    const int zc = zerocopy_ok(c, c->npend);
+    size_t need = 0;
+    const uint32_t cnt = zc ? c->npend : staged_fit(c, &need);
+    if (cnt == 0)
+      return set_err(-EINVAL, "flush: frame of %zu B exceeds the staging slot", need);
+    /* the slot's previous flush (t - NSLOT) must be complete */
+    if ((rc = flush_wait(c, t - NSLOT)) != 0)
       return rc;
-    for (i = 0; i < cnt; i++) {
-      memcpy(c->pend_ip[start + i] + 10, &c->h_out[s][2 * i], 2);
-      memcpy(c->pend_l4[start + i] + 16, &c->h_out[s][2 * i + 1], 2);
-    }
-    start += cnt;
+    if ((rc = flush_launch(c, t, cnt, zc)) != 0)
+      return rc;
   }
-  c->npend = 0;
+  if (ticket)
+    *ticket = c->next_ticket;
   return 0;
+}
+
+int tasx_flush_poll(unsigned ctx_id, uint32_t ticket)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!ticket_le(ticket, c->next_ticket))
+    return set_err(-EINVAL, "flush ticket %u not submitted (last %u)", ticket, c->next_ticket);
+  return flush_reap(c, ticket);
+}
+
+int tasx_flush_wait(unsigned ctx_id, uint32_t ticket)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!ticket_le(ticket, c->next_ticket))
+    return set_err(-EINVAL, "flush ticket %u not submitted (last %u)", ticket, c->next_ticket);
+  return flush_wait(c, ticket);
+}
+
+int tasx_flush(unsigned ctx_id)
+{
+  uint32_t t;
+  int rc = tasx_flush_submit(ctx_id, &t);
+  return rc ? rc : tasx_flush_wait(ctx_id, t);
 }
 
 /* ---------------------------------------------------------------------- */

@@ -872,83 +872,13 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // general row body.
 enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3 };
 
-template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
+// The row body after the loads: v[] holds the row's chunks (lane gl: chunks
+// gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
+// the general body for a row the fast path cannot take.
+template <int U, int MODE, bool VERIFY, bool OFFS>
+__device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t i, int gl, const uint8_t *fb,
+                                             uint32_t a0, uint32_t hend, bool in_range, const u32x4 (&v)[U])
 {
-  static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
-  static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return;
-  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
-  uint32_t a0;
-  bool row_ok = true;
-  if constexpr (OFFS) {
-    const uint64_t fo = (uint64_t) (uintptr_t) p.base + ldg(p.off, i) + (p.ip_off & ~15u);
-    row_ok = (fo & 15u) == 0u;
-    fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
-    a0 = 0;
-  } else {
-    a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
-  }
-  // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
-  uint32_t have = 65535u;
-  if constexpr (VERIFY && MODE != kHint) {
-    const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
-    have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-  }
-  // the datagram [ip, ip + hend): uniform from the hint, or per row from the
-  // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
-  const uint32_t lo = a0 + 16u * (uint32_t) gl;
-  uint32_t hend;
-  bool in_range = true;
-  u32x4 v[U];
-  if constexpr (MODE == kHint) {
-    hend = p.flen0 - p.ip_off;
-    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kTlFirst) {
-    const uint32_t tl0 = bswap16(ld16nt_off(fb, a0 + (row_ok ? 16u : 0u)).x & 0xffffu);
-    // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
-    // the end never include the masked field; pure ACKs, ip.len 52, qualify)
-    // to 1522 (96 chunks)
-    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kHead5) {
-    v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
-    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
-    // from 51: the last chunk is chunk 4 or later, so lane 15 holds it
-    in_range = row_ok && tl0 >= 51u && tl0 <= 1522u && tl0 <= have;
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4;
-    if (last > 4u) { // the datagram goes on past chunk 4
-      const uint32_t lastoff = a0 + 16u * last;
-      if (gl > 4)
-        v[0] = ld16nt_off(fb, min(lo, lastoff));
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    } else {
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = v[0]; // excluded below; lane 15's v[U-1] = chunk 4, the last one
-    }
-  } else { // kRoom
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, row_ok ? lo + 256u * u : a0);
-    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
-    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-  }
   const uint32_t last = (14u + hend - 1u) >> 4;
   const uint32_t tail = 14u + hend - 16u * last; // bytes of the last chunk inside, 1..16
 
@@ -1034,6 +964,124 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
   }
 }
 
+template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock>
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
+{
+  static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
+  static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
+  uint32_t a0;
+  bool row_ok = true;
+  if constexpr (OFFS) {
+    const uint64_t fo = (uint64_t) (uintptr_t) p.base + ldg(p.off, i) + (p.ip_off & ~15u);
+    row_ok = (fo & 15u) == 0u;
+    fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
+    a0 = 0;
+  } else {
+    a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  }
+  // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
+  uint32_t have = 65535u;
+  if constexpr (VERIFY && MODE != kHint) {
+    const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
+    have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
+  }
+  // the datagram [ip, ip + hend): uniform from the hint, or per row from the
+  // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
+  const uint32_t lo = a0 + 16u * (uint32_t) gl;
+  uint32_t hend;
+  bool in_range = true;
+  u32x4 v[U];
+  if constexpr (MODE == kHint) {
+    hend = p.flen0 - p.ip_off;
+    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  } else if constexpr (MODE == kTlFirst) {
+    const uint32_t tl0 = bswap16(ld16nt_off(fb, a0 + (row_ok ? 16u : 0u)).x & 0xffffu);
+    // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
+    // the end never include the masked field; pure ACKs, ip.len 52, qualify)
+    // to 1522 (96 chunks)
+    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
+    // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
+    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  } else if constexpr (MODE == kHead5) {
+    v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
+    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
+    // from 51: the last chunk is chunk 4 or later, so lane 15 holds it
+    in_range = row_ok && tl0 >= 51u && tl0 <= 1522u && tl0 <= have;
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
+    const uint32_t last = (14u + hend - 1u) >> 4;
+    if (last > 4u) { // the datagram goes on past chunk 4
+      const uint32_t lastoff = a0 + 16u * last;
+      if (gl > 4)
+        v[0] = ld16nt_off(fb, min(lo, lastoff));
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+    } else {
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = v[0]; // excluded below; lane 15's v[U-1] = chunk 4, the last one
+    }
+  } else { // kRoom
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, row_ok ? lo + 256u * u : a0);
+    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
+    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
+    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
+  }
+  tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
+}
+
+// tcp4_tas14_kernel's total_length-first rows as a persistent loop: row r
+// takes frames r, r + R, r + 2R, ... (R rows in the grid) and loads the next
+// frame's total_length while the current frame's data is in flight, so in the
+// steady state a frame costs one dependent memory latency instead of two
+// (stride mode; TX and RX as tcp4_tas14_kernel<kTlFirst>).
+template <int U, bool VERIFY = false, int WPE = 8>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_rows_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t R = gridDim.x * (kBlock / 16);
+  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint8_t *fb = p.base;
+  const uint32_t ipa = p.ip_off & ~15u;
+  uint32_t tln = bswap16(ldg((const uint32_t *) (fb + i * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
+  for (; i < p.n; i += R) { // row-uniform
+    const uint32_t a0 = i * (uint32_t) p.stride + ipa;
+    uint32_t have = 65535u;
+    if constexpr (VERIFY) {
+      const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
+      have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
+    }
+    const uint32_t tl0 = tln;
+    const bool in_range = tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
+    const uint32_t hend = in_range ? tl0 : 20u;
+    const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+    const uint32_t inext = i + R;
+    if (inext < p.n) // the next frame's total_length, in flight with this frame's data
+      tln = bswap16(ldg((const uint32_t *) (fb + inext * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
+    tas14_finish<U, kTlFirst, VERIFY, false>(p, i, gl, fb, a0, hend, in_range, v);
+  }
+}
+
 // Dynamic LDS reserved (never used) by the v_sad_u16 kernels to cap residency
 // at 5 blocks = 20 waves per CU: with ~100 VALU per wave they would otherwise
 // run 8 waves per SIMD, and the extra bytes in flight only lengthen the queue
@@ -1052,20 +1100,20 @@ constexpr uint32_t kOccLds = 30u * 1024u;
 // the launched kernel's name, per calling thread (tasx_last_kernel)
 static thread_local const char *t_last_kernel = "";
 
-template <int G = 16, typename K, typename Prm>
+template <int G = 16, int BS = kBlock, typename K, typename Prm>
 int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
-  // one G-lane group per packet, kBlock / G groups per block: the grid covers
+  // one G-lane group per packet, BS / G groups per block: the grid covers
   // the batch once (measured faster than persistent grids at these batch
   // sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
-  constexpr uint64_t fpb = kBlock / G;
+  constexpr uint64_t fpb = BS / G;
   const uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
   if (blocks == 0)
     return 0;
   if (blocks > 0x7fffffffull)
     return -2;
   t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1248,6 +1296,31 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
   }
 }
 
+// persistent grids: blocks resident at once on the current device (8 waves of
+// 64 VGPRs per SIMD = 8 blocks of 256 threads per CU)
+static uint32_t resident_blocks()
+{
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return (uint32_t) cus * 8u;
+}
+
+template <typename K>
+static int launch_rows(const char *name, K kern, const tasx_tcp4_params &p, uint32_t frames_per_row, hipStream_t s)
+{
+  const uint64_t need = ((uint64_t) p.n + 16u * frames_per_row - 1) / (16u * frames_per_row);
+  uint64_t blocks = frames_per_row ? need : resident_blocks();
+  if (!frames_per_row && blocks > ((uint64_t) p.n + 15u) / 16u)
+    blocks = ((uint64_t) p.n + 15u) / 16u;
+  if (blocks == 0)
+    return 0;
+  t_last_kernel = name;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
@@ -1264,6 +1337,21 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
       mode = m;
     variant = 0;
   }
+  // 12 / 13 / 14: the persistent total_length-first rows (resident grid / 2 /
+  // 4 frames per row) where tcp4_tas14_kernel's stride form applies
+  // 15 / 16 / 17 / 18: tcp4_tas14_kernel<tl_first> (stride mode) in blocks of
+  // 64 / 128 / 512 / 1024 threads instead of 256
+  if (variant >= 15 && variant <= 18 && !tas14_ok(*p) && tas14_nohint_ok(*p)) {
+    switch (variant) {
+    case 15: return launch_groups<16, 64>("tcp4_tas14_kernel<tl_first,bs64>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 64>, *p, s);
+    case 16: return launch_groups<16, 128>("tcp4_tas14_kernel<tl_first,bs128>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 128>, *p, s);
+    case 17: return launch_groups<16, 512>("tcp4_tas14_kernel<tl_first,bs512>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 512>, *p, s);
+    default: return launch_groups<16, 1024>("tcp4_tas14_kernel<tl_first,bs1024>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 1024>, *p, s);
+    }
+  }
+  if (variant >= 12 && variant <= 14 && !tas14_ok(*p) && tas14_nohint_ok(*p))
+    return launch_rows("tcp4_tas14_rows_kernel", tcp4_tas14_rows_kernel<6>, *p,
+                       variant == 12 ? 0u : variant == 13 ? 2u : 4u, s);
   if (variant == 8 && p->l4_off == p->ip_off + 20u) {
     static const uint32_t lds = env_lds("TASX_WAVE_TCP4_LDS", 0u);
     return launch_groups("tcp4_wave_kernel", tcp4_wave_kernel<TASX_WAVE_U>, *p, s, lds);

@@ -73,6 +73,9 @@ SIGNATURES = {
     "tasx_defer_tcp4": (_c_int, [_uns, _vp, _c_u16, _c_u16]),
     "tasx_pending": (_c_int, [_uns]),
     "tasx_flush": (_c_int, [_uns]),
+    "tasx_flush_submit": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
+    "tasx_flush_poll": (_c_int, [_uns, _c_u32]),
+    "tasx_flush_wait": (_c_int, [_uns, _c_u32]),
     "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
     "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
@@ -352,6 +355,22 @@ def pending(ctx_id: int) -> int:
 
 def tx_flush(ctx_id: int) -> None:
     _check(lib().tasx_flush(ctx_id), "tasx_flush")
+
+
+def flush_submit(ctx_id: int) -> int:
+    """Launch every recorded frame's checksums; returns the flush ticket."""
+    t = ctypes.c_uint32()
+    _check(lib().tasx_flush_submit(ctx_id, ctypes.byref(t)), "tasx_flush_submit")
+    return t.value
+
+
+def flush_poll(ctx_id: int, ticket: int) -> bool:
+    """True once flush `ticket` (and every earlier one) has stored its results."""
+    return bool(_check(lib().tasx_flush_poll(ctx_id, ticket), "tasx_flush_poll"))
+
+
+def flush_wait(ctx_id: int, ticket: int) -> None:
+    _check(lib().tasx_flush_wait(ctx_id, ticket), "tasx_flush_wait")
 
 
 def register_frames(ctx_id: int, base_addr: int, nbytes: int) -> None:

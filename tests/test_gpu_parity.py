@@ -28,7 +28,7 @@ def _lib():
 
 
 # variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = {1, 4, 5, 8, 9, 10, 11}
+AB_VARIANTS = set(range(8, 19)) | {1, 4, 5}
 
 
 @contextlib.contextmanager
@@ -573,6 +573,53 @@ def test_zero_copy_flush(oracle):
         xsum.ctx_destroy(3)
 
 
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_async_flush_pipeline(oracle, zero_copy):
+    """tasx_flush_submit / _poll / _wait: tx_flush-sized batches (32 frames,
+    data segments and ACK sizes) submitted back to back with up to 3 in flight
+    per context (the 4th submit completes the 1st), completions in ticket
+    order, each batch's frames finished only when its ticket completes; the
+    staged path and the zero-copy one (frames in a registered pool)."""
+    ctx = 5
+    xsum.ctx_init(ctx, 0, 1 << 20)
+    try:
+        nb, n = 7, 32
+        pay = np.where(np.arange(nb * n) % 3 == 0, 0, (np.arange(nb * n) * 53) % 1449)
+        frames = pktgen.tcp4_frames(nb * n, payload=pay, stride=2048, seed=73)
+        ref = frames.copy()
+        oracle.tcp4_batch(ref, nb * n, stride=2048, inplace=True)
+        if zero_copy:
+            pin = xsum.PinnedBuffer(frames.size)
+            pin.array[:] = frames
+            xsum.register_frames(ctx, pin.addr, pin.nbytes)
+            buf, addr = pin.array, pin.addr
+        else:
+            buf, addr = frames, frames.ctypes.data
+        assert xsum.flush_submit(ctx) == 0 and xsum.flush_poll(ctx, 0)   # nothing submitted yet
+        tickets = []
+        for b in range(nb):
+            for i in range(n):
+                xsum.tcp_checksums(ctx, addr + (b * n + i) * 2048)
+            tickets.append(xsum.flush_submit(ctx))
+            assert xsum.pending(ctx) == 0
+        assert tickets == list(range(1, nb + 1))
+        with pytest.raises(xsum.TasxError):
+            xsum.flush_poll(ctx, nb + 1)                               # not submitted
+        # poll the last ticket until it completes; earlier ones are then done too
+        while not xsum.flush_poll(ctx, tickets[-1]):
+            pass
+        assert all(xsum.flush_poll(ctx, t) for t in tickets)
+        np.testing.assert_array_equal(buf, ref)
+        assert xsum.flush_submit(ctx) == nb                            # empty: the last ticket
+        xsum.flush_wait(ctx, nb)
+        z, st = xsum.ctx_stats(ctx)
+        assert (z, st) == ((nb, 0) if zero_copy else (0, nb))
+        if zero_copy:
+            pin.free()
+    finally:
+        xsum.ctx_destroy(ctx)
+
+
 def test_zero_copy_pageable_region(oracle):
     """hipHostRegister of ordinary (numpy) memory as the frame region."""
     xsum.ctx_init(4, 0, 1 << 20)
@@ -768,7 +815,7 @@ def test_verify_uniform_hint(oracle, variant):
 # rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
 
 @pytest.mark.parametrize("room", [80, 1536, 2048])
-@pytest.mark.parametrize("variant", [0, 9, 10, 11])
+@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
 def test_tcp4_rooms_every_row_mode(oracle, room, variant):
     """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
     selection and every forced row mode (9 total_length first, 10 head-5, 11
