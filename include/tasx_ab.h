@@ -12,6 +12,13 @@
  *      datagrams (TCP4; needs l4_off == ip_off + 20)
  *   9, 10, 11  tcp4_tas14_kernel without a uniform hint forced into its
  *      total_length-first / head-5 / whole-room row mode where the room allows
+ *   12, 13, 14  tcp4_tas14_rows_kernel: persistent total_length-first rows
+ *      (resident grid / 2 / 4 frames per row; stride mode, no uniform hint)
+ *   15..18  tcp4_tas14_kernel<tl_first> in blocks of 64 / 128 / 512 / 1024
+ *   19  tcp4_mix_kernel (16 frames per wave, short frames one per lane, data
+ *      frames compacted onto rows; TASX_MIX_F8=1: 8 frames per wave) where a
+ *      room of 80 B allows; measured slower than the default for data/ACK
+ *      mixes
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
  * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
  */

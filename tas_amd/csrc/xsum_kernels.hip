@@ -870,12 +870,12 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned loads
 // only the aligned chunk holding the IPv4 header start and is redone by the
 // general row body.
-enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3 };
+enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */ };
 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
 // the general body for a row the fast path cannot take.
-template <int U, int MODE, bool VERIFY, bool OFFS>
+template <int U, int MODE, bool VERIFY, bool OFFS, bool FALLBACK = true>
 __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t i, int gl, const uint8_t *fb,
                                              uint32_t a0, uint32_t hend, bool in_range, const u32x4 (&v)[U])
 {
@@ -952,7 +952,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
       st8(ip + 37, tcpc >> 8);
     }
   }
-  if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
+  if (FALLBACK && __builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
     const bool rbad = MODE == kHint ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
     if (rbad) {
@@ -1043,6 +1043,136 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
   tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
 }
+
+#ifdef TASX_AB
+// A whole short datagram (ip.len 38..66: a pure ACK, flow_tx_ack
+// fast_flows.c:957-1030, is 52) in ONE lane: c[] = chunks 0..4 of the frame
+// (IPv4 at a0 + 14, tcp4_tas14_kernel's chunk map), both results stored.
+__device__ __forceinline__ void tas14_short_lane(const tasx_tcp4_params &p, uint32_t i, const uint8_t *fb, uint32_t a0,
+                                                 uint32_t tl, const u32x4 (&c)[5])
+{
+  const uint32_t addrs = sadw(c[1].z & 0xffff0000u, sadw(c[1].w, sadw(c[2].x & 0xffffu, 0u))); // src, dst
+  const uint32_t ph = sadw(c[1].y & 0xff000000u, addrs);                                      // + proto
+  const uint32_t ipsum = sadw(c[0].w & 0xffff0000u, sadw(c[1].x, sadw(c[1].y, addrs)));      // ip.chksum left out
+  // L4 = frame bytes [34, 14 + tl): chunk 2 from byte 2, chunk 3 without
+  // tcp.chksum (its bytes 2..3), chunk 4 up to the datagram's end
+  const int end = 14 + (int) tl; // 52..80
+  u32x4 c3 = mask_chunk(c[3], 0, min(end - 48, 16));
+  c3.x &= 0x0000ffffu;
+  uint32_t l4 = sad4(mask_chunk(c[2], 2, 16), 0u);
+  l4 = sad4(c3, l4);
+  l4 = sad4(mask_chunk(c[4], 0, max(end - 64, 0)), l4);
+  const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
+  const uint32_t r = fold32_to_16(l4) + fold32_to_16(ph) + bswap16(tl - 20u);
+  const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
+  if (p.out)
+    stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
+  if (p.flags & TASX_F_INPLACE) {
+    uint8_t *ip = (uint8_t *) fb + a0 + 14u;
+    st8(ip + 10, ipc);
+    st8(ip + 11, ipc >> 8);
+    st8(ip + 36, tcpc);
+    st8(ip + 37, tcpc >> 8);
+  }
+}
+
+// tcp4_mix_kernel: TX batches that mix data segments and pure ACKs (what
+// tx_flush sends: flow_tx_segment's ~1.5 KB frames and flow_tx_ack's 66 B
+// frames, fastemu.c:544-566), TAS frames in stride mode, a room of >= 80 B.
+// One wave takes 16 frames.  Phase 1: lane l < 16 loads chunks 0..4 of frame
+// 16w + l (a whole ACK) and classifies the frame by its own total_length:
+// short (38..66: finished by that lane alone, one memory latency), data
+// (67..1522) or other (the general body, tcp4_tas_frame).  Phase 2: the data
+// frames, compacted by a forward lane permute, go 4 per pass to the wave's
+// 16-lane rows, and every pass's loads are in flight before the first is
+// summed (tcp4_tas14_kernel's row body).  kTlFirst spends a 16-lane row and
+// a second dependent latency on every ACK, and needs two generations of
+// resident waves for 64K frames; here an ACK costs one lane and the 64K-frame
+// batch fits one generation (4 waves per SIMD x 16 frames).
+// A/B only (variant 19; TASX_MIX_F8=1: 8 frames per wave): bit-exact, but
+// slower than kTlFirst wherever data frames are present (64K frames in 2048 B
+// rooms, 0 / 50 / 100 % ACKs: 19.5-20.2 / 12.6-12.9 / 6.5-6.6 us with 16
+// frames per wave, 18.7 / 12.2-12.3 / 6.1 us with 8, against 16.9-17.3 /
+// 10.7-10.9 / 6.9 us; profiles/r02/r02m, r02n): a wave issues its data only
+// after the slowest of its frames' phase-1 loads, a kTlFirst row as soon as
+// its own total_length lands.
+template <int U, int F = 16>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(F == 16 ? 4 : 6))) void tcp4_mix_kernel(tasx_tcp4_params p)
+{
+  static_assert(U == 6, "96 chunks cover the 1522-byte datagram bound");
+  static_assert(F == 8 || F == 16, "frames per wave: 2 or 4 passes of 4 rows");
+  constexpr int NP = F / 4;
+  const int lane = (int) (threadIdx.x & 63u), gl = lane & 15, row = lane >> 4;
+  const uint32_t w0 = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) * (uint32_t) F; // the wave's first frame
+  if (w0 >= p.n)
+    return; // the whole wave leaves together
+  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets (tas14_stride_ok)
+  const uint32_t ipa = p.ip_off & ~15u, nf = min(p.n - w0, (uint32_t) F);
+  const uint32_t st = (uint32_t) p.stride;
+
+  // phase 1: frame w0 + lane on lanes 0..15
+  const bool mine = lane < 16 && (uint32_t) lane < nf;
+  const uint32_t a0 = (w0 + (uint32_t) gl) * st + ipa;
+  u32x4 c[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    c[k] = u32x4{0u, 0u, 0u, 0u};
+  if (mine) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      c[k] = ld16nt_off(fb, a0 + 16u * (uint32_t) k);
+  }
+  const uint32_t tl = bswap16(c[1].x & 0xffffu);
+  const bool shortf = mine && tl >= 38u && tl <= 66u;
+  const bool data = mine && tl > 66u && tl <= 1522u;
+  const bool other = mine && !shortf && !data;
+  const uint64_t dm = __builtin_amdgcn_ballot_w64(data), om = __builtin_amdgcn_ballot_w64(other);
+  // compaction: data frame of rank r -> lane r, other frame of rank r -> lane
+  // 32 + r (everything else lands in lanes 16..31 / 48..63, never read)
+  const uint32_t below = (1u << (lane & 31)) - 1u; // lanes < 16 only matter
+  const uint32_t rd = (uint32_t) __builtin_popcount((uint32_t) dm & below);
+  const uint32_t ro = (uint32_t) __builtin_popcount((uint32_t) om & below);
+  const int dst = data ? (int) rd : other ? 32 + (int) ro : lane < 16 ? 48 + lane : 16 + (lane & 15);
+  const uint32_t pk = (uint32_t) __builtin_amdgcn_ds_permute(dst * 4, (int) ((uint32_t) gl | (tl << 8)));
+  if (shortf)
+    tas14_short_lane(p, w0 + (uint32_t) gl, fb, a0, tl, c);
+
+  // phase 2: data frames 4 per pass, all passes' loads issued first.  The
+  // loads are unconditional (an idle row reads the wave's first frame's
+  // chunk 1, a line phase 1 just fetched) so that the waits before each pass
+  // count exactly the loads ahead of it: under a branch the compiler must wait
+  // for all of them before the first pass.
+  const uint32_t nd = (uint32_t) __builtin_popcountll(dm);
+  u32x4 v[NP][U];
+  uint32_t q[NP];
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps) {
+    q[ps] = (uint32_t) __shfl((int) pk, 4 * ps + row, 64);
+    const bool act = 4u * ps + (uint32_t) row < nd;
+    const uint32_t hend = act ? q[ps] >> 8 : 20u;
+    const uint32_t r0 = (w0 + (act ? (q[ps] & 15u) : 0u)) * st + ipa;
+    const uint32_t lastoff = r0 + 16u * ((14u + hend - 1u) >> 4), lo = r0 + 16u * (uint32_t) gl;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[ps][u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  }
+#pragma unroll
+  for (int ps = 0; ps < NP; ++ps) {
+    if (nd > 4u * ps && 4u * ps + (uint32_t) row < nd) {
+      const uint32_t r0 = (w0 + (q[ps] & 15u)) * st + ipa;
+      tas14_finish<U, kTlFirst, false, false, false>(p, w0 + (q[ps] & 15u), gl, fb, r0, q[ps] >> 8, true, v[ps]);
+    }
+  }
+
+  // other frames (total_length outside 38..1522): the general body, 4 per pass
+  const uint32_t no = (uint32_t) __builtin_popcountll(om);
+  for (uint32_t o = 0; o < no; o += 4u) {
+    const uint32_t qo = (uint32_t) __shfl((int) pk, 32 + (int) o + row, 64);
+    if (o + (uint32_t) row < no)
+      tcp4_tas_frame<U, 0, 16, false>(p, w0 + (qo & 15u), gl, lane & ~15);
+  }
+}
+#endif
 
 // tcp4_tas14_kernel's total_length-first rows as a persistent loop: row r
 // takes frames r, r + R, r + 2R, ... (R rows in the grid) and loads the next
@@ -1283,7 +1413,13 @@ template <bool OFFS>
 static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
 {
   const uint32_t lds = TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u);
-  switch (mode) {
+  switch (OFFS && mode == kMix ? kTlFirst : mode) { // the mix kernel is a stride-mode form
+#ifdef TASX_AB
+  case kMix:
+    if (getenv("TASX_MIX_F8"))
+      return launch_groups<8>("tcp4_mix_kernel<f8>", tcp4_mix_kernel<6, 8>, p, s);
+    return launch_groups<4>("tcp4_mix_kernel", tcp4_mix_kernel<6>, p, s);
+#endif
   case kRoom:
     return launch_groups(OFFS ? "tcp4_tas14_kernel<room,offs>" : "tcp4_tas14_kernel<room>",
                          tcp4_tas14_kernel<6, kRoom, false, 8, OFFS>, p, s, lds);
@@ -1330,10 +1466,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 #ifdef TASX_AB
   // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
   // where its room requirement holds (else as 0)
-  if (variant >= 9 && variant <= 11) {
+  if ((variant >= 9 && variant <= 11) || variant == 19) {
     const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
-    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : kRoom;
-    if ((m == kTlFirst) || (m == kHead5 && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
+    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : kMix;
+    if ((m == kTlFirst) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
       mode = m;
     variant = 0;
   }

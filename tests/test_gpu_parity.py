@@ -28,7 +28,7 @@ def _lib():
 
 
 # variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = set(range(8, 19)) | {1, 4, 5}
+AB_VARIANTS = set(range(8, 20)) | {1, 4, 5}
 
 
 @contextlib.contextmanager
@@ -815,11 +815,11 @@ def test_verify_uniform_hint(oracle, variant):
 # rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
 
 @pytest.mark.parametrize("room", [80, 1536, 2048])
-@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
+@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 def test_tcp4_rooms_every_row_mode(oracle, room, variant):
     """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
     selection and every forced row mode (9 total_length first, 10 head-5, 11
-    whole room) over data segments, ACKs, total_length 0..90 and 1523..2034
+    whole room, 19 the mix kernel) over data segments, ACKs, total_length 0..90 and 1523..2034
     (rows the fast path hands to the general body), with no hint, per-frame
     hints (exact, short, long) and a uniform hint; out of place and in place."""
     n = 5000
@@ -874,6 +874,45 @@ def test_tcp4_room_selects_row_mode():
         xsum.tcp4_cksum_batch(frames, n, **kw)
         assert xsum.last_kernel() == name, (kw, xsum.last_kernel())
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("ip_off", [14, 30])
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 4099])
+def test_tcp4_mix_kernel_edges(oracle, ip_off, n):
+    """tcp4_mix_kernel (A/B variant 19: per-frame hints + room): batches that end inside a
+    wave's 16 frames, the IPv4 header at 14 and at 30 (the frame start 16 B
+    into the stride slot), every total_length from 0 to 1600 (short frames
+    38..66 done by one lane, data frames 67..1522 by rows, the rest by the
+    general body) and waves with 0..16 data frames; out of place and in place."""
+    stride = 2048
+    rng = np.random.default_rng(1000 + n + ip_off)
+    tl = rng.permutation(np.arange(n) % 1601) if n > 1 else np.array([52])
+    if n >= 64:  # whole waves of one kind: all short, all data, all general
+        tl[:16], tl[16:32], tl[32:48] = 52, 1500, 1600
+    pay = np.clip(tl - 52, 0, pktgen.TCP_MSS).astype(np.int64)
+    base = pktgen.tcp4_frames(n, payload=pay, stride=stride, seed=n)
+    frames = np.zeros_like(base)
+    sh = ip_off - 14
+    frames.reshape(n, stride)[:, sh:] = base.reshape(n, stride)[:, :stride - sh]
+    f = frames.reshape(n, stride)
+    f[:, ip_off + 2] = (tl >> 8) & 0xFF
+    f[:, ip_off + 3] = tl & 0xFF
+    exp = oracle.tcp4_batch(frames.copy(), n, stride=stride, ip_off=ip_off, l4_off=ip_off + 20)
+    hint = to_dev((ip_off + tl).astype(np.int32))
+    kw = dict(stride=stride, ip_off=ip_off, l4_off=ip_off + 20, frame_len=hint, room=stride)
+    d = to_dev(frames)
+    with kernel_variant(19):
+        got = u16(xsum.tcp4_cksum_batch(d, n, **kw))
+        assert xsum.last_kernel() == "tcp4_mix_kernel"
+        np.testing.assert_array_equal(got, exp)
+        xsum.tcp4_cksum_batch(d, n, inplace=True, want_out=False, **kw)
+    h = d.cpu().numpy().reshape(n, stride)
+    np.testing.assert_array_equal(h[:, ip_off + 10:ip_off + 12].copy().view(np.uint16).ravel(), exp[0::2])
+    np.testing.assert_array_equal(h[:, ip_off + 36:ip_off + 38].copy().view(np.uint16).ravel(), exp[1::2])
+    # nothing but the two fields changed
+    h[:, ip_off + 10:ip_off + 12] = f[:, ip_off + 10:ip_off + 12]
+    h[:, ip_off + 36:ip_off + 38] = f[:, ip_off + 36:ip_off + 38]
+    np.testing.assert_array_equal(h, f)
 
 
 @pytest.mark.parametrize("ip_off", [14, 30])
