@@ -990,7 +990,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     mix = None
     if not args.no_flushmix:
         mw = FlushMixWorkload(min(rot, 12), pktgen.SEED + 500 + rank)
-        mix = leg(mw.loop(), mw.bytes_per_step, args, ws, FlushMixWorkload.desc, "tcp4_tas14_kernel<tl_first>")
+        mix = leg(mw.loop(), mw.bytes_per_step, args, ws, FlushMixWorkload.desc, "tcp4_tas14_kernel<hints>")
         mix["parity"] = "tests/test_bench_configs.py::test_bench_flush_mix"
         del mw
         torch.cuda.empty_cache()

@@ -108,8 +108,9 @@ int tasx_tcp4_cksum_batch_dev_hint(void *base, const uint64_t *off,
  * a full MTU (IPv4 at 14 mod 16: room >= 1536 from the 16-byte aligned start)
  * is read at the uniform-hint speed (rows load the whole MTU at once and mask
  * by their own total_length).  Per-frame hints mark a data/ACK mix, whose rows
- * read their own total_length first instead (whole-room reads would cost every
- * ACK 1.5 KB).  Results still follow ip.total_length only. */
+ * read exactly their hinted bytes instead (whole-room reads would cost every
+ * ACK 1.5 KB); a hint beyond the room is not trusted for reads.  Results still
+ * follow ip.total_length only. */
 int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
     uint64_t stride, const uint32_t *flen, uint32_t flen0, uint32_t room,
     uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,

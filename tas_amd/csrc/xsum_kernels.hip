@@ -858,6 +858,12 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 //   kTlFirst the row reads chunk 1 (ip.total_length; all 16 lanes, one line)
 //            first, then exactly its datagram: two dependent latencies, no
 //            byte read past ip.total_length (DPDK's own trust in the header).
+//   kHintArr per-frame hints (the mbuf data_len of each frame): the row's own
+//            hint fixes its geometry and lane 15 checks it against
+//            ip.total_length after the loads (a mismatch, or a hint outside
+//            [ip_off + 38, ip_off + 1522] or beyond the room, is redone by
+//            the general body).  One dependent latency after the hint load,
+//            which 4 rows share a line of.
 //   kHead5   chunks 0..4 (a whole pure ACK, ip.len 52) are loaded with the
 //            total_length, the rest after it: ACK rows take one latency, data
 //            rows two.  Needs a room of 80 B (the chunk-4 read).
@@ -870,7 +876,8 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned loads
 // only the aligned chunk holding the IPv4 header start and is redone by the
 // general row body.
-enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */ };
+enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */,
+                       kHintArr = 5 /* per-frame hints as the geometry */ };
 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
@@ -926,7 +933,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  const bool bad = MODE == kHint ? tl15 != hend : !in_range; // kHint: meaningful on lane 15
+  const bool bad = MODE == kHint ? tl15 != hend : MODE == kHintArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
     if (gl == 15 && !bad) {
@@ -954,7 +961,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   if (FALLBACK && __builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
-    const bool rbad = MODE == kHint ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
+    const bool rbad = (MODE == kHint || MODE == kHintArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
     if (rbad) {
       if constexpr (OFFS)
         tcp4_frame_row<3, VERIFY>(p, i, gl);
@@ -1010,6 +1017,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
+    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+  } else if constexpr (MODE == kHintArr) {
+    // the row's own hint (mbuf data_len) fixes its geometry; lane 15 checks
+    // it against total_length afterwards, as kHint does for a uniform hint
+    const uint32_t h = ldg(p.flen, i);
+    const uint32_t hl = h > p.ip_off ? h - p.ip_off : 0u;
+    in_range = row_ok && hl >= 38u && hl <= 1522u && (!p.room || h <= p.room); // reads stay inside the room
+    hend = in_range ? hl : (row_ok ? 20u : 1u);
     const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1314,8 +1332,8 @@ static bool tas14_ok(const tasx_tcp4_params &p)
   return ((14u + (p.flen0 - p.ip_off) + 15u) >> 4) <= 16u * 6u;
 }
 
-// ... without a uniform hint (per-frame hints only steer reads: each row reads
-// its own total_length), stride mode or frames by an offsets array (IPv4 at 14
+// ... without a uniform hint (per-frame hints only steer reads: a row's
+// results follow its own total_length), stride mode or frames by an offsets array (IPv4 at 14
 // mod 16 from the frame start; frames not 16-byte aligned are checked per row)
 static bool tas14_nohint_ok(const tasx_tcp4_params &p)
 {
@@ -1333,12 +1351,17 @@ static bool tas14_offs_ok(const tasx_tcp4_params &p)
 // reads cost every ACK row 1.5 KB (16.0 us at any ACK share) and total_length
 // first wins (25 / 50 / 75 % ACKs: 13.6 / 10.6 / 8.5 us); the head-5 mode
 // (an ACK's 80 bytes with the total_length) lost to it everywhere but all-ACK
-// batches (6.3 against 6.8 us) and is an A/B variant (10).
-// tools/ackmix_probe.py, profiles/r02/r02d_ackmix_modes.jsonl.
+// batches (6.3 against 6.8 us) and is an A/B variant (10).  With per-frame
+// hints each row takes its own hint as its geometry (kHintArr: no dependent
+// total_length read; 0 / 25 / 50 / 75 % ACKs 16.5 / 13.2 / 10.4-10.5 / 8.3 us
+// against 17.0 / 13.6-13.7 / 10.6-10.8 / 8.6 us, all-ACK 7.2 against 6.9).
+// tools/ackmix_probe.py, profiles/r02/r02d_ackmix_modes.jsonl, r02o.
 static int tas14_mode(const tasx_tcp4_params &p)
 {
   const uint32_t from_a0 = p.room > (p.ip_off & ~15u) ? p.room - (p.ip_off & ~15u) : 0u;
-  return !p.flen && from_a0 >= 1536u ? kRoom : kTlFirst;
+  if (p.flen)
+    return kHintArr;
+  return from_a0 >= 1536u ? kRoom : kTlFirst;
 }
 
 // completion word: stream-ordered after the work before it, one lane stores
@@ -1414,6 +1437,9 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
 {
   const uint32_t lds = TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u);
   switch (OFFS && mode == kMix ? kTlFirst : mode) { // the mix kernel is a stride-mode form
+  case kHintArr:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,offs>" : "tcp4_tas14_kernel<hints>",
+                         tcp4_tas14_kernel<6, kHintArr, false, 8, OFFS>, p, s, lds);
 #ifdef TASX_AB
   case kMix:
     if (getenv("TASX_MIX_F8"))
@@ -1466,10 +1492,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 #ifdef TASX_AB
   // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
   // where its room requirement holds (else as 0)
-  if ((variant >= 9 && variant <= 11) || variant == 19) {
+  if ((variant >= 9 && variant <= 11) || variant == 19 || variant == 20) {
     const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
-    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : kMix;
-    if ((m == kTlFirst) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
+    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : variant == 19 ? kMix : kHintArr;
+    if ((m == kTlFirst) || (m == kHintArr && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
       mode = m;
     variant = 0;
   }

@@ -76,7 +76,7 @@ def test_bench_flush_mix(oracle):
     per-frame hints and the mbuf room (tasx_tcp4_cksum_batch_dev_room)."""
     mw = bench.FlushMixWorkload(1, pktgen.SEED + 500)
     mw.loop()(0, 1)
-    assert xsum.last_kernel() == "tcp4_tas14_kernel<tl_first>"
+    assert xsum.last_kernel() == "tcp4_tas14_kernel<hints>"
     exp = oracle.tcp4_batch(mw.host.copy(), mw.n, stride=mw.stride)
     np.testing.assert_array_equal(host(mw.outs[0]).view(np.uint16), exp)
 

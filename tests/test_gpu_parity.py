@@ -28,7 +28,7 @@ def _lib():
 
 
 # variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = set(range(8, 20)) | {1, 4, 5}
+AB_VARIANTS = set(range(8, 21)) | {1, 4, 5}
 
 
 @contextlib.contextmanager
@@ -815,7 +815,7 @@ def test_verify_uniform_hint(oracle, variant):
 # rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
 
 @pytest.mark.parametrize("room", [80, 1536, 2048])
-@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
+@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20])
 def test_tcp4_rooms_every_row_mode(oracle, room, variant):
     """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
     selection and every forced row mode (9 total_length first, 10 head-5, 11
@@ -849,8 +849,8 @@ def test_tcp4_rooms_every_row_mode(oracle, room, variant):
 
 def test_tcp4_room_selects_row_mode():
     """Which tcp4_tas14_kernel mode a call takes (tasx_last_kernel): a full-MTU
-    room and no per-frame hints -> whole-room rows; per-frame hints or less
-    room -> total_length first; a uniform hint -> the hinted kernel; an offsets
+    room and no per-frame hints -> whole-room rows; per-frame hints -> each
+    row's hint as its geometry; neither -> total_length first; a uniform hint -> the hinted kernel; an offsets
     array -> the OFFS forms."""
     n = 64
     frames = to_dev(pktgen.tcp4_frames(n, stride=2048))
@@ -862,11 +862,11 @@ def test_tcp4_room_selects_row_mode():
         (dict(stride=2048, room=1536), "tcp4_tas14_kernel<room>"),
         (dict(stride=2048, room=1535), "tcp4_tas14_kernel<tl_first>"),
         (dict(stride=2048, room=79), "tcp4_tas14_kernel<tl_first>"),
-        (dict(stride=2048, room=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first>"),
-        (dict(stride=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first>"),
+        (dict(stride=2048, room=2048, frame_len=flen), "tcp4_tas14_kernel<hints>"),
+        (dict(stride=2048, frame_len=flen), "tcp4_tas14_kernel<hints>"),
         (dict(stride=2048, room=2048, frame_len=1514), "tcp4_tas14_kernel<hint>"),
         (dict(offsets=offs, room=2048), "tcp4_tas14_kernel<room,offs>"),
-        (dict(offsets=offs, room=2048, frame_len=flen), "tcp4_tas14_kernel<tl_first,offs>"),
+        (dict(offsets=offs, room=2048, frame_len=flen), "tcp4_tas14_kernel<hints,offs>"),
         (dict(offsets=offs), "tcp4_tas14_kernel<tl_first,offs>"),
         (dict(stride=2048, ip_off=14, l4_off=38), "tcp4_frame_kernel"),
     ]
