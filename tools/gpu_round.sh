@@ -4,7 +4,7 @@
 # kernel-trace summary of the bench.  Each step has its own time limit; a
 # crash / timeout / abort ends the script.  Usage: bash tools/gpu_round.sh TAG
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -23,9 +23,9 @@ step bench 400 python bench.py
 for w in mixed shard8m tso; do
   step bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3
 done
-# the N>1 code path (2 ranks on this one GPU; gloo carries the barrier and the
-# two scalar reductions, as TASX_DIST_BACKEND allows)
-step bench_n2 300 env TASX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts --no-flushmix
+# the N>1 code path: bench.py spawns 2 ranks itself; --rehearse lets them
+# share this one GPU (gloo control plane; not a scaling measurement)
+step bench_n2 300 python bench.py --gpus 2 --rehearse --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts --no-flushmix --no-e2e
 export TMPDIR=/tmp
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --no-flushmix --steps 100 --warmup 10
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --steps 100 --warmup 10
 echo done
