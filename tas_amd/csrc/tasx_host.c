@@ -788,17 +788,30 @@ static int zerocopy_ok(const struct tasx_ctx *c, uint32_t n)
   return 1;
 }
 
+/* staged record of a frame with ip.total_length tl: the L4 bytes copied (the
+ * kernel reads the checksum field of short segments too) and the record size
+ * (14-byte lead + IPv4 header + L4, 16-byte multiple) */
+static uint32_t staged_l4(uint32_t tl)
+{
+  const uint32_t l4len = tl > 20 ? tl - 20 : 0;
+  return l4len < 18 ? 18 : l4len;
+}
+static size_t staged_rec(uint32_t tl)
+{
+  return ((size_t) TASX_TAS_IP_OFF + 20 + staged_l4(tl) + 15) & ~(size_t) 15;
+}
+
 /* Submit the first `cnt` pending frames as flush `t` into slot t % NSLOT
  * (whose previous flush the caller has completed), and drop them from the
  * open batch.
  *   zero-copy: every frame in the registered region, TAS layout: the kernel
  *     reads the frames over PCIe (only the bytes it sums) and stores both
- *     fields in place; descriptors (offset, frame-length hint) from pinned
- *     memory.
- *   staged: [20-byte IPv4 header | L4 segment] of each frame gathered into the
- *     slot's pinned staging (16-byte aligned records: the sums are relative to
- *     the header / segment start, so where a record sits does not change
- *     them); the kernel reads the records and writes the results to pinned
+ *     fields in place; descriptors (frame-start offset, frame-length hint)
+ *     from pinned memory.
+ *   staged: [14-byte lead | 20-byte IPv4 header | L4 segment] of each frame
+ *     gathered into the slot's pinned staging (16-byte aligned records, TAS's
+ *     frame layout: the sums are relative to the header / segment start, so
+ *     where a record sits does not change them); the kernel reads the records and writes the results to pinned
  *     memory directly (no copy-engine work), and the completion copies them
  *     into the frames. */
 static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
@@ -806,40 +819,49 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   const int s = (int) (t % NSLOT);
   struct flush_slot *f = &c->fl[s];
   tasx_tcp4_params p;
-  uint32_t i;
+  uint32_t i, lead = TASX_TAS_IP_OFF;
   memset(&p, 0, sizeof(p));
   p.n = cnt;
-  p.ip_off = 0;
-  p.l4_off = 20;
   p.off = f->d_off;
+  p.flen = f->d_flen;
+#ifdef TASX_AB
+  if (getenv("TASX_FLUSH_HEADER_RECORDS")) /* A/B: round-1 records at the IPv4 header */
+    lead = 0;
+#endif
   if (zc) {
+    /* frame starts (ip - 14) where the region holds them: the TAS-layout
+     * kernels (tcp4_tas14_kernel<hints,offs>); else records at the header */
+    for (i = 0; i < cnt && lead; i++)
+      if (c->pend_ip[i] < c->zc_host + TASX_TAS_IP_OFF)
+        lead = 0;
     for (i = 0; i < cnt; i++) {
       const uint8_t *ip = c->pend_ip[i];
       const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-      c->h_off[s][i] = (uint64_t) (ip - c->zc_host);
-      f->h_flen[i] = (tl < 20 ? 20 : tl);
+      c->h_off[s][i] = (uint64_t) (ip - lead - c->zc_host);
+      f->h_flen[i] = lead + (tl < 20 ? 20 : tl);
     }
     p.base = c->zc_dev;
     p.flags = TASX_F_INPLACE;
-    p.flen = f->d_flen;
     c->n_zerocopy_flushes++;
   } else {
     size_t pos = 0;
     for (i = 0; i < cnt; i++) {
       const uint8_t *ip = c->pend_ip[i];
       const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-      const uint32_t l4len = tl > 20 ? tl - 20 : 0;
-      /* the kernel reads the checksum field of short segments too */
-      const uint32_t cp = l4len < 18 ? 18 : l4len;
-      memcpy(c->h_stage[s] + pos, ip, 20);
-      memcpy(c->h_stage[s] + pos + 20, c->pend_l4[i], cp);
+      /* TAS's frame layout in the slot: 14 bytes of (unread) lead, the IPv4
+       * header at 14 mod 16, the L4 segment right after it */
+      memcpy(c->h_stage[s] + pos + lead, ip, 20);
+      memcpy(c->h_stage[s] + pos + lead + 20, c->pend_l4[i], staged_l4(tl));
       c->h_off[s][i] = pos;
-      pos += (20 + (size_t) cp + 15) & ~(size_t) 15;
+      f->h_flen[i] = lead + (tl < 20 ? 20 : tl);
+      pos += staged_rec(tl);
     }
     p.base = f->d_stage;
     p.out = f->d_out;
     c->n_staged_flushes++;
   }
+  p.ip_off = lead;
+  p.l4_off = lead + 20;
   memcpy(f->ip, c->pend_ip, (size_t) cnt * sizeof(*f->ip));
   memcpy(f->l4, c->pend_l4, (size_t) cnt * sizeof(*f->l4));
   f->n = cnt;
@@ -865,9 +887,7 @@ static uint32_t staged_fit(const struct tasx_ctx *c, size_t *need)
   uint32_t i;
   for (i = 0; i < c->npend; i++) {
     const uint8_t *ip = c->pend_ip[i];
-    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
-    const uint32_t l4len = tl > 20 ? tl - 20 : 0;
-    const size_t rec = (20 + (size_t) (l4len < 18 ? 18 : l4len) + 15) & ~(size_t) 15;
+    const size_t rec = staged_rec(((uint32_t) ip[2] << 8) | ip[3]);
     if (pos + rec > c->slot_bytes) {
       *need = rec;
       break;

@@ -578,8 +578,8 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 // descriptor's room (the mbuf data room) covers the frame's last 16-byte
 // chunk, that chunk is written whole, its bytes past the frame with their own
 // values, instead of by dword and byte stores.
-template <int U, bool NTS>
-__global__ __launch_bounds__(kBlock) void tx_segment_tas_kernel(tasx_txseg_params p)
+template <int U, bool NTS, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
@@ -757,6 +757,8 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 4: tasx_note_kernel("tx_segment_kernel"); hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;  // aligned-gather kernel
   case 5: tasx_note_kernel("tx_segment_u_kernel"); hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // general layout
   case 6: tasx_note_kernel("tx_segment_tas_kernel<plain>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // plain stores
+  case 7: tasx_note_kernel("tx_segment_tas_kernel<wpe6>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 6>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 80 VGPRs
+  case 8: tasx_note_kernel("tx_segment_tas_kernel<wpe8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 64 VGPRs
   default: break;
   }
 #else

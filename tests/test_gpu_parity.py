@@ -574,6 +574,57 @@ def test_zero_copy_flush(oracle):
 
 
 @pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("shift", [0, 1, 9])
+def test_flush_records_as_frame_starts(oracle, zero_copy, shift):
+    """tasx_flush hands its records over as TAS frame starts (IPv4 at 14, TCP
+    at 34, per-frame hints 14 + total_length) so both flush paths take
+    tcp4_tas14_kernel<hints,offs>: frames shifted off 16-byte alignment (rows
+    redone by the general row body), total_length 0..60 next to data
+    segments, and -- zero-copy -- a region that starts at a frame's IPv4
+    header (no room for the 14-byte lead: that flush keeps header records)."""
+    ctx = 6
+    xsum.ctx_init(ctx, 0, 1 << 20)
+    try:
+        n = 40
+        pay = np.where(np.arange(n) % 4 == 0, 0, (np.arange(n) * 37) % 1449)
+        frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=81 + shift)
+        f = frames.reshape(n, 2048)
+        short = np.arange(0, n, 5)
+        tl = (np.arange(len(short)) * 7) % 61           # 0, 7, ..., 56: the general body's cases
+        f[short, 16] = tl >> 8
+        f[short, 17] = tl & 0xFF
+        buf = np.zeros(n * 2048 + 64, np.uint8)
+        if zero_copy:
+            pin = xsum.PinnedBuffer(buf.size)
+            buf, base = pin.array, pin.addr
+        else:
+            base = buf.ctypes.data
+        view = buf[shift:shift + n * 2048].reshape(n, 2048)
+        view[:] = f
+        ref = f.copy()
+        oracle.tcp4_batch(ref.reshape(-1), n, stride=2048, inplace=True)
+        if zero_copy:
+            # the region starts at frame 0's IPv4 header: frame 0 has no lead
+            xsum.register_frames(ctx, base + shift + 14, n * 2048 - 14)
+        addrs = [base + shift + i * 2048 for i in range(n)]
+        for i in range(1, n):
+            xsum.tcp_checksums(ctx, addrs[i])
+        xsum.tx_flush(ctx)
+        assert xsum.last_kernel() == "tcp4_tas14_kernel<hints,offs>"
+        np.testing.assert_array_equal(view[1:], ref[1:])
+        xsum.tcp_checksums(ctx, addrs[0])
+        xsum.tx_flush(ctx)
+        assert xsum.last_kernel() == ("tcp4_frame_kernel" if zero_copy else "tcp4_tas14_kernel<hints,offs>")
+        np.testing.assert_array_equal(view, ref)
+        z, st = xsum.ctx_stats(ctx)
+        assert (z, st) == ((2, 0) if zero_copy else (0, 2))
+        if zero_copy:
+            pin.free()
+    finally:
+        xsum.ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
 def test_async_flush_pipeline(oracle, zero_copy):
     """tasx_flush_submit / _poll / _wait: tx_flush-sized batches (32 frames,
     data segments and ACK sizes) submitted back to back with up to 3 in flight
