@@ -552,6 +552,30 @@ def flow_bounds(fw: "FlowLookupWorkload", avg_us: float, launches: int = 100) ->
     }
 
 
+def copy_ceiling(nbytes: int, copies: int = 50, rotate: int = 4) -> dict:
+    """The device's read+write streaming rate, measured live: the runtime's
+    D2D copy (hipMemcpyAsync) of `nbytes` between rotating buffer pairs (4
+    pairs: more than the MALL holds), events around `copies` copies.  The TX
+    segment build moves about as many bytes each way."""
+    src = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(rotate)]
+    dst = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(rotate)]
+    for k in range(8):
+        dst[k % rotate].copy_(src[k % rotate])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for k in range(copies):
+        dst[k % rotate].copy_(src[k % rotate])
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / copies
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"bytes_each_way": nbytes, "us": round(us, 3), "GBps": round(2 * nbytes / us / 1e3, 1),
+            "frac_of_spec": round(2 * nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "how": "hipMemcpyAsync D2D between 4 rotating buffer pairs, HIP events around 50 copies"}
+
+
 def prewarm(run, seconds: float = 0.25):
     """Bring the GPU out of idle clocks before any measured step (not part of
     W or K)."""
@@ -1010,6 +1034,10 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         txseg = leg(tw.loop(), tw.bytes_per_step, args, ws, TxSegWorkload.desc, "tx_segment_tas_kernel")
         txseg["algorithmic_bytes_per_segment"] = tw.bytes_per_seg
         txseg["block_floor"] = dict(tw.block_floor)
+        # bytes each way of the 128-byte block floor (the kernel's reads and writes)
+        cc = copy_ceiling(int(tw.block_floor["bytes"]) // 2)
+        cc["alg_frac_of_copy"] = round(txseg["roofline"]["achieved"] / cc["GBps"], 4)
+        txseg["copy_ceiling"] = cc
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             txseg["cpu_baseline"] = tw.cpu_check(3.0)
         del tw
@@ -1055,6 +1083,11 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                     fl = txseg.get("block_floor")
                     if fl:
                         fl["traffic_over_floor"] = round(pt["hbm_bytes_per_launch"] / fl["bytes"], 4)
+                    cc = txseg.get("copy_ceiling")
+                    if cc:  # the kernel's own HBM traffic rate against the copy's
+                        rate = pt["hbm_bytes_per_launch"] / txseg["roofline"]["launch_avg_us"] / 1e3
+                        cc["traffic_GBps"] = round(rate, 1)
+                        cc["traffic_frac_of_copy"] = round(rate / cc["GBps"], 4)
                 txseg["pmc"] = pt
 
     if rank == 0:

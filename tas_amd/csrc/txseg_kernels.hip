@@ -578,7 +578,10 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 // descriptor's room (the mbuf data room) covers the frame's last 16-byte
 // chunk, that chunk is written whole, its bytes past the frame with their own
 // values, instead of by dword and byte stores.
-template <int U, bool NTS, int WPE = 1>
+// ABL (A/B ablations, timing only -- results are wrong): bit 0 = no scratch
+// zero stores, 1 = no first-block write-back, 2 = no chunk-4 / piece-2 window
+// loads, 3 = no general-body fallback, 4 = no payload stores.
+template <int U, bool NTS, int WPE = 1, int ABL = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -623,8 +626,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // up front: the header chunk, chunk 4's window (payload [-2, 14)), the piece-2 window
     const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4));
     const uint32_t o4 = s1 - 2u;
-    const u32x4 w4 = ld16u(shm, min(o4, smax));
-    const u32x4 xw = ld16u(shm, min(xoff, smax));
+    const u32x4 w4 = (ABL & 4) ? hv : ld16u(shm, min(o4, smax));
+    const u32x4 xw = (ABL & 4) ? hv : ld16u(shm, min(xoff, smax));
     u32x4 tv = {0u, 0u, 0u, 0u};
     if (!scratch)
       tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
@@ -634,10 +637,52 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // in vfb and stored at the end together with the header chunks, so the
     // block's lines are written whole by one instruction (a line written in two
     // parts at different times costs an HBM read-modify-write).
-    const int fbe = aoff <= 10 ? 16 - aoff : 0;
+    int fbe = aoff <= 10 ? 16 - aoff : 0;
+    if (ABL & 32) { // A/B: keep only the payload chunks of chunk 4's 128-byte line
+      const int lo8 = aoff & 7;
+      fbe = min(fbe, 8 * ((lo8 + 4) / 8 + 1) - lo8);
+    }
+    if (ABL & 64) // A/B: keep nothing; the write-back stores chunks 1, 3, 4 only
+      fbe = 0;
     u32x4 vfb = hv;
     uint32_t acc = 0;
-    for (int base = 5 - ((5 + aoff) & 15); base < K; base += 16 * U) {
+    const int base0 = 5 - ((5 + aoff) & 15);
+    // the common case, wave-wide: every row a fast one with no wrap inside its
+    // payload, every window inside the region, one round of chunks.  Its loop
+    // has no per-chunk branches but the store's predicate (sums by select)
+    const bool simple_row = fast && wrapc == 0x7fffffff && o4 <= smax && base0 + 16 * U >= K &&
+                            s1 + (uint32_t) (16 * (K - 1) - 66) <= smax;
+    const bool simple = (ABL & 128) && __builtin_amdgcn_ballot_w64(!simple_row) == 0ull;
+    if (simple) {
+      u32x4 a[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = min(max(base0 + gl + 16 * u, 5), K - 1);
+        a[u] = ld16u(shm, s1 + (uint32_t) (16 * k - 66));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = base0 + gl + 16 * u, hi = fend - 16 * k;
+        const u32x4 v = a[u];
+        const bool in = k >= 5 && k < K, full = in && hi >= 16;
+        const bool keep = u == 0 && k < fbe;
+        if (full && !keep)
+          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
+        if (u == 0)
+          vfb = full && keep ? v : vfb;
+        const uint32_t sv = sad4(v, 0u);
+        acc += full ? sv : 0u;
+        if (in && hi < 16) { // the frame's last chunk (one lane per row)
+          acc += sad_below(v, (uint32_t) hi);
+          uint8_t *const cp = f + 16 * k;
+          if (whole)
+            *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
+          else
+            store_range(cp, v, 0, hi, false);
+        }
+      }
+    }
+    for (int base = base0; !simple && base < K; base += 16 * U) {
       u32x4 a[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -661,7 +706,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           vfb = v;
           acc = sad4(v, acc);
         } else if (hi >= 16) {
-          if (NTS)
+          if (ABL & 16)
+            ;
+          else if (NTS)
             __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
           else
             *(__attribute__((address_space(1))) u32x4 *) cp = v;
@@ -676,7 +723,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       }
     }
 
-    if (scratch) { // the scratch chunks past the frame outside its first block
+    if (scratch && !(ABL & 1)) { // the scratch chunks past the frame outside its first block
       const int k = K + gl;
       if (k < kend && k >= fbe)
         __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
@@ -708,7 +755,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const uint32_t len = 32u + (uint32_t) pay;
     const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph1) + bswap16(len))));
     const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
-    if (fast) {
+    if (fast && !(ABL & 2)) {
       if (gl == 15 && p.out)
         stg(p.out, i, res);
       // the first block: header chunks with the checksums inserted (ip.chksum:
@@ -719,17 +766,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         h.x = (h.x & 0x0000ffffu) | (res & 0xffff0000u);
       uint8_t *const cp = f + 16 * kh;
       const int hi = fend - 16 * kh;
-      if ((kh < 5 || kh < fbe) && hi >= 16)
+      if ((ABL & 64) && (kh == 0 || kh == 2))
+        ; // unchanged header chunks
+      else if ((kh < 5 || kh < fbe) && hi >= 16)
         *(__attribute__((address_space(1))) u32x4 *) cp = kh < 5 ? h : vfb;
       else if (kh < 5 && whole && kh < K) // h holds the frame's own bytes past its end
         *(__attribute__((address_space(1))) u32x4 *) cp = h;
       else if (kh < 5)
         store_range(cp, h, 0, hi, false);
-      else if (kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
+      else if (!(ABL & 1) && kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
         *(__attribute__((address_space(1))) u32x4 *) cp = u32x4{0u, 0u, 0u, 0u};
     }
   }
-  if (!fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
+  if (!(ABL & 8) && !fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
     txseg_row<3, NTS>(p, i, gl);
 }
 
@@ -759,6 +808,17 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 6: tasx_note_kernel("tx_segment_tas_kernel<plain>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // plain stores
   case 7: tasx_note_kernel("tx_segment_tas_kernel<wpe6>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 6>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 80 VGPRs
   case 8: tasx_note_kernel("tx_segment_tas_kernel<wpe8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 64 VGPRs
+  case 15: tasx_note_kernel("tx_segment_tas_kernel<line_keep>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 32>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 17: tasx_note_kernel("tx_segment_tas_kernel<simple>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 128>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 18: tasx_note_kernel("tx_segment_tas_kernel<simple,fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 192>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 64>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  // 9..14: ablations (timing only)
+  case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 10: tasx_note_kernel("tx_segment_tas_kernel<abl2>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 11: tasx_note_kernel("tx_segment_tas_kernel<abl4>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 12: tasx_note_kernel("tx_segment_tas_kernel<abl8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 13: tasx_note_kernel("tx_segment_tas_kernel<abl15>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 15>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 14: tasx_note_kernel("tx_segment_tas_kernel<abl16>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   default: break;
   }
 #else

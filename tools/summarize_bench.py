@@ -15,7 +15,9 @@ for path in sys.argv[1:]:
         r = v["roofline"]
         extra = ""
         if k == "tx_segment" and v.get("pmc"):
-            extra = f" traffic/alg {r['traffic'] / r['algorithmic_bytes_per_launch']:.3f} pmc {v['pmc']}"
+            extra = f" traffic/alg {r['traffic'] / r['algorithmic_bytes_per_launch']:.3f}"
+        if k == "tx_segment" and v.get("copy_ceiling"):
+            extra += f" copy_ceiling {v['copy_ceiling']}"
         if k == "flow_lookup":
             extra = f" line {v.get('line_roofline', {}).get('frac')} ceiling {v.get('pattern_ceiling')}"
         print(f"  {k:17s} {v['value']:8.1f} GiB/s  step {v['ms_per_step'] * 1e3:7.3f} us  launch {r['launch_avg_us']:7.3f} us"
