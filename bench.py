@@ -552,6 +552,34 @@ def flow_bounds(fw: "FlowLookupWorkload", avg_us: float, launches: int = 100) ->
     }
 
 
+def tcp4_pattern_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200) -> dict:
+    """The headline's access pattern with no checksum logic
+    (tasx_ab_tcp4_pattern, the A/B build), timed over the same rotation."""
+    ab = xsum._load(xsum.AB_LIB_PATH)
+    s = torch.cuda.current_stream().cuda_stream
+    R = len(wl.bufs)
+    outs = [torch.empty(wl.n, dtype=torch.int32, device="cuda") for _ in range(2)]  # not the checked results
+
+    def pat(k):
+        rc = ab.tasx_ab_tcp4_pattern(wl.bufs[k % R].data_ptr(), wl.stride, wl.n, wl.hint, IP_OFF,
+                                     outs[k % 2].data_ptr(), s)
+        if rc:
+            raise xsum.TasxError(rc, "tasx_ab_tcp4_pattern")
+    for k in range(20):
+        pat(k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for k in range(launches):
+        pat(k)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / launches
+    return {"bound": "the access pattern", "us": round(us, 3), "frac": round(us / avg_us, 4),
+            "kernel": "tcp4_pattern_kernel (libtasx_ab.so): the headline's rows, loads, result stores and "
+                      "residency, words xor-folded instead of summed"}
+
+
 def copy_ceiling(nbytes: int, copies: int = 50, rotate: int = 4) -> dict:
     """The device's read+write streaming rate, measured live: the runtime's
     D2D copy (hipMemcpyAsync) of `nbytes` between rotating buffer pairs (4
@@ -976,6 +1004,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     rot = max(1, args.rotate)
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
     head = leg(wl.loop(HINT), wl.bytes_per_step, args, ws, Tcp4Workload.desc, "tcp4_tas14_kernel<hint>")
+    head["roofline"]["pattern_ceiling"] = tcp4_pattern_ceiling(wl, head["roofline"]["launch_avg_us"])
     ctx2 = None
     if not args.no_contexts:
         streams = [torch.cuda.Stream() for _ in range(2)]

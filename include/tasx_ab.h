@@ -45,6 +45,13 @@ int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t
     const void *flowht, uint32_t ht_entries, const void *flowst, uint32_t fs_num, uint32_t fs_stride,
     uint32_t fs_key_off, uint32_t *out, void *stream);
 
+/* The headline kernel's access pattern (tcp4_tas14_kernel<hint>: same rows,
+ * loads, result store and residency) with no checksum logic -- the ceiling
+ * that pattern allows, timed by bench.py beside the headline.  Uniform-hint
+ * stride-mode TAS batches only (-EINVAL otherwise); out[i] is not a checksum. */
+int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
+    uint32_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <errno.h>
+#include <string.h>
 
 #include "tasx_kernels.h"
 
@@ -1380,6 +1382,53 @@ extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
   hipLaunchKernelGGL(post_done_kernel, dim3(1), dim3(64), 0, (hipStream_t) stream, word, seq);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#ifdef TASX_AB
+// The headline kernel's access pattern with no checksum logic: the same rows,
+// the same 6 clamped chunk loads per lane at 32-bit offsets from the SGPR
+// base, the same 4-byte result store per frame and LDS reservation; the
+// loaded words are only xor-folded.  bench.py times it beside the headline
+// (its pattern_ceiling).
+namespace {
+__global__ __launch_bounds__(kBlock) void tcp4_pattern_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u), hend = p.flen0 - p.ip_off;
+  const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4), lo = a0 + 16u * (uint32_t) gl;
+  u32x4 v[6];
+#pragma unroll
+  for (int u = 0; u < 6; ++u)
+    v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
+  uint32_t x = 0;
+#pragma unroll
+  for (int u = 0; u < 6; ++u)
+    x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  x = row_sum16(x);
+  if (gl == 15)
+    stg((uint32_t *) p.out, i, x);
+}
+} // namespace
+
+extern "C" int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
+                                    uint32_t *out, void *stream)
+{
+  tasx_tcp4_params p;
+  memset(&p, 0, sizeof(p));
+  p.base = (uint8_t *) base;
+  p.stride = stride;
+  p.n = n;
+  p.flen0 = flen0;
+  p.ip_off = ip_off;
+  p.l4_off = ip_off + 20u;
+  p.out = (uint16_t *) out;
+  if (!out || !tas14_ok(p))
+    return -EINVAL;
+  return launch_groups("tcp4_pattern_kernel", tcp4_pattern_kernel, p, (hipStream_t) stream, kOccLds);
+}
+#endif
 
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {

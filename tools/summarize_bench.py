@@ -7,7 +7,8 @@ for path in sys.argv[1:]:
     d = json.loads(line)
     print(f"== {path}: value {d['value']} GiB/s, ms_per_step {d['ms_per_step'] * 1e3:.3f} us, "
           f"launch_avg {d['roofline']['launch_avg_us']} us, frac {d['roofline']['frac']}, "
-          f"traffic {d['roofline'].get('traffic')}, kernel {d.get('kernel')}")
+          f"traffic {d['roofline'].get('traffic')}, kernel {d.get('kernel')}, "
+          f"pattern_ceiling {d['roofline'].get('pattern_ceiling', {}).get('us')} us")
     for k in ("tcp4_nohint", "tcp4_frames_only", "rx_verify", "flush_mix", "raw", "tx_segment", "flow_lookup"):
         v = d.get(k)
         if not v:
