@@ -19,9 +19,9 @@
  *      frames compacted onto rows; TASX_MIX_F8=1: 8 frames per wave) where a
  *      room of 80 B allows; measured slower than the default for data/ACK
  *      mixes
- *   20  tcp4_tas14_kernel<hint_arr>: each row's per-frame hint as its
- *      geometry, checked against total_length after the loads (needs
- *      per-frame hints)
+ *   20  tcp4_tas14_kernel<hints> forced (the per-frame-hint default)
+ *   21  tcp4_tas14_kernel<hints_pred>: the same with lanes past a row's last
+ *      chunk loading nothing (needs per-frame hints)
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
  * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
  */

@@ -879,7 +879,8 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // only the aligned chunk holding the IPv4 header start and is redone by the
 // general row body.
 enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */,
-                       kHintArr = 5 /* per-frame hints as the geometry */ };
+                       kHintArr = 5 /* per-frame hints as the geometry */,
+                       kHintArrP = 6 /* the same, lanes past the last chunk load nothing (A/B) */ };
 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
@@ -922,7 +923,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
     }
     u32x4 t = v[U - 1];
     uint32_t tlane = 15u;
-    if constexpr (MODE == kRoom) {
+    if constexpr (MODE == kRoom || MODE == kHintArrP) {
       const uint32_t ut = last >> 4;
       t = v[0];
 #pragma unroll
@@ -935,7 +936,8 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  const bool bad = MODE == kHint ? tl15 != hend : MODE == kHintArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
+  constexpr bool kArr = MODE == kHintArr || MODE == kHintArrP;
+  const bool bad = MODE == kHint ? tl15 != hend : kArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
     if (gl == 15 && !bad) {
@@ -963,7 +965,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   if (FALLBACK && __builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
-    const bool rbad = (MODE == kHint || MODE == kHintArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
+    const bool rbad = (MODE == kHint || kArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
     if (rbad) {
       if constexpr (OFFS)
         tcp4_frame_row<3, VERIFY>(p, i, gl);
@@ -1023,17 +1025,24 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
     for (int u = 0; u < U; ++u)
       v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kHintArr) {
+  } else if constexpr (MODE == kHintArr || MODE == kHintArrP) {
     // the row's own hint (mbuf data_len) fixes its geometry; lane 15 checks
     // it against total_length afterwards, as kHint does for a uniform hint
     const uint32_t h = ldg(p.flen, i);
     const uint32_t hl = h > p.ip_off ? h - p.ip_off : 0u;
     in_range = row_ok && hl >= 38u && hl <= 1522u && (!p.room || h <= p.room); // reads stay inside the room
     hend = in_range ? hl : (row_ok ? 20u : 1u);
-    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
+    const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+    for (int u = 0; u < U; ++u) {
+      if constexpr (MODE == kHintArrP) {
+        v[u] = u32x4{0u, 0u, 0u, 0u};
+        if ((uint32_t) gl + 16u * u <= last) // the tail comes from v[last / 16] on lane last % 16
+          v[u] = ld16nt_off(fb, lo + 256u * u);
+      } else {
+        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+      }
+    }
   } else if constexpr (MODE == kHead5) {
     v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
     const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
@@ -1490,6 +1499,9 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
     return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,offs>" : "tcp4_tas14_kernel<hints>",
                          tcp4_tas14_kernel<6, kHintArr, false, 8, OFFS>, p, s, lds);
 #ifdef TASX_AB
+  case kHintArrP:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints_pred,offs>" : "tcp4_tas14_kernel<hints_pred>",
+                         tcp4_tas14_kernel<6, kHintArrP, false, 8, OFFS>, p, s, lds);
   case kMix:
     if (getenv("TASX_MIX_F8"))
       return launch_groups<8>("tcp4_mix_kernel<f8>", tcp4_mix_kernel<6, 8>, p, s);
@@ -1541,10 +1553,11 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 #ifdef TASX_AB
   // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
   // where its room requirement holds (else as 0)
-  if ((variant >= 9 && variant <= 11) || variant == 19 || variant == 20) {
+  if ((variant >= 9 && variant <= 11) || (variant >= 19 && variant <= 21)) {
     const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
-    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : variant == 19 ? kMix : kHintArr;
-    if ((m == kTlFirst) || (m == kHintArr && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
+    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : variant == 19 ? kMix
+                : variant == 20 ? kHintArr : kHintArrP;
+    if ((m == kTlFirst) || ((m == kHintArr || m == kHintArrP) && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
       mode = m;
     variant = 0;
   }
