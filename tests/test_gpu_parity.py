@@ -624,6 +624,32 @@ def test_flush_records_as_frame_starts(oracle, zero_copy, shift):
         xsum.ctx_destroy(ctx)
 
 
+def test_zero_copy_needs_chunk_slack(oracle):
+    """A frame whose datagram ends less than 16 bytes before the registered
+    region's end is not read in place (rows read whole 16-byte chunks): that
+    flush goes through staging, and its checksums are still exact."""
+    ctx = 7
+    xsum.ctx_init(ctx, 0, 1 << 20)
+    try:
+        frames = pktgen.tcp4_frames(2, payload=np.array([1448, 100]), stride=2048, seed=91)
+        ref = frames.copy()
+        oracle.tcp4_batch(ref, 2, stride=2048, inplace=True)
+        pin = xsum.PinnedBuffer(frames.size)
+        pin.array[:] = frames
+        end1 = 2048 + 14 + 152                       # frame 1's datagram end (ip.len 152)
+        xsum.register_frames(ctx, pin.addr, end1 + 8)  # 8 bytes of slack only
+        xsum.tcp_checksums(ctx, pin.addr)
+        xsum.tx_flush(ctx)
+        assert xsum.ctx_stats(ctx) == (1, 0)
+        xsum.tcp_checksums(ctx, pin.addr + 2048)
+        xsum.tx_flush(ctx)
+        assert xsum.ctx_stats(ctx) == (1, 1)
+        np.testing.assert_array_equal(pin.array, ref)
+        pin.free()
+    finally:
+        xsum.ctx_destroy(ctx)
+
+
 @pytest.mark.parametrize("zero_copy", [False, True])
 def test_async_flush_pipeline(oracle, zero_copy):
     """tasx_flush_submit / _poll / _wait: tx_flush-sized batches (32 frames,
