@@ -69,7 +69,10 @@ int tasx_device_count(void);
 /* ---------------------------------------------------------------------- */
 /* Device-resident batches.  All pointers are device pointers (or host memory
  * the device can address).  Packet i starts at base + off[i], or at
- * base + i * stride when off == NULL.  Asynchronous on `stream`. */
+ * base + i * stride when off == NULL.  Asynchronous on `stream`.  Kernels
+ * read whole 16-byte aligned chunks: only chunks holding at least one byte of
+ * the packet (or of the hinted / room range below), so a read never leaves
+ * the pages the packet lies in, and bytes outside it never enter a result. */
 
 /* RAW: out[i] = rte_raw_cksum(base + off_i, len_i); len_i = len[i], or len0
  * when len == NULL; len_i <= TASX_RAW_MAX_LEN (device-side lengths are the
