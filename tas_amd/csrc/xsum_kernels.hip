@@ -1475,10 +1475,21 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
   if (auto6 && tas14_ok(*p))
     return launch_groups("tcp4_tas14_kernel<hint,verify>", tcp4_tas14_kernel<6, kHint, true>, *p, s,
                          TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
+  // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
+  // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
+  // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt).
+  // With the received lengths as per-frame hints each row reads exactly its
+  // received bytes at once (kHintArr; a total_length that disagrees -- padding,
+  // truncation, a forged length -- is redone by the bounded general body).
+  bool hints = p->flen != nullptr;
+#ifdef TASX_AB
+  if (variant == 9) // A/B: total_length first also with hints
+    hints = false;
+#endif
+  if (auto6 && tas14_nohint_ok(*p) && hints)
+    return launch_groups("tcp4_tas14_kernel<hints,verify>", tcp4_tas14_kernel<6, kHintArr, true, 8>, *p, s,
+                         TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
   if (auto6 && tas14_nohint_ok(*p))
-    // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
-    // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
-    // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt)
     return launch_groups("tcp4_tas14_kernel<tl_first,verify>", tcp4_tas14_kernel<6, kTlFirst, true, 8>, *p, s,
                          TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
   return launch_groups("tcp4_frame_kernel<verify>", tcp4_frame_kernel<6, true>, *p, s);

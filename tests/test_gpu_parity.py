@@ -1049,6 +1049,37 @@ def test_tcp4_room_tso_rows(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("variant", [0, 9])
+def test_verify_mix_received_lengths(oracle, variant):
+    """An RX burst of data segments and pure ACKs with each frame's received
+    length as its hint (tcp4_tas14_kernel<hints,verify>; A/B variant 9: the
+    total_length-first rows): honest frames, Ethernet-padded short frames
+    (received length > 14 + total_length), truncated frames, corrupted bytes
+    and checksum fields.  Bit-exact against the bounded oracle."""
+    n, stride = 8192, 2048
+    rng = np.random.default_rng(17 + variant)
+    pay = np.where(rng.random(n) < 0.5, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
+    frames = pktgen.tcp4_frames(n, payload=pay, stride=stride, seed=170)
+    oracle.tcp4_batch(frames, n, stride=stride, inplace=True)
+    f = frames.reshape(n, stride)
+    rcv = 14 + 52 + pay
+    pad = np.arange(n) % 7 == 1
+    rcv[pad] = np.maximum(rcv[pad], 60) + 4 + (np.arange(n)[pad] % 9)   # padding / trailer bytes
+    trunc = np.arange(n) % 11 == 2
+    rcv[trunc] = np.maximum(rcv[trunc] - 1 - np.arange(n)[trunc] % 40, 20)
+    bad = np.arange(n) % 5 == 3
+    pos = 14 + (rng.integers(0, 10 ** 6, n) % (rcv - 14))
+    f[np.nonzero(bad)[0], pos[bad]] ^= 0x20
+    f[4::13, 24] ^= 0x01                                                   # ip.chksum
+    f[6::17, 50] ^= 0x80                                                   # tcp.chksum
+    exp = oracle.tcp4_verify_batch_bounded(frames, n, rcv.astype(np.uint32), stride=stride)
+    with kernel_variant(variant):
+        got = xsum.tcp4_verify_batch(to_dev(frames), n, stride=stride, frame_len=to_dev(rcv.astype(np.int32)))
+        assert xsum.last_kernel() == ("tcp4_tas14_kernel<hints,verify>" if variant == 0
+                                      else "tcp4_tas14_kernel<tl_first,verify>")
+        np.testing.assert_array_equal(got.cpu().numpy(), exp)
+
+
 # ---------------------------------------------------------------------------
 # RX: received frames are untrusted (ADVICE r1: forged total_length)
 
