@@ -1468,6 +1468,20 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
   }
 }
 
+template <bool OFFS>
+static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t s)
+{
+  const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u);
+  switch (mode) {
+  case kHintArr:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,verify,offs>" : "tcp4_tas14_kernel<hints,verify>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, OFFS>, p, s, lds);
+  default:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,verify,offs>" : "tcp4_tas14_kernel<tl_first,verify>",
+                         tcp4_tas14_kernel<6, kTlFirst, true, 8, OFFS>, p, s, lds);
+  }
+}
+
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
@@ -1477,21 +1491,21 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
                          TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
   // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
   // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
-  // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt).
-  // With the received lengths as per-frame hints each row reads exactly its
-  // received bytes at once (kHintArr; a total_length that disagrees -- padding,
-  // truncation, a forged length -- is redone by the bounded general body).
-  bool hints = p->flen != nullptr;
+  // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt),
+  // and the TX form's row modes: the received lengths as per-frame hints ->
+  // each row reads exactly its received bytes at once (a total_length that
+  // disagrees -- padding, truncation, a forged length -- is redone by the
+  // bounded general body; profiles/r02/r02ac), else total_length first: RX
+  // bursts are mixes, where whole-room rows lose (64K frames, room 2048, 0 /
+  // 50 % ACKs: 16.3 / 16.3 us against 16.9 / 10.8-11.1; profiles/r02/r02ad).
+  if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
+    int mode = p->flen ? kHintArr : kTlFirst;
 #ifdef TASX_AB
-  if (variant == 9) // A/B: total_length first also with hints
-    hints = false;
+    if (variant == 9) // A/B: total_length first whatever the call carries
+      mode = kTlFirst;
 #endif
-  if (auto6 && tas14_nohint_ok(*p) && hints)
-    return launch_groups("tcp4_tas14_kernel<hints,verify>", tcp4_tas14_kernel<6, kHintArr, true, 8>, *p, s,
-                         TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
-  if (auto6 && tas14_nohint_ok(*p))
-    return launch_groups("tcp4_tas14_kernel<tl_first,verify>", tcp4_tas14_kernel<6, kTlFirst, true, 8>, *p, s,
-                         TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
+    return p->off ? launch_tas14_verify<true>(*p, mode, s) : launch_tas14_verify<false>(*p, mode, s);
+  }
   return launch_groups("tcp4_frame_kernel<verify>", tcp4_frame_kernel<6, true>, *p, s);
 }
 

@@ -1050,14 +1050,18 @@ def test_tcp4_room_tso_rows(oracle):
 
 
 @pytest.mark.parametrize("variant", [0, 9])
-def test_verify_mix_received_lengths(oracle, variant):
-    """An RX burst of data segments and pure ACKs with each frame's received
-    length as its hint (tcp4_tas14_kernel<hints,verify>; A/B variant 9: the
-    total_length-first rows): honest frames, Ethernet-padded short frames
-    (received length > 14 + total_length), truncated frames, corrupted bytes
-    and checksum fields.  Bit-exact against the bounded oracle."""
+@pytest.mark.parametrize("offs", [False, True])
+@pytest.mark.parametrize("bound", ["len", "room", "none"])
+def test_verify_mix_received_lengths(oracle, variant, offs, bound):
+    """An RX burst of data segments and pure ACKs: honest frames,
+    Ethernet-padded short frames (received length > 14 + total_length),
+    truncated frames, corrupted bytes and checksum fields; stride mode and an
+    offsets array; bounded by each frame's received length (its hint: row mode
+    <hints,verify>), by a 2048 B room or by nothing but the stride slot / the
+    frame's own total_length (both <tl_first,verify>); A/B variant
+    9 forces total_length-first rows.  Bit-exact against the bounded oracle."""
     n, stride = 8192, 2048
-    rng = np.random.default_rng(17 + variant)
+    rng = np.random.default_rng(17 + variant + 2 * offs)
     pay = np.where(rng.random(n) < 0.5, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
     frames = pktgen.tcp4_frames(n, payload=pay, stride=stride, seed=170)
     oracle.tcp4_batch(frames, n, stride=stride, inplace=True)
@@ -1072,11 +1076,20 @@ def test_verify_mix_received_lengths(oracle, variant):
     f[np.nonzero(bad)[0], pos[bad]] ^= 0x20
     f[4::13, 24] ^= 0x01                                                   # ip.chksum
     f[6::17, 50] ^= 0x80                                                   # tcp.chksum
-    exp = oracle.tcp4_verify_batch_bounded(frames, n, rcv.astype(np.uint32), stride=stride)
+    kw = dict(offsets=to_dev(np.arange(n, dtype=np.int64) * stride)) if offs else dict(stride=stride)
+    if bound == "len":
+        kw["frame_len"] = to_dev(rcv.astype(np.int32))
+        b, mode = rcv.astype(np.uint32), "hints"
+    elif bound == "room":
+        kw["room"] = stride
+        b, mode = stride, "tl_first"
+    else:
+        b, mode = (0 if offs else stride), "tl_first"
+    exp = oracle.tcp4_verify_batch_bounded(frames, n, b, stride=stride)
     with kernel_variant(variant):
-        got = xsum.tcp4_verify_batch(to_dev(frames), n, stride=stride, frame_len=to_dev(rcv.astype(np.int32)))
-        assert xsum.last_kernel() == ("tcp4_tas14_kernel<hints,verify>" if variant == 0
-                                      else "tcp4_tas14_kernel<tl_first,verify>")
+        got = xsum.tcp4_verify_batch(to_dev(frames), n, **kw)
+        name = f"tcp4_tas14_kernel<{'tl_first' if variant == 9 else mode},verify{',offs' if offs else ''}>"
+        assert xsum.last_kernel() == name
         np.testing.assert_array_equal(got.cpu().numpy(), exp)
 
 
