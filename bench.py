@@ -340,6 +340,28 @@ class RxVerifyWorkload:
         return benchloop.Loop("tcp4", args, _stream_ptrs(streams), VERIFY, "tasx_tcp4_verify_batch_dev_room")
 
 
+class RxMixWorkload:
+    """Receive-side verification of a FlushMixWorkload's frames after their TX
+    checksums (an RX burst of data segments and pure ACKs), each frame's
+    received length (the mbuf data_len) as its per-frame hint and read bound."""
+    desc = (f"{N_FRAMES} received TAS frames in {STRIDE} B rooms, 50% data segments and 50% pure ACKs, "
+            "per-frame received lengths (tasx_tcp4_verify_batch_dev_hint)")
+
+    def __init__(self, mw: "FlushMixWorkload"):
+        self.mw = mw
+        for b in mw.bufs:  # TX checksums in place: the frames as a receiver gets them
+            xsum.tcp4_cksum_batch(b, mw.n, stride=mw.stride, frame_len=mw.flen, room=mw.stride, inplace=True,
+                                  want_out=False)
+        self.flags = [torch.empty(mw.n, dtype=torch.uint8, device="cuda") for _ in mw.bufs]
+        self.bytes_per_step = mw.bytes_per_step - 3 * mw.n  # total_length read + 1 B of flags per frame
+
+    def loop(self, streams=None) -> benchloop.Loop:
+        mw = self.mw
+        args = [benchloop.Tcp4Args(b.data_ptr(), None, mw.stride, mw.flen.data_ptr(), 0, 0, mw.n, IP_OFF, L4_OFF, 0,
+                                   f.data_ptr()) for b, f in zip(mw.bufs, self.flags)]
+        return benchloop.Loop("tcp4", args, _stream_ptrs(streams), VERIFY, "tasx_tcp4_verify_batch_dev_hint")
+
+
 class RawWorkload:
     desc = f"{N_FRAMES} x {RAW_LEN} B packed payloads, rte_raw_cksum per packet"
 
@@ -1040,12 +1062,17 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     for b in wl.bufs:  # restore the un-checksummed frames for the legs below
         b.copy_(src)
     del src
-    mix = None
+    mix = rx_mix = None
     if not args.no_flushmix:
         mw = FlushMixWorkload(min(rot, 12), pktgen.SEED + 500 + rank)
         mix = leg(mw.loop(), mw.bytes_per_step, args, ws, FlushMixWorkload.desc, "tcp4_tas14_kernel<hints>")
         mix["parity"] = "tests/test_bench_configs.py::test_bench_flush_mix"
-        del mw
+        rm = RxMixWorkload(mw)
+        rx_mix = leg(rm.loop(), rm.bytes_per_step, args, ws, RxMixWorkload.desc, "tcp4_tas14_kernel<hints,verify>")
+        torch.cuda.synchronize()
+        rx_mix["all_frames_verified"] = bool(all((f == 3).all().item() for f in rm.flags))
+        rx_mix["parity"] = "tests/test_bench_configs.py::test_bench_rx_mix"
+        del mw, rm
         torch.cuda.empty_cache()
     raw = None
     if not args.no_raw:
@@ -1139,6 +1166,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             "tcp4_frames_only": frames_only,
             "two_contexts": ctx2,
             "rx_verify": rx,
+            "rx_verify_mix": rx_mix,
             "flush_mix": mix,
         }
         if raw is not None:

@@ -81,6 +81,21 @@ def test_bench_flush_mix(oracle):
     np.testing.assert_array_equal(host(mw.outs[0]).view(np.uint16), exp)
 
 
+def test_bench_rx_mix(oracle):
+    """The rx_verify_mix leg: the flush_mix frames after their TX checksums,
+    verified with per-frame received lengths (tasx_tcp4_verify_batch_dev_hint)
+    -- every frame verifies, bit-exact against the bounded oracle."""
+    mw = bench.FlushMixWorkload(1, pktgen.SEED + 500)
+    rm = bench.RxMixWorkload(mw)
+    rm.loop()(0, 1)
+    assert xsum.last_kernel() == "tcp4_tas14_kernel<hints,verify>"
+    frames = host(mw.bufs[0])
+    got = host(rm.flags[0])
+    np.testing.assert_array_equal(got, oracle.tcp4_verify_batch_bounded(frames, mw.n, host(mw.flen).astype(np.uint32),
+                                                                        stride=mw.stride))
+    assert np.all(got == 3)
+
+
 def test_bench_config3_mixed_mtu(oracle):
     """Config 3: 1,048,576 RAW packets, {64, 576, 1500, 9000} B in random order,
     per-packet offsets and lengths (tasx_raw_cksum_batch_dev)."""

@@ -9,7 +9,7 @@ for path in sys.argv[1:]:
           f"launch_avg {d['roofline']['launch_avg_us']} us, frac {d['roofline']['frac']}, "
           f"traffic {d['roofline'].get('traffic')}, kernel {d.get('kernel')}, "
           f"pattern_ceiling {d['roofline'].get('pattern_ceiling', {}).get('us')} us")
-    for k in ("tcp4_nohint", "tcp4_frames_only", "rx_verify", "flush_mix", "raw", "tx_segment", "flow_lookup"):
+    for k in ("tcp4_nohint", "tcp4_frames_only", "rx_verify", "flush_mix", "rx_verify_mix", "raw", "tx_segment", "flow_lookup"):
         v = d.get(k)
         if not v:
             continue
