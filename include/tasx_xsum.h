@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 2
+#define TASX_ABI_VERSION 3
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -305,6 +305,28 @@ int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes);
 /* counts of zero-copy and staged flushes since tasx_ctx_init */
 int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes,
     uint32_t *staged_flushes);
+
+/* Shared feeder: one thread per GPU serves the zero-copy flushes of every
+ * attached context with one launch per sweep, so the launch and completion
+ * round trip is paid once per sweep by the feeder's core, not once per flush
+ * by each fast-path core.  An attached context's tasx_flush_submit() hands its
+ * batch over by copying the frame pointers into its own lock-free queue (8
+ * batches deep; it spins only when all 8 are waiting) -- no HIP call on the
+ * fast-path core; tasx_flush_poll/_wait see the feeder's completions, in
+ * ticket order as before.  A batch with a frame outside the context's
+ * registered region (or without 14 bytes before its IPv4 header there) is
+ * flushed by the context itself after its feeder tickets complete.
+ *   tasx_feeder_start(device): the feeder thread for `device` (one per GPU)
+ *   tasx_ctx_use_feeder(ctx, 1 / 0): attach (needs a running feeder and a
+ *     registered frame region) / detach (waits for the context's tickets)
+ *   tasx_feeder_stop(device): -EBUSY while contexts are attached
+ *   tasx_feeder_stats: sweeps launched and frames done since start
+ *   tasx_ctx_feeder_flushes: batches the context handed to the feeder */
+int tasx_feeder_start(int device);
+int tasx_feeder_stop(int device);
+int tasx_feeder_stats(int device, uint64_t *sweeps, uint64_t *frames);
+int tasx_ctx_use_feeder(unsigned ctx_id, int on);
+int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for tests and A/B runs.  Per calling thread (TAS runs one

@@ -10,6 +10,8 @@
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -351,6 +353,15 @@ struct tasx_ctx {
   size_t zc_bytes;
   int zc_registered; /* we called hipHostRegister on it */
   uint32_t n_zerocopy_flushes, n_staged_flushes;
+  /* shared feeder (tasx_ctx_use_feeder): zero-copy batches go to the GPU's
+   * feeder thread through a single-producer / single-consumer queue */
+  struct feeder *fd;
+  struct fbatch *fq;  /* FQ batch slots */
+  uint32_t fq_head;   /* batches queued (this context's thread, release) */
+  uint32_t fq_tail;   /* batches taken (the feeder, release) */
+  uint32_t fd_done;   /* the last of its tickets the feeder has completed (release) */
+  uint32_t local_last; /* the last ticket this thread launched itself */
+  uint32_t n_feeder_flushes;
 };
 
 #define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
@@ -418,6 +429,7 @@ static void ctx_release(struct tasx_ctx *c)
     hipHostUnregister(c->zc_host);
   free(c->pend_ip);
   free(c->pend_l4);
+  free(c->fq);
   memset(c, 0, sizeof(*c));
 }
 
@@ -494,6 +506,8 @@ int tasx_ctx_destroy(unsigned ctx_id)
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   hipSetDevice(c->device);
+  if (c->fd)
+    (void) tasx_ctx_use_feeder(ctx_id, 0);
   (void) flush_wait(c, c->next_ticket);
   for (int s = 0; s < NSLOT; s++)
     hipStreamSynchronize(c->st[s]);
@@ -734,6 +748,11 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
  * `upto` is complete, 0 if not yet. */
 static int flush_reap(struct tasx_ctx *c, uint32_t upto)
 {
+  if (c->fd) { /* tickets the feeder completed (all of its tickets before them too) */
+    const uint32_t fdone = __atomic_load_n(&c->fd_done, __ATOMIC_ACQUIRE);
+    if (!ticket_le(fdone, c->done_ticket))
+      c->done_ticket = fdone;
+  }
   while (!ticket_le(upto, c->done_ticket)) {
     const uint32_t t = c->done_ticket + 1;
     struct flush_slot *f = &c->fl[t % NSLOT];
@@ -756,11 +775,18 @@ static int flush_reap(struct tasx_ctx *c, uint32_t upto)
 /* Spin until flush `ticket` (and every earlier one) is complete.  Every 4096
  * polls (a few microseconds) the stream is queried, so an error or a lost word
  * ends the wait instead of spinning on. */
+static int feeder_error(const struct tasx_ctx *c);
+
 static int flush_wait(struct tasx_ctx *c, uint32_t ticket)
 {
   uint32_t k = 0;
   while (!flush_reap(c, ticket)) {
-    if ((++k & 4095u) == 0) {
+    if ((++k & 4095u) == 0 && c->fd && feeder_error(c))
+      return set_err(-EIO, "flush: the feeder thread failed");
+    /* only feeder tickets outstanding: this context's stream has nothing to do */
+    if ((k & 4095u) == 0 && c->fd && ticket_le(c->local_last, c->done_ticket))
+      continue;
+    if ((k & 4095u) == 0) {
       hipError_t e = hipStreamQuery(c->st[0]);
       if (e == hipSuccess && !flush_reap(c, ticket))
         return set_err(-EIO, "flush: stream idle but flush %u not complete", c->done_ticket + 1);
@@ -868,6 +894,7 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   f->n = cnt;
   f->zerocopy = zc;
   f->ticket = t;
+  c->local_last = t;
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
   if (tasx_launch_post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
@@ -898,13 +925,18 @@ static uint32_t staged_fit(const struct tasx_ctx *c, size_t *need)
   return i;
 }
 
+static int feeder_submit(struct tasx_ctx *c);
+
 int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
   int rc;
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
-  HIPCHK(hipSetDevice(c->device));
+  if (c->fd && (rc = feeder_submit(c)) != 0)
+    return rc;
+  if (c->npend > 0)
+    HIPCHK(hipSetDevice(c->device));
   while (c->npend > 0) {
     const uint32_t t = c->next_ticket + 1;
     const int zc = zerocopy_ok(c, c->npend);
@@ -948,6 +980,361 @@ int tasx_flush(unsigned ctx_id)
   uint32_t t;
   int rc = tasx_flush_submit(ctx_id, &t);
   return rc ? rc : tasx_flush_wait(ctx_id, t);
+}
+
+/* ---------------------------------------------------------------------- */
+/* Shared feeder: one thread per GPU serves the zero-copy flushes of every
+ * attached context with one launch per sweep.  A fast-path core hands its
+ * batch over by copying the frame pointers into its own single-producer /
+ * single-consumer queue (no lock, no HIP call); the feeder gathers every
+ * queue, writes the descriptors (frame start, 14 + total_length) into pinned
+ * memory, launches tcp4_tas14_kernel<hints,offs> over all of them (in place,
+ * absolute device addresses) and, when the sweep's completion word arrives,
+ * publishes each context's last ticket.  Two sweeps are in flight: the next
+ * is gathered while one runs.  The launch and completion round trip (~13 us)
+ * is paid once per sweep by the feeder's core, not once per batch by each
+ * fast-path core. */
+
+#define FQ 8u            /* batches queued per context */
+#define FB_MAX 1024u     /* frames per queued batch */
+#define SWEEP_MAX 32768u /* frames per launch */
+#define SWEEP_REC 256u   /* (context, ticket) records per sweep */
+#define NSWEEP 2u
+#define MAX_DEVICES 64
+
+struct fbatch {
+  uint32_t ticket, n;
+  uint8_t *ip[FB_MAX];
+};
+
+struct fsweep {
+  uint64_t *h_off, *d_off;   /* frame start, absolute device address */
+  uint32_t *h_flen, *d_flen; /* 14 + total_length */
+  uint32_t n, nrec;
+  uint16_t rec_ctx[SWEEP_REC];
+  uint32_t rec_ticket[SWEEP_REC];
+};
+
+struct feeder {
+  int device;
+  int running; /* cleared by tasx_feeder_stop */
+  int failed;  /* a HIP error in the feeder thread (sticky) */
+  uint32_t attached; /* bit i: context i is served */
+  uint32_t gathers;  /* gather passes done (a detaching context waits for two) */
+  pthread_t thr;
+  hipStream_t st;
+  uint32_t *h_done, *d_done; /* one completion word per sweep buffer */
+  struct fsweep sw[NSWEEP];
+  uint64_t sweeps, frames;   /* statistics */
+};
+
+static struct feeder *g_feeder[MAX_DEVICES];
+static pthread_mutex_t g_feeder_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static int feeder_error(const struct tasx_ctx *c)
+{
+  return __atomic_load_n(&c->fd->failed, __ATOMIC_ACQUIRE);
+}
+
+/* every frame in the context's registered region with its 14-byte lead and
+ * the slack of whole-chunk reads (zerocopy_ok) */
+static int feeder_ok(const struct tasx_ctx *c, uint32_t n)
+{
+  if (!zerocopy_ok(c, n))
+    return 0;
+  for (uint32_t i = 0; i < n; i++)
+    if (c->pend_ip[i] < c->zc_host + TASX_TAS_IP_OFF)
+      return 0;
+  return 1;
+}
+
+/* hand the open batch to the feeder (frames outside the region: after the
+ * context's feeder tickets complete, the local path takes them) */
+static int feeder_submit(struct tasx_ctx *c)
+{
+  while (c->npend > 0) {
+    if (!feeder_ok(c, c->npend))
+      return flush_wait(c, c->next_ticket); /* in ticket order before the local flushes */
+    const uint32_t cnt = c->npend < FB_MAX ? c->npend : FB_MAX;
+    uint32_t k = 0;
+    while (c->fq_head - __atomic_load_n(&c->fq_tail, __ATOMIC_ACQUIRE) >= FQ) {
+      if ((++k & 4095u) == 0 && feeder_error(c))
+        return set_err(-EIO, "flush: the feeder thread failed");
+    }
+    struct fbatch *b = &c->fq[c->fq_head % FQ];
+    b->ticket = ++c->next_ticket;
+    b->n = cnt;
+    memcpy(b->ip, c->pend_ip, (size_t) cnt * sizeof(*b->ip));
+    __atomic_store_n(&c->fq_head, c->fq_head + 1, __ATOMIC_RELEASE);
+    c->n_feeder_flushes++;
+    if (cnt < c->npend) {
+      memmove(c->pend_ip, c->pend_ip + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_ip));
+      memmove(c->pend_l4, c->pend_l4 + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_l4));
+    }
+    c->npend -= cnt;
+  }
+  return 0;
+}
+
+/* take every queued batch that fits into sweep `w` */
+static void feeder_gather(struct feeder *F, struct fsweep *w)
+{
+  const uint32_t att = __atomic_load_n(&F->attached, __ATOMIC_ACQUIRE);
+  for (unsigned id = 0; id < TASX_MAX_CTX; id++) {
+    if (!(att & (1u << id)))
+      continue;
+    struct tasx_ctx *c = &g_ctx[id];
+    uint32_t tail = c->fq_tail;
+    const uint32_t head = __atomic_load_n(&c->fq_head, __ATOMIC_ACQUIRE), tail0 = tail;
+    while (tail != head && w->nrec < SWEEP_REC) {
+      const struct fbatch *b = &c->fq[tail % FQ];
+      if (w->n + b->n > SWEEP_MAX)
+        break;
+      for (uint32_t i = 0; i < b->n; i++) {
+        const uint8_t *ip = b->ip[i];
+        const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+        w->h_off[w->n + i] = (uint64_t) (uintptr_t) (c->zc_dev + (ip - TASX_TAS_IP_OFF - c->zc_host));
+        w->h_flen[w->n + i] = TASX_TAS_IP_OFF + (tl < 20 ? 20 : tl);
+      }
+      w->n += b->n;
+      w->rec_ctx[w->nrec] = (uint16_t) id;
+      w->rec_ticket[w->nrec] = b->ticket;
+      w->nrec++;
+      tail++;
+    }
+    if (tail != tail0)
+      __atomic_store_n(&c->fq_tail, tail, __ATOMIC_RELEASE); /* the slots are free again */
+  }
+}
+
+static int feeder_launch(struct feeder *F, struct fsweep *w, uint32_t seq)
+{
+  tasx_tcp4_params p;
+  memset(&p, 0, sizeof(p));
+  p.base = NULL; /* absolute device addresses in off[] */
+  p.off = w->d_off;
+  p.flen = w->d_flen;
+  p.n = w->n;
+  p.ip_off = TASX_TAS_IP_OFF;
+  p.l4_off = TASX_TAS_L4_OFF;
+  p.flags = TASX_F_INPLACE;
+  if (tasx_launch_tcp4(&p, 0, F->st) != 0)
+    return -1;
+  return tasx_launch_post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
+}
+
+static void *feeder_main(void *arg)
+{
+  struct feeder *F = arg;
+  uint32_t launched = 0, published = 0, idle = 0;
+  if (hipSetDevice(F->device) != hipSuccess) {
+    __atomic_store_n(&F->failed, 1, __ATOMIC_RELEASE);
+    return NULL;
+  }
+  for (;;) {
+    int did = 0;
+    /* publish completed sweeps, oldest first */
+    while (published != launched) {
+      const uint32_t s = published + 1;
+      struct fsweep *w = &F->sw[s % NSWEEP];
+      if (__atomic_load_n(F->h_done + DONE_STRIDE * (s % NSWEEP), __ATOMIC_ACQUIRE) != s)
+        break;
+      for (uint32_t r = 0; r < w->nrec; r++)
+        __atomic_store_n(&g_ctx[w->rec_ctx[r]].fd_done, w->rec_ticket[r], __ATOMIC_RELEASE);
+      __atomic_fetch_add(&F->frames, (uint64_t) w->n, __ATOMIC_RELAXED);
+      __atomic_fetch_add(&F->sweeps, (uint64_t) 1, __ATOMIC_RELAXED);
+      w->n = w->nrec = 0;
+      published = s;
+      did = 1;
+    }
+    /* gather into a free sweep buffer and launch it */
+    if (launched - published < NSWEEP) {
+      struct fsweep *w = &F->sw[(launched + 1) % NSWEEP];
+      feeder_gather(F, w);
+      __atomic_fetch_add(&F->gathers, 1u, __ATOMIC_RELEASE);
+      if (w->nrec > 0) {
+        if (feeder_launch(F, w, launched + 1) != 0) {
+          __atomic_store_n(&F->failed, 1, __ATOMIC_RELEASE);
+          return NULL;
+        }
+        launched++;
+        did = 1;
+      }
+    }
+    if (did) {
+      idle = 0;
+      continue;
+    }
+    if (!__atomic_load_n(&F->running, __ATOMIC_ACQUIRE) && published == launched)
+      return NULL;
+    if ((++idle & 4095u) == 0) {
+      if (published != launched) { /* a sweep in flight: is the stream healthy? */
+        const hipError_t e = hipStreamQuery(F->st);
+        if (e != hipSuccess && e != hipErrorNotReady) {
+          __atomic_store_n(&F->failed, 1, __ATOMIC_RELEASE);
+          return NULL;
+        }
+      } else {
+        sched_yield();
+      }
+    }
+  }
+}
+
+static void feeder_free(struct feeder *F)
+{
+  for (unsigned k = 0; k < NSWEEP; k++) {
+    if (F->sw[k].h_off)
+      hipHostFree(F->sw[k].h_off);
+    if (F->sw[k].h_flen)
+      hipHostFree(F->sw[k].h_flen);
+  }
+  if (F->h_done)
+    hipHostFree(F->h_done);
+  if (F->st)
+    hipStreamDestroy(F->st);
+  free(F);
+}
+
+int tasx_feeder_start(int device)
+{
+  int ndev = 0, rc = 0;
+  hipError_t e;
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "feeder: device %d out of range", device);
+  if ((e = hipGetDeviceCount(&ndev)) != hipSuccess)
+    return hip_err(e, "hipGetDeviceCount");
+  if (device >= ndev)
+    return set_err(-ENODEV, "device %d not present (%d GPUs)", device, ndev);
+  pthread_mutex_lock(&g_feeder_mu);
+  if (g_feeder[device]) {
+    pthread_mutex_unlock(&g_feeder_mu);
+    return set_err(-EINVAL, "feeder for device %d already running", device);
+  }
+  struct feeder *F = calloc(1, sizeof(*F));
+  if (!F) {
+    pthread_mutex_unlock(&g_feeder_mu);
+    return set_err(-ENOMEM, "feeder: out of host memory");
+  }
+  F->device = device;
+  F->running = 1;
+  if ((e = hipSetDevice(device)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&F->st, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP, hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &F->d_done, F->h_done, 0)) != hipSuccess)
+    rc = hip_err(e, "feeder allocation");
+  for (unsigned k = 0; !rc && k < NSWEEP; k++) {
+    struct fsweep *w = &F->sw[k];
+    if ((e = hipHostMalloc((void **) &w->h_off, 8u * SWEEP_MAX, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void **) &w->h_flen, 4u * SWEEP_MAX, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &w->d_off, w->h_off, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **) &w->d_flen, w->h_flen, 0)) != hipSuccess)
+      rc = hip_err(e, "feeder sweep buffers");
+  }
+  if (!rc) {
+    memset(F->h_done, 0, 4u * DONE_STRIDE * NSWEEP);
+    if (pthread_create(&F->thr, NULL, feeder_main, F) != 0)
+      rc = set_err(-ENOMEM, "feeder: pthread_create failed");
+  }
+  if (rc) {
+    feeder_free(F);
+    pthread_mutex_unlock(&g_feeder_mu);
+    return rc;
+  }
+  g_feeder[device] = F;
+  pthread_mutex_unlock(&g_feeder_mu);
+  return 0;
+}
+
+int tasx_feeder_stop(int device)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "feeder: device %d out of range", device);
+  pthread_mutex_lock(&g_feeder_mu);
+  struct feeder *F = g_feeder[device];
+  if (!F) {
+    pthread_mutex_unlock(&g_feeder_mu);
+    return set_err(-EINVAL, "no feeder running for device %d", device);
+  }
+  if (__atomic_load_n(&F->attached, __ATOMIC_ACQUIRE) != 0) {
+    pthread_mutex_unlock(&g_feeder_mu);
+    return set_err(-EBUSY, "feeder for device %d still serves contexts", device);
+  }
+  __atomic_store_n(&F->running, 0, __ATOMIC_RELEASE);
+  pthread_join(F->thr, NULL);
+  const int failed = F->failed;
+  g_feeder[device] = NULL;
+  hipSetDevice(device);
+  hipStreamSynchronize(F->st);
+  feeder_free(F);
+  pthread_mutex_unlock(&g_feeder_mu);
+  return failed ? set_err(-EIO, "the feeder thread for device %d had failed", device) : 0;
+}
+
+int tasx_feeder_stats(int device, uint64_t *sweeps, uint64_t *frames)
+{
+  if (device < 0 || device >= MAX_DEVICES || !g_feeder[device])
+    return set_err(-EINVAL, "no feeder running for device %d", device);
+  /* read by the caller while the feeder runs: a snapshot */
+  if (sweeps)
+    *sweeps = __atomic_load_n(&g_feeder[device]->sweeps, __ATOMIC_RELAXED);
+  if (frames)
+    *frames = __atomic_load_n(&g_feeder[device]->frames, __ATOMIC_RELAXED);
+  return 0;
+}
+
+int tasx_ctx_use_feeder(unsigned ctx_id, int on)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  int rc;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  const unsigned id = (unsigned) (c - g_ctx);
+  if (on) {
+    if (c->fd)
+      return 0;
+    struct feeder *F = c->device < MAX_DEVICES ? g_feeder[c->device] : NULL;
+    if (!F)
+      return set_err(-EINVAL, "no feeder running for device %d (tasx_feeder_start)", c->device);
+    if (!c->zc_host)
+      return set_err(-EINVAL, "ctx %u has no frame region (tasx_ctx_register_frames)", ctx_id);
+    if ((rc = flush_wait(c, c->next_ticket)) != 0)
+      return rc;
+    c->fq = calloc(FQ, sizeof(*c->fq));
+    if (!c->fq)
+      return set_err(-ENOMEM, "feeder queue: out of host memory");
+    c->fq_head = c->fq_tail = 0;
+    c->fd_done = c->next_ticket;
+    c->fd = F;
+    __atomic_or_fetch(&F->attached, 1u << id, __ATOMIC_RELEASE);
+    return 0;
+  }
+  if (!c->fd)
+    return 0;
+  /* every ticket handed over completes first; the feeder then never reads the queue again */
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
+  struct feeder *F = c->fd;
+  __atomic_and_fetch(&F->attached, ~(1u << id), __ATOMIC_RELEASE);
+  /* a gather pass that read the old mask may still look at the queue's
+   * indices: wait until two more passes have started and ended */
+  const uint32_t g0 = __atomic_load_n(&F->gathers, __ATOMIC_ACQUIRE);
+  while (__atomic_load_n(&F->gathers, __ATOMIC_ACQUIRE) - g0 < 2u && !__atomic_load_n(&F->failed, __ATOMIC_ACQUIRE))
+    sched_yield();
+  c->fd = NULL;
+  free(c->fq);
+  c->fq = NULL;
+  return 0;
+}
+
+int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (feeder_flushes)
+    *feeder_flushes = c->n_feeder_flushes;
+  return 0;
 }
 
 /* ---------------------------------------------------------------------- */

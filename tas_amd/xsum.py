@@ -78,6 +78,11 @@ SIGNATURES = {
     "tasx_flush_wait": (_c_int, [_uns, _c_u32]),
     "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
     "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
+    "tasx_feeder_start": (_c_int, [_c_int]),
+    "tasx_feeder_stop": (_c_int, [_c_int]),
+    "tasx_feeder_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
+    "tasx_ctx_use_feeder": (_c_int, [_uns, _c_int]),
+    "tasx_ctx_feeder_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_last_kernel": (ctypes.c_char_p, []),
     "tasx_host_alloc": (_vp, [_sz]),
@@ -383,6 +388,32 @@ def ctx_stats(ctx_id: int) -> tuple[int, int]:
     z, st = ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib().tasx_ctx_stats(ctx_id, ctypes.byref(z), ctypes.byref(st)), "tasx_ctx_stats")
     return z.value, st.value
+
+
+def feeder_start(device: int = 0) -> None:
+    """The shared feeder thread for `device` (tasx_feeder_start)."""
+    _check(lib().tasx_feeder_start(device), "tasx_feeder_start")
+
+
+def feeder_stop(device: int = 0) -> None:
+    _check(lib().tasx_feeder_stop(device), "tasx_feeder_stop")
+
+
+def feeder_stats(device: int = 0) -> tuple[int, int]:
+    sw, fr = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().tasx_feeder_stats(device, ctypes.byref(sw), ctypes.byref(fr)), "tasx_feeder_stats")
+    return sw.value, fr.value
+
+
+def use_feeder(ctx_id: int, on: bool = True) -> None:
+    """Attach the context to (or detach it from) its GPU's feeder."""
+    _check(lib().tasx_ctx_use_feeder(ctx_id, 1 if on else 0), "tasx_ctx_use_feeder")
+
+
+def feeder_flushes(ctx_id: int) -> int:
+    n = ctypes.c_uint32()
+    _check(lib().tasx_ctx_feeder_flushes(ctx_id, ctypes.byref(n)), "tasx_ctx_feeder_flushes")
+    return n.value
 
 
 def tcp4_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, n: int, out_addr: int | None,

@@ -624,6 +624,159 @@ def test_flush_records_as_frame_starts(oracle, zero_copy, shift):
         xsum.ctx_destroy(ctx)
 
 
+def _feeder_frames(nframes: int, seed: int):
+    """tx_flush-shaped frames (data segments, ACKs, short total_length) in a
+    pinned region with their expected in-place checksums."""
+    pay = np.where(np.arange(nframes) % 3 == 0, 0, (np.arange(nframes) * 53 + seed) % 1449)
+    frames = pktgen.tcp4_frames(nframes, payload=pay, stride=2048, seed=seed)
+    f = frames.reshape(nframes, 2048)
+    short = np.arange(5, nframes, 97)
+    f[short, 16], f[short, 17] = 0, (np.arange(len(short)) * 7) % 38   # total_length < 38: general body
+    ref = frames.copy()
+    oracle_ref = ref  # filled by the caller's oracle
+    pin = xsum.PinnedBuffer(frames.size + 4096)
+    pin.array[:] = 0
+    pin.array[:frames.size] = frames
+    return pin, frames, oracle_ref
+
+
+def test_shared_feeder(oracle):
+    """tasx_feeder_start + tasx_ctx_use_feeder: three contexts' flushes,
+    submitted interleaved, served by the GPU's one feeder thread (one launch
+    per sweep, absolute frame addresses from several regions); completions in
+    each context's ticket order; a batch with a frame outside the region is
+    flushed by its context after its feeder tickets; stop refuses while
+    contexts are attached; detach, stop."""
+    ctxs, nb, n = (8, 9, 10), 12, 32
+    xsum.feeder_start(0)
+    pins = []
+    try:
+        with pytest.raises(xsum.TasxError):
+            xsum.feeder_start(0)                       # one feeder per GPU
+        for k, c in enumerate(ctxs):
+            xsum.ctx_init(c, 0, 1 << 20)
+            pin, frames, ref = _feeder_frames(nb * n, 300 + k)
+            oracle.tcp4_batch(ref, nb * n, stride=2048, inplace=True)
+            with pytest.raises(xsum.TasxError):
+                xsum.use_feeder(c)                     # no frame region yet
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_feeder(c)
+            pins.append((pin, ref))
+        tickets = {c: [] for c in ctxs}
+        for b in range(nb):
+            for k, c in enumerate(ctxs):
+                for i in range(n):
+                    xsum.tcp_checksums(c, pins[k][0].addr + (b * n + i) * 2048)
+                tickets[c].append(xsum.flush_submit(c))
+        for c in ctxs:
+            assert tickets[c] == list(range(1, nb + 1))
+            xsum.flush_wait(c, tickets[c][-1])
+            assert all(xsum.flush_poll(c, t) for t in tickets[c])
+            assert xsum.feeder_flushes(c) == nb and xsum.ctx_stats(c) == (0, 0)
+        for k, c in enumerate(ctxs):
+            pin, ref = pins[k]
+            np.testing.assert_array_equal(pin.array[:ref.size], ref)
+        sweeps, frames_done = xsum.feeder_stats(0)
+        assert frames_done == len(ctxs) * nb * n and 1 <= sweeps <= len(ctxs) * nb
+        # a frame outside the region: that batch goes through the context itself
+        outside = pktgen.tcp4_frames(2, payload=np.array([100, 1448]), stride=2048, seed=401)
+        ref_out = outside.copy()
+        oracle.tcp4_batch(ref_out, 2, stride=2048, inplace=True)
+        pin, ref = pins[0]
+        pin.array[:2048] = 0
+        pin.array[:2048] = ref[:2048]
+        pin.array[24:26] = 0                                                  # stale field
+        xsum.tcp_checksums(ctxs[0], pin.addr)                                 # a feeder batch
+        t1 = xsum.flush_submit(ctxs[0])
+        xsum.tcp_checksums(ctxs[0], outside.ctypes.data)
+        xsum.tcp_checksums(ctxs[0], outside.ctypes.data + 2048)
+        t2 = xsum.flush_submit(ctxs[0])
+        assert t2 == t1 + 1
+        xsum.flush_wait(ctxs[0], t2)
+        np.testing.assert_array_equal(outside, ref_out)
+        np.testing.assert_array_equal(pin.array[:2048], ref[:2048])
+        assert xsum.ctx_stats(ctxs[0]) == (0, 1) and xsum.feeder_flushes(ctxs[0]) == nb + 1
+        with pytest.raises(xsum.TasxError):
+            xsum.feeder_stop(0)                                               # contexts attached
+        for c in ctxs:
+            xsum.use_feeder(c, False)
+        xsum.feeder_stop(0)
+    finally:
+        for c in ctxs:
+            try:
+                xsum.ctx_destroy(c)
+            except xsum.TasxError:
+                pass
+        try:
+            xsum.feeder_stop(0)
+        except xsum.TasxError:
+            pass
+        for pin, _ in pins:
+            pin.free()
+
+
+def test_shared_feeder_threads(oracle):
+    """Four fast-path threads, each with its own context bound
+    (tasx_set_thread_ctx) and attached to the feeder, each submitting 60
+    tx_flush batches with up to 3 in flight (poll, then wait for the oldest),
+    concurrently: every frame of every thread checksummed exactly."""
+    import threading
+    ctxs, nb, n = (11, 12, 13, 14), 60, 32
+    xsum.feeder_start(0)
+    pins, errs = [], []
+    try:
+        for k, c in enumerate(ctxs):
+            xsum.ctx_init(c, 0, 1 << 20)
+            pin, frames, ref = _feeder_frames(nb * n, 500 + k)
+            oracle.tcp4_batch(ref, nb * n, stride=2048, inplace=True)
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_feeder(c)
+            pins.append((pin, ref))
+
+        def core(k, c):
+            try:
+                xsum.set_thread_ctx(c)
+                inflight = []
+                for b in range(nb):
+                    for i in range(n):
+                        xsum.tcp_checksums(xsum.CTX_SELF, pins[k][0].addr + (b * n + i) * 2048)
+                    inflight.append(xsum.flush_submit(xsum.CTX_SELF))
+                    while inflight and xsum.flush_poll(xsum.CTX_SELF, inflight[0]):
+                        inflight.pop(0)
+                    if len(inflight) >= 3:
+                        xsum.flush_wait(xsum.CTX_SELF, inflight.pop(0))
+                if inflight:
+                    xsum.flush_wait(xsum.CTX_SELF, inflight[-1])
+                xsum.set_thread_ctx(xsum.CTX_SELF)
+            except Exception as e:  # reported below
+                errs.append(e)
+        th = [threading.Thread(target=core, args=(k, c)) for k, c in enumerate(ctxs)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not errs, errs
+        for k, c in enumerate(ctxs):
+            pin, ref = pins[k]
+            np.testing.assert_array_equal(pin.array[:ref.size], ref)
+            assert xsum.feeder_flushes(c) == nb
+        for c in ctxs:
+            xsum.use_feeder(c, False)
+        xsum.feeder_stop(0)
+    finally:
+        for c in ctxs:
+            try:
+                xsum.ctx_destroy(c)
+            except xsum.TasxError:
+                pass
+        try:
+            xsum.feeder_stop(0)
+        except xsum.TasxError:
+            pass
+        for pin, _ in pins:
+            pin.free()
+
+
 def test_zero_copy_needs_chunk_slack(oracle):
     """A frame whose datagram ends less than 16 bytes before the registered
     region's end is not read in place (rows read whole 16-byte chunks): that
