@@ -11,7 +11,8 @@
  * tests/c/gen_ref_frames.c built with the reference's header code, then the
  * tx_flush checksum step, and checks every frame against the committed
  * expectations: the unit-test frame's a3 bb / cf d7 and a 32-frame
- * TXBUF_SIZE batch, staged and zero-copy (mbufs in a registered pool), with
+ * TXBUF_SIZE batch, staged, zero-copy (mbufs in a registered pool) and through
+ * the shared feeder, with
  * the thread-bound context (TASX_CTX_SELF) as the only context plumbing.
  *
  *   usage: boundary_test tests/golden/ref_frames.bin
@@ -164,10 +165,25 @@ int main(int argc, char **argv)
   tasx_ctx_stats(TASX_CTX_SELF, &zc1, &st1);
   CHECK(zc1 == zc0 + 1 && st1 == st0, "zero-copy flush not taken (%u/%u -> %u/%u)", zc0, st0, zc1, st1);
 
+  /* the same batch through the GPU's shared feeder */
+  uint32_t ff = 0;
+  if (tasx_feeder_start(0) != 0 || tasx_ctx_use_feeder(TASX_CTX_SELF, 1) != 0) {
+    fprintf(stderr, "feeder: %s\n", tasx_last_error());
+    return 1;
+  }
+  run_batch("feeder", pm, frames, r, 0, n, room);
+  tasx_ctx_feeder_flushes(TASX_CTX_SELF, &ff);
+  CHECK(ff == 1, "feeder flush not taken (%u)", ff);
+  CHECK(tasx_feeder_stop(0) != 0, "feeder stopped while a context is attached");
+  if (tasx_ctx_use_feeder(TASX_CTX_SELF, 0) != 0 || tasx_feeder_stop(0) != 0) {
+    fprintf(stderr, "feeder: %s\n", tasx_last_error());
+    return 1;
+  }
+
   tasx_ctx_destroy(TASX_CTX_SELF);
   tasx_set_thread_ctx(TASX_CTX_SELF);
   CHECK(tasx_thread_ctx() < 0, "thread context still bound");
-  printf("boundary_test: %u frames (unit-test KAT + %u-frame tx_flush batch), staged and zero-copy: %s\n", n,
+  printf("boundary_test: %u frames (unit-test KAT + %u-frame tx_flush batch), staged, zero-copy and feeder: %s\n", n,
          n - 1, fails ? "FAILED" : "OK");
   return fails ? 1 : 0;
 }

@@ -76,9 +76,9 @@ def test_boundary_binary_links_only_libtasx():
 @pytest.mark.gpu
 def test_c_boundary_glue_on_gpu():
     """INTEGRATION.md's glue, compiled against the reference's types, over fake
-    mbufs: the unit-test frame and a 32-frame tx_flush batch, staged and
-    zero-copy, bit-exact against the fixture."""
+    mbufs: the unit-test frame and a 32-frame tx_flush batch, staged,
+    zero-copy and through the shared feeder, bit-exact against the fixture."""
     assert BIN.exists(), f"{BIN} not built (python -c 'import __graft_entry__ as g; g.build()' with /root/reference)"
     r = subprocess.run([str(BIN), str(FIXTURE)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "staged and zero-copy: OK" in r.stdout
+    assert "staged, zero-copy and feeder: OK" in r.stdout
