@@ -90,6 +90,18 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint16_t *out, uint32_t flags, void *stream);
 
+/* The offload branch of tcp_checksums() (config.fp_xsumoffload set,
+ * tas/fast/fast_flows.c:1060-1064): per frame, ip.chksum = 0 and tcp.chksum =
+ * tx_xsum_enable() = network_ip_phdr_xsum(ip.src, ip.dest, IP_PROTO_TCP,
+ * l3_paylen) (tas/fast/fastemu.h:97-102, tas/fast/network.h:157-173): the
+ * pseudo-header sum folded twice and not inverted, for the NIC to finish, with
+ * l3_paylen = ip.total_length - 20 (what every caller passes).  out[i] (may be
+ * NULL with TASX_F_INPLACE, which stores both fields in the frame).  The mbuf's
+ * offload flags (network_buf_tcpxsums, network.h:175-187) stay with TAS. */
+int tasx_tcp4_offload_batch_dev(void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags, void *stream);
+
 /* Same, with frame-length hints: flen[i] (or flen0 when flen == NULL) is the
  * frame's length from its start -- the mbuf data_len that tx_send() sets
  * (tas/fast/fastemu.h:81-95) before tx_flush().  Hints only let the kernel

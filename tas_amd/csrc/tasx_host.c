@@ -188,6 +188,33 @@ int tasx_tcp4_cksum_batch_dev(void *base, const uint64_t *off,
       l4_off, out, flags, stream);
 }
 
+int tasx_tcp4_offload_batch_dev(void *base, const uint64_t *off,
+    uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    uint16_t *out, uint32_t flags, void *stream)
+{
+  tasx_tcp4_params p;
+  if (n == 0)
+    return 0;
+  if ((!base && !off) || (!out && !(flags & TASX_F_INPLACE)))
+    return set_err(-EINVAL, "tcp4 offload batch: NULL base/out");
+  if (out && ((uintptr_t) out & 1))
+    return set_err(-EINVAL, "tcp4 offload batch: out must be 2-byte aligned");
+  if (flags & ~TASX_F_INPLACE)
+    return set_err(-EINVAL, "tcp4 offload batch: unknown flags 0x%x", flags);
+  memset(&p, 0, sizeof(p));
+  p.base = (uint8_t *) base;
+  p.off = off;
+  p.out = out;
+  p.stride = stride;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  p.flags = flags;
+  if (tasx_launch_tcp4_offload(&p, stream) != 0)
+    return hip_err(hipGetLastError(), "tcp4_offload_kernel launch");
+  return 0;
+}
+
 int tasx_tcp4_verify_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint8_t *flags, void *stream)

@@ -81,6 +81,8 @@ TASX_INTERNAL int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant
 /* one-lane kernel storing seq into *word (pinned host memory, device view)
  * with system-scope release, after everything before it on the stream */
 TASX_INTERNAL int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
+/* offload branch of tcp_checksums: pseudo-header sums into tcp.chksum */
+TASX_INTERNAL int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 TASX_INTERNAL int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 /* record the name of the kernel the calling thread launches (tasx_last_kernel) */

@@ -1392,6 +1392,41 @@ extern "C" int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream)
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// The offload branch of tcp_checksums() (fast_flows.c:1060-1064): ip.chksum
+// = 0 and tcp.chksum = tx_xsum_enable() = network_ip_phdr_xsum(ip.src,
+// ip.dest, IP_PROTO_TCP, l3_paylen) (fastemu.h:97-102, network.h:157-173):
+// the pseudo-header words (the address fields' bytes as native little-endian
+// 16-bit words, proto << 8, the L3 payload length in network order), folded
+// twice, NOT inverted -- the NIC finishes the checksum.  l3_paylen =
+// ip.total_length - 20 as a 16-bit value (what every caller passes,
+// fast_flows.c:936,1012,1074).  One lane per frame; 12 header bytes read.
+namespace {
+__global__ __launch_bounds__(kBlock) void tcp4_offload_kernel(tasx_tcp4_params p)
+{
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= p.n)
+    return;
+  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
+  uint8_t *ip = f + p.ip_off;
+  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  uint32_t sum = (6u << 8) + bswap16((tl - 20u) & 0xffffu);
+#pragma unroll
+  for (int k = 12; k < 20; k += 2)
+    sum += ld8(ip + k) | (ld8(ip + k + 1) << 8);
+  sum = (sum >> 16) + (sum & 0xffffu);
+  sum = (sum >> 16) + (sum & 0xffffu);
+  if (p.out)
+    stg(p.out, i, (uint16_t) sum);
+  if (p.flags & TASX_F_INPLACE) {
+    uint8_t *tcp = f + p.l4_off;
+    st8(ip + 10, 0u);
+    st8(ip + 11, 0u);
+    st8(tcp + 16, sum);
+    st8(tcp + 17, sum >> 8);
+  }
+}
+} // namespace
+
 #ifdef TASX_AB
 // The headline kernel's access pattern with no checksum logic: the same rows,
 // the same 6 clamped chunk loads per lane at 32-bit offsets from the SGPR
@@ -1438,6 +1473,18 @@ extern "C" int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t 
   return launch_groups("tcp4_pattern_kernel", tcp4_pattern_kernel, p, (hipStream_t) stream, kOccLds);
 }
 #endif
+
+extern "C" int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream)
+{
+  const uint64_t blocks = ((uint64_t) p->n + kBlock - 1) / kBlock;
+  if (blocks == 0)
+    return 0;
+  if (blocks > 0x7fffffffull)
+    return -2;
+  t_last_kernel = "tcp4_offload_kernel";
+  hipLaunchKernelGGL(tcp4_offload_kernel, dim3((uint32_t) blocks), dim3(kBlock), 0, (hipStream_t) stream, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {

@@ -78,6 +78,7 @@ SIGNATURES = {
     "tasx_flush_wait": (_c_int, [_uns, _c_u32]),
     "tasx_ctx_register_frames": (_c_int, [_uns, _vp, _sz]),
     "tasx_ctx_stats": (_c_int, [_uns, ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
+    "tasx_tcp4_offload_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp]),
     "tasx_feeder_start": (_c_int, [_c_int]),
     "tasx_feeder_stop": (_c_int, [_c_int]),
     "tasx_feeder_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
@@ -388,6 +389,22 @@ def ctx_stats(ctx_id: int) -> tuple[int, int]:
     z, st = ctypes.c_uint32(), ctypes.c_uint32()
     _check(lib().tasx_ctx_stats(ctx_id, ctypes.byref(z), ctypes.byref(st)), "tasx_ctx_stats")
     return z.value, st.value
+
+
+def tcp4_offload_batch(frames: torch.Tensor, n: int, *, offsets: torch.Tensor | None = None, stride: int = 0,
+                       ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF, inplace: bool = False,
+                       want_out: bool = True, stream=None) -> torch.Tensor | None:
+    """The offload branch of tcp_checksums (tasx_tcp4_offload_batch_dev):
+    uint16 network_ip_phdr_xsum per frame, and/or stored in place with
+    ip.chksum zeroed."""
+    out = torch.empty(n, dtype=torch.int16, device=frames.device) if want_out else None
+    if offsets is not None:
+        assert offsets.dtype == torch.int64 and offsets.numel() >= n
+    _check(lib().tasx_tcp4_offload_batch_dev(frames.data_ptr(), None if offsets is None else offsets.data_ptr(),
+                                             stride, n, ip_off, l4_off, None if out is None else out.data_ptr(),
+                                             TASX_F_INPLACE if inplace else 0, _stream(stream)),
+           "tasx_tcp4_offload_batch_dev")
+    return out
 
 
 def feeder_start(device: int = 0) -> None:

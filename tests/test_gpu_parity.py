@@ -777,6 +777,38 @@ def test_shared_feeder_threads(oracle):
             pin.free()
 
 
+@pytest.mark.parametrize("offs", [False, True])
+def test_offload_branch_phdr(oracle, offs):
+    """tasx_tcp4_offload_batch_dev, the fp_xsumoffload branch of tcp_checksums
+    (network_ip_phdr_xsum via tx_xsum_enable, not inverted, ip.chksum zeroed):
+    random addresses, total_length 0..65535 (the 16-bit l3_paylen wraps below
+    20), odd frame starts; against the oracle's restatement, out of place and in
+    place (nothing else in the frame changes)."""
+    n, stride = 5003, 96
+    rng = np.random.default_rng(33 + offs)
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    starts = np.arange(n, dtype=np.int64) * stride + (np.arange(n) % 3 if offs else 0)
+    tl = rng.integers(0, 65536, n)
+    tl[:40] = np.arange(40)
+    for k, st in enumerate(starts):
+        buf[st + 16], buf[st + 17] = tl[k] >> 8, tl[k] & 0xFF
+    exp = np.array([oracle.ip_phdr_xsum(int(buf[st + 26:st + 30].view(np.uint32)[0]),
+                                        int(buf[st + 30:st + 34].view(np.uint32)[0]), 6, int(tl[k] - 20) & 0xFFFF)
+                    for k, st in enumerate(starts)], np.uint16)
+    d = to_dev(buf)
+    kw = dict(offsets=to_dev(starts)) if offs else dict(stride=stride)
+    got = u16(xsum.tcp4_offload_batch(d, n, **kw))
+    assert xsum.last_kernel() == "tcp4_offload_kernel"
+    np.testing.assert_array_equal(got, exp)
+    xsum.tcp4_offload_batch(d, n, inplace=True, want_out=False, **kw)
+    h = d.cpu().numpy()
+    want = buf.copy()
+    for k, st in enumerate(starts):
+        want[st + 24:st + 26] = 0
+        want[st + 50:st + 52] = np.frombuffer(int(exp[k]).to_bytes(2, "little"), np.uint8)
+    np.testing.assert_array_equal(h, want)
+
+
 def test_zero_copy_needs_chunk_slack(oracle):
     """A frame whose datagram ends less than 16 bytes before the registered
     region's end is not read in place (rows read whole 16-byte chunks): that
