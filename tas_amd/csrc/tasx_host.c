@@ -855,6 +855,21 @@ static size_t staged_rec(uint32_t tl)
   return ((size_t) TASX_TAS_IP_OFF + 20 + staged_l4(tl) + 15) & ~(size_t) 15;
 }
 
+/* Post a completion word after the stream's earlier work (A/B: the
+ * command-processor write hipStreamWriteValue32 instead of the one-lane
+ * kernel, TASX_POST_WRITEVALUE=1) */
+static int post_done(uint32_t *word, uint32_t seq, hipStream_t st)
+{
+#ifdef TASX_AB
+  static int cp_write = -1;
+  if (cp_write < 0)
+    cp_write = getenv("TASX_POST_WRITEVALUE") != NULL;
+  if (cp_write)
+    return hipStreamWriteValue32(st, word, seq, 0) == hipSuccess ? 0 : -1;
+#endif
+  return tasx_launch_post_done(word, seq, st);
+}
+
 /* Submit the first `cnt` pending frames as flush `t` into slot t % NSLOT
  * (whose previous flush the caller has completed), and drop them from the
  * open batch.
@@ -924,7 +939,7 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   c->local_last = t;
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-  if (tasx_launch_post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
+  if (post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "completion-word launch");
   c->next_ticket = t;
   if (cnt < c->npend) {
@@ -1147,7 +1162,7 @@ static int feeder_launch(struct feeder *F, struct fsweep *w, uint32_t seq)
   p.flags = TASX_F_INPLACE;
   if (tasx_launch_tcp4(&p, 0, F->st) != 0)
     return -1;
-  return tasx_launch_post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
+  return post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
 }
 
 static void *feeder_main(void *arg)
