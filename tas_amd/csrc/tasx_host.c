@@ -1315,14 +1315,18 @@ int tasx_feeder_stop(int device)
 
 int tasx_feeder_stats(int device, uint64_t *sweeps, uint64_t *frames)
 {
-  if (device < 0 || device >= MAX_DEVICES || !g_feeder[device])
+  if (device < 0 || device >= MAX_DEVICES)
     return set_err(-EINVAL, "no feeder running for device %d", device);
-  /* read by the caller while the feeder runs: a snapshot */
-  if (sweeps)
-    *sweeps = __atomic_load_n(&g_feeder[device]->sweeps, __ATOMIC_RELAXED);
-  if (frames)
-    *frames = __atomic_load_n(&g_feeder[device]->frames, __ATOMIC_RELAXED);
-  return 0;
+  pthread_mutex_lock(&g_feeder_mu); /* not freed by a concurrent stop meanwhile */
+  const struct feeder *F = g_feeder[device];
+  if (F) { /* a snapshot of counters the feeder keeps updating */
+    if (sweeps)
+      *sweeps = __atomic_load_n(&F->sweeps, __ATOMIC_RELAXED);
+    if (frames)
+      *frames = __atomic_load_n(&F->frames, __ATOMIC_RELAXED);
+  }
+  pthread_mutex_unlock(&g_feeder_mu);
+  return F ? 0 : set_err(-EINVAL, "no feeder running for device %d", device);
 }
 
 int tasx_ctx_use_feeder(unsigned ctx_id, int on)
@@ -1335,20 +1339,28 @@ int tasx_ctx_use_feeder(unsigned ctx_id, int on)
   if (on) {
     if (c->fd)
       return 0;
-    struct feeder *F = c->device < MAX_DEVICES ? g_feeder[c->device] : NULL;
-    if (!F)
-      return set_err(-EINVAL, "no feeder running for device %d (tasx_feeder_start)", c->device);
     if (!c->zc_host)
       return set_err(-EINVAL, "ctx %u has no frame region (tasx_ctx_register_frames)", ctx_id);
     if ((rc = flush_wait(c, c->next_ticket)) != 0)
       return rc;
-    c->fq = calloc(FQ, sizeof(*c->fq));
-    if (!c->fq)
+    struct fbatch *fq = calloc(FQ, sizeof(*fq));
+    if (!fq)
       return set_err(-ENOMEM, "feeder queue: out of host memory");
-    c->fq_head = c->fq_tail = 0;
-    c->fd_done = c->next_ticket;
-    c->fd = F;
-    __atomic_or_fetch(&F->attached, 1u << id, __ATOMIC_RELEASE);
+    /* look the feeder up and attach under the lock tasx_feeder_stop takes */
+    pthread_mutex_lock(&g_feeder_mu);
+    struct feeder *F = c->device < MAX_DEVICES ? g_feeder[c->device] : NULL;
+    if (F) {
+      c->fq = fq;
+      c->fq_head = c->fq_tail = 0;
+      c->fd_done = c->next_ticket;
+      c->fd = F;
+      __atomic_or_fetch(&F->attached, 1u << id, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&g_feeder_mu);
+    if (!F) {
+      free(fq);
+      return set_err(-EINVAL, "no feeder running for device %d (tasx_feeder_start)", c->device);
+    }
     return 0;
   }
   if (!c->fd)
