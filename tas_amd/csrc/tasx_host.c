@@ -374,6 +374,7 @@ struct tasx_ctx {
    * (tasx_launch_post_done); the caller polls them instead of
    * hipStreamSynchronize (~3.5 us less per flush) */
   uint32_t *h_done, *d_done;
+  uint32_t *d_count; /* per slot: blocks finished (flush kernels posting their own word) */
   /* zero-copy frame region (tasx_ctx_register_frames) */
   uint8_t *zc_host;
   uint8_t *zc_dev;
@@ -452,6 +453,8 @@ static void ctx_release(struct tasx_ctx *c)
   }
   if (c->h_done)
     hipHostFree(c->h_done);
+  if (c->d_count)
+    hipFree(c->d_count);
   if (c->zc_registered)
     hipHostUnregister(c->zc_host);
   free(c->pend_ip);
@@ -515,6 +518,11 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
     return hip_err(e, "tasx_ctx_init completion words");
   }
   memset(c->h_done, 0, 4u * DONE_STRIDE * NSLOT);
+  if ((e = hipMalloc((void **) &c->d_count, 4u * DONE_STRIDE * NSLOT)) != hipSuccess ||
+      (e = hipMemset(c->d_count, 0, 4u * DONE_STRIDE * NSLOT)) != hipSuccess) {
+    ctx_release(c);
+    return hip_err(e, "tasx_ctx_init completion counters");
+  }
   c->pend_ip = calloc(c->slot_frames, sizeof(*c->pend_ip));
   c->pend_l4 = calloc(c->slot_frames, sizeof(*c->pend_l4));
   if (!c->pend_ip || !c->pend_l4) {
@@ -855,6 +863,24 @@ static size_t staged_rec(uint32_t tl)
   return ((size_t) TASX_TAS_IP_OFF + 20 + staged_l4(tl) + 15) & ~(size_t) 15;
 }
 
+/* A/B: flush kernels that post their own completion word (TASX_FUSED_DONE=1;
+ * xsum_kernels.hip block_done) */
+static void fused_done(tasx_tcp4_params *p, uint32_t *word, uint32_t *count, uint32_t seq)
+{
+#ifdef TASX_AB
+  static int on = -1;
+  if (on < 0)
+    on = getenv("TASX_FUSED_DONE") != NULL;
+  if (on) {
+    p->done_word = word;
+    p->done_count = count;
+    p->done_seq = seq;
+  }
+#else
+  (void) p, (void) word, (void) count, (void) seq;
+#endif
+}
+
 /* Post a completion word after the stream's earlier work (A/B: the
  * command-processor write hipStreamWriteValue32 instead of the one-lane
  * kernel, TASX_POST_WRITEVALUE=1) */
@@ -937,9 +963,10 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   f->zerocopy = zc;
   f->ticket = t;
   c->local_last = t;
+  fused_done(&p, c->d_done + DONE_STRIDE * (uint32_t) s, c->d_count + DONE_STRIDE * (uint32_t) s, t);
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-  if (post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
+  if (!tasx_last_launch_posted_done() && post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "completion-word launch");
   c->next_ticket = t;
   if (cnt < c->npend) {
@@ -1066,6 +1093,7 @@ struct feeder {
   pthread_t thr;
   hipStream_t st;
   uint32_t *h_done, *d_done; /* one completion word per sweep buffer */
+  uint32_t *d_count;         /* per sweep buffer: blocks finished (device memory) */
   struct fsweep sw[NSWEEP];
   uint64_t sweeps, frames;   /* statistics */
 };
@@ -1160,9 +1188,10 @@ static int feeder_launch(struct feeder *F, struct fsweep *w, uint32_t seq)
   p.ip_off = TASX_TAS_IP_OFF;
   p.l4_off = TASX_TAS_L4_OFF;
   p.flags = TASX_F_INPLACE;
+  fused_done(&p, F->d_done + DONE_STRIDE * (seq % NSWEEP), F->d_count + DONE_STRIDE * (seq % NSWEEP), seq);
   if (tasx_launch_tcp4(&p, 0, F->st) != 0)
     return -1;
-  return post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
+  return tasx_last_launch_posted_done() ? 0 : post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
 }
 
 static void *feeder_main(void *arg)
@@ -1233,6 +1262,8 @@ static void feeder_free(struct feeder *F)
   }
   if (F->h_done)
     hipHostFree(F->h_done);
+  if (F->d_count)
+    hipFree(F->d_count);
   if (F->st)
     hipStreamDestroy(F->st);
   free(F);
@@ -1263,7 +1294,9 @@ int tasx_feeder_start(int device)
   if ((e = hipSetDevice(device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&F->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP, hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &F->d_done, F->h_done, 0)) != hipSuccess)
+      (e = hipHostGetDevicePointer((void **) &F->d_done, F->h_done, 0)) != hipSuccess ||
+      (e = hipMalloc((void **) &F->d_count, 4u * DONE_STRIDE * NSWEEP)) != hipSuccess ||
+      (e = hipMemset(F->d_count, 0, 4u * DONE_STRIDE * NSWEEP)) != hipSuccess)
     rc = hip_err(e, "feeder allocation");
   for (unsigned k = 0; !rc && k < NSWEEP; k++) {
     struct fsweep *w = &F->sw[k];

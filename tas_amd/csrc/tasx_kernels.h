@@ -40,6 +40,13 @@ typedef struct tasx_tcp4_params {
   uint32_t room;         /* bytes from each frame's start that may be read (the
                           * mbuf data room); 0 = unknown */
   uint64_t *diag;        /* diagnostic timestamp buffer (TASX_AB diag variant) */
+  /* completion posted by the kernel itself (flushes): the last block to finish
+   * resets *done_count and stores done_seq into *done_word (system scope).
+   * done_word == NULL: none; tasx_last_launch_posted_done() tells whether the
+   * launched kernel did it (else the caller posts the word itself). */
+  uint32_t *done_word;
+  uint32_t *done_count;  /* device memory, 0 between launches */
+  uint32_t done_seq;
 } tasx_tcp4_params;
 
 typedef struct tasx_txseg_params {
@@ -81,6 +88,8 @@ TASX_INTERNAL int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant
 /* one-lane kernel storing seq into *word (pinned host memory, device view)
  * with system-scope release, after everything before it on the stream */
 TASX_INTERNAL int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
+/* 1 if the calling thread's last tasx_launch_tcp4 posted p->done_word itself */
+TASX_INTERNAL int tasx_last_launch_posted_done(void);
 /* offload branch of tcp_checksums: pseudo-header sums into tcp.chksum */
 TASX_INTERNAL int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */

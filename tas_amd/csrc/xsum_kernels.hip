@@ -975,7 +975,31 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
 }
 
-template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock>
+// A/B (TASX_FUSED_DONE=1 with libtasx_ab.so): the kernel's own completion word
+// (DONE, the flush forms).  Measured against the product's second one-lane
+// launch: the submitting core pays less (5.5 -> 3.4 us per 32-frame flush) and
+// a synchronous flush is ~2 us shorter, but every block's agent-scope release
+// writes back L2 (gfx950: agent scope spans the XCDs' separate L2s), and the
+// feeder's sweeps and concurrent flushes get slower (8 threads: 26 against 31
+// M frames/s; profiles/r02/r02am).  Every block makes its stores visible at
+// agent scope and counts itself in (acquire-release on a device-memory
+// counter); the last one resets the counter and release-stores the sequence
+// number into the pinned word the host polls, at system scope.  Vector atomics
+// on device memory only.
+__device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
+{
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(p.done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {
+      __hip_atomic_store(p.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.done_word, p.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
@@ -1071,6 +1095,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
   tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
+  if constexpr (DONE)
+    block_done(p);
 }
 
 #ifdef TASX_AB
@@ -1258,6 +1284,8 @@ constexpr uint32_t kOccLds = 30u * 1024u;
 
 // the launched kernel's name, per calling thread (tasx_last_kernel)
 static thread_local const char *t_last_kernel = "";
+// whether the calling thread's last tasx_launch_tcp4 posted p->done_word
+static thread_local int t_posted_done = 0;
 
 template <int G = 16, int BS = kBlock, typename K, typename Prm>
 int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
@@ -1304,6 +1332,11 @@ extern "C" const char *tasx_last_kernel(void)
 extern "C" void tasx_note_kernel(const char *name)
 {
   t_last_kernel = name;
+}
+
+extern "C" int tasx_last_launch_posted_done(void)
+{
+  return t_posted_done;
 }
 
 #ifdef TASX_AB
@@ -1568,6 +1601,14 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
   const uint32_t lds = TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u);
   switch (OFFS && mode == kMix ? kTlFirst : mode) { // the mix kernel is a stride-mode form
   case kHintArr:
+#ifdef TASX_AB
+    if (OFFS && p.done_word && p.done_count) { // a flush whose kernel posts its own completion
+      const int r = launch_groups("tcp4_tas14_kernel<hints,offs,done>",
+                                  tcp4_tas14_kernel<6, kHintArr, false, 8, true, kBlock, true>, p, s, lds);
+      t_posted_done = r == 0 && p.n > 0;
+      return r;
+    }
+#endif
     return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,offs>" : "tcp4_tas14_kernel<hints>",
                          tcp4_tas14_kernel<6, kHintArr, false, 8, OFFS>, p, s, lds);
 #ifdef TASX_AB
@@ -1619,6 +1660,7 @@ static int launch_rows(const char *name, K kern, const tasx_tcp4_params &p, uint
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
+  t_posted_done = 0;
   int mode = tas14_mode(*p);
   if (variant == 7) // RAW-only variant
     variant = 0;
