@@ -22,6 +22,7 @@
  *   20  tcp4_tas14_kernel<hints> forced (the per-frame-hint default)
  *   21  tcp4_tas14_kernel<hints_pred>: the same with lanes past a row's last
  *      chunk loading nothing (needs per-frame hints)
+ *   22..25  tcp4_tas14_kernel<hints> in blocks of 64 / 128 / 512 / 1024
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
  * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
  */

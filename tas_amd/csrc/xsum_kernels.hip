@@ -1679,6 +1679,16 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   // 4 frames per row) where tcp4_tas14_kernel's stride form applies
   // 15 / 16 / 17 / 18: tcp4_tas14_kernel<tl_first> (stride mode) in blocks of
   // 64 / 128 / 512 / 1024 threads instead of 256
+  // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
+  // in blocks of 64 / 128 / 512 / 1024 threads
+  if (variant >= 22 && variant <= 25 && p->flen && tas14_nohint_ok(*p)) {
+    switch (variant) {
+    case 22: return launch_groups<16, 64>("tcp4_tas14_kernel<hints,bs64>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 64>, *p, s);
+    case 23: return launch_groups<16, 128>("tcp4_tas14_kernel<hints,bs128>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 128>, *p, s);
+    case 24: return launch_groups<16, 512>("tcp4_tas14_kernel<hints,bs512>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 512>, *p, s);
+    default: return launch_groups<16, 1024>("tcp4_tas14_kernel<hints,bs1024>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 1024>, *p, s);
+    }
+  }
   if (variant >= 15 && variant <= 18 && !tas14_ok(*p) && tas14_nohint_ok(*p)) {
     switch (variant) {
     case 15: return launch_groups<16, 64>("tcp4_tas14_kernel<tl_first,bs64>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 64>, *p, s);

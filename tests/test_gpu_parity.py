@@ -28,7 +28,7 @@ def _lib():
 
 
 # variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = set(range(8, 22)) | {1, 4, 5}
+AB_VARIANTS = set(range(8, 26)) | {1, 4, 5}
 
 
 @contextlib.contextmanager
@@ -1077,7 +1077,7 @@ def test_verify_uniform_hint(oracle, variant):
 # rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
 
 @pytest.mark.parametrize("room", [80, 1536, 2048])
-@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 25])
 def test_tcp4_rooms_every_row_mode(oracle, room, variant):
     """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
     selection and every forced row mode (9 total_length first, 10 head-5, 11
