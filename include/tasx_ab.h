@@ -53,6 +53,11 @@ int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t
 int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
     uint32_t *out, void *stream);
 
+/* The device's read+write streaming rate: a grid-stride copy of `bytes` (16-byte
+ * multiple, 16-byte aligned), one non-temporal 16-byte load and store per
+ * lane -- the TX segment build's ceiling, timed by bench.py. */
+int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

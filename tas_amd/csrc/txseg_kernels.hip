@@ -578,10 +578,26 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 // descriptor's room (the mbuf data room) covers the frame's last 16-byte
 // chunk, that chunk is written whole, its bytes past the frame with their own
 // values, instead of by dword and byte stores.
-// ABL (A/B ablations, timing only -- results are wrong): bit 0 = no scratch
-// zero stores, 1 = no first-block write-back, 2 = no chunk-4 / piece-2 window
-// loads, 3 = no general-body fallback, 4 = no payload stores.
-template <int U, bool NTS, int WPE = 1, int ABL = 0>
+// OPT: how the frame's first block is written, and A/B ablations.
+//   kTxHeaderFirst (the product): chunks 0..4 (headers with stale checksum
+//     fields, chunk 4's payload) are stored right after the first round's loads
+//     are issued, every payload chunk as soon as it lands, and at the end only
+//     the two 16-bit checksum fields -- into lines the kernel has just written,
+//     merged in L2 (44.9-45.0 against 46.0 us, traffic 1.126 against 1.143 x
+//     algorithmic; profiles/r02/r02ar).
+//   0: the round-1 form -- the first 256-byte block (headers with both
+//     checksums + the payload chunks kept in vfb) written by one instruction
+//     at the end; kTxLineKeep: keep only chunk 4's 128-byte line; kTxFieldsOnly:
+//     keep nothing, write back chunks 1, 3, 4; kTxSimple: branch-free loop for
+//     the common case (profiles/r02/r02v, r02x).
+//   Ablations (timing only, results wrong; profiles/r02/r02u): kTxNoScratch,
+//     kTxNoWriteBack, kTxNoWindows (chunk-4 / piece-2 window loads),
+//     kTxNoFallback (general body not compiled in), kTxNoPayloadStores.
+enum : int {
+  kTxNoScratch = 1, kTxNoWriteBack = 2, kTxNoWindows = 4, kTxNoFallback = 8, kTxNoPayloadStores = 16,
+  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256
+};
+template <int U, bool NTS, int WPE = 1, int OPT = kTxHeaderFirst>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -626,8 +642,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // up front: the header chunk, chunk 4's window (payload [-2, 14)), the piece-2 window
     const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4));
     const uint32_t o4 = s1 - 2u;
-    const u32x4 w4 = (ABL & 4) ? hv : ld16u(shm, min(o4, smax));
-    const u32x4 xw = (ABL & 4) ? hv : ld16u(shm, min(xoff, smax));
+    const u32x4 w4 = (OPT & kTxNoWindows) ? hv : ld16u(shm, min(o4, smax));
+    const u32x4 xw = (OPT & kTxNoWindows) ? hv : ld16u(shm, min(xoff, smax));
     u32x4 tv = {0u, 0u, 0u, 0u};
     if (!scratch)
       tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
@@ -638,12 +654,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // block's lines are written whole by one instruction (a line written in two
     // parts at different times costs an HBM read-modify-write).
     int fbe = aoff <= 10 ? 16 - aoff : 0;
-    if (ABL & 32) { // A/B: keep only the payload chunks of chunk 4's 128-byte line
+    if (OPT & kTxLineKeep) { // A/B: keep only the payload chunks of chunk 4's 128-byte line
       const int lo8 = aoff & 7;
       fbe = min(fbe, 8 * ((lo8 + 4) / 8 + 1) - lo8);
     }
-    if (ABL & 64) // A/B: keep nothing; the write-back stores chunks 1, 3, 4 only
-      fbe = 0;
+    if (OPT & (kTxFieldsOnly | kTxHeaderFirst)) // A/B: keep nothing (64: the write-back stores chunks 1, 3, 4 only;
+      fbe = 0;          // 256: chunks 0..4 stored early, the two checksum fields at the end)
+    // chunks 0..4 (tcp4_tas14_kernel's map for 0..3; chunk 4 = option pad + payload [0, 14))
+    auto header_chunk = [&]() -> u32x4 {
+      u32x4 h = hv;
+      if (kh == 4) {
+        u32x4 win = o4 <= smax ? w4 : gather16(shm, o4, p.shm_len);
+        if (ks == 4)
+          win = splice(win, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap + 2, 16);
+        h = splice(hv, win, 2, fend - 64);
+      }
+      return h;
+    };
+    auto store_header = [&](const u32x4 &h) {
+      uint8_t *const cp = f + 16 * kh;
+      const int hi = fend - 16 * kh;
+      if (kh < 5 && hi >= 16)
+        *(__attribute__((address_space(1))) u32x4 *) cp = h;
+      else if (kh < 5 && whole && kh < K) // h holds the frame's own bytes past its end
+        *(__attribute__((address_space(1))) u32x4 *) cp = h;
+      else if (kh < 5)
+        store_range(cp, h, 0, hi, false);
+    };
     u32x4 vfb = hv;
     uint32_t acc = 0;
     const int base0 = 5 - ((5 + aoff) & 15);
@@ -652,7 +689,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // has no per-chunk branches but the store's predicate (sums by select)
     const bool simple_row = fast && wrapc == 0x7fffffff && o4 <= smax && base0 + 16 * U >= K &&
                             s1 + (uint32_t) (16 * (K - 1) - 66) <= smax;
-    const bool simple = (ABL & 128) && __builtin_amdgcn_ballot_w64(!simple_row) == 0ull;
+    const bool simple = (OPT & kTxSimple) && __builtin_amdgcn_ballot_w64(!simple_row) == 0ull;
     if (simple) {
       u32x4 a[U];
 #pragma unroll
@@ -689,6 +726,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const int k = min(max(base + gl + 16 * u, 5), K - 1);
         a[u] = ld16u(shm, min(woff(16 * k - 66), smax));
       }
+      if ((OPT & kTxHeaderFirst) && base == base0) // the header chunks (stale checksum fields) go out first
+        store_header(header_chunk());
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = base + gl + 16 * u, j0 = 16 * k - 66;
@@ -706,7 +745,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           vfb = v;
           acc = sad4(v, acc);
         } else if (hi >= 16) {
-          if (ABL & 16)
+          if (OPT & kTxNoPayloadStores)
             ;
           else if (NTS)
             __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
@@ -723,20 +762,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       }
     }
 
-    if (scratch && !(ABL & 1)) { // the scratch chunks past the frame outside its first block
+    if (scratch && !(OPT & kTxNoScratch)) { // the scratch chunks past the frame outside its first block
       const int k = K + gl;
       if (k < kend && k >= fbe)
         __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
     }
 
-    // chunks 0..4 (tcp4_tas14_kernel's map for 0..3; chunk 4 = option pad + payload [0, 14))
-    u32x4 h = hv;
-    if (kh == 4) {
-      u32x4 win = o4 <= smax ? w4 : gather16(shm, o4, p.shm_len);
-      if (ks == 4)
-        win = splice(win, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap + 2, 16);
-      h = splice(hv, win, 2, fend - 64);
-    }
+    u32x4 h = header_chunk();
     const uint32_t m0 = kh == 2 ? 0xffff0000u : (kh == 3 ? 0x0000ffffu : 0xffffffffu);
     uint32_t l4 = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
     if (kh == 4 && fend < 80)
@@ -755,7 +787,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const uint32_t len = 32u + (uint32_t) pay;
     const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph1) + bswap16(len))));
     const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
-    if (fast && !(ABL & 2)) {
+    if ((OPT & kTxHeaderFirst) && fast) { // only the two fields are left to write
+      if (gl == 15 && p.out)
+        stg(p.out, i, res);
+      if (kh == 1)
+        *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) res;
+      if (kh == 3)
+        *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) (res >> 16);
+    } else if (fast && !(OPT & kTxNoWriteBack)) {
       if (gl == 15 && p.out)
         stg(p.out, i, res);
       // the first block: header chunks with the checksums inserted (ip.chksum:
@@ -766,7 +805,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         h.x = (h.x & 0x0000ffffu) | (res & 0xffff0000u);
       uint8_t *const cp = f + 16 * kh;
       const int hi = fend - 16 * kh;
-      if ((ABL & 64) && (kh == 0 || kh == 2))
+      if ((OPT & kTxFieldsOnly) && (kh == 0 || kh == 2))
         ; // unchanged header chunks
       else if ((kh < 5 || kh < fbe) && hi >= 16)
         *(__attribute__((address_space(1))) u32x4 *) cp = kh < 5 ? h : vfb;
@@ -774,15 +813,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         *(__attribute__((address_space(1))) u32x4 *) cp = h;
       else if (kh < 5)
         store_range(cp, h, 0, hi, false);
-      else if (!(ABL & 1) && kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
+      else if (!(OPT & kTxNoScratch) && kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
         *(__attribute__((address_space(1))) u32x4 *) cp = u32x4{0u, 0u, 0u, 0u};
     }
   }
-  if (!(ABL & 8) && !fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
+  if (!(OPT & kTxNoFallback) && !fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
     txseg_row<3, NTS>(p, i, gl);
 }
 
 } // namespace
+
+#ifdef TASX_AB
+// The device's read+write streaming rate for the TX segment build's ceiling
+// (bench.py copy_ceiling): a grid-stride copy, one non-temporal 16-byte load
+// and store per lane, grid of 4 blocks per CU (tools/copy_ceiling.hip: 6.2
+// TB/s, against 5.2 for hipMemcpyAsync D2D).
+namespace {
+__global__ __launch_bounds__(256) void stream_copy_kernel(const u32x4 *src, u32x4 *dst, size_t nchunks)
+{
+  for (size_t c = (size_t) blockIdx.x * 256u + threadIdx.x; c < nchunks; c += (size_t) gridDim.x * 256u)
+    __builtin_nontemporal_store(__builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *) (src + c)),
+                                (__attribute__((address_space(1))) u32x4 *) (dst + c));
+}
+} // namespace
+
+extern "C" int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream)
+{
+  if (!src || !dst || (bytes & 15) || ((uintptr_t) src & 15) || ((uintptr_t) dst & 15))
+    return -22;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  hipLaunchKernelGGL(stream_copy_kernel, dim3((uint32_t) cus * 4u), dim3(256), 0, (hipStream_t) stream,
+                     (const u32x4 *) src, (u32x4 *) dst, bytes / 16);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
 {
@@ -805,20 +871,21 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 3: tasx_note_kernel("tx_segment_kernel<nostore>"); hipLaunchKernelGGL((tx_segment_kernel<6, 25>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // no stores at all
   case 4: tasx_note_kernel("tx_segment_kernel"); hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;  // aligned-gather kernel
   case 5: tasx_note_kernel("tx_segment_u_kernel"); hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // general layout
-  case 6: tasx_note_kernel("tx_segment_tas_kernel<plain>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, false>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // plain stores
-  case 7: tasx_note_kernel("tx_segment_tas_kernel<wpe6>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 6>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 80 VGPRs
-  case 8: tasx_note_kernel("tx_segment_tas_kernel<wpe8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 64 VGPRs
-  case 15: tasx_note_kernel("tx_segment_tas_kernel<line_keep>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 32>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 17: tasx_note_kernel("tx_segment_tas_kernel<simple>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 128>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 18: tasx_note_kernel("tx_segment_tas_kernel<simple,fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 192>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 64>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 6: tasx_note_kernel("tx_segment_tas_kernel<plain>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, false, 1, kTxHeaderFirst>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // plain stores
+  case 7: tasx_note_kernel("tx_segment_tas_kernel<wpe6>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 6, kTxHeaderFirst>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 80 VGPRs
+  case 8: tasx_note_kernel("tx_segment_tas_kernel<wpe8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 8, kTxHeaderFirst>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; // <= 64 VGPRs
+  case 15: tasx_note_kernel("tx_segment_tas_kernel<line_keep>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxLineKeep>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 19: tasx_note_kernel("tx_segment_tas_kernel<block_writeback>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 17: tasx_note_kernel("tx_segment_tas_kernel<simple>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxSimple>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 18: tasx_note_kernel("tx_segment_tas_kernel<simple,fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxSimple | kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   // 9..14: ablations (timing only)
-  case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 10: tasx_note_kernel("tx_segment_tas_kernel<abl2>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 11: tasx_note_kernel("tx_segment_tas_kernel<abl4>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 12: tasx_note_kernel("tx_segment_tas_kernel<abl8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoScratch>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 10: tasx_note_kernel("tx_segment_tas_kernel<abl2>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoWriteBack>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 11: tasx_note_kernel("tx_segment_tas_kernel<abl4>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoWindows>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 12: tasx_note_kernel("tx_segment_tas_kernel<abl8>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoFallback>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 13: tasx_note_kernel("tx_segment_tas_kernel<abl15>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 15>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 14: tasx_note_kernel("tx_segment_tas_kernel<abl16>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 14: tasx_note_kernel("tx_segment_tas_kernel<abl16>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoPayloadStores>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   default: break;
   }
 #else
