@@ -667,19 +667,32 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
     torch.cuda.synchronize()
     cur = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # torch creates an event's HIP handle on its first record(): do that here,
+    # not inside the timed region (10-44 us per event, profiles/r02/r02aw)
+    e0.record(cur)
+    e1.record(cur)
+    torch.cuda.synchronize()
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(cur)
     for s in streams or []:
         s.wait_event(e0)
+    ta = time.perf_counter()
     run(warmup, steps)
+    tb = time.perf_counter()
     for s in streams or []:
         cur.wait_stream(s)
     e1.record(cur)
+    tc = time.perf_counter()
     torch.cuda.synchronize()
     barrier(ws)
     t1 = time.perf_counter()
+    if os.environ.get("TASX_BENCH_TRACE"):
+        print(json.dumps({"K": steps, "rec0_us": round((ta - t0) * 1e6, 2), "issue_us": round((tb - ta) * 1e6, 2),
+                          "rec1_us": round((tc - tb) * 1e6, 2), "sync_us": round((t1 - tc) * 1e6, 2),
+                          "host_us": round((t1 - t0) * 1e6, 2),
+                          "event_us": round(e0.elapsed_time(e1) * 1e3, 2)}), file=sys.stderr)
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
