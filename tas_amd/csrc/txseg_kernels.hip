@@ -585,6 +585,13 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 //     the two 16-bit checksum fields -- into lines the kernel has just written,
 //     merged in L2 (44.9-45.0 against 46.0 us, traffic 1.126 against 1.143 x
 //     algorithmic; profiles/r02/r02ar).
+//   kTxDppTail (the product, with kTxHeaderFirst): the row total reaches every
+//     lane by row rotations and the lane holding chunk 1 finishes and writes
+//     both fields, instead of four ds_bpermute round trips to and from lane 15
+//     (0.1-0.3 us better in 4 of 4 same-box pairs; profiles/r02/r02ax, r02ay).
+//     Occupancy: the kernel holds 105 VGPRs (4 waves per SIMD); 5 waves
+//     (WPE 5: 96 VGPRs, a small spill) costs 48 us and residency capped at 3
+//     or 2 blocks per CU 46 / 50 us.
 //   0: the round-1 form -- the first 256-byte block (headers with both
 //     checksums + the payload chunks kept in vfb) written by one instruction
 //     at the end; kTxLineKeep: keep only chunk 4's 128-byte line; kTxFieldsOnly:
@@ -595,9 +602,9 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 //     kTxNoFallback (general body not compiled in), kTxNoPayloadStores.
 enum : int {
   kTxNoScratch = 1, kTxNoWriteBack = 2, kTxNoWindows = 4, kTxNoFallback = 8, kTxNoPayloadStores = 16,
-  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256
+  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256, kTxDppTail = 512
 };
-template <int U, bool NTS, int WPE = 1, int OPT = kTxHeaderFirst>
+template <int U, bool NTS, int WPE = 1, int OPT = kTxHeaderFirst | kTxDppTail>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -778,8 +785,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u)));
     const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
     const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
-    acc = row_sum16(acc);
     const int l1 = (int) ((threadIdx.x & 63u) & ~15u) + ((1 + aoff) & 15); // lane holding chunk 1
+    if ((OPT & kTxDppTail) && (OPT & kTxHeaderFirst)) {
+      // no LDS round trips: every lane gets the row total by row rotations,
+      // and the lane holding chunk 1 (ip.len, the IP header and pseudo-header
+      // sums) finishes both checksums and writes both fields itself
+      acc += row_ror<8>(acc);
+      acc += row_ror<4>(acc);
+      acc += row_ror<2>(acc);
+      acc += row_ror<1>(acc);
+      const bool ok1 = kh == 1 && bswap16(h.x & 0xffffu) == 52u + (uint32_t) pay;
+      fast = (__builtin_amdgcn_ballot_w64(ok1) >> l1) & 1ull; // otherwise the general body redoes the segment
+      if (ok1) {
+        const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
+        const uint32_t tcpc = inv_result(
+            residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph) + bswap16(32u + (uint32_t) pay))));
+        if (p.out)
+          stg(p.out, i, ipc | (tcpc << 16));
+        *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
+        *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
+      }
+    } else {
+    acc = row_sum16(acc);
     const uint32_t ip1 = (uint32_t) __shfl((int) ipsum, l1, 64), ph1 = (uint32_t) __shfl((int) ph, l1, 64);
     const uint32_t tl = bswap16((uint32_t) __shfl((int) (h.x & 0xffffu), l1, 64));
     fast = tl == 52u + (uint32_t) pay; // otherwise the general body redoes the segment
@@ -815,6 +842,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         store_range(cp, h, 0, hi, false);
       else if (!(OPT & kTxNoScratch) && kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
         *(__attribute__((address_space(1))) u32x4 *) cp = u32x4{0u, 0u, 0u, 0u};
+    }
     }
   }
   if (!(OPT & kTxNoFallback) && !fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
@@ -878,6 +906,14 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 19: tasx_note_kernel("tx_segment_tas_kernel<block_writeback>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, 0>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 17: tasx_note_kernel("tx_segment_tas_kernel<simple>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxSimple>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 18: tasx_note_kernel("tx_segment_tas_kernel<simple,fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxSimple | kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 20: tasx_note_kernel("tx_segment_tas_kernel<shfl_tail>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 21: tasx_note_kernel("tx_segment_tas_kernel<shfl_tail,wpe5>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 5, kTxHeaderFirst>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 22: tasx_note_kernel("tx_segment_tas_kernel<wpe5>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 5>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  // 23-25: the product with residency capped by dynamic LDS (the kernel uses none):
+  // 48 KiB -> 3 blocks per CU, 64 KiB -> 2, 40 KiB -> 3 (timing probes)
+  case 23: tasx_note_kernel("tx_segment_tas_kernel<shfl_tail,lds48k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst>), grid, block, 48u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 24: tasx_note_kernel("tx_segment_tas_kernel<lds64k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 64u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 25: tasx_note_kernel("tx_segment_tas_kernel<lds48k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 48u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   // 9..14: ablations (timing only)
   case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoScratch>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;

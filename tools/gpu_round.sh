@@ -20,6 +20,8 @@ step() {  # name timeout cmd...
 step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()'
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step bench 400 python bench.py
+# the driver's step count: ms_per_step against the event-timed launch
+step bench_k20 300 python bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline
 for w in mixed shard8m tso; do
   step bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3
 done
