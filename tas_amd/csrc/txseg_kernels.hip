@@ -602,7 +602,8 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 //     kTxNoFallback (general body not compiled in), kTxNoPayloadStores.
 enum : int {
   kTxNoScratch = 1, kTxNoWriteBack = 2, kTxNoWindows = 4, kTxNoFallback = 8, kTxNoPayloadStores = 16,
-  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256, kTxDppTail = 512
+  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256, kTxDppTail = 512,
+  kTxNoHeaderStore = 1024, kTxNoFields = 2048, kTxNoSums = 4096 // timing-only ablations (profiles/r02/r02az)
 };
 template <int U, bool NTS, int WPE = 1, int OPT = kTxHeaderFirst | kTxDppTail>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
@@ -733,7 +734,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const int k = min(max(base + gl + 16 * u, 5), K - 1);
         a[u] = ld16u(shm, min(woff(16 * k - 66), smax));
       }
-      if ((OPT & kTxHeaderFirst) && base == base0) // the header chunks (stale checksum fields) go out first
+      if ((OPT & kTxHeaderFirst) && !(OPT & kTxNoHeaderStore) && base == base0) // the header chunks (stale checksum fields) go out first
         store_header(header_chunk());
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -758,7 +759,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
             __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
           else
             *(__attribute__((address_space(1))) u32x4 *) cp = v;
-          acc = sad4(v, acc);
+          if (!(OPT & kTxNoSums))
+            acc = sad4(v, acc);
         } else {
           acc += sad_below(v, (uint32_t) hi);
           if (whole)
@@ -802,8 +804,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
             residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph) + bswap16(32u + (uint32_t) pay))));
         if (p.out)
           stg(p.out, i, ipc | (tcpc << 16));
-        *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
-        *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
+        if (!(OPT & kTxNoFields)) {
+          *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
+          *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
+        }
       }
     } else {
     acc = row_sum16(acc);
@@ -914,6 +918,10 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 23: tasx_note_kernel("tx_segment_tas_kernel<shfl_tail,lds48k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst>), grid, block, 48u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 24: tasx_note_kernel("tx_segment_tas_kernel<lds64k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 64u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 25: tasx_note_kernel("tx_segment_tas_kernel<lds48k>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 48u << 10, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  // 26-28: timing-only ablations of the product (results wrong)
+  case 26: tasx_note_kernel("tx_segment_tas_kernel<no_header_store>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoHeaderStore>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 27: tasx_note_kernel("tx_segment_tas_kernel<no_fields>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoFields>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 28: tasx_note_kernel("tx_segment_tas_kernel<no_sums>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoSums>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   // 9..14: ablations (timing only)
   case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoScratch>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
