@@ -724,6 +724,55 @@ def leg(run, bytes_per_step: int, args, ws, desc, kernel: str = "", streams=None
 # ---------------------------------------------------------------------------
 # end to end (PCIe-inclusive; never the headline)
 
+def txseg_host_leg(ws: int, rank: int, reps: int) -> dict:
+    """The fused TX segment build as TAS would run it: the
+    app's TX buffers (tas_shm), the mbuf frames and the descriptors all in
+    pinned host memory mapped for the GPU; the kernel gathers each payload and
+    writes each frame over PCIe.  The same 64K segments as the device-resident
+    tx_segment leg; tests/test_txseg.py::test_gpu_txseg_host_memory checks it."""
+    n = N_FRAMES
+    _, _, segs, shm_len = pktgen.tx_segments(n, seed=pktgen.SEED + 2000 + rank, nflows=8192, tx_len=16384,
+                                             make_shm=False, room=STRIDE)
+    pins = []
+    try:
+        hs = xsum.PinnedBuffer(shm_len)
+        pins.append(hs)
+        hs.array[:] = device_random(shm_len, pktgen.SEED + 7 + rank).cpu().numpy()
+        hf = xsum.PinnedBuffer(n * STRIDE)
+        pins.append(hf)
+        hf.array[:] = device_tcp4_frames(n, STRIDE, IP_TOTAL, pktgen.SEED + rank).cpu().numpy()
+        hd = xsum.PinnedBuffer(segs.nbytes)
+        pins.append(hd)
+        hd.array[:] = segs.view(np.uint8)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+
+        def run():
+            xsum.tx_segment_batch(hs.dev_addr, hf.dev_addr, hd.dev_addr, n, shm_len=shm_len, out=out)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.25:  # clocks and PCIe out of idle (~3 ms per launch)
+            run()
+        torch.cuda.synchronize()
+        barrier(ws)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        tm = max_over_ranks(t, ws)
+        hdr = pktgen.HDRS_LEN - pktgen.ETH_LEN - pktgen.IP_LEN
+        alg = n * (2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4)
+        return {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s (algorithmic, as tx_segment)",
+                "ms_per_batch": tm / reps * 1e3, "segments_per_s": sum_over_ranks(n * reps, ws) / tm,
+                "pcie_h2d_bytes_per_rank": n * (pktgen.TCP_MSS + pktgen.HDRS_LEN + 32),
+                "pcie_d2h_bytes_per_rank": n * (pktgen.HDRS_LEN + pktgen.TCP_MSS),
+                "kernel": xsum.last_kernel(),
+                "note": "tas_shm, frames and descriptors in pinned host memory; payload read and frame "
+                        "written over PCIe in one pass"}
+    finally:
+        for pb in pins:
+            pb.free()
+
+
 def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
     """Every rank at once, each from its own NUMA-local host thread (this
     process, pinned by numa_pin before these buffers were touched):
@@ -786,6 +835,7 @@ def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
             res["flush32_note"] = ("32 x tasx_defer_tcp4 + tasx_flush via ctypes (Python call overhead "
                                    "included); tools/flush_bench.c has the C-side numbers")
             f32.free()
+        res["tx_segment_host"] = txseg_host_leg(ws, rank, 2 * reps)
     finally:
         xsum.ctx_destroy(0)
         pin.free()

@@ -1430,7 +1430,15 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
 void *tasx_host_alloc(size_t bytes)
 {
   void *p = NULL;
-  hipError_t e = hipHostMalloc(&p, bytes, 0);
+  unsigned flags = 0;
+#ifdef TASX_AB
+  { /* A/B: hipHostMalloc flags (TASX_HOST_ALLOC_FLAGS, e.g. 0x80000000 = non-coherent) */
+    const char *fe = getenv("TASX_HOST_ALLOC_FLAGS");
+    if (fe)
+      flags = (unsigned) strtoul(fe, NULL, 0);
+  }
+#endif
+  hipError_t e = hipHostMalloc(&p, bytes, flags);
   if (e != hipSuccess) {
     hip_err(e, "hipHostMalloc");
     return NULL;

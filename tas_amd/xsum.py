@@ -310,18 +310,25 @@ def flow_lookup_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst
     return h, fid
 
 
-def tx_segment_batch(shm: torch.Tensor, frames: torch.Tensor, segs: torch.Tensor, n: int, *,
+def tx_segment_batch(shm, frames, segs, n: int, *, shm_len: int | None = None,
                      ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
                      out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
     """Fused TX segment build: flow_tx_read() of each segment's payload from the
     shared-memory TX buffers into its frame, then tcp_checksums() in place
     (tas/fast/fast_flows.c:930-936).  `segs` holds n 32-byte tasx_tx_seg
     descriptors (pktgen.TX_SEG_DTYPE bytes, 16-byte aligned on the device).
-    Returns int32 ip.chksum | tcp.chksum << 16 per segment (0 = rejected)."""
-    assert segs.numel() * segs.element_size() >= 32 * n
+    shm, frames and segs are device tensors or device addresses (ints: e.g. a
+    PinnedBuffer's dev_addr, the tas_shm region or mbuf pool mapped for the
+    GPU); an int shm needs shm_len.  Returns int32 ip.chksum | tcp.chksum << 16
+    per segment (0 = rejected)."""
+    if isinstance(segs, torch.Tensor):
+        assert segs.numel() * segs.element_size() >= 32 * n
+    if shm_len is None:
+        shm_len = shm.numel() * shm.element_size()
     if out is None:
-        out = torch.empty(n, dtype=torch.int32, device=frames.device)
-    _check(lib().tasx_tx_segment_batch_dev(_ptr(shm), shm.numel() * shm.element_size(), _ptr(frames),
+        out = torch.empty(n, dtype=torch.int32,
+                          device=frames.device if isinstance(frames, torch.Tensor) else "cuda")
+    _check(lib().tasx_tx_segment_batch_dev(_ptr(shm), shm_len, _ptr(frames),
                                            _ptr(segs), n, ip_off, l4_off, _ptr(out), _stream(stream)),
            "tasx_tx_segment_batch_dev")
     return out

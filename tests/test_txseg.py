@@ -212,6 +212,52 @@ def test_gpu_txseg_wrap_positions_and_region_edges(oracle, room):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("where", ["shm", "shm+frames", "all"])
+def test_gpu_txseg_host_memory(oracle, where):
+    """SURVEY 8f row 1 as TAS would run it: the app's TX buffers (tas_shm) in
+    pinned host memory mapped for the GPU, optionally the mbuf frames and the
+    descriptors too; the kernel gathers and writes over PCIe."""
+    import torch
+    from tas_amd import xsum
+    dev = "cuda:0"
+    n = 2048
+    pay = np.where(np.arange(n) % 7 == 0, (np.arange(n) * 53) % 1449, pktgen.TCP_MSS)
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=256, odd=True, seed=0x5EED,
+                                           room=pktgen.MBUF_ROOM)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    pins = []
+    try:
+        hs = xsum.PinnedBuffer(sl)
+        pins.append(hs)
+        hs.array[:] = shm[:sl]
+        if where == "shm":
+            dfr = torch.from_numpy(fr.copy()).to(dev)
+            frames = dfr
+        else:
+            hf = xsum.PinnedBuffer(fr.size)
+            pins.append(hf)
+            hf.array[:] = fr
+            frames = hf.dev_addr
+        if where == "all":
+            hd = xsum.PinnedBuffer(segs.nbytes)
+            pins.append(hd)
+            hd.array[:] = segs.view(np.uint8)
+            dsegs = hd.dev_addr
+        else:
+            dsegs = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+        out = xsum.tx_segment_batch(hs.dev_addr, frames, dsegs, n, shm_len=sl)
+        torch.cuda.synchronize()
+        assert xsum.last_kernel() == "tx_segment_tas_kernel"
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+        got = dfr.cpu().numpy() if where == "shm" else pins[1].array.copy()
+        np.testing.assert_array_equal(got, exp_fr)
+    finally:
+        for pb in pins:
+            pb.free()
+
+
+@pytest.mark.gpu
 def test_gpu_txseg_errors():
     import torch
     from tas_amd import xsum

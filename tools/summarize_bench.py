@@ -32,3 +32,7 @@ for path in sys.argv[1:]:
         e = d["e2e"]
         print(f"  e2e staged {e['staged']['value']:.1f} zero-copy {e['zero_copy']['value']:.1f} GiB/s "
               f"flush32 {e.get('flush32_staged_us', 0):.1f} / {e.get('flush32_zero_copy_us', 0):.1f} us")
+        if e.get("tx_segment_host"):
+            h = e["tx_segment_host"]
+            print(f"  e2e tx_segment_host {h['value']:.1f} GiB/s alg, {h['ms_per_batch']:.3f} ms per 64K segments, "
+                  f"{h['segments_per_s'] / 1e6:.1f} M segments/s")
