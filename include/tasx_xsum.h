@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 3
+#define TASX_ABI_VERSION 4
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -231,6 +231,22 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
 #define TASX_FLOW_NONE 0xffffffffu
 int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
+    const void *flowht, uint32_t ht_entries, const void *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out, void *stream);
+
+/* One RX pass (ABI 4): tasx_tcp4_verify_batch_dev_room() and
+ * tasx_flow_lookup_batch_dev() of the same frames, with the same arguments,
+ * read bounds, errors and outputs (flags[i]; fid_out[i], hash_out[i]) as the
+ * two calls in turn.  Where the verify call would take a TAS row kernel (IPv4
+ * at 14 mod 16, TCP at +20, stride mode or offsets), the lookup runs inside it:
+ * the frame's header line is read once, and the lookup's dependent
+ * bucket/flow-state loads overlap the checksum loads.  Other batches run the
+ * two kernels in turn.  The lookup reads the 12 key bytes at ip_off + 12 of
+ * every frame, as tasx_flow_lookup_batch_dev does.  Asynchronous on `stream`. */
+int tasx_rx_batch_dev(const void *base, const uint64_t *off, uint64_t stride,
+    const uint32_t *flen, uint32_t flen0, uint32_t room, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint8_t *flags,
     const void *flowht, uint32_t ht_entries, const void *flowst,
     uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
     uint32_t *hash_out, uint32_t *fid_out, void *stream);

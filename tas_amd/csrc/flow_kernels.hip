@@ -96,8 +96,6 @@ __device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
   return funnel16(ld16(c0, 0), ld16(c1, 0), (int) (a & 15));
 }
 
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-typedef uint32_t u32x3u __attribute__((ext_vector_type(3), aligned(1)));
 
 // CRC: 0 bitwise on the VALU, 1 slice-by-4 from LDS, 2 byte-position tables
 // from LDS (3: no CRC, a diagnostic build only -- wrong flow ids); CHUNK: key

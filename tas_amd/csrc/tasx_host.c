@@ -294,6 +294,53 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   return 0;
 }
 
+int tasx_rx_batch_dev(const void *base, const uint64_t *off, uint64_t stride,
+    const uint32_t *flen, uint32_t flen0, uint32_t room, uint32_t n,
+    uint32_t ip_off, uint32_t l4_off, uint8_t *flags,
+    const void *flowht, uint32_t ht_entries, const void *flowst,
+    uint32_t fs_num, uint32_t fs_stride, uint32_t fs_key_off,
+    uint32_t *hash_out, uint32_t *fid_out, void *stream)
+{
+  tasx_tcp4_params p;
+  int r;
+  if (n == 0)
+    return 0;
+  if ((!base && !off) || !flags)
+    return set_err(-EINVAL, "rx batch: NULL base/flags");
+  if ((r = check_room(room, stride, off, ip_off, l4_off, "rx batch")) != 0)
+    return r;
+  if (!flowht || !flowst || !fid_out)
+    return set_err(-EINVAL, "rx batch: NULL flowht/flowst/fid_out");
+  if (ht_entries == 0 || fs_num == 0)
+    return set_err(-EINVAL, "rx batch: empty flow table");
+  if ((fs_stride & 3u) || (fs_key_off & 3u) || ((uintptr_t) flowst & 3u) || ((uintptr_t) flowht & 7u))
+    return set_err(-EINVAL, "rx batch: misaligned flow table");
+  if (((uintptr_t) fid_out & 3u) || ((uintptr_t) hash_out & 3u))
+    return set_err(-EINVAL, "rx batch: outputs must be 4-byte aligned");
+  memset(&p, 0, sizeof(p));
+  p.base = (uint8_t *) base;
+  p.off = off;
+  p.out = (uint16_t *) (void *) flags;
+  p.stride = stride;
+  p.n = n;
+  p.ip_off = ip_off;
+  p.l4_off = l4_off;
+  p.flen = flen;
+  p.flen0 = flen0;
+  p.room = room;
+  p.flowht = (const uint32_t *) flowht;
+  p.flowst = (const uint8_t *) flowst;
+  p.fid_out = fid_out;
+  p.hash_out = hash_out;
+  p.ht_entries = ht_entries;
+  p.fs_num = fs_num;
+  p.fs_stride = fs_stride;
+  p.fs_key_off = fs_key_off;
+  if (tasx_launch_tcp4_rx(&p, g_variant, stream) != 0)
+    return hip_err(hipGetLastError(), "rx kernel launch");
+  return 0;
+}
+
 int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
     uint64_t stride, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     const void *flowht, uint32_t ht_entries, const void *flowst,

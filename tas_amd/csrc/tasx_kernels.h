@@ -47,6 +47,15 @@ typedef struct tasx_tcp4_params {
   uint32_t *done_word;
   uint32_t *done_count;  /* device memory, 0 between launches */
   uint32_t done_seq;
+  /* the RX flow lookup fused into verification (tasx_rx_batch_dev) */
+  const uint32_t *flowht; /* {flow_id, flow_hash} pairs */
+  const uint8_t *flowst;
+  uint32_t *fid_out;
+  uint32_t *hash_out;     /* or NULL */
+  uint32_t ht_entries;
+  uint32_t fs_num;
+  uint32_t fs_stride;
+  uint32_t fs_key_off;
 } tasx_tcp4_params;
 
 typedef struct tasx_txseg_params {
@@ -83,6 +92,10 @@ TASX_INTERNAL int tasx_launch_raw(const tasx_raw_params *p, int variant, void *s
 TASX_INTERNAL int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
 /* receive-side verification; p->out points to n flag bytes */
 TASX_INTERNAL int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream);
+/* RX verification (flags to p->out) and the flow lookup (p->fid_out,
+ * p->hash_out) of the same frames: one pass where the row kernel takes the
+ * batch, else the two kernels in turn */
+TASX_INTERNAL int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void *stream);
 /* RX flow lookup (flow_kernels.hip) */
 TASX_INTERNAL int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream);
 /* one-lane kernel storing seq into *word (pinned host memory, device view)

@@ -17,6 +17,8 @@ constexpr int kBlock = 256;
 // generic to the compiler and would lower to flat_load; these lower to
 // global_load_dwordx4 / global_load_ubyte / global_store_*.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x3u __attribute__((ext_vector_type(3), aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4 gcu4;
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 typedef __attribute__((address_space(1))) uint8_t gu8;
@@ -325,6 +327,22 @@ __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
     }
   }
   return fold64_to_18(acc);
+}
+
+// flow_hash (tas/fast/fast_flows.c:1078-1082): SSE4.2 crc32 semantics,
+// crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0)), bit by bit on
+// the VALU (the same arithmetic as flow_kernels.hip's product form)
+__device__ __forceinline__ uint32_t crc32c_u32(uint32_t crc, uint32_t w)
+{
+  crc ^= w;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    crc = (crc >> 1) ^ (0x82f63b78u & (0u - (crc & 1u)));
+  return crc;
+}
+__device__ __forceinline__ uint32_t tas_flow_hash(uint32_t lip, uint32_t rip, uint32_t ports)
+{
+  return crc32c_u32(crc32c_u32(crc32c_u32(0u, lip), rip), ports);
 }
 
 } // namespace

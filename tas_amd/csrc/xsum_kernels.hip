@@ -999,16 +999,26 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
   }
 }
 
-template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false>
+// FLOW (RX, with VERIFY): the frame's flow lookup in the same pass
+// (fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163, as
+// flow_kernels.hip): lanes 0..3 of the row load the 12-byte key (ip.src,
+// ip.dst, ports: a line the row's chunk loads fetch anyway) BEFORE the chunk
+// loads -- vector loads complete in order, so the hash waits on the key
+// alone -- hash it, probe bucket entry h + lane, and load that candidate's key
+// while the chunks land; the first matching entry's lane writes the flow id.
+template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
+          bool FLOW = false>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
+  static_assert(!FLOW || VERIFY, "the fused flow lookup is an RX form");
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
   const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
+  const uint8_t *ipp;         // the IPv4 header (FLOW)
   uint32_t a0;
   bool row_ok = true;
   if constexpr (OFFS) {
@@ -1016,8 +1026,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     row_ok = (fo & 15u) == 0u;
     fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
     a0 = 0;
+    ipp = (const uint8_t *) (uintptr_t) (fo + 14u);
   } else {
     a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+    ipp = fb + a0 + 14u;
+  }
+  constexpr int kNb = (int) TASX_FLOWHT_NBSZ;
+  u32x3 fkey = {0u, 0u, 0u};
+  if constexpr (FLOW) {
+    if (gl < kNb) // ip.src, ip.dst, tcp.src | tcp.dst << 16 (little-endian dwords)
+      fkey = *(__attribute__((address_space(1))) const u32x3u *) (ipp + 12);
   }
   // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
   uint32_t have = 65535u;
@@ -1094,7 +1112,34 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
+  // FLOW: the hash and the bucket probe go out while the chunks are in flight
+  uint32_t fh = 0, ffid = 0;
+  u32x3 ck = {0u, 0u, 0u};
+  bool fcand = false;
+  if constexpr (FLOW) {
+    if (gl < kNb) {
+      const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16); // tcp.dest | tcp.src << 16
+      fh = tas_flow_hash(fkey.y, fkey.x, ports);
+      const uint64_t e = ldg((const uint64_t *) p.flowht, (fh + (uint32_t) gl) % p.ht_entries);
+      const uint32_t ef = (uint32_t) e, eh = (uint32_t) (e >> 32);
+      ffid = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
+      fcand = (ef & TASX_FLOWHTE_VALID) && eh == fh && ffid < p.fs_num;
+      ck = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
+                                                              (uint64_t) (fcand ? ffid : 0u) * p.fs_stride +
+                                                              p.fs_key_off);
+    }
+  }
   tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
+  if constexpr (FLOW) {
+    const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16);
+    const bool match = gl < kNb && fcand && ck.x == fkey.y && ck.y == fkey.x && ck.z == ports;
+    const uint32_t rm = (uint32_t) (__builtin_amdgcn_ballot_w64(match) >> ((threadIdx.x & 63u) & ~15u)) & 0xfu;
+    const int first = rm ? __builtin_ctz(rm) : 0; // the first matching entry wins
+    if (gl == first)
+      stg(p.fid_out, i, rm ? ffid : TASX_FLOW_NONE);
+    if (gl == 0 && p.hash_out)
+      stg(p.hash_out, i, fh);
+  }
   if constexpr (DONE)
     block_done(p);
 }
@@ -1560,6 +1605,59 @@ static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t 
     return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,verify,offs>" : "tcp4_tas14_kernel<tl_first,verify>",
                          tcp4_tas14_kernel<6, kTlFirst, true, 8, OFFS>, p, s, lds);
   }
+}
+
+template <bool OFFS>
+static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s)
+{
+  const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u);
+  switch (mode) {
+  case kHintArr:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,verify,offs,flow>" : "tcp4_tas14_kernel<hints,verify,flow>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, OFFS, kBlock, false, true>, p, s, lds);
+  default:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,verify,offs,flow>"
+                              : "tcp4_tas14_kernel<tl_first,verify,flow>",
+                         tcp4_tas14_kernel<6, kTlFirst, true, 8, OFFS, kBlock, false, true>, p, s, lds);
+  }
+}
+
+// RX verification + flow lookup: the row kernels' selection (as
+// tasx_launch_tcp4_verify) with the lookup fused in; batches no row kernel
+// takes run the general verify kernel and then flow_lookup_kernel
+extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void *stream)
+{
+  hipStream_t s = (hipStream_t) stream;
+  const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
+  if (auto6 && tas14_ok(*p))
+    return launch_groups("tcp4_tas14_kernel<hint,verify,flow>",
+                         tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, true>, *p, s,
+                         TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
+  if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
+    const int mode = p->flen ? kHintArr : kTlFirst;
+    return p->off ? launch_tas14_rx<true>(*p, mode, s) : launch_tas14_rx<false>(*p, mode, s);
+  }
+  int r = tasx_launch_tcp4_verify(p, variant, stream);
+  if (r != 0)
+    return r;
+  tasx_flow_params fp = {};
+  fp.base = p->base;
+  fp.off = p->off;
+  fp.stride = p->stride;
+  fp.flowht = p->flowht;
+  fp.flowst = p->flowst;
+  fp.hash_out = p->hash_out;
+  fp.fid_out = p->fid_out;
+  fp.n = p->n;
+  fp.ip_off = p->ip_off;
+  fp.l4_off = p->l4_off;
+  fp.ht_entries = p->ht_entries;
+  fp.fs_num = p->fs_num;
+  fp.fs_stride = p->fs_stride;
+  fp.fs_key_off = p->fs_key_off;
+  r = tasx_launch_flow_lookup(&fp, 0, stream);
+  tasx_note_kernel("tcp4 verify + flow_lookup_kernel");
+  return r;
 }
 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)

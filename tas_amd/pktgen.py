@@ -218,13 +218,21 @@ def rx_frames(keys: np.ndarray, stride: int = MBUF_ROOM, seed: int = SEED) -> np
     local port (the key fast_flows_packet_fss builds, :1097-1101).  Only the
     first 64 bytes of each frame are filled (headers); the rest is random."""
     n = len(keys)
-    f = tcp4_frames(n, payload=0, stride=stride, seed=seed).reshape(n, stride)
+    f = tcp4_frames(n, payload=0, stride=stride, seed=seed)
+    set_flow_keys(f, keys, stride)
+    return f
+
+
+def set_flow_keys(frames: np.ndarray, keys: np.ndarray, stride: int) -> None:
+    """Write each flow key into its frame's headers as the peer sends it
+    (rx_frames' mapping), in place; checksums are not updated."""
+    n = len(keys)
+    f = frames[:n * stride].reshape(n, stride)
     ip, t = ETH_LEN, ETH_LEN + IP_LEN
     f[:, ip + 16: ip + 20] = keys[:, 0:4]
     f[:, ip + 12: ip + 16] = keys[:, 4:8]
     f[:, t + 2: t + 4] = keys[:, 8:10]
     f[:, t: t + 2] = keys[:, 10:12]
-    return f.reshape(-1)
 
 
 def kat_frame() -> bytearray:

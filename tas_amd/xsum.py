@@ -61,6 +61,8 @@ SIGNATURES = {
                                                  _vp]),
     "tasx_flow_lookup_batch_dev": (_c_int, [_vp, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32,
                                             _c_u32, _c_u32, _vp, _vp, _vp]),
+    "tasx_rx_batch_dev": (_c_int, [_vp, _vp, _c_u64, _vp, _c_u32, _c_u32, _c_u32, _c_u32, _c_u32, _vp, _vp, _c_u32,
+                                   _vp, _c_u32, _c_u32, _c_u32, _vp, _vp, _vp]),
     "tasx_tx_segment_batch_dev": (_c_int, [_vp, _c_u64, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ctx_init": (_c_int, [_uns, _c_int, _sz]),
     "tasx_ctx_destroy": (_c_int, [_uns]),
@@ -308,6 +310,29 @@ def flow_lookup_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst
                                             ent, _ptr(flowst), fs_num, fs_stride, fs_key_off, _ptr(h), _ptr(fid),
                                             _stream(stream)), "tasx_flow_lookup_batch_dev")
     return h, fid
+
+
+def rx_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst: torch.Tensor, fs_num: int, *,
+             offsets: torch.Tensor | None = None, stride: int = 0, ip_off: int = TAS_IP_OFF,
+             l4_off: int = TAS_L4_OFF, frame_len: torch.Tensor | int | None = None, room: int = 0,
+             fs_stride: int = 128, fs_key_off: int = 32, want_hash: bool = True, flags=None, fid=None, h=None,
+             stream=None):
+    """One RX pass: tcp4_verify_batch and flow_lookup_batch of the same frames
+    (tasx_rx_batch_dev).  Returns (flags uint8, hashes int32 or None, flow
+    ids int32)."""
+    dev = frames.device if isinstance(frames, torch.Tensor) else "cuda"
+    flags = torch.empty(n, dtype=torch.uint8, device=dev) if flags is None else flags
+    fid = torch.empty(n, dtype=torch.int32, device=dev) if fid is None else fid
+    if h is None and want_hash:
+        h = torch.empty(n, dtype=torch.int32, device=dev)
+    if offsets is not None:
+        assert offsets.dtype == torch.int64 and offsets.numel() >= n
+    flen, flen0 = _hints(frame_len, n) if frame_len is not None else (None, 0)
+    ent = flowht.numel() * flowht.element_size() // 8
+    _check(lib().tasx_rx_batch_dev(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0, room, n, ip_off, l4_off,
+                                   _ptr(flags), _ptr(flowht), ent, _ptr(flowst), fs_num, fs_stride, fs_key_off,
+                                   _ptr(h), _ptr(fid), _stream(stream)), "tasx_rx_batch_dev")
+    return flags, h, fid
 
 
 def tx_segment_batch(shm, frames, segs, n: int, *, shm_len: int | None = None,
