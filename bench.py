@@ -482,6 +482,7 @@ class FlowLookupWorkload:
 
     def __init__(self, rotate: int, seed: int):
         keys = pktgen.flow_keys(self.NFLOWS, seed=seed)
+        self.keys = keys
         self.fs_np = pktgen.flow_state(keys, seed=seed)
         self.fs = torch.from_numpy(self.fs_np).cuda()
         # hashes of the flows' own keys through the kernel (one-entry dummy table)
@@ -527,6 +528,53 @@ class FlowLookupWorkload:
                 "sample": f"rotation 0's {self.N} frames, oracle fast_flows_packet_fss restatement, "
                           f"median of {reps} passes",
                 "parity_vs_gpu": "bit-exact" if np.array_equal(exp, gpu_fid) else "MISMATCH"}
+
+
+class RxPassWorkload:
+    """One RX pass (tasx_rx_batch_dev): checksum verification and the flow
+    lookup of the same received frames in one kernel (SURVEY.md section 8f rows
+    3 + 4; fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163).  An RX burst
+    of 50% data segments and 50% pure ACKs in 2048 B mbufs, each frame's
+    received length as its hint and read bound, flow keys drawn from the
+    TAS-sized flow table of FlowLookupWorkload (10% unknown).  Algorithmic bytes
+    per frame: ip.total_length + 2 B total_length read + 1 B flags (verify), 32
+    B bucket + 12 B flow key read + 8 B hash and flow id written (lookup; the
+    frame's key is inside the header verify reads)."""
+    desc = (f"{N_FRAMES} received TAS frames in {STRIDE} B rooms, 50% data segments and 50% pure ACKs, per-frame "
+            f"received lengths, looked up in a {FlowLookupWorkload.NFLOWS}-flow / {FlowLookupWorkload.ENTRIES}-"
+            "entry flow table (10% unknown keys): tasx_rx_batch_dev")
+
+    def __init__(self, fw: "FlowLookupWorkload", rotate: int, seed: int, n: int = N_FRAMES, ack_frac: float = 0.5):
+        rng = np.random.default_rng(seed)
+        pay = np.where(rng.random(n) < ack_frac, 0, IP_TOTAL - 52).astype(np.int64)
+        keys = fw.keys[rng.integers(0, fw.NFLOWS, n)].copy()
+        keys[rng.random(n) < 0.1, 4] ^= 0x5A
+        host = pktgen.tcp4_frames(n, payload=pay, stride=STRIDE, seed=seed)
+        pktgen.set_flow_keys(host, keys, STRIDE)
+        self.n, self.fw = n, fw
+        first = torch.from_numpy(host).cuda()
+        self.flen = torch.from_numpy((pktgen.ETH_LEN + 52 + pay).astype(np.int32)).cuda()
+        xsum.tcp4_cksum_batch(first, n, stride=STRIDE, frame_len=self.flen, room=STRIDE, inplace=True,
+                              want_out=False)
+        self.bufs = [first] + [first.clone() for _ in range(rotate - 1)]
+        self.flags = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in self.bufs]
+        self.fids = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in self.bufs]
+        self.hashes = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in self.bufs]
+        self.bytes_per_step = int((52 + pay + 3).sum()) + n * (32 + 12 + 8)
+
+    def loop(self, which: int = benchloop.RX_FUSED, streams=None, uniform: bool = False) -> benchloop.Loop:
+        """uniform: the received length as one uniform hint (all-data bursts)."""
+        fw = self.fw
+        flen, flen0 = (None, FRAME_LEN) if uniform else (self.flen.data_ptr(), 0)
+        args = [benchloop.RxArgs(
+            benchloop.Tcp4Args(b.data_ptr(), None, STRIDE, flen, flen0, 0, self.n, IP_OFF, L4_OFF, 0,
+                               fl.data_ptr()),
+            benchloop.FlowArgs(b.data_ptr(), None, STRIDE, self.n, IP_OFF, L4_OFF, fw.ht.data_ptr(), fw.ENTRIES,
+                               fw.fs.data_ptr(), fw.NFLOWS, pktgen.FLOWST_SIZE, pktgen.FLOWST_KEY_OFF,
+                               h.data_ptr(), f.data_ptr()))
+            for b, fl, h, f in zip(self.bufs, self.flags, self.hashes, self.fids)]
+        what = "tasx_rx_batch_dev" if which == benchloop.RX_FUSED else "verify + flow lookup"
+        return benchloop.Loop("rx", args, _stream_ptrs(streams), which, what)
 
 
 # Flow lookup bounds (DESIGN.md section 5.4).  The lookup is a dependent chain
@@ -1106,6 +1154,26 @@ def main(argv=None):
             dist.destroy_process_group()
 
 
+def rx_pass_leg(fw: FlowLookupWorkload, rot: int, args, ws: int, rank: int) -> dict:
+    """The fused RX pass against the two calls it replaces, timed the same way
+    on the same frames and outputs (tests/test_rx_fused.py checks both)."""
+    rp = RxPassWorkload(fw, min(rot, 12), pktgen.SEED + 4000 + rank)
+    r = leg(rp.loop(benchloop.RX_FUSED), rp.bytes_per_step, args, ws, RxPassWorkload.desc,
+            "tcp4_tas14_kernel<hints,verify,flow>")
+    sep = leg(rp.loop(benchloop.RX_SEPARATE), rp.bytes_per_step, args, ws,
+              "same frames: tasx_tcp4_verify_batch_dev_room, then tasx_flow_lookup_batch_dev")
+    torch.cuda.synchronize()
+    r["separate"] = {"ms_per_step": sep["ms_per_step"], "launch_pair_avg_us": sep["roofline"]["launch_avg_us"],
+                     "kernels": "tcp4_tas14_kernel<hints,verify> + flow_lookup_kernel"}
+    r["speedup_vs_separate"] = round(sep["roofline"]["launch_avg_us"] / r["roofline"]["launch_avg_us"], 3)
+    r["all_frames_verified"] = bool(all((f == 3).all().item() for f in rp.flags))
+    r["found_frac"] = round(float((rp.fids[0] != -1).float().mean().item()), 4)
+    r["parity"] = "tests/test_rx_fused.py::test_rx_fused_forms[hints]"
+    del rp
+    torch.cuda.empty_cache()
+    return r
+
+
 def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     rot = max(1, args.rotate)
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
@@ -1187,7 +1255,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         del tw
         torch.cuda.empty_cache()
 
-    flow = None
+    flow = rx_pass = None
     if not args.no_flow:
         fw = FlowLookupWorkload(min(rot, 4), pktgen.SEED + 3000 + rank)
         flow = leg(fw.loop(), fw.bytes_per_step, args, ws, FlowLookupWorkload.desc, "flow_lookup_kernel")
@@ -1206,6 +1274,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                             "algorithmic_bytes_per_launch": hbm["algorithmic_bytes_per_launch"], "hbm": hbm}
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             flow["cpu_baseline"] = fw.cpu_check(3.0)
+        rx_pass = rx_pass_leg(fw, rot, args, ws, rank)
         del fw
         torch.cuda.empty_cache()
 
@@ -1272,6 +1341,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             line["tx_segment"] = txseg
         if flow is not None:
             line["flow_lookup"] = flow
+        if rx_pass is not None:
+            line["rx_pass"] = rx_pass
         if "e2e" in extra:
             line["e2e"] = extra["e2e"]
         if "pmc" in extra:

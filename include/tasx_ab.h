@@ -23,6 +23,9 @@
  *   21  tcp4_tas14_kernel<hints_pred>: the same with lanes past a row's last
  *      chunk loading nothing (needs per-frame hints)
  *   22..25  tcp4_tas14_kernel<hints> in blocks of 64 / 128 / 512 / 1024
+ *   26  tasx_rx_batch_dev with the flow lookup inside the verify rows
+ *      (tcp4_tas14_kernel<...,flow_row>) instead of in lookup blocks ahead of
+ *      the verify blocks; slower wherever ACKs are present
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
  * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
  */

@@ -37,6 +37,13 @@ class FlowArgs(ctypes.Structure):
                 ("fs_key_off", _u32), ("hash_out", _vp), ("fid_out", _vp)]
 
 
+class RxArgs(ctypes.Structure):
+    _fields_ = [("v", Tcp4Args), ("f", FlowArgs)]
+
+
+# tasxb_rx_loop entry points
+RX_FUSED, RX_SEPARATE = 0, 1
+
 _lib = None
 
 
@@ -59,7 +66,9 @@ def lib() -> ctypes.CDLL:
                                        ctypes.c_int]
         L.tasxb_flow_loop.argtypes = [ctypes.POINTER(FlowArgs), ctypes.c_int, ctypes.c_int, ctypes.c_int, pp,
                                       ctypes.c_int]
-        for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop):
+        L.tasxb_rx_loop.argtypes = [ctypes.c_int, ctypes.POINTER(RxArgs), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, pp, ctypes.c_int]
+        for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop, L.tasxb_rx_loop):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -69,19 +78,19 @@ class Loop:
     """run(first, K): K steps, batch (first + k) % R on stream (first + k) % S."""
 
     def __init__(self, kind: str, args: list, streams: list[int], which: int = 0, what: str = ""):
-        cls = {"tcp4": Tcp4Args, "raw": RawArgs, "txseg": TxSegArgs, "flow": FlowArgs}[kind]
+        cls = {"tcp4": Tcp4Args, "raw": RawArgs, "txseg": TxSegArgs, "flow": FlowArgs, "rx": RxArgs}[kind]
         self.arr = (cls * len(args))(*args)
         self.streams = (_vp * len(streams))(*streams)
         self.R, self.S, self.which, self.kind = len(args), len(streams), which, kind
         self.what = what or kind
         L = lib()
         self.fn = {"tcp4": L.tasxb_tcp4_loop, "raw": L.tasxb_raw_loop, "txseg": L.tasxb_txseg_loop,
-                   "flow": L.tasxb_flow_loop}[kind]
+                   "flow": L.tasxb_flow_loop, "rx": L.tasxb_rx_loop}[kind]
 
     def __call__(self, first: int, K: int) -> None:
         if K <= 0:
             return
-        if self.kind == "tcp4":
+        if self.kind in ("tcp4", "rx"):
             rc = self.fn(self.which, self.arr, self.R, first, K, self.streams, self.S)
         else:
             rc = self.fn(self.arr, self.R, first, K, self.streams, self.S)

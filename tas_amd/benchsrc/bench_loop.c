@@ -135,3 +135,35 @@ int tasxb_flow_loop(const tasxb_flow *a, int R, int first, int K, void *const *s
   }
   return 0;
 }
+
+/* one RX pass: tasx_rx_batch_dev (which = 0), or the two calls it replaces in
+ * turn, tasx_tcp4_verify_batch_dev_room then tasx_flow_lookup_batch_dev
+ * (which = 1), over the same frames and outputs */
+typedef struct tasxb_rx {
+  tasxb_tcp4 v;     /* verify arguments (out = uint8_t flags) */
+  tasxb_flow f;     /* lookup arguments (base/off/stride/n/ip_off/l4_off as v's) */
+} tasxb_rx;
+
+int tasxb_rx_loop(int which, const tasxb_rx *a, int R, int first, int K, void *const *streams, int S)
+{
+  for (int k = 0; k < K; k++) {
+    const tasxb_rx *b = &a[(first + k) % R];
+    void *s = streams[(first + k) % S];
+    const tasxb_tcp4 *v = &b->v;
+    const tasxb_flow *f = &b->f;
+    int rc;
+    if (which == 0) {
+      rc = tasx_rx_batch_dev(v->base, v->off, v->stride, v->flen, v->flen0, v->room, v->n, v->ip_off,
+          v->l4_off, (uint8_t *) v->out, f->flowht, f->ht_entries, f->flowst, f->fs_num, f->fs_stride,
+          f->fs_key_off, f->hash_out, f->fid_out, s);
+    } else {
+      rc = tcp4_call(TASXB_VERIFY, v, s);
+      if (!rc)
+        rc = tasx_flow_lookup_batch_dev(f->base, f->off, f->stride, f->n, f->ip_off, f->l4_off, f->flowht,
+            f->ht_entries, f->flowst, f->fs_num, f->fs_stride, f->fs_key_off, f->hash_out, f->fid_out, s);
+    }
+    if (rc)
+      return rc;
+  }
+  return 0;
+}

@@ -999,22 +999,46 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
   }
 }
 
-// FLOW (RX, with VERIFY): the frame's flow lookup in the same pass
-// (fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163, as
-// flow_kernels.hip): lanes 0..3 of the row load the 12-byte key (ip.src,
-// ip.dst, ports: a line the row's chunk loads fetch anyway) BEFORE the chunk
-// loads -- vector loads complete in order, so the hash waits on the key
-// alone -- hash it, probe bucket entry h + lane, and load that candidate's key
-// while the chunks land; the first matching entry's lane writes the flow id.
+// FLOW (RX, with VERIFY): the frames' flow lookup (fast_flows_packet_fss,
+// tas/fast/fast_flows.c:1084-1163) in the same launch.
+//  kFlowSplit (the product): the grid's first blocks run flow_lookup_lane, one
+//   frame per lane (BS frames per block), the rest are the verify blocks.  The
+//   lookup's dependent chain (key -> bucket -> flow key) is the long one, so
+//   its blocks start first and overlap the verify rows instead of forming the
+//   grid's tail; 64 hashes per wave.  64K received frames: 15-23 % below the
+//   two kernels in turn.
+//  kFlowRow (A/B variant 26): lanes 0..3 of each verify row load the 12-byte
+//   key before the chunk loads, hash it, probe bucket entry h + lane and load
+//   that candidate's key while the chunks land.  Each wave of 4 rows pays a
+//   whole bitwise CRC for 4 frames, and the bucket (issued after the chunks,
+//   vector loads return in order) waits for all of them: slower wherever
+//   ACKs are present.  Measured and not taken either: lookup blocks
+//   interleaved one per BS frames (their chains end the grid), and the key
+//   hashed beside the row's first load with the bucket issued before the
+//   chunks (the per-row CRC stays).
+enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2 };
 template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
-          bool FLOW = false>
+          int FLOW = kFlowNone>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
-  static_assert(!FLOW || VERIFY, "the fused flow lookup is an RX form");
+  static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
+  static_assert(FLOW != kFlowSplit || !DONE, "split grids post no completion word");
   const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (BS / 16) + threadIdx.x / 16;
+  uint32_t vb = blockIdx.x; // this block's verify block
+  if constexpr (FLOW == kFlowSplit) {
+    // the lookup blocks first: their dependent chains are the long ones, so
+    // they start at once and overlap the verify blocks instead of forming the
+    // grid's tail (interleaved one per BS frames they did: DESIGN.md 5.2)
+    const uint32_t nl = (p.n + BS - 1u) / BS;
+    if (blockIdx.x < nl) {
+      flow_lookup_lane(p, blockIdx.x * BS + threadIdx.x);
+      return;
+    }
+    vb = blockIdx.x - nl;
+  }
+  const uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
   const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
@@ -1033,7 +1057,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
   constexpr int kNb = (int) TASX_FLOWHT_NBSZ;
   u32x3 fkey = {0u, 0u, 0u};
-  if constexpr (FLOW) {
+  if constexpr (FLOW == kFlowRow) {
     if (gl < kNb) // ip.src, ip.dst, tcp.src | tcp.dst << 16 (little-endian dwords)
       fkey = *(__attribute__((address_space(1))) const u32x3u *) (ipp + 12);
   }
@@ -1116,10 +1140,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   uint32_t fh = 0, ffid = 0;
   u32x3 ck = {0u, 0u, 0u};
   bool fcand = false;
-  if constexpr (FLOW) {
+  if constexpr (FLOW == kFlowRow) {
     if (gl < kNb) {
-      const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16); // tcp.dest | tcp.src << 16
-      fh = tas_flow_hash(fkey.y, fkey.x, ports);
+      fh = tas_flow_hash(fkey.y, fkey.x, (fkey.z >> 16) | (fkey.z << 16));
       const uint64_t e = ldg((const uint64_t *) p.flowht, (fh + (uint32_t) gl) % p.ht_entries);
       const uint32_t ef = (uint32_t) e, eh = (uint32_t) (e >> 32);
       ffid = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
@@ -1130,7 +1153,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
   }
   tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
-  if constexpr (FLOW) {
+  if constexpr (FLOW == kFlowRow) {
     const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16);
     const bool match = gl < kNb && fcand && ck.x == fkey.y && ck.y == fkey.x && ck.z == ports;
     const uint32_t rm = (uint32_t) (__builtin_amdgcn_ballot_w64(match) >> ((threadIdx.x & 63u) & ~15u)) & 0xfu;
@@ -1607,35 +1630,72 @@ static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t 
   }
 }
 
+// the split grid of tcp4_tas14_kernel<..., kFlowSplit>: one lookup block per
+// BS frames, then the verify blocks
+template <int BS = kBlock, typename K>
+static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
+{
+  const uint64_t nv = ((uint64_t) p.n + BS / 16 - 1) / (BS / 16), nl = ((uint64_t) p.n + BS - 1) / BS;
+  if (nv == 0)
+    return 0;
+  if (nv + nl > 0x7fffffffull)
+    return -2;
+  t_last_kernel = name;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) (nv + nl)), dim3(BS), lds, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <bool OFFS, int MODE, int FLOW>
+static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
+{
+  static const char *const names[2][2][3] = {
+      {{"", "tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow>"},
+       {"", "tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>"}},
+      {{"", "tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow>"},
+       {"", "tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow>"}}};
+  const char *name = names[MODE == kHintArr][OFFS][FLOW];
+  auto kern = tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kBlock, false, FLOW>;
+  if constexpr (FLOW == kFlowSplit)
+    return launch_split(name, kern, p, s, lds);
+  return launch_groups(name, kern, p, s, lds);
+}
+
 template <bool OFFS>
-static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s)
+static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, int variant)
 {
   const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u);
-  switch (mode) {
-  case kHintArr:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,verify,offs,flow>" : "tcp4_tas14_kernel<hints,verify,flow>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, OFFS, kBlock, false, true>, p, s, lds);
-  default:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,verify,offs,flow>"
-                              : "tcp4_tas14_kernel<tl_first,verify,flow>",
-                         tcp4_tas14_kernel<6, kTlFirst, true, 8, OFFS, kBlock, false, true>, p, s, lds);
-  }
+#ifdef TASX_AB
+  if (variant == 26) // A/B: the lookup inside the rows
+    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowRow>(p, s, lds)
+                            : launch_rx_rows<OFFS, kTlFirst, kFlowRow>(p, s, lds);
+#else
+  (void) variant;
+#endif
+  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
+                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
 }
 
 // RX verification + flow lookup: the row kernels' selection (as
-// tasx_launch_tcp4_verify) with the lookup fused in; batches no row kernel
-// takes run the general verify kernel and then flow_lookup_kernel
+// tasx_launch_tcp4_verify) with the lookup blocks first in the same grid
+// (kFlowSplit); batches no row kernel takes run the general verify kernel and
+// then flow_lookup_kernel
 extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
   const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
-  if (auto6 && tas14_ok(*p))
-    return launch_groups("tcp4_tas14_kernel<hint,verify,flow>",
-                         tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, true>, *p, s,
-                         TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
+  if (auto6 && tas14_ok(*p)) {
+    const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds);
+#ifdef TASX_AB
+    if (variant == 26)
+      return launch_groups("tcp4_tas14_kernel<hint,verify,flow_row>",
+                           tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowRow>, *p, s, lds);
+#endif
+    return launch_split("tcp4_tas14_kernel<hint,verify,flow>",
+                        tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit>, *p, s, lds);
+  }
   if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
     const int mode = p->flen ? kHintArr : kTlFirst;
-    return p->off ? launch_tas14_rx<true>(*p, mode, s) : launch_tas14_rx<false>(*p, mode, s);
+    return p->off ? launch_tas14_rx<true>(*p, mode, s, variant) : launch_tas14_rx<false>(*p, mode, s, variant);
   }
   int r = tasx_launch_tcp4_verify(p, variant, stream);
   if (r != 0)

@@ -161,3 +161,28 @@ def test_bench_flow_lookup_leg():
     fw.loop()(0, 1)
     assert xsum.last_kernel() == "flow_lookup_kernel"
     assert fw.cpu_check(0.05)["parity_vs_gpu"] == "bit-exact"
+
+
+def test_bench_rx_pass_leg(oracle):
+    """The rx_pass leg as timed: tasx_rx_batch_dev on 64K received frames (50%
+    data / 50% ACKs, per-frame received lengths) in the TAS-sized flow table,
+    and the two calls it replaces (RX_SEPARATE) -- both bit-exact against the
+    oracles."""
+    from tas_amd import benchloop
+    fw = bench.FlowLookupWorkload(1, pktgen.SEED + 3000)
+    rp = bench.RxPassWorkload(fw, 1, pktgen.SEED + 4000)
+    frames = host(rp.bufs[0])
+    flen = host(rp.flen).astype(np.uint32)
+    exp_flags = oracle.tcp4_verify_batch_bounded(frames, rp.n, flen, stride=bench.STRIDE)
+    exp_h, exp_fid = oracle.flow_lookup_batch(frames, rp.n, fw.ht_np, fw.fs_np, fs_num=fw.NFLOWS,
+                                              stride=bench.STRIDE)
+    assert np.all(exp_flags == 3)
+    for which, kernel in ((benchloop.RX_FUSED, "tcp4_tas14_kernel<hints,verify,flow>"),
+                          (benchloop.RX_SEPARATE, "flow_lookup_kernel")):
+        for a in (rp.flags[0], rp.fids[0], rp.hashes[0]):
+            a.fill_(0x5A)
+        rp.loop(which)(0, 1)
+        assert xsum.last_kernel() == kernel
+        np.testing.assert_array_equal(host(rp.flags[0]), exp_flags)
+        np.testing.assert_array_equal(host(rp.hashes[0]).view(np.uint32), exp_h)
+        np.testing.assert_array_equal(host(rp.fids[0]).view(np.uint32), exp_fid)

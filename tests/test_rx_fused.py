@@ -124,3 +124,72 @@ def test_rx_fused_ragged_and_errors():
         xsum.rx_batch(fr, 4, ht, fs, 4, stride=2048, fs_stride=130)         # misaligned flow table
     with pytest.raises(xsum.TasxError):
         xsum.rx_batch(fr, 4, ht, fs, 4, stride=2048, room=4096)             # room past the stride
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["hint", "hints", "tl_first", "tl_first_offs"])
+def test_rx_fused_row_variant_ab(oracle, form):
+    """A/B variant 26 (libtasx_ab.so): the lookup inside the verify rows
+    instead of in lookup blocks ahead of them -- the same results."""
+    import torch
+    from tas_amd import xsum
+    stride, offs, bound, uniform, kernel = FORMS[form]
+    kernel = kernel.replace(",flow>", ",flow_row>")
+    n = 4096
+    frames, rcv, ht, fs, nflows, _ = _burst(oracle, n, stride, seed=700 + len(form), uniform=uniform)
+    dev = "cuda:0"
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    kw = dict(offsets=t(np.arange(n, dtype=np.int64) * stride)) if offs else dict(stride=stride)
+    if bound == "uniform":
+        kw["frame_len"] = int(rcv[0])
+        b = int(rcv[0])
+    elif bound == "len":
+        kw["frame_len"] = t(rcv.astype(np.int32))
+        b = rcv.astype(np.uint32)
+    else:
+        b = 0 if offs else stride
+    exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, b, stride=stride)
+    exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=stride)
+    with xsum.using_library(xsum.AB_LIB_PATH):
+        xsum.set_kernel_variant(26)
+        try:
+            flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nflows, **kw)
+            torch.cuda.synchronize()
+            assert xsum.last_kernel() == kernel
+        finally:
+            xsum.set_kernel_variant(0)
+    np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+    np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 26])
+def test_rx_fused_batch_edges(oracle, variant):
+    """Batch sizes around row, block and lookup-block boundaries (16 frames
+    per verify block, 256 frames per lookup block): every frame verified and looked
+    up once, in the product's split grid and the row form (A/B 26)."""
+    import contextlib
+    import torch
+    from tas_amd import xsum
+    frames, rcv, ht, fs, nflows, _ = _burst(oracle, 1300, 2048, seed=911)
+    dev = "cuda:0"
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    fr = t(frames)
+    ctx = xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()
+    kernel = "tcp4_tas14_kernel<hints,verify,flow_row>" if variant else "tcp4_tas14_kernel<hints,verify,flow>"
+    with ctx:
+        xsum.set_kernel_variant(variant)
+        try:
+            for n in (1, 15, 16, 17, 255, 256, 257, 511, 1024, 1300):
+                exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
+                exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, rcv[:n].astype(np.uint32), stride=2048)
+                flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048,
+                                              frame_len=t(rcv[:n].astype(np.int32)))
+                torch.cuda.synchronize()
+                assert xsum.last_kernel() == kernel
+                np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+                np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+                np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
+        finally:
+            xsum.set_kernel_variant(0)

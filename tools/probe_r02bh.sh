@@ -1,0 +1,7 @@
+# split-grid RX pass: parity, then the A/B probe and the bench leg
+set -e
+O=gpurun_out/r02bh
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_rx_fused.py tests/test_bench_configs.py -x -v -m gpu --timeout 120 --timeout-method thread -k "rx" > $O/tests.log 2>&1
+TASX_LIB=tas_amd/_lib/libtasx_ab.so timeout -k 10 200 python tools/rx_probe.py --fracs 0,0.5,1 --rounds 3 > $O/rx_probe.jsonl 2>&1
+echo done
