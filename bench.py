@@ -950,6 +950,13 @@ def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> 
         "host_cpus": os.cpu_count(), "cpus_this_rank": allowed,
         "cores_note": (f"{threads} threads = the box's CPU share for one GPU; the host's other "
                        f"{(os.cpu_count() or 0) - threads} CPUs serve the other GPUs' jobs and are not used"),
+        # BASELINE.md asks for all host cores too; running them would take the
+        # other GPUs' CPU shares, so the figure is the measured per-thread rate
+        # at `threads` scaled linearly to every host CPU: an upper bound (the
+        # host's DRAM bandwidth caps it long before), never a measurement
+        "all_cores_estimate": {"value": alg / tn / GIB / threads * (os.cpu_count() or threads),
+                               "unit": "GiB/s", "cores": os.cpu_count(), "measured": False,
+                               "how": f"{threads}-thread rate / {threads} x host CPUs (linear upper bound)"},
         "parity_vs_gpu": "bit-exact" if parity else "MISMATCH",
     }
 
