@@ -15,10 +15,15 @@
  * ack packet"), so the oracle is pinned by (1) the published RFC 1071 section 3
  * vector, (2) a known-answer frame built exactly as the reference unit test
  * scenario builds it (tests/tas_unit/fastpath.c:187-207 ->
- * tas/fast/fast_flows.c:877-955), hand-derived, and (3) an independent numpy
- * restatement (oracle/xsum_ref.py) over committed random fixtures.  No
- * reference-produced output exists for this path: parity is unpinned by the
- * reference itself ("Parity status").
+ * tas/fast/fast_flows.c:877-955), hand-derived, (3) the Linux TCP/IP stack
+ * -- the check the reference's own end-to-end test relies on
+ * (tests/full/fulltest.c:103: TAS with --fp-no-xsumoffload against Linux,
+ * which drops bad checksums): 51 frames Linux checksummed and 41 frames this
+ * oracle checksummed that Linux accepted (tests/golden/gen_linux_frames.py,
+ * tests/test_linux_frames.py), and (4) an independent numpy restatement
+ * (oracle/xsum_ref.py) over committed random fixtures.  No output of the
+ * reference itself exists for this path (it cannot be built here; see
+ * DESIGN.md section 4).
  */
 #ifndef TASX_ORACLE_H_
 #define TASX_ORACLE_H_

@@ -1,0 +1,112 @@
+"""Parity against the Linux TCP/IP stack's own checksums
+(tests/golden/linux_frames.npz, made by tests/golden/gen_linux_frames.py).
+
+The reference's end-to-end test pins TAS's software checksums by running TAS
+with --fp-no-xsumoffload against the Linux stack, which drops segments with a
+wrong checksum (/root/reference/tests/full/fulltest.c:103).  The fixture holds
+one TCP connection over a TUN device: the frames Linux sent (its checksums,
+computed in software) and the frames checksummed by the C oracle that Linux
+accepted.  Here every frame gets its checksum fields overwritten and
+recomputed -- by the C oracle, the numpy restatement and the GPU kernels in
+each batch form -- and must come out as on the wire; and every frame must
+verify.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import xsum_ref
+
+FIX = Path(__file__).resolve().parent / "golden" / "linux_frames.npz"
+ROOM = 2048
+
+
+def _load():
+    d = np.load(FIX)
+    n = len(d["lens"])
+    frames = d["frames"].reshape(n, ROOM)
+    wire_ip = frames[:, 24:26].copy().view(np.uint16).ravel()
+    wire_tcp = frames[:, 50:52].copy().view(np.uint16).ravel()
+    scrubbed = frames.copy()
+    scrubbed[:, 24:26] = 0x5A  # stale checksum fields, as tcp_checksums() finds them
+    scrubbed[:, 50:52] = 0xA5
+    return n, frames.ravel().copy(), scrubbed.ravel().copy(), d["lens"].astype(np.uint32), d["origin"], \
+        wire_ip, wire_tcp
+
+
+def test_fixture_shape():
+    n, frames, _, lens, origin, _, _ = _load()
+    assert n >= 60 and (origin == 0).sum() >= 30 and (origin == 1).sum() >= 20
+    assert ((lens == 1514) & (origin == 0)).sum() >= 10          # TAS-sized MSS segments from Linux
+    f = frames.reshape(n, ROOM)
+    assert (f[:, 14] == 0x45).all() and (f[:, 23] == 6).all()     # IPv4, IHL 5, TCP: TAS's layout
+    tl = f[:, 16].astype(np.uint32) << 8 | f[:, 17]
+    np.testing.assert_array_equal(tl + 14, lens)
+    assert len(set(tl.tolist())) >= 20 and (tl % 2 == 1).any()   # many lengths, odd ones included
+
+
+def test_oracle_reproduces_linux(oracle):
+    n, _, scrubbed, _, _, wire_ip, wire_tcp = _load()
+    out = oracle.tcp4_batch(scrubbed, n, stride=ROOM)
+    np.testing.assert_array_equal(out[0::2], wire_ip)
+    np.testing.assert_array_equal(out[1::2], wire_tcp)
+
+
+def test_numpy_restatement_reproduces_linux():
+    n, _, scrubbed, _, _, wire_ip, wire_tcp = _load()
+    f = scrubbed.reshape(n, ROOM)
+    for i in range(n):
+        fr = bytearray(f[i].tobytes())
+        ip, tcp = xsum_ref.tcp_checksums(fr)
+        assert (ip, tcp) == (wire_ip[i], wire_tcp[i]), i
+
+
+def test_oracle_verifies_linux_frames(oracle):
+    n, frames, _, lens, _, _, _ = _load()
+    assert (oracle.tcp4_verify_batch(frames, n, stride=ROOM) == 3).all()
+    assert (oracle.tcp4_verify_batch_bounded(frames, n, lens, stride=ROOM) == 3).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["frames", "hints", "room", "offsets", "inplace"])
+def test_gpu_reproduces_linux(form):
+    import torch
+    from tas_amd import xsum
+    n, _, scrubbed, lens, _, wire_ip, wire_tcp = _load()
+    dev = torch.from_numpy(scrubbed).cuda()
+    kw = {"stride": ROOM}
+    if form == "hints":
+        kw["frame_len"] = torch.from_numpy(lens.astype(np.int32)).cuda()
+    elif form == "room":
+        kw["room"] = ROOM
+    elif form == "offsets":
+        kw = {"offsets": torch.from_numpy(np.arange(n, dtype=np.int64) * ROOM).cuda()}
+    if form == "inplace":
+        xsum.tcp4_cksum_batch(dev, n, stride=ROOM, inplace=True, want_out=False)
+        torch.cuda.synchronize()
+        f = dev.cpu().numpy().reshape(n, ROOM)
+        np.testing.assert_array_equal(f[:, 24:26].copy().view(np.uint16).ravel(), wire_ip)
+        np.testing.assert_array_equal(f[:, 50:52].copy().view(np.uint16).ravel(), wire_tcp)
+        return
+    out = xsum.tcp4_cksum_batch(dev, n, **kw)
+    torch.cuda.synchronize()
+    assert xsum.last_kernel().startswith("tcp4_tas14_kernel")
+    o = out.cpu().numpy().view(np.uint16)
+    np.testing.assert_array_equal(o[0::2], wire_ip)
+    np.testing.assert_array_equal(o[1::2], wire_tcp)
+
+
+@pytest.mark.gpu
+def test_gpu_verifies_linux_frames():
+    import torch
+    from tas_amd import xsum
+    n, frames, _, lens, _, _, _ = _load()
+    dev = torch.from_numpy(frames).cuda()
+    hints = torch.from_numpy(lens.astype(np.int32)).cuda()
+    flags = xsum.tcp4_verify_batch(dev, n, stride=ROOM, frame_len=hints)
+    torch.cuda.synchronize()
+    assert (flags.cpu().numpy() == 3).all()
+    flags2 = xsum.tcp4_verify_batch(dev, n, stride=ROOM)
+    torch.cuda.synchronize()
+    assert (flags2.cpu().numpy() == 3).all()
