@@ -737,8 +737,11 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
     e1.record(cur)
     tc = time.perf_counter()
     torch.cuda.synchronize()
-    barrier(ws)
     t1 = time.perf_counter()
+    # the closing barrier aligns the ranks for what follows; it stays out of
+    # each rank's interval (an RCCL round trip at N > 1), and the MAX over
+    # ranks taken by the caller is the slowest rank's K steps
+    barrier(ws)
     if os.environ.get("TASX_BENCH_TRACE"):
         print(json.dumps({"K": steps, "rec0_us": round((ta - t0) * 1e6, 2), "issue_us": round((tb - ta) * 1e6, 2),
                           "rec1_us": round((tc - tb) * 1e6, 2), "sync_us": round((t1 - tc) * 1e6, 2),
