@@ -27,7 +27,8 @@
  *      (tcp4_tas14_kernel<...,flow_row>) instead of in lookup blocks ahead of
  *      the verify blocks; slower wherever ACKs are present
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
- * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels) apply.
+ * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels; 29 =
+ * tx_segment_wave_kernel, one segment per wave from aligned loads) apply.
  */
 #ifndef TASX_AB_H_
 #define TASX_AB_H_

@@ -853,6 +853,199 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     txseg_row<3, NTS>(p, i, gl);
 }
 
+// ---------------------------------------------------------------------------
+// tx_segment_wave_kernel: the TAS-layout build with ONE segment per wave.  The
+// segment's geometry is wave-uniform, so the descriptor comes in by scalar
+// loads and every branch on it is uniform.  The payload is read by ALIGNED
+// 16-byte loads: lane L holds the aligned source chunks under frame chunks L
+// and L + 64 and gets the next aligned chunk from lane L + 1 by DPP wave_rol:1
+// (lane 63: lane 0's second chunk by readlane), then funnel-shifts the pair
+// by the segment's source shift (a uniform dword select + v_alignbyte).  The
+// bare copy pattern measured 36.6 us this way against 38.6 us for unaligned
+// window loads on 16-lane rows (tools/copy_unaligned.hip, profiles/r02/r02bp).
+// A segment whose payload wraps in its circular buffer, or whose aligned
+// span leaves the shm region, takes unaligned window loads (the row kernel's
+// woff / splice / gather scheme) on the same lanes; one that is not TAS's
+// data-segment geometry goes to the general row body (txseg_row, lanes 0-15).
+// Frame chunk k of lane L, round r: k = L + 64 r.  Chunks 0..3 are headers
+// read from the frame, chunk 4 = header bytes 64-65 + payload [0, 14), chunks
+// 5.. K-1 payload [16k - 66, +16).  Header-first stores as the row kernel's
+// product form: every chunk stored as soon as it is built (stale checksum
+// fields), the two 16-bit fields at the end.
+__device__ __forceinline__ uint32_t wave_rol1(uint32_t x)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x134, 0xf, 0xf, false); // lane L <- lane L + 1
+}
+__device__ __forceinline__ u32x4 wave_rol1_4(u32x4 v)
+{
+  return u32x4{wave_rol1(v.x), wave_rol1(v.y), wave_rol1(v.z), wave_rol1(v.w)};
+}
+__device__ __forceinline__ u32x4 readlane0_4(u32x4 v)
+{
+  return u32x4{(uint32_t) __builtin_amdgcn_readlane((int) v.x, 0), (uint32_t) __builtin_amdgcn_readlane((int) v.y, 0),
+               (uint32_t) __builtin_amdgcn_readlane((int) v.z, 0), (uint32_t) __builtin_amdgcn_readlane((int) v.w, 0)};
+}
+// bytes [sh, sh + 16) of a:b, sh wave-uniform
+__device__ __forceinline__ u32x4 funnel_uniform(u32x4 a, u32x4 b, uint32_t sh)
+{
+  const uint32_t r8 = sh & 3u;
+  uint32_t w0, w1, w2, w3, w4;
+  switch (sh >> 2) {
+  case 0: w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; break;
+  case 1: w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; break;
+  case 2: w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; break;
+  default: w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; break;
+  }
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r8), __builtin_amdgcn_alignbyte(w2, w1, r8),
+               __builtin_amdgcn_alignbyte(w3, w2, r8), __builtin_amdgcn_alignbyte(w4, w3, r8)};
+}
+__device__ __forceinline__ uint32_t rl(uint32_t v, int lane)
+{
+  return (uint32_t) __builtin_amdgcn_readlane((int) v, lane);
+}
+
+template <bool NTS>
+__global__ __launch_bounds__(kBlock) void tx_segment_wave_kernel(tasx_txseg_params p)
+{
+  const uint32_t L = threadIdx.x & 63u;
+  const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u);
+  if (i >= p.n)
+    return; // the whole wave
+  const uint32_t *sd = (const uint32_t *) p.segs + 8u * i; // scalar loads: i is uniform
+  const uint64_t frame_off = sd[0] | ((uint64_t) sd[1] << 32);
+  const uint64_t tx_base = sd[2] | ((uint64_t) sd[3] << 32);
+  const uint32_t tx_len = sd[4], pos = sd[5], pay = sd[6] & 0xffffu, hl = sd[6] >> 16, roomw = sd[7];
+  const bool ok = (pay == 0 || pos < tx_len) && pay <= tx_len && tx_base <= p.shm_len &&
+                  tx_len <= p.shm_len - tx_base && hl >= p.l4_off + 20;
+  uint8_t *const f = p.frames + frame_off;
+  bool fast = ok && hl == 66u && ((uintptr_t) f & 15u) == 0 && p.shm_len >= 16u;
+  if (fast) {
+    const uint32_t fend = 66u + pay, K = (fend + 15u) >> 4;
+    const uint32_t room = roomw & ~TASX_TXSEG_SCRATCH;
+    const bool whole = room >= 16u * K, scratch = (roomw & TASX_TXSEG_SCRATCH) != 0u && whole;
+    uint32_t kend = K; // scratch zeros in chunks [K, kend): up to the frame's last 128-byte block end
+    if (scratch) {
+      const uint64_t be = (frame_off + fend + 127u) & ~127ull;
+      kend = max(K, min((uint32_t) ((be - frame_off + 15u) >> 4), room >> 4));
+    }
+    const uint8_t *const shm = p.shm;
+    const uint64_t s1 = tx_base + pos;
+    const uint32_t wrap = tx_len - pos;                     // payload index where piece 2 starts
+    const bool wraps = pay > 0 && wrap < pay;
+    // aligned span: frame chunk k >= 4 reads source [s1 - 2 + 16 (k - 4), +16)
+    const uint64_t a0 = s1 - 2u, abase = a0 & ~15ull;
+    const uint32_t sh = (uint32_t) (a0 & 15u);
+    const uint32_t na = K - 3u;                              // aligned chunks abase .. abase + 16 (na - 1)
+    const bool aligned = !wraps && s1 >= 2u && abase + 16ull * na <= p.shm_len;
+    // the frame's header chunks (lanes 0..4) and, if kept, its last chunk
+    const u32x4 hv = ld16((const u32x4 *) f, min(L, 4u));
+    const u32x4 tv = (!scratch && whole) ? ld16((const u32x4 *) f, K - 1u) : u32x4{0u, 0u, 0u, 0u};
+    // unaligned windows: payload index j at s1 + j before the wrap, at
+    // s1 + j - tx_len (= tx_base + j - wrap) from it on; a window outside
+    // the region is gathered byte by byte (bytes outside it as 0)
+    const int64_t smax = (int64_t) p.shm_len - 16;
+    auto load_at = [&](int64_t off) -> u32x4 {
+      if (off >= 0 && off <= smax)
+        return __builtin_nontemporal_load((gcu4u *) (shm + off));
+      return gather16(shm, (uint32_t) off, p.shm_len);
+    };
+    auto window = [&](uint32_t k) -> u32x4 {
+      const int j0 = 16 * (int) k - 66;
+      const bool in2 = wraps && j0 >= (int) wrap;
+      u32x4 v = load_at((int64_t) s1 + j0 - (in2 ? (int64_t) tx_len : 0));
+      if (wraps && j0 < (int) wrap && j0 + 16 > (int) wrap) // the straddle chunk: piece 2 from byte wrap - j0 on
+        v = splice(v, load_at((int64_t) s1 + j0 - (int64_t) tx_len), (int) wrap - j0, 16);
+      return v;
+    };
+    auto aload = [&](uint32_t c) -> u32x4 { // aligned source chunk c (clamped to the span)
+      return __builtin_nontemporal_load(
+          (const __attribute__((address_space(1))) u32x4 *) (shm + abase + 16ull * min(c, na - 1u)));
+    };
+    // build, store and sum frame chunk k from its payload window v
+    uint32_t acc = 0u;
+    auto emit = [&](uint32_t k, u32x4 v) {
+      if (k >= kend)
+        return;
+      uint8_t *const cp = f + 16u * k;
+      if (k >= K) { // scratch past the frame
+        __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) cp);
+        return;
+      }
+      const int hi = (int) fend - 16 * (int) k; // frame bytes in this chunk (>= 1)
+      if (k < 4u) {
+        // L4 bytes of the header chunks: chunk 2 from byte 34, chunk 3 without tcp.chksum
+        const uint32_t m0 = k == 2u ? 0xffff0000u : (k == 3u ? 0x0000ffffu : 0u);
+        if (k >= 2u)
+          acc = sad4(u32x4{hv.x & m0, hv.y, hv.z, hv.w}, acc);
+        *(__attribute__((address_space(1))) u32x4 *) cp = hv;
+        return;
+      }
+      if (k == 4u)
+        v = splice(hv, v, 2, hi); // header bytes 64-65, payload [0, 14); past the frame: its own bytes
+      if (hi >= 16) {
+        acc = sad4(v, acc);
+        if (k == 4u || !NTS)
+          *(__attribute__((address_space(1))) u32x4 *) cp = v;
+        else
+          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
+      } else { // the frame's last chunk
+        acc += sad_below(v, (uint32_t) hi);
+        if (k == 4u && whole)
+          *(__attribute__((address_space(1))) u32x4 *) cp = v;
+        else if (whole)
+          *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
+        else
+          store_range(cp, v, 0, hi, false);
+      }
+    };
+    // 128 frame chunks per round: lane L builds chunks base + L and base + 64 + L
+    for (uint32_t base = 0; base < kend; base += 128u) {
+      const uint32_t k0 = base + L, k1 = base + 64u + L;
+      u32x4 w0, w1;
+      if (aligned) { // frame chunk k >= 4 = aligned chunks k - 4 and k - 3 funnelled by sh
+        const u32x4 v0 = aload(k0 >= 4u ? k0 - 4u : 0u), v1 = aload(k1 - 4u);
+        const u32x4 vx = aload(base + 124u); // under chunk base + 128: lane 63's second neighbour
+        u32x4 n0 = wave_rol1_4(v0), n1 = wave_rol1_4(v1);
+        const u32x4 l0 = readlane0_4(v1);
+        if (L == 63u) {
+          n0 = l0;
+          n1 = vx;
+        }
+        w0 = funnel_uniform(v0, n0, sh);
+        w1 = funnel_uniform(v1, n1, sh);
+      } else {
+        w0 = window(max(k0, 4u));
+        w1 = window(min(k1, K - 1u));
+      }
+      emit(k0, w0);
+      emit(k1, w1);
+    }
+    // wave totals: 16-lane rows by DPP, the four rows by readlane
+    acc += row_ror<8>(acc);
+    acc += row_ror<4>(acc);
+    acc += row_ror<2>(acc);
+    acc += row_ror<1>(acc);
+    const uint32_t l4 = rl(acc, 0) + rl(acc, 16) + rl(acc, 32) + rl(acc, 48);
+    // the IPv4 header (bytes 14..33, ip.chksum as 0) and pseudo-header from chunks 0..2
+    const uint32_t h0w = rl(hv.w, 0), h1x = rl(hv.x, 1), h1y = rl(hv.y, 1), h1z = rl(hv.z, 1), h1w = rl(hv.w, 1),
+                   h2x = rl(hv.x, 2);
+    const uint32_t addrs = sadw(h1z & 0xffff0000u, sadw(h1w, sadw(h2x & 0xffffu, 0u)));
+    const uint32_t ph = sadw(h1y & 0xff000000u, addrs);
+    const uint32_t ipsum = sadw(h0w & 0xffff0000u, sadw(h1x, sadw(h1y, addrs)));
+    fast = bswap16(h1x & 0xffffu) == 52u + pay; // otherwise the general body redoes the segment
+    if (fast && L == 0u) {
+      const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
+      const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(l4) + fold32_to_16(ph) + bswap16(32u + pay))));
+      if (p.out)
+        stg(p.out, i, ipc | (tcpc << 16));
+      *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
+      *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
+    }
+  }
+  if (!fast && L < 16u)
+    txseg_row<3, NTS>(p, i, (int) L);
+}
+
 } // namespace
 
 #ifdef TASX_AB
@@ -922,6 +1115,7 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 26: tasx_note_kernel("tx_segment_tas_kernel<no_header_store>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoHeaderStore>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 27: tasx_note_kernel("tx_segment_tas_kernel<no_fields>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoFields>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 28: tasx_note_kernel("tx_segment_tas_kernel<no_sums>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoSums>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
+  case 29: if (tas) { tasx_note_kernel("tx_segment_wave_kernel"); hipLaunchKernelGGL((tx_segment_wave_kernel<true>), dim3((uint32_t) ((p->n + 3u) / 4u)), block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   // 9..14: ablations (timing only)
   case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoScratch>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;

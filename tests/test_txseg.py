@@ -70,7 +70,28 @@ def test_generator_wraps_and_flows():
 # ---------------------------------------------------------------------------
 # GPU parity
 
-def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
+# "wave": the one-segment-per-wave build (A/B variant TASX_TXSEG_DEBUG=29 of
+# libtasx_ab.so) on the same cases as the product
+IMPLS = ["product", "wave"]
+
+
+def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):
+    import os
+    from tas_amd import xsum
+    if impl == "product":
+        return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
+    os.environ["TASX_TXSEG_DEBUG"] = "29"
+    try:
+        with xsum.using_library(xsum.AB_LIB_PATH):
+            r = _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
+            if ip_off == 14 and l4_off == 34:
+                assert xsum.last_kernel() == "tx_segment_wave_kernel", xsum.last_kernel()
+            return r
+    finally:
+        del os.environ["TASX_TXSEG_DEBUG"]
+
+
+def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
     import torch
     from tas_amd import xsum
     dev = "cuda:0"
@@ -89,19 +110,21 @@ def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("shift", [0, 1, 2, 7])
-def test_gpu_txseg_golden(txseg_golden, shift):
+def test_gpu_txseg_golden(txseg_golden, shift, impl):
     g = txseg_golden
-    out, fr = _gpu_run(g["shm"], int(g["shm_len"]), g["frames_in"], _segs(g), frame_shift=shift)
+    out, fr = _gpu_run(g["shm"], int(g["shm_len"]), g["frames_in"], _segs(g), frame_shift=shift, impl=impl)
     np.testing.assert_array_equal(out, g["expected"])
     np.testing.assert_array_equal(fr, g["frames_out"])
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("room", [0, pktgen.MBUF_ROOM])
 @pytest.mark.parametrize("odd,tx_len,nflows", [(False, 16384, 512), (True, 16384, 512), (True, 1500, 7),
                                                (False, 1448, 3)])
-def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows, room):
+def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows, room, impl):
     n = 4096
     pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 131) % 1449, pktgen.TCP_MSS)
     pay = np.minimum(pay, tx_len - (7 if odd else 0))
@@ -109,13 +132,14 @@ def test_gpu_txseg_vs_oracle(oracle, odd, tx_len, nflows, room):
                                            seed=0xC0FFEE + tx_len, room=room)
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
-    out, got = _gpu_run(shm, sl, fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs, impl=impl)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
 
 
 @pytest.mark.gpu
-def test_gpu_txseg_packed_odd_frames(oracle):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_gpu_txseg_packed_odd_frames(oracle, impl):
     """Frames packed back to back at an odd stride (chunks shared between
     neighbours): the build must not clobber a neighbour's bytes."""
     n, stride = 1024, 1515
@@ -127,25 +151,26 @@ def test_gpu_txseg_packed_odd_frames(oracle):
     segs["frame_off"] = np.arange(n, dtype=np.uint64) * np.uint64(stride)
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
-    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=3)
+    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=3, impl=impl)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
 
 
 @pytest.mark.gpu
-def test_gpu_txseg_tso(oracle):
+@pytest.mark.parametrize("impl", IMPLS)
+def test_gpu_txseg_tso(oracle, impl):
     """64 KB segments: payload 65483 (ip.len 65535), wrap inside."""
     n, pay = 64, 65535 - 52
     shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, stride=65536 + 64, tx_len=98304 + 5, nflows=8,
                                            odd=True)
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
-    out, got = _gpu_run(shm, sl, fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs, impl=impl)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
     # with the mbuf room given, the same frames (tail chunks written whole)
     segs["room"] = 65536 + 64
-    out, got = _gpu_run(shm, sl, fr, segs)
+    out, got = _gpu_run(shm, sl, fr, segs, impl=impl)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
 
@@ -173,8 +198,9 @@ def test_gpu_txseg_other_layouts(oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("room", [0, 2048])
-def test_gpu_txseg_wrap_positions_and_region_edges(oracle, room):
+def test_gpu_txseg_wrap_positions_and_region_edges(oracle, room, impl):
     """Every buffer wrap after 1..60 payload bytes (inside the frame's chunk 4,
     on chunk boundaries, in the first whole payload chunks) and payloads at the
     very start and the very end of the shared region (windows that would reach
@@ -206,7 +232,7 @@ def test_gpu_txseg_wrap_positions_and_region_edges(oracle, room):
     segs["room"] = room
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, shm_len, exp_fr, segs)
-    out, got = _gpu_run(shm, shm_len, fr, segs)
+    out, got = _gpu_run(shm, shm_len, fr, segs, impl=impl)
     np.testing.assert_array_equal(out, exp)
     np.testing.assert_array_equal(got, exp_fr)
 
@@ -273,8 +299,9 @@ def test_gpu_txseg_errors():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("shift", [0, 16, 48])
-def test_gpu_txseg_scratch_room(oracle, shift):
+def test_gpu_txseg_scratch_room(oracle, shift, impl):
     """room | TASX_TXSEG_SCRATCH (the mbuf holds nothing past data_len): frames
     bit-exact up to their end, results equal, and only the bytes from each
     frame's end to the end of its 128-byte block (counted from `frames`, within
@@ -288,7 +315,7 @@ def test_gpu_txseg_scratch_room(oracle, shift):
     segs["room"] = np.uint32(pktgen.MBUF_ROOM | xsum.TXSEG_SCRATCH)
     exp_fr = fr.copy()
     exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
-    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=shift)
+    out, got = _gpu_run(shm, sl, fr, segs, frame_shift=shift, impl=impl)
     np.testing.assert_array_equal(out, exp)
     mask = np.ones(fr.size, bool)
     fend = segs["frame_off"].astype(np.int64) + pktgen.HDRS_LEN + segs["payload"].astype(np.int64)

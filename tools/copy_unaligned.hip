@@ -80,6 +80,58 @@ __global__ __launch_bounds__(256) void seg_copy(const uint8_t *src, const uint32
     out[0] = acc;
 }
 
+// One segment per WAVE, aligned loads only: the segment's start shift sh is
+// wave-uniform, lane L loads aligned chunks L and L + 64 of the source span,
+// gets aligned chunk L + 1 from lane L + 1 by DPP wave_rol:1 (lane 63: lane
+// 0's second chunk by readlane) and funnel-shifts the pair by sh (a uniform
+// dword select + v_alignbyte).  NCH + 1 aligned chunks cover the 16 * NCH
+// bytes at any shift.
+__device__ __forceinline__ uint32_t wave_rol1(uint32_t x)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x134, 0xf, 0xf, false); // wave_rol:1
+}
+__device__ __forceinline__ u32x4 funnel_u(const u32x4 a, const u32x4 b, uint32_t q, uint32_t r8)
+{
+  // bytes [4q + r8, 4q + r8 + 16) of a:b, q and r8 wave-uniform
+  uint32_t w0, w1, w2, w3, w4;
+  switch (q) {
+  case 0: w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; break;
+  case 1: w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; break;
+  case 2: w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; break;
+  default: w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; break;
+  }
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r8), __builtin_amdgcn_alignbyte(w2, w1, r8),
+               __builtin_amdgcn_alignbyte(w3, w2, r8), __builtin_amdgcn_alignbyte(w4, w3, r8)};
+}
+__global__ __launch_bounds__(256) void seg_copy_wave(const uint8_t *src, const uint32_t *soff, uint8_t *dst, uint32_t n,
+                                                     uint32_t *out)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i = blockIdx.x * 4u + threadIdx.x / 64u;
+  if (i >= n)
+    return;
+  const uint32_t so = __builtin_amdgcn_readfirstlane(soff[i]);
+  const uint32_t A = so & ~15u, q = (so >> 2) & 3u, r8 = so & 3u;
+  const uint8_t *sa = src + A;
+  const u32x4 v0 = __builtin_nontemporal_load((gcu4 *) (sa + 16u * lane));
+  const u32x4 v1 = __builtin_nontemporal_load((gcu4 *) (sa + 16u * min(lane + 64u, (uint32_t) NCH)));
+  u32x4 n0, n1;
+  n0.x = wave_rol1(v0.x); n0.y = wave_rol1(v0.y); n0.z = wave_rol1(v0.z); n0.w = wave_rol1(v0.w);
+  n1.x = wave_rol1(v1.x); n1.y = wave_rol1(v1.y); n1.z = wave_rol1(v1.z); n1.w = wave_rol1(v1.w);
+  const u32x4 l0 = {(uint32_t) __builtin_amdgcn_readlane((int) v1.x, 0), (uint32_t) __builtin_amdgcn_readlane((int) v1.y, 0),
+                    (uint32_t) __builtin_amdgcn_readlane((int) v1.z, 0), (uint32_t) __builtin_amdgcn_readlane((int) v1.w, 0)};
+  if (lane == 63u)
+    n0 = l0;
+  const u32x4 o0 = funnel_u(v0, n0, q, r8), o1 = funnel_u(v1, n1, q, r8);
+  uint8_t *d = dst + i * 2048u + 64u;
+  __builtin_nontemporal_store(o0, (gu4 *) (d + 16u * lane));
+  if (lane + 64u < (uint32_t) NCH)
+    __builtin_nontemporal_store(o1, (gu4 *) (d + 16u * (lane + 64u)));
+  uint32_t acc = __builtin_amdgcn_sad_u16(o0.x, 0, __builtin_amdgcn_sad_u16(o0.y, 0, o0.z + o0.w));
+  if (acc == 0x12345678u)
+    out[0] = acc;
+}
+
 struct Res { double min_us, med_us; };
 
 template <typename F>
@@ -142,11 +194,38 @@ int main(int argc, char **argv)
     fflush(stdout);
   };
   const dim3 g(n / 16), b(256);
+  hipFuncAttributes fa;
+  CHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(seg_copy<6, 0, false, true, 2048, 64, 3>)));
+  printf("seg_copy<+both>: %d VGPRs\n", fa.numRegs);
+  { // the wave form copies the same bytes as seg_copy<6, 0, false> (checked once)
+    std::vector<uint8_t> h(n * 2048), h2(n * 2048);
+    for (uint32_t k = 0; k < 64; ++k) // a source with a byte pattern
+      ;
+    std::vector<uint8_t> pat(shm);
+    for (size_t k = 0; k < shm; ++k) pat[k] = (uint8_t) (k * 131u + (k >> 9));
+    CHK(hipMemcpy(src[0], pat.data(), shm, hipMemcpyHostToDevice));
+    CHK(hipMemset(dst[0], 0, fr)); CHK(hipMemset(dst[1 % R], 0, fr));
+    hipLaunchKernelGGL((seg_copy<6, 0, false>), g, b, 0, s, src[0], d_un, dst[0], n, out);
+    hipLaunchKernelGGL(seg_copy_wave, dim3(n / 4), b, 0, s, src[0], d_un, dst[1 % R], n, out);
+    CHK(hipStreamSynchronize(s));
+    CHK(hipMemcpy(h.data(), dst[0], fr, hipMemcpyDeviceToHost));
+    CHK(hipMemcpy(h2.data(), dst[1 % R], fr, hipMemcpyDeviceToHost));
+    printf("wave form copies the same bytes: %s\n", h == h2 ? "yes" : "NO");
+  }
   for (int pass = 0; pass < 2; ++pass) {
+    rep("one segment per wave, aligned loads + DPP funnel", run([&](int r) { hipLaunchKernelGGL(seg_copy_wave, dim3(n / 4), b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
     rep("unaligned src, copy", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
     rep("  + 32 B descriptor", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 1>), g, b, 0, s, src[r], d_desc, dst[r], n, out); }, R, K, s), bytes);
     rep("  + frame header reads", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 2>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
     rep("  + both", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 3>), g, b, 0, s, src[r], d_desc, dst[r], n, out); }, R, K, s), bytes);
+    // residency: the same "+ both" copy with blocks per CU capped by reserved
+    // LDS (160 KiB per CU): 5 / 4 / 3 blocks = 5 / 4 / 3 waves per SIMD, the
+    // TX segment kernel holding 105 VGPRs runs at 4
+    for (uint32_t lds_kib : {32u, 36u, 48u}) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "  + both, %u KiB LDS reserved (%u blocks/CU)", lds_kib, 160u / lds_kib);
+      rep(nm, run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 3>), g, b, lds_kib * 1024u, s, src[r], d_desc, dst[r], n, out); }, R, K, s), bytes);
+    }
     rep("loads only", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 1, false>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes / 2);
     rep("loads only + both", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 1, false, true, 2048, 64, 3>), g, b, 0, s, src[r], d_desc, dst[r], n, out); }, R, K, s), bytes / 2);
   }
