@@ -1172,7 +1172,13 @@ def rx_pass_leg(fw: FlowLookupWorkload, rot: int, args, ws: int, rank: int) -> d
             "tcp4_tas14_kernel<hints,verify,flow>")
     sep = leg(rp.loop(benchloop.RX_SEPARATE), rp.bytes_per_step, args, ws,
               "same frames: tasx_tcp4_verify_batch_dev_room, then tasx_flow_lookup_batch_dev")
+    # verification alone on the same frames: the floor any pass that also looks up can reach
+    vloop = benchloop.Loop("tcp4", [a.v for a in rp.loop(benchloop.RX_FUSED).arr], _stream_ptrs(None), VERIFY,
+                           "tasx_tcp4_verify_batch_dev_room")
+    _, v_ms = timed_run(vloop, args.steps, args.warmup, ws)
     torch.cuda.synchronize()
+    r["verify_only_us"] = round(v_ms * 1e3, 3)
+    r["lookup_cost_us"] = round(r["roofline"]["launch_avg_us"] - v_ms * 1e3, 3)
     r["separate"] = {"ms_per_step": sep["ms_per_step"], "launch_pair_avg_us": sep["roofline"]["launch_avg_us"],
                      "kernels": "tcp4_tas14_kernel<hints,verify> + flow_lookup_kernel"}
     r["speedup_vs_separate"] = round(sep["roofline"]["launch_avg_us"] / r["roofline"]["launch_avg_us"], 3)
