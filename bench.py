@@ -88,7 +88,7 @@ def parse(argv=None):
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
-    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed"], help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx"], help=argparse.SUPPRESS)
     ap.add_argument("--control-selftest", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank plumbing
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
@@ -1008,6 +1008,8 @@ def pmc_child(mode: str, steps: int):
         run = RawWorkload(16, pktgen.SEED).loop()
     elif mode == "txseg":
         run = TxSegWorkload(16, pktgen.SEED + 2000).loop()
+    elif mode == "rx":
+        run = RxPassWorkload(FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000).loop()
     else:
         run = mixed_workload(0).loop()
     run(0, steps)
@@ -1327,6 +1329,11 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                         cc["traffic_GBps"] = round(rate, 1)
                         cc["traffic_frac_of_copy"] = round(rate / cc["GBps"], 4)
                 txseg["pmc"] = pt
+            if rx_pass is not None:  # the one-pass RX kernel (tcp4_tas14_kernel<..., kFlowSplit = 2>)
+                prx = pmc_leg("rx", "256, false, 2>", 48)
+                if prx and "hbm_bytes_per_launch" in prx:
+                    rx_pass["roofline"]["traffic"] = int(prx["hbm_bytes_per_launch"])
+                rx_pass["pmc"] = prx
 
     if rank == 0:
         line = {
