@@ -124,3 +124,21 @@ def test_bench_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--control-selftest"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=str(ROOT))
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_gpu_rehearsal():
+    """The N > 1 bench path on the GPU box: `bench.py --gpus 2 --rehearse`
+    starts two rank processes itself, each checksums its own 64K-frame batches
+    on the GPU (here both share the one visible GPU, gloo control plane), and
+    rank 0 prints the aggregate over both ranks (shards,
+    no data-path collective)."""
+    import json
+    r = _bench("--gpus", "2", "--rehearse", "--steps", "5", "--warmup", "2", "--no-txseg", "--no-flow",
+               "--no-contexts", "--no-flushmix", "--no-e2e", "--no-raw", "--no-cpu-baseline", "--no-pmc",
+               timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and len(line["per_rank_value"]) == 2 and line["ranks"]["rehearse"] is True
+    assert line["kernel"] == "tcp4_tas14_kernel<hint>" and line["value"] > 0
+    assert line["rx_verify"]["all_frames_verified"] is True
