@@ -132,6 +132,61 @@ __global__ __launch_bounds__(256) void seg_copy_wave(const uint8_t *src, const u
     out[0] = acc;
 }
 
+// 16-lane rows (one segment per row, four per wave) reading ALIGNED chunks:
+// lane gl holds aligned chunks gl + 16u, gets chunk + 1 from lane gl + 1 by
+// DPP row_ror:15 (lane 15: lane 0's next round), and funnel-shifts by the
+// row's own shift (per-lane dword select + v_alignbyte)
+__device__ __forceinline__ uint32_t ror15(uint32_t x)
+{
+  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x12F, 0xf, 0xf, false); // row_ror:15
+}
+__device__ __forceinline__ u32x4 funnel_lane(const u32x4 a, const u32x4 b, uint32_t sh)
+{
+  const uint32_t q = sh >> 2, r8 = sh & 3u;
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t o[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const uint32_t lo = (q & 1u) ? w[j + 1] : w[j], hi = (q & 1u) ? w[j + 3] : w[j + 2];
+    o[j] = (q & 2u) ? hi : lo;
+  }
+  return u32x4{__builtin_amdgcn_alignbyte(o[1], o[0], r8), __builtin_amdgcn_alignbyte(o[2], o[1], r8),
+               __builtin_amdgcn_alignbyte(o[3], o[2], r8), __builtin_amdgcn_alignbyte(o[4], o[3], r8)};
+}
+template <int U>
+__global__ __launch_bounds__(256) void seg_copy_row_aligned(const uint8_t *src, const uint32_t *soff, uint8_t *dst,
+                                                            uint32_t n, uint32_t *out)
+{
+  const uint32_t gl = threadIdx.x & 15u;
+  const uint32_t i = blockIdx.x * 16 + threadIdx.x / 16;
+  if (i >= n)
+    return;
+  const uint32_t so = soff[i], A = so & ~15u, sh = so & 15u;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = __builtin_nontemporal_load((gcu4 *) (src + A + 16u * min(gl + 16u * u, (uint32_t) NCH)));
+  uint32_t acc = 0;
+  const uint32_t dbase = i * 2048u + 64u;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    u32x4 nx = {ror15(v[u].x), ror15(v[u].y), ror15(v[u].z), ror15(v[u].w)};
+    if (u + 1 < U) {
+      const u32x4 nn = {ror15(v[u + 1].x), ror15(v[u + 1].y), ror15(v[u + 1].z), ror15(v[u + 1].w)};
+      if (gl == 15u)
+        nx = nn;
+    }
+    const u32x4 o = funnel_lane(v[u], nx, sh);
+    const uint32_t c = gl + 16u * u;
+    if (c < (uint32_t) NCH) {
+      __builtin_nontemporal_store(o, (gu4 *) (dst + dbase + 16u * c));
+      acc = __builtin_amdgcn_sad_u16(o.x, 0, __builtin_amdgcn_sad_u16(o.y, 0, __builtin_amdgcn_sad_u16(o.z, 0, __builtin_amdgcn_sad_u16(o.w, 0, acc))));
+    }
+  }
+  if (acc == 0x12345678u)
+    out[0] = acc;
+}
+
 struct Res { double min_us, med_us; };
 
 template <typename F>
@@ -211,9 +266,15 @@ int main(int argc, char **argv)
     CHK(hipMemcpy(h.data(), dst[0], fr, hipMemcpyDeviceToHost));
     CHK(hipMemcpy(h2.data(), dst[1 % R], fr, hipMemcpyDeviceToHost));
     printf("wave form copies the same bytes: %s\n", h == h2 ? "yes" : "NO");
+    CHK(hipMemset(dst[1 % R], 0, fr));
+    hipLaunchKernelGGL((seg_copy_row_aligned<6>), g, b, 0, s, src[0], d_un, dst[1 % R], n, out);
+    CHK(hipStreamSynchronize(s));
+    CHK(hipMemcpy(h2.data(), dst[1 % R], fr, hipMemcpyDeviceToHost));
+    printf("aligned row form copies the same bytes: %s\n", h == h2 ? "yes" : "NO");
   }
   for (int pass = 0; pass < 2; ++pass) {
     rep("one segment per wave, aligned loads + DPP funnel", run([&](int r) { hipLaunchKernelGGL(seg_copy_wave, dim3(n / 4), b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
+    rep("16-lane rows, aligned loads + DPP funnel", run([&](int r) { hipLaunchKernelGGL((seg_copy_row_aligned<6>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
     rep("unaligned src, copy", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
     rep("  + 32 B descriptor", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 1>), g, b, 0, s, src[r], d_desc, dst[r], n, out); }, R, K, s), bytes);
     rep("  + frame header reads", run([&](int r) { hipLaunchKernelGGL((seg_copy<6, 0, false, true, 2048, 64, 2>), g, b, 0, s, src[r], d_un, dst[r], n, out); }, R, K, s), bytes);
