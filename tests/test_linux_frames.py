@@ -110,3 +110,65 @@ def test_gpu_verifies_linux_frames():
     flags2 = xsum.tcp4_verify_batch(dev, n, stride=ROOM)
     torch.cuda.synchronize()
     assert (flags2.cpu().numpy() == 3).all()
+
+
+def _txseg_case():
+    """The Linux data segments (66-byte headers: TCP with NOP NOP timestamp,
+    TAS's layout) rebuilt by the TX segment build (SURVEY.md section 8f row 1,
+    flow_tx_read + tcp_checksums, /root/reference/tas/fast/fast_flows.c:930-936):
+    each payload placed in its own 4 KiB ring in a shared region -- every third
+    one wrapping around its ring's end -- the frames handed over with the
+    payload and both checksum fields scrambled, a descriptor per frame.  The
+    build must give back Linux's frames byte for byte."""
+    from tas_amd import pktgen
+    n, frames, _, lens, origin, _, _ = _load()
+    f = frames.reshape(n, ROOM)
+    doff = f[:, 46] >> 4
+    pay = lens.astype(np.int64) - 66
+    sel = np.nonzero((origin == 0) & (doff == 8) & (pay > 0))[0]
+    m = len(sel)
+    ring = 4096
+    shm = np.zeros(m * ring + 16, np.uint8)
+    segs = np.zeros(m, pktgen.TX_SEG_DTYPE)
+    want = f[sel].copy()
+    got = want.copy()
+    rng = np.random.default_rng(5)
+    for j, i in enumerate(sel):
+        p = int(pay[i])
+        body = f[i, 66:66 + p]
+        pos = ring - max(1, p // 2) if j % 3 == 0 else int(rng.integers(0, ring - p))
+        base = j * ring
+        idx = (pos + np.arange(p)) % ring
+        shm[base + idx] = body
+        got[j, 66:66 + p] = rng.integers(0, 256, p, dtype=np.uint8)
+        got[j, 24:26] = 0x5A
+        got[j, 50:52] = 0xA5
+        segs[j] = (j * ROOM, base, ring, pos, p, 66, ROOM)
+    wraps = int((segs["pos"].astype(np.int64) + segs["payload"] > ring).sum())
+    return shm, len(shm), got.ravel().copy(), segs, want, wraps
+
+
+def test_oracle_txseg_rebuilds_linux_frames(oracle):
+    shm, sl, fr, segs, want, wraps = _txseg_case()
+    assert len(segs) >= 20 and wraps >= 5 and (segs["payload"] == 1448).sum() >= 10
+    out = oracle.tx_segment_batch(shm, sl, fr, segs)
+    np.testing.assert_array_equal(fr.reshape(want.shape), want)
+    np.testing.assert_array_equal(out & 0xFFFF, want[:, 24:26].copy().view(np.uint16).ravel())
+    np.testing.assert_array_equal(out >> 16, want[:, 50:52].copy().view(np.uint16).ravel())
+
+
+@pytest.mark.gpu
+def test_gpu_txseg_rebuilds_linux_frames():
+    import torch
+    from tas_amd import xsum
+    shm, sl, fr, segs, want, _ = _txseg_case()
+    dshm = torch.from_numpy(shm).cuda()
+    dfr = torch.from_numpy(fr).cuda()
+    dsegs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
+    out = xsum.tx_segment_batch(dshm, dfr, dsegs, len(segs), shm_len=sl)
+    torch.cuda.synchronize()
+    assert xsum.last_kernel() == "tx_segment_tas_kernel"
+    np.testing.assert_array_equal(dfr.cpu().numpy().reshape(want.shape), want)
+    o = out.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(o & 0xFFFF, want[:, 24:26].copy().view(np.uint16).ravel())
+    np.testing.assert_array_equal(o >> 16, want[:, 50:52].copy().view(np.uint16).ravel())
