@@ -28,7 +28,8 @@ JSON line with the aggregate and per-rank rates.
 Extra legs (all ranks unless noted): the same frames with no hint and a room
 (the mbuf data room: the TAS drop-in form) and with neither, the same batches
 over two streams, RX verification, a data/ACK flush mix, the RAW payload fold,
-the TX segment build, the flow lookup, the end-to-end host-memory rate (one
+the TX segment build, the flow lookup, the one-launch RX pass (verification +
+lookup, against the two calls), the end-to-end host-memory rate (one
 NUMA-local host thread per GPU), and on rank 0 at N == 1 the CPU oracle
 baseline, tx_flush latencies and HBM traffic from rocprofv3 counters (child
 runs; --no-pmc skips them).  --workload {shard8m,mixed,tso} measures the other
