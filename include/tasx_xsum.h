@@ -202,7 +202,10 @@ typedef struct tasx_tx_seg {
  * the header bytes [0, hdrs_len) are rewritten with their own values (whole
  * cache lines avoid HBM read-modify-write), and so are the bytes between the
  * frame's end and the end of its last 16-byte chunk when `room` covers them.
- * Asynchronous on `stream`. */
+ * TX frames are trusted (TAS's own header code writes ip.total_length =
+ * hdrs_len - ip_off + payload, :897): a frame whose total_length claims more
+ * than that is summed over what it claims, so its buffer must hold
+ * ip_off + total_length bytes.  Asynchronous on `stream`. */
 int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
     const tasx_tx_seg *segs, uint32_t n, uint32_t ip_off, uint32_t l4_off,
     uint32_t *out, void *stream);
