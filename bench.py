@@ -726,10 +726,12 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
     torch.cuda.synchronize()
     barrier(ws)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    # the start event goes in just before t0: it brackets the launches (the
+    # roofline's kernel time) without its host cost inside the timed region
     e0.record(cur)
     for s in streams or []:
         s.wait_event(e0)
+    t0 = time.perf_counter()
     ta = time.perf_counter()
     run(warmup, steps)
     tb = time.perf_counter()
