@@ -243,7 +243,7 @@ int tasx_flow_lookup_batch_dev(const void *base, const uint64_t *off,
  * read bounds, errors and outputs (flags[i]; fid_out[i], hash_out[i]) as the
  * two calls in turn.  Where the verify call would take a TAS row kernel (IPv4
  * at 14 mod 16, TCP at +20, stride mode or offsets), both run in ONE launch:
- * the grid's first blocks look up 256 frames each (one lane per frame), the
+ * the grid's first blocks look up 256 frames each (512 with a uniform flen0), the
  * rest verify, so the lookup's dependent bucket / flow-state loads overlap
  * the checksum loads (64K received frames: 15-23 % below the two calls).
  * Other batches run the two kernels in turn.  The lookup reads the 12 key

@@ -5,12 +5,12 @@
 // FLEXNIC_PL_FLOWHT_NBSZ hash-table entries, each candidate confirmed against
 // the 4-tuple in its flow state.
 //
-// Layout: one lane per frame.  The work is latency-bound random access (a
+// Layout: two frames per lane.  The work is latency-bound random access (a
 // dependent chain frame header -> bucket -> flow state), not bandwidth: every
-// load of a phase is issued before any is used (the four bucket entries
-// together, then the four candidates' keys together, clamped to flow 0 when
-// not a candidate), and the kernel keeps few registers so many frames are in
-// flight per CU.  CRC32C is computed bit by bit on the VALU by default (a
+// load of a phase is issued before any is used (both frames' keys, then their
+// eight bucket entries together, then the candidates' keys together, clamped
+// to flow 0 when not a candidate), and the kernel keeps few registers so many
+// chains are in flight per CU.  CRC32C is computed bit by bit on the VALU by default (a
 // slice-by-4 variant from LDS tables built at compile time measured the same:
 // the CRC is not on the critical path).
 #include <hip/hip_runtime.h>
@@ -101,38 +101,45 @@ __device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
 // from LDS (3: no CRC, a diagnostic build only -- wrong flow ids); CHUNK: key
 // fields from 16-byte chunk loads (else byte loads)
 enum { kCrcBitwise = 0, kCrcSlice4 = 1, kCrcKeyTab = 2, kCrcNone = 3 };
+constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
 
-template <int CRC, bool CHUNK>
+// F frames per lane (frames blockIdx.x * 256 F + f * 256 + lane): every
+// level's loads of all F frames are issued together, so each lane keeps F
+// dependent chains in flight -- at 8 waves per SIMD one frame per lane leaves
+// 256K frames two generations of waves deep, each paying the whole chain.
+template <int CRC, bool CHUNK, int F = 1>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
   constexpr bool TAB = CRC == kCrcSlice4;
   __shared__ uint32_t lt[TAB ? 4 : 1][256];
   __shared__ uint32_t kt[CRC == kCrcKeyTab ? 12 : 1][256];
-  const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t i = min(i0, p.n - 1u); // lanes past the batch repeat the last frame (no store)
-  const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  // key = (local = destination, remote = source), network byte order:
-  // ip.src/ip.dst are bytes [12, 20) of the IPv4 header, the ports bytes
-  // [0, 4) of the TCP header
-  uint32_t rip, lip, l4x;
-  if constexpr (CHUNK) {
-    const u32x4 ipw = load_window(f + p.ip_off + 12, 8), l4w = load_window(f + p.l4_off, 4);
-    rip = ipw.x;
-    lip = ipw.y;
-    l4x = l4w.x;
-  } else if (p.l4_off == p.ip_off + 20u) {
-    // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
-    // unaligned dwordx3 load (gfx950 global loads take any byte address)
-    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (f + p.ip_off + 12);
-    rip = k.x;
-    lip = k.y;
-    l4x = k.z;
-  } else {
-    rip = ld32b(f + p.ip_off + 12);
-    lip = ld32b(f + p.ip_off + 16);
-    l4x = ld32b(f + p.l4_off);
+  uint32_t i0[F], i[F], rip[F], lip[F], l4x[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    i0[f] = blockIdx.x * (256u * F) + 256u * (uint32_t) f + threadIdx.x;
+    i[f] = min(i0[f], p.n - 1u); // lanes past the batch repeat the last frame (no store)
+    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
+    // key = (local = destination, remote = source), network byte order:
+    // ip.src/ip.dst are bytes [12, 20) of the IPv4 header, the ports bytes
+    // [0, 4) of the TCP header
+    if constexpr (CHUNK) {
+      const u32x4 ipw = load_window(fr + p.ip_off + 12, 8), l4w = load_window(fr + p.l4_off, 4);
+      rip[f] = ipw.x;
+      lip[f] = ipw.y;
+      l4x[f] = l4w.x;
+    } else if (p.l4_off == p.ip_off + 20u) {
+      // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
+      // unaligned dwordx3 load (gfx950 global loads take any byte address)
+      const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+      rip[f] = k.x;
+      lip[f] = k.y;
+      l4x[f] = k.z;
+    } else {
+      rip[f] = ld32b(fr + p.ip_off + 12);
+      lip[f] = ld32b(fr + p.ip_off + 16);
+      l4x[f] = ld32b(fr + p.l4_off);
+    }
   }
-  const uint32_t ports = (l4x >> 16) | (l4x << 16); // tcp.dest | tcp.src << 16
   // tables into LDS while the key loads are in flight
   if constexpr (TAB) {
 #pragma unroll
@@ -147,46 +154,56 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
   if constexpr (TAB || CRC == kCrcKeyTab)
     __syncthreads();
   // flow_hash: crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0))
-  uint32_t h;
-  if constexpr (CRC == kCrcKeyTab) {
-    h = 0;
+  uint32_t ports[F], h[F];
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
-      h ^= kt[b][(lip >> (8 * b)) & 0xffu] ^ kt[4 + b][(rip >> (8 * b)) & 0xffu] ^
-           kt[8 + b][(ports >> (8 * b)) & 0xffu];
-  } else if constexpr (CRC == kCrcNone) {
-    h = lip ^ rip ^ ports;
-  } else {
-    h = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip), rip), ports);
+  for (int f = 0; f < F; ++f) {
+    ports[f] = (l4x[f] >> 16) | (l4x[f] << 16); // tcp.dest | tcp.src << 16
+    if constexpr (CRC == kCrcKeyTab) {
+      h[f] = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        h[f] ^= kt[b][(lip[f] >> (8 * b)) & 0xffu] ^ kt[4 + b][(rip[f] >> (8 * b)) & 0xffu] ^
+                kt[8 + b][(ports[f] >> (8 * b)) & 0xffu];
+    } else if constexpr (CRC == kCrcNone) {
+      h[f] = lip[f] ^ rip[f] ^ ports[f];
+    } else {
+      h[f] = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip[f]), rip[f]), ports[f]);
+    }
   }
-  // bucket: entries (h + j) % ht_entries, j < NBSZ, loaded together
-  uint64_t e[TASX_FLOWHT_NBSZ];
+  // buckets: entries (h + j) % ht_entries, j < NBSZ, all frames' loaded together
+  uint64_t e[F][TASX_FLOWHT_NBSZ];
 #pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-    e[j] = ldg((const uint64_t *) p.flowht, (h + j) % p.ht_entries);
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
   // candidates' keys, loaded together (non-candidates read flow 0)
-  bool cand[TASX_FLOWHT_NBSZ];
-  uint32_t fid[TASX_FLOWHT_NBSZ];
-  u32x3 key[TASX_FLOWHT_NBSZ];
+  bool cand[F][TASX_FLOWHT_NBSZ];
+  uint32_t fid[F][TASX_FLOWHT_NBSZ];
+  u32x3 key[F][TASX_FLOWHT_NBSZ];
 #pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-    const uint32_t ffid = (uint32_t) e[j], eh = (uint32_t) (e[j] >> 32);
-    fid[j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-    cand[j] = (ffid & TASX_FLOWHTE_VALID) && eh == h && fid[j] < p.fs_num;
-    key[j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
-                                                                 (uint64_t) (cand[j] ? fid[j] : 0u) * p.fs_stride +
-                                                                 p.fs_key_off);
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
+      const uint32_t ffid = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
+      fid[f][j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
+      cand[f][j] = (ffid & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
+      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
+          p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
+    }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    uint32_t res = TASX_FLOW_NONE;
+#pragma unroll
+    for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j) // first match wins
+      if (cand[f][j] && key[f][j].x == lip[f] && key[f][j].y == rip[f] && key[f][j].z == ports[f])
+        res = fid[f][j];
+    if (i0[f] < p.n) {
+      stg(p.fid_out, i[f], res);
+      if (p.hash_out)
+        stg(p.hash_out, i[f], h[f]);
+    }
   }
-  uint32_t res = TASX_FLOW_NONE;
-#pragma unroll
-  for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j) // first match wins
-    if (cand[j] && key[j].x == lip && key[j].y == rip && key[j].z == ports)
-      res = fid[j];
-  if (i0 >= p.n)
-    return;
-  stg(p.fid_out, i, res);
-  if (p.hash_out)
-    stg(p.hash_out, i, h);
 }
 
 #ifdef TASX_AB
@@ -204,28 +221,46 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x)
 
 __global__ __launch_bounds__(256) void flow_pattern_kernel(tasx_flow_params p)
 {
-  const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t i = min(i0, p.n - 1u);
-  const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (f + p.ip_off + 12);
-  const uint32_t h = mix32(k.x ^ k.y ^ k.z);
-  uint64_t e[TASX_FLOWHT_NBSZ];
+  constexpr int F = kFlowFramesPerLane; // the product's frames per lane
+  uint32_t i0[F], i[F], h[F], r[F];
 #pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-    e[j] = ldg((const uint64_t *) p.flowht, (h + j) % p.ht_entries);
-  uint32_t r = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-    r += (uint32_t) e[j] ^ (uint32_t) (e[j] >> 32);
-#pragma unroll
-  for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-    const uint32_t fid = j == 0 ? mix32(h ^ r) % p.fs_num : 0u;
-    const u32x3 key = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst + (uint64_t) fid * p.fs_stride +
-                                                                           p.fs_key_off);
-    r ^= key.x ^ key.y ^ key.z;
+  for (int f = 0; f < F; ++f) {
+    i0[f] = blockIdx.x * (256u * F) + 256u * (uint32_t) f + threadIdx.x;
+    i[f] = min(i0[f], p.n - 1u);
+    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
+    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+    h[f] = mix32(k.x ^ k.y ^ k.z);
   }
-  if (i0 < p.n)
-    stg(p.fid_out, i, r);
+  uint64_t e[F][TASX_FLOWHT_NBSZ];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    r[f] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+      r[f] += (uint32_t) e[f][j] ^ (uint32_t) (e[f][j] >> 32);
+  }
+  u32x3 key[F][TASX_FLOWHT_NBSZ];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
+      const uint32_t fid = j == 0 ? mix32(h[f] ^ r[f]) % p.fs_num : 0u;
+      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst + (uint64_t) fid * p.fs_stride +
+                                                                      p.fs_key_off);
+    }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+#pragma unroll
+    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
+      r[f] ^= key[f][j].x ^ key[f][j].y ^ key[f][j].z;
+    if (i0[f] < p.n)
+      stg(p.fid_out, i[f], r[f]);
+  }
 }
 #endif
 
@@ -252,17 +287,25 @@ extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t 
   if (n == 0)
     return 0;
   tasx_note_kernel("flow_pattern_kernel");
-  hipLaunchKernelGGL(flow_pattern_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t) stream, p);
+  hipLaunchKernelGGL(flow_pattern_kernel, dim3((n + 256u * kFlowFramesPerLane - 1) / (256u * kFlowFramesPerLane)),
+                     dim3(256), 0, (hipStream_t) stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 #endif
 
+template <int F>
+static int launch_flow_f(const char *name, const tasx_flow_params *p, hipStream_t s)
+{
+  const uint64_t blocks = ((uint64_t) p->n + 256u * F - 1) / (256u * F);
+  tasx_note_kernel(name);
+  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream)
 {
-  const uint64_t blocks = ((uint64_t) p->n + 255) / 256;
-  if (blocks == 0)
+  if (p->n == 0)
     return 0;
-  const dim3 g((uint32_t) blocks), b(256);
   hipStream_t s = (hipStream_t) stream;
   // A/B (TASX_AB builds, tasx_set_kernel_variant; tools/flow_probe.py,
   // profiles/r01_flow_variants.jsonl): bitwise CRC + byte loads (the product
@@ -271,6 +314,7 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   // dependent load chain (frame header -> bucket -> flow state), not by the
   // CRC arithmetic
 #ifdef TASX_AB
+  const dim3 g((uint32_t) (((uint64_t) p->n + 255) / 256)), b(256); // one frame per lane
   switch (variant) {
   case 2: tasx_note_kernel("flow_lookup_kernel<bitwise,chunk>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, true>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 3: tasx_note_kernel("flow_lookup_kernel<slice4>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -280,12 +324,15 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
 #else
   case 5: tasx_note_kernel("flow_lookup_kernel<keytab>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcKeyTab, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
 #endif
+  case 6: return launch_flow_f<1>("flow_lookup_kernel<f1>", p, s); // 1 / 4 frames per lane
+  case 7: return launch_flow_f<4>("flow_lookup_kernel<f4>", p, s);
+  case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
   default: break;
   }
 #else
   (void) variant;
 #endif
-  tasx_note_kernel("flow_lookup_kernel");
-  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false>), g, b, 0, s, *p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  // two frames per lane: 256K lookups 11.85 us against 12.53 with one and
+  // 12.98 with four (register pressure; profiles/r02/r02ca)
+  return launch_flow_f<kFlowFramesPerLane>("flow_lookup_kernel", p, s);
 }

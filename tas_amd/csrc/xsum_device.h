@@ -345,47 +345,63 @@ __device__ __forceinline__ uint32_t tas_flow_hash(uint32_t lip, uint32_t rip, ui
   return crc32c_u32(crc32c_u32(crc32c_u32(0u, lip), rip), ports);
 }
 
-// One frame's fast_flows_packet_fss lookup (fast_flows.c:1084-1163) on one
-// lane, TAS's header layout (l4_off == ip_off + 20: the 12 key bytes in one
-// unaligned dwordx3 load), every load of a level issued before any is used:
-// the split-grid blocks of tcp4_tas14_kernel<...,flow> (xsum_kernels.hip) run
-// it; flow_kernels.hip's flow_lookup_kernel is the same arithmetic for any
-// layout.  P: tasx_tcp4_params or tasx_flow_params.
-template <typename P>
-__device__ __forceinline__ void flow_lookup_lane(const P &p, uint32_t i0)
+// fast_flows_packet_fss lookups (fast_flows.c:1084-1163), F frames per lane:
+// lookup block `blk` of BS lanes takes frames blk * BS * F + f * BS + lane,
+// TAS's header layout (l4_off == ip_off + 20: the 12 key bytes in one
+// unaligned dwordx3 load), every load of a level issued for all F frames
+// before any is used.  The split-grid blocks of tcp4_tas14_kernel<...,flow>
+// (xsum_kernels.hip) run it; flow_kernels.hip's flow_lookup_kernel is the same
+// arithmetic for any layout.  P: tasx_tcp4_params or tasx_flow_params.
+template <int F, int BS, typename P>
+__device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
 {
   constexpr uint32_t kNb = TASX_FLOWHT_NBSZ;
-  const uint32_t i = min(i0, p.n - 1u); // lanes past the batch repeat the last frame (no store)
-  const uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (f + p.ip_off + 12);
-  const uint32_t rip = k.x, lip = k.y, ports = (k.z >> 16) | (k.z << 16); // tcp.dest | tcp.src << 16
-  const uint32_t h = tas_flow_hash(lip, rip, ports);
-  uint64_t e[kNb];
+  uint32_t i0[F], i[F], rip[F], lip[F], ports[F], h[F];
 #pragma unroll
-  for (uint32_t j = 0; j < kNb; ++j)
-    e[j] = ldg((const uint64_t *) p.flowht, (h + j) % p.ht_entries);
-  bool cand[kNb];
-  uint32_t fid[kNb];
-  u32x3 key[kNb];
-#pragma unroll
-  for (uint32_t j = 0; j < kNb; ++j) {
-    const uint32_t ef = (uint32_t) e[j], eh = (uint32_t) (e[j] >> 32);
-    fid[j] = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-    cand[j] = (ef & TASX_FLOWHTE_VALID) && eh == h && fid[j] < p.fs_num;
-    key[j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
-                                                                 (uint64_t) (cand[j] ? fid[j] : 0u) * p.fs_stride +
-                                                                 p.fs_key_off);
+  for (int f = 0; f < F; ++f) {
+    i0[f] = blk * (uint32_t) (BS * F) + (uint32_t) (BS * f) + threadIdx.x;
+    i[f] = min(i0[f], p.n - 1u); // lanes past the batch repeat the last frame (no store)
+    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
+    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+    rip[f] = k.x;
+    lip[f] = k.y;
+    ports[f] = (k.z >> 16) | (k.z << 16); // tcp.dest | tcp.src << 16
   }
-  uint32_t res = TASX_FLOW_NONE;
 #pragma unroll
-  for (int j = (int) kNb - 1; j >= 0; --j) // first match wins
-    if (cand[j] && key[j].x == lip && key[j].y == rip && key[j].z == ports)
-      res = fid[j];
-  if (i0 >= p.n)
-    return;
-  stg(p.fid_out, i, res);
-  if (p.hash_out)
-    stg(p.hash_out, i, h);
+  for (int f = 0; f < F; ++f)
+    h[f] = tas_flow_hash(lip[f], rip[f], ports[f]);
+  uint64_t e[F][kNb];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < kNb; ++j)
+      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
+  bool cand[F][kNb];
+  uint32_t fid[F][kNb];
+  u32x3 key[F][kNb];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+#pragma unroll
+    for (uint32_t j = 0; j < kNb; ++j) {
+      const uint32_t ef = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
+      fid[f][j] = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
+      cand[f][j] = (ef & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
+      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
+          p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
+    }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    uint32_t res = TASX_FLOW_NONE;
+#pragma unroll
+    for (int j = (int) kNb - 1; j >= 0; --j) // first match wins
+      if (cand[f][j] && key[f][j].x == lip[f] && key[f][j].y == rip[f] && key[f][j].z == ports[f])
+        res = fid[f][j];
+    if (i0[f] < p.n) {
+      stg(p.fid_out, i[f], res);
+      if (p.hash_out)
+        stg(p.hash_out, i[f], h[f]);
+    }
+  }
 }
 
 } // namespace

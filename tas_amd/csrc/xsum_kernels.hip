@@ -1001,8 +1001,8 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 
 // FLOW (RX, with VERIFY): the frames' flow lookup (fast_flows_packet_fss,
 // tas/fast/fast_flows.c:1084-1163) in the same launch.
-//  kFlowSplit (the product): the grid's first blocks run flow_lookup_lane, one
-//   frame per lane (BS frames per block), the rest are the verify blocks.  The
+//  kFlowSplit* (the product): the grid's first blocks run flow_lookup_lanes,
+//   F frames per lane (F BS frames per block), the rest are the verify blocks.  The
 //   lookup's dependent chain (key -> bucket -> flow key) is the long one, so
 //   its blocks start first and overlap the verify rows instead of forming the
 //   grid's tail; 64 hashes per wave.  64K received frames: 15-23 % below the
@@ -1016,7 +1016,13 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   interleaved one per BS frames (their chains end the grid), and the key
 //   hashed beside the row's first load with the bucket issued before the
 //   chunks (the per-row CRC stays).
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2 };
+//  kFlowSplit / kFlowSplit1: two / one frames per lookup lane -- two for
+//   uniform-length (data) bursts, one for the row forms (data/ACK mixes),
+//   the other choice as A/B variant 27.
+enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3 };
+// frames per lane of a split grid's lookup blocks
+template <int FLOW>
+constexpr uint32_t split_frames() { return FLOW == kFlowSplit1 ? 1u : 2u; }
 template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
           int FLOW = kFlowNone>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
@@ -1024,16 +1030,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
   static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
-  static_assert(FLOW != kFlowSplit || !DONE, "split grids post no completion word");
+  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1) || !DONE, "split grids post no completion word");
   const int gl = threadIdx.x & 15;
   uint32_t vb = blockIdx.x; // this block's verify block
-  if constexpr (FLOW == kFlowSplit) {
+  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1) {
     // the lookup blocks first: their dependent chains are the long ones, so
     // they start at once and overlap the verify blocks instead of forming the
     // grid's tail (interleaved one per BS frames they did: DESIGN.md 5.2)
-    const uint32_t nl = (p.n + BS - 1u) / BS;
+    constexpr uint32_t kF = split_frames<FLOW>(); // frames per lookup lane (flow_kernels.hip: kFlowFramesPerLane)
+    const uint32_t nl = (p.n + BS * kF - 1u) / (BS * kF);
     if (blockIdx.x < nl) {
-      flow_lookup_lane(p, blockIdx.x * BS + threadIdx.x);
+      flow_lookup_lanes<kF, BS>(p, blockIdx.x);
       return;
     }
     vb = blockIdx.x - nl;
@@ -1631,11 +1638,11 @@ static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t 
 }
 
 // the split grid of tcp4_tas14_kernel<..., kFlowSplit>: one lookup block per
-// BS frames, then the verify blocks
-template <int BS = kBlock, typename K>
+// 2 BS frames, then the verify blocks
+template <uint32_t F = 2, int BS = kBlock, typename K>
 static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
-  const uint64_t nv = ((uint64_t) p.n + BS / 16 - 1) / (BS / 16), nl = ((uint64_t) p.n + BS - 1) / BS;
+  const uint64_t nv = ((uint64_t) p.n + BS / 16 - 1) / (BS / 16), nl = ((uint64_t) p.n + F * BS - 1) / (F * BS);
   if (nv == 0)
     return 0;
   if (nv + nl > 0x7fffffffull)
@@ -1648,15 +1655,19 @@ static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hip
 template <bool OFFS, int MODE, int FLOW>
 static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
-  static const char *const names[2][2][3] = {
-      {{"", "tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow>"},
-       {"", "tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>"}},
-      {{"", "tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow>"},
-       {"", "tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow>"}}};
+  static const char *const names[2][2][4] = {
+      {{"", "tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow_f2>",
+        "tcp4_tas14_kernel<tl_first,verify,flow>"},
+       {"", "tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow_f2>",
+        "tcp4_tas14_kernel<tl_first,verify,offs,flow>"}},
+      {{"", "tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow_f2>",
+        "tcp4_tas14_kernel<hints,verify,flow>"},
+       {"", "tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow_f2>",
+        "tcp4_tas14_kernel<hints,verify,offs,flow>"}}};
   const char *name = names[MODE == kHintArr][OFFS][FLOW];
   auto kern = tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kBlock, false, FLOW>;
-  if constexpr (FLOW == kFlowSplit)
-    return launch_split(name, kern, p, s, lds);
+  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1)
+    return launch_split<split_frames<FLOW>()>(name, kern, p, s, lds);
   return launch_groups(name, kern, p, s, lds);
 }
 
@@ -1668,11 +1679,17 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 26) // A/B: the lookup inside the rows
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowRow>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowRow>(p, s, lds);
+  if (variant == 27) // A/B: two frames per lookup lane
+    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
+                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
 #else
   (void) variant;
 #endif
-  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
-                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
+  // RX bursts without a uniform length are data/ACK mixes: one frame per
+  // lookup lane (64K frames, half / all ACKs 12.8 / 8.7 us against 13.6 / 9.3
+  // with two; profiles/r02/r02cc)
+  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
+                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
 }
 
 // RX verification + flow lookup: the row kernels' selection (as
@@ -1689,7 +1706,12 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
     if (variant == 26)
       return launch_groups("tcp4_tas14_kernel<hint,verify,flow_row>",
                            tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowRow>, *p, s, lds);
+    if (variant == 27)
+      return launch_split<1>("tcp4_tas14_kernel<hint,verify,flow_f1>",
+                             tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit1>, *p, s, lds);
 #endif
+    // a uniform received length is a data burst: two frames per lookup lane
+    // (17.6 against 18.1 us with one; profiles/r02/r02cc)
     return launch_split("tcp4_tas14_kernel<hint,verify,flow>",
                         tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit>, *p, s, lds);
   }

@@ -102,10 +102,10 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7])
 def test_gpu_flow_golden(flow_golden, variant):
     """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
-    chunks) on the fixture."""
+    chunks, 2 / 4 frames per lane) on the fixture."""
     from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
@@ -123,9 +123,13 @@ def test_gpu_flow_golden(flow_golden, variant):
 
 
 @pytest.mark.gpu
-def test_gpu_flow_vs_oracle_large(oracle):
+@pytest.mark.parametrize("variant", [0, 6, 7])
+def test_gpu_flow_vs_oracle_large(oracle, variant):
     """64K flows in a TAS-sized table (2x entries), 256K frames: hits in random
-    order, misses (unknown keys), hash-out off."""
+    order, misses (unknown keys), hash-out off; the product and the 2 / 4
+    frames-per-lane forms (A/B 6, 7), with a ragged batch end."""
+    import contextlib
+    from tas_amd import xsum
     nflows, ent, n = 65536, 131072, 262144
     keys = pktgen.flow_keys(nflows, seed=5)
     fs = pktgen.flow_state(keys, seed=5)
@@ -140,12 +144,21 @@ def test_gpu_flow_vs_oracle_large(oracle):
     fkeys[miss, 4] ^= 0x5A  # unknown remote ip
     fr = pktgen.rx_frames(fkeys, stride=128, seed=6)
     eh, ef = oracle.flow_lookup_batch(fr, n, ht, fs, fs_num=nflows, stride=128)
-    h, fid = _gpu(fr, n, ht, fs, nflows, stride=128)
-    np.testing.assert_array_equal(h, eh)
-    np.testing.assert_array_equal(fid, ef)
-    assert (fid[miss] == 0xFFFFFFFF).all()
-    _, fid2 = _gpu(fr, n, ht, fs, nflows, stride=128, want_hash=False)
-    np.testing.assert_array_equal(fid2, ef)
+    with (xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()):
+        xsum.set_kernel_variant(variant)
+        try:
+            h, fid = _gpu(fr, n, ht, fs, nflows, stride=128)
+            np.testing.assert_array_equal(h, eh)
+            np.testing.assert_array_equal(fid, ef)
+            assert (fid[miss] == 0xFFFFFFFF).all()
+            _, fid2 = _gpu(fr, n, ht, fs, nflows, stride=128, want_hash=False)
+            np.testing.assert_array_equal(fid2, ef)
+            m = n - 777                                          # ragged end
+            h3, fid3 = _gpu(fr, m, ht, fs, nflows, stride=128)
+            np.testing.assert_array_equal(fid3, ef[:m])
+            np.testing.assert_array_equal(h3, eh[:m])
+        finally:
+            xsum.set_kernel_variant(0)
 
 
 @pytest.mark.gpu

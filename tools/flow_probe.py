@@ -3,7 +3,7 @@
 Builds bench.py's FlowLookupWorkload once and times each variant
 (tasx_set_kernel_variant: 0/1 = bitwise CRC + byte loads, 2 = bitwise + chunk
 loads, 3 = LDS slice-by-4 + byte loads, 4 = LDS + chunks, 5 = LDS
-byte-position tables + byte loads) in interleaved
+byte-position tables + byte loads, 6 / 7 = 2 / 4 frames per lane) in interleaved
 rounds; every variant's flow ids must equal variant 1's.
 
     python tools/flow_probe.py [--rounds 5] [--steps 100]
@@ -39,14 +39,12 @@ def main():
     for r in range(a.rounds):
         for v in variants:
             xsum.set_kernel_variant(v)
-            launch = wl.launcher()
-            for k in range(8):
-                launch(k)
+            launch = wl.loop()
+            launch(0, 8)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for k in range(a.steps):
-                launch(k)
+            launch(0, a.steps)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / a.steps * 1e3)

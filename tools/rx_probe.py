@@ -53,7 +53,7 @@ def main():
         rp = bench.RxPassWorkload(fw, a.rotate, pktgen.SEED + 4000, ack_frac=frac)
         cases = [("product", benchloop.RX_FUSED, 0), ("separate", benchloop.RX_SEPARATE, 0)]
         if ab:
-            cases.append(("row", benchloop.RX_FUSED, 26))
+            cases += [("row", benchloop.RX_FUSED, 26), ("split_other_f", benchloop.RX_FUSED, 27)]
         ref = None
         res = {k: [] for k, _, _ in cases}
         for _ in range(a.rounds):
