@@ -1332,8 +1332,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                         cc["traffic_GBps"] = round(rate, 1)
                         cc["traffic_frac_of_copy"] = round(rate / cc["GBps"], 4)
                 txseg["pmc"] = pt
-            if rx_pass is not None:  # the one-pass RX kernel (tcp4_tas14_kernel<..., kFlowSplit = 2>)
-                prx = pmc_leg("rx", "256, false, 2>", 48)
+            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplit1 = 3>)
+                prx = pmc_leg("rx", "256, false, 3>", 48)
                 if prx and "hbm_bytes_per_launch" in prx:
                     rx_pass["roofline"]["traffic"] = int(prx["hbm_bytes_per_launch"])
                 rx_pass["pmc"] = prx
