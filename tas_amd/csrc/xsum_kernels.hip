@@ -1005,8 +1005,8 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   F frames per lane (F BS frames per block), the rest are the verify blocks.  The
 //   lookup's dependent chain (key -> bucket -> flow key) is the long one, so
 //   its blocks start first and overlap the verify rows instead of forming the
-//   grid's tail; 64 hashes per wave.  64K received frames: 15-23 % below the
-//   two kernels in turn.
+//   grid's tail.  64K received frames: 1.24-1.40x the two kernels in turn
+//   (DESIGN.md section 5.2).
 //  kFlowRow (A/B variant 26): lanes 0..3 of each verify row load the 12-byte
 //   key before the chunk loads, hash it, probe bucket entry h + lane and load
 //   that candidate's key while the chunks land.  Each wave of 4 rows pays a
@@ -1637,8 +1637,8 @@ static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t 
   }
 }
 
-// the split grid of tcp4_tas14_kernel<..., kFlowSplit>: one lookup block per
-// 2 BS frames, then the verify blocks
+// the split grid of tcp4_tas14_kernel<..., kFlowSplit*>: one lookup block per
+// F * BS frames, then the verify blocks
 template <uint32_t F = 2, int BS = kBlock, typename K>
 static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
