@@ -172,3 +172,60 @@ def test_gpu_txseg_rebuilds_linux_frames():
     o = out.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(o & 0xFFFF, want[:, 24:26].copy().view(np.uint16).ravel())
     np.testing.assert_array_equal(o >> 16, want[:, 50:52].copy().view(np.uint16).ravel())
+
+
+def _rx_tables(oracle):
+    """A flow table holding the captured connection as the receiving end at
+    10.77.0.2 sees it (local = ip.dest / tcp.dest, remote = ip.src / tcp.src of
+    Linux's frames) among 63 other flows."""
+    from tas_amd import pktgen
+    n, frames, _, _, origin, _, _ = _load()
+    f = frames.reshape(n, ROOM)
+    i = int(np.nonzero(origin == 0)[0][0])
+    conn = np.concatenate([f[i, 30:34], f[i, 26:30], f[i, 36:38], f[i, 34:36]]).astype(np.uint8)
+    keys = np.concatenate([conn[None, :], pktgen.flow_keys(63, seed=77)])
+    fs = pktgen.flow_state(keys, seed=77)
+    hashes, _ = oracle.flow_lookup_batch(pktgen.rx_frames(keys, stride=128, seed=78), len(keys),
+                                         np.zeros(2, np.uint32), fs, fs_num=len(keys), stride=128)
+    ht, ok = pktgen.flow_table(hashes, 1024)
+    assert ok[0]                                   # the connection is in the table
+    return ht, fs, len(keys)
+
+
+def test_oracle_rx_lookup_linux_frames(oracle):
+    """The flow lookup finds the connection for every frame Linux sent and for
+    none of the frames sent the other way."""
+    n, frames, _, _, origin, _, _ = _load()
+    ht, fs, nf = _rx_tables(oracle)
+    _, fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nf, stride=ROOM)
+    assert (fid[origin == 0] == 0).all() and (fid[origin == 1] == 0xFFFFFFFF).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("uniform", [False, True])
+def test_gpu_rx_pass_linux_frames(oracle, uniform):
+    """One RX pass (tasx_rx_batch_dev) over the captured connection: every frame
+    verifies, Linux's frames find their flow, the others do not -- against
+    both oracles.  uniform: only Linux's full-MSS segments, with their received
+    length as the uniform hint."""
+    import torch
+    from tas_amd import xsum
+    n, frames, _, lens, origin, _, _ = _load()
+    ht, fs, nf = _rx_tables(oracle)
+    if uniform:
+        sel = np.nonzero((origin == 0) & (lens == 1514))[0]
+        frames = frames.reshape(n, ROOM)[sel].ravel().copy()
+        n, lens, origin = len(sel), lens[sel], origin[sel]
+        kw = {"frame_len": 1514}
+    else:
+        kw = {"frame_len": torch.from_numpy(lens.astype(np.int32)).cuda()}
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nf, stride=ROOM, **kw)
+    torch.cuda.synchronize()
+    assert xsum.last_kernel() == ("tcp4_tas14_kernel<hint,verify,flow>" if uniform
+                                  else "tcp4_tas14_kernel<hints,verify,flow>")
+    assert (flags.cpu().numpy() == 3).all()
+    eh, ef = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nf, stride=ROOM)
+    np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), ef)
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), eh)
+    assert (ef[origin == 0] == 0).all() and (ef[origin == 1] == 0xFFFFFFFF).all()
