@@ -26,6 +26,8 @@
  *   26  tasx_rx_batch_dev with the flow lookup inside the verify rows
  *      (tcp4_tas14_kernel<...,flow_row>) instead of in lookup blocks ahead of
  *      the verify blocks; slower wherever ACKs are present
+ *   28  tcp4_tas14_kernel<hints_sorted>: per-frame hints, a block's rows take
+ *      its frames long ones first, so waves of short frames load one chunk
  * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
  * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels; 29 =
  * tx_segment_wave_kernel, one segment per wave from aligned loads) apply.

@@ -76,7 +76,7 @@ int tasx_set_diag_buffer(void *dev_buf)
   g_diag = (uint64_t *) dev_buf;
   return 0;
 }
-#define TASX_MAX_VARIANT 27
+#define TASX_MAX_VARIANT 28
 #else
 #define TASX_MAX_VARIANT 7
 #endif

@@ -880,7 +880,12 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 // general row body.
 enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */,
                        kHintArr = 5 /* per-frame hints as the geometry */,
-                       kHintArrP = 6 /* the same, lanes past the last chunk load nothing (A/B) */ };
+                       kHintArrP = 6 /* the same, lanes past the last chunk load nothing (A/B) */,
+                       kHintArrS = 7 /* kHintArr, a block's rows sorted long frames first (A/B, variant 28):
+                                        bit-exact, slower at every ACK fraction (64K frames, 0 / 50 / 100 %
+                                        ACKs: 16.7-17.0 / 10.9-11.1 / 7.9-8.0 us against 16.5 / 10.2 / 7.1-7.2;
+                                        profiles/r02/r02cg) -- the block's 16 hints and two ballots per
+                                        row cost more than the loads pure-ACK waves skip */ };
 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
@@ -936,7 +941,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  constexpr bool kArr = MODE == kHintArr || MODE == kHintArrP;
+  constexpr bool kArr = MODE == kHintArr || MODE == kHintArrP || MODE == kHintArrS;
   const bool bad = MODE == kHint ? tl15 != hend : kArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
@@ -1045,7 +1050,28 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     vb = blockIdx.x - nl;
   }
-  const uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
+  uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
+  uint32_t hs = 0; // kHintArrS: the row's hint
+  if constexpr (MODE == kHintArrS) {
+    // The block's rows take its frames long ones first (stable), so that the
+    // frames that fit in one chunk per lane (pure ACKs) share waves, and those
+    // waves issue one load instead of U.  Every row reads the block's BS / 16
+    // hints, one per lane, and computes the same permutation: no LDS, no barrier.
+    static_assert(BS / 16 <= 16, "one lane per frame of the block");
+    const uint32_t f0 = vb * (BS / 16), fi = f0 + (uint32_t) gl;
+    const bool mine = gl < BS / 16 && fi < p.n;
+    const uint32_t hh = mine ? ldg(p.flen, fi) : 0u;
+    const bool lng = mine && hh > p.ip_off + 242u; // more than one chunk per lane of a row
+    const uint32_t sh = (threadIdx.x & 63u) & ~15u;
+    const uint32_t lm = (uint32_t) (__builtin_amdgcn_ballot_w64(lng) >> sh) & 0xffffu;
+    const uint32_t below = __builtin_popcount(lm & ((1u << gl) - 1u));
+    const uint32_t dest = lng ? below : (uint32_t) __builtin_popcount(lm) + (uint32_t) gl - below;
+    const uint32_t row = threadIdx.x / 16u;
+    const uint32_t fm = (uint32_t) (__builtin_amdgcn_ballot_w64(dest == row && gl < BS / 16) >> sh) & 0xffffu;
+    const int f = fm ? __builtin_ctz(fm) : 0;
+    hs = (uint32_t) __shfl((int) hh, (int) sh + f, 64);
+    i = f0 + (uint32_t) f;
+  }
   if (i >= p.n)
     return;
   const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
@@ -1071,7 +1097,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
   uint32_t have = 65535u;
   if constexpr (VERIFY && MODE != kHint) {
-    const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
+    const uint32_t b = rx_bound(p, MODE == kHintArrS ? hs : p.flen ? ldg(p.flen, i) : p.flen0);
     have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
   }
   // the datagram [ip, ip + hend): uniform from the hint, or per row from the
@@ -1115,6 +1141,21 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       } else {
         v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
       }
+    }
+  } else if constexpr (MODE == kHintArrS) {
+    const uint32_t hl = hs > p.ip_off ? hs - p.ip_off : 0u;
+    in_range = row_ok && hl >= 38u && hl <= 1522u && (!p.room || hs <= p.room);
+    hend = in_range ? hl : (row_ok ? 20u : 1u);
+    const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
+    v[0] = ld16nt_off(fb, min(lo, lastoff));
+    if (__builtin_amdgcn_ballot_w64(last >= 16u) != 0ull) { // a wave-uniform branch
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
+    } else { // every row of the wave ends in its first 256 bytes; lane 15's v[U-1] = the last chunk
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        v[u] = v[0];
     }
   } else if constexpr (MODE == kHead5) {
     v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
@@ -1795,6 +1836,9 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
   case kHintArrP:
     return launch_groups(OFFS ? "tcp4_tas14_kernel<hints_pred,offs>" : "tcp4_tas14_kernel<hints_pred>",
                          tcp4_tas14_kernel<6, kHintArrP, false, 8, OFFS>, p, s, lds);
+  case kHintArrS:
+    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints_sorted,offs>" : "tcp4_tas14_kernel<hints_sorted>",
+                         tcp4_tas14_kernel<6, kHintArrS, false, 8, OFFS>, p, s, lds);
   case kMix:
     if (getenv("TASX_MIX_F8"))
       return launch_groups<8>("tcp4_mix_kernel<f8>", tcp4_mix_kernel<6, 8>, p, s);
@@ -1847,11 +1891,11 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
 #ifdef TASX_AB
   // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
   // where its room requirement holds (else as 0)
-  if ((variant >= 9 && variant <= 11) || (variant >= 19 && variant <= 21)) {
+  if ((variant >= 9 && variant <= 11) || (variant >= 19 && variant <= 21) || variant == 28) {
     const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
     const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : variant == 19 ? kMix
-                : variant == 20 ? kHintArr : kHintArrP;
-    if ((m == kTlFirst) || ((m == kHintArr || m == kHintArrP) && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
+                : variant == 20 ? kHintArr : variant == 28 ? kHintArrS : kHintArrP;
+    if ((m == kTlFirst) || ((m == kHintArr || m == kHintArrP || m == kHintArrS) && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
       mode = m;
     variant = 0;
   }
