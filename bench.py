@@ -89,7 +89,7 @@ def parse(argv=None):
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
-    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx"], help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx", "flushmix", "tso", "shard8m"], help=argparse.SUPPRESS)
     ap.add_argument("--control-selftest", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank plumbing
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
@@ -1013,6 +1013,12 @@ def pmc_child(mode: str, steps: int):
         run = TxSegWorkload(16, pktgen.SEED + 2000).loop()
     elif mode == "rx":
         run = RxPassWorkload(FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000).loop()
+    elif mode == "flushmix":
+        run = FlushMixWorkload(12, pktgen.SEED + 500).loop()
+    elif mode == "tso":
+        run = tso_workload(0).loop(HINT)
+    elif mode == "shard8m":
+        run = shard8m_workload(1, 0).loop()
     else:
         run = mixed_workload(0).loop()
     run(0, steps)
@@ -1069,8 +1075,10 @@ def other_workload(args, ws, rank, info):
         torch.cuda.synchronize()
         cpu = other_cpu_baseline(name, wl, args.cpu_seconds / 2)
     pmc = None
-    if rank == 0 and ws == 1 and not args.no_pmc and name == "mixed":
-        pmc = pmc_leg("mixed", "raw_wave_kernel", 8)
+    if rank == 0 and ws == 1 and not args.no_pmc:
+        # rocprofv3's kernel names (the template, not tasx_last_kernel's label)
+        pmc = pmc_leg(name, {"mixed": "raw_wave_kernel", "shard8m": "raw_sad_kernel", "tso": "tcp4_tas_kernel<"}[name],
+                      4 if name == "shard8m" else 8)
         if pmc and "hbm_bytes_per_launch" in pmc:
             r["roofline"]["traffic"] = int(pmc["hbm_bytes_per_launch"])
     if rank == 0:
@@ -1332,6 +1340,11 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                         cc["traffic_GBps"] = round(rate, 1)
                         cc["traffic_frac_of_copy"] = round(rate / cc["GBps"], 4)
                 txseg["pmc"] = pt
+            if mix is not None:  # tcp4_tas14_kernel<hints>: MODE kHintArr = 5, TX, 8 waves per SIMD, stride mode
+                pm = pmc_leg("flushmix", "<6, 5, false, 8, false,", 48)
+                if pm and "hbm_bytes_per_launch" in pm:
+                    mix["roofline"]["traffic"] = int(pm["hbm_bytes_per_launch"])
+                mix["pmc"] = pm
             if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplit1 = 3>)
                 prx = pmc_leg("rx", "256, false, 3>", 48)
                 if prx and "hbm_bytes_per_launch" in prx:
