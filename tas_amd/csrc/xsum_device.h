@@ -299,23 +299,39 @@ __device__ __forceinline__ Chunks<U> chunk_range(const uint8_t *start, uint32_t 
 template <int U, int G = 16>
 __device__ __forceinline__ uint32_t group_lane_sum(const Chunks<U> &r, int gl)
 {
+  static_assert(G * U >= 8, "the 128-byte phase lies in the first round");
   uint64_t acc = 0;
   if (r.nch == 0)
     return 0;
-  for (uint32_t c = (uint32_t) gl; c < r.nch; c += (uint32_t) G * U) {
+  // Rounds start on 128-byte lines: the range is indexed from the line holding
+  // chunk 0 (ph chunks earlier, same line, never loaded past).  With rounds at
+  // the range's own 16-byte phase, the line a round ends in is the next one's
+  // first line, and the non-temporal loads fetch it twice (a 64 KB TSO segment:
+  // ~43 extra lines).
+  const uint32_t ph = (uint32_t) (((uintptr_t) r.c0p >> 4) & 7u);
+  const u32x4 *cp = r.c0p - ph;
+  const uint32_t n = r.nch + ph;
+  for (uint32_t c = (uint32_t) gl; c < n; c += (uint32_t) G * U) {
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(r.c0p, min(c + (uint32_t) G * u, r.nch - 1));
+      v[u] = ld16nt(cp, max(min(c + (uint32_t) G * u, n - 1), ph));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool keep = c + (uint32_t) G * u < r.nch;
+      const uint32_t k = c + (uint32_t) G * u;
+      const bool keep = k >= ph && k < n;
       acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
     }
-    // boundary fix-ups: drop bytes [0, head) of chunk 0, [tail, 16) of chunk nch-1
-    if (c == 0 && r.head)
-      acc -= chunk_prefix_sum(v[0], r.head);
-    const uint32_t last = r.nch - 1;
+    // boundary fix-ups: drop bytes [0, head) of chunk 0 (index ph), [tail, 16) of chunk nch-1
+    if (r.head && c == ph % G) {
+      u32x4 h = v[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u)
+        if (ph / G == (uint32_t) u)
+          h = v[u];
+      acc -= chunk_prefix_sum(h, r.head);
+    }
+    const uint32_t last = n - 1;
     if (last >= c && last < c + (uint32_t) G * U && ((last - c) % G) == 0 && r.tail < 16) {
       const uint32_t ut = (last - c) / G;
       u32x4 t = v[0];
