@@ -753,6 +753,17 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
     return t1 - t0, e0.elapsed_time(e1) / steps
 
 
+def drop_rehearsal_fractions(obj):
+    """--rehearse: ranks share one GPU, so no fraction of a roofline, a ceiling
+    or N x HBM is a claim; any such fraction above 1 is dropped (None)."""
+    if isinstance(obj, dict):
+        return {k: (None if "frac" in k and isinstance(v, (int, float)) and v > 1 else drop_rehearsal_fractions(v))
+                for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [drop_rehearsal_fractions(v) for v in obj]
+    return obj
+
+
 def roofline(bytes_per_launch: int, avg_ms: float, traffic):
     avg_s = avg_ms / 1e3
     achieved = bytes_per_launch / avg_s / 1e9
@@ -767,7 +778,7 @@ def leg(run, bytes_per_step: int, args, ws, desc, kernel: str = "", streams=None
     dtm = max_over_ranks(dt, ws)
     total = sum_over_ranks(float(bytes_per_step * args.steps), ws)
     r = {"value": total / dtm / GIB, "unit": "GiB/s", "ms_per_step": dtm / args.steps * 1e3,
-         "workload": desc, "roofline": roofline(bytes_per_step, avg_ms, None)}
+         "workload": desc, "roofline": roofline(bytes_per_step, avg_ms, None), "seconds": dt}
     if kernel:
         r["kernel"] = kernel
     if ws > 1:
@@ -825,6 +836,104 @@ def txseg_host_leg(ws: int, rank: int, reps: int) -> dict:
     finally:
         for pb in pins:
             pb.free()
+
+
+def timed_host_batch(call, alg: int, reps: int, ws: int, *, pcie_h2d_bytes: int, what: str) -> dict:
+    """One warm call, then `reps` timed calls of a host batch (each returns
+    after its results are in host memory) between a barrier and the slowest
+    rank's time."""
+    call()
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    t = time.perf_counter() - t0
+    tm = max_over_ranks(t, ws)
+    return {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s (algorithmic)",
+            "ms_per_batch": tm / reps * 1e3, "pcie_h2d_bytes_per_rank": pcie_h2d_bytes, "entry_point": what,
+            "kernel": xsum.last_kernel()}
+
+
+def e2e_mixed_leg(ws: int, rank: int, reps: int = 3) -> dict:
+    """Config 3 from host memory: the 1M mixed-MTU packets (2.92 GB, this rank's
+    byte-balanced shard at N > 1) at their packed offsets in pinned memory,
+    through tasx_raw_cksum_batch_host_offs: staged (the CPU gathers each
+    packet's bytes into pinned staging, H2D, raw_wave_kernel, D2H) and
+    zero-copy (the kernel reads the packets in place over PCIe).  Both results
+    are checked against the device-resident kernel on the same packets."""
+    wl = mixed_workload(ws, rank)
+    n = wl.n
+    offs = wl.off.cpu().numpy().astype(np.uint64)
+    lens = wl.lens.cpu().numpy().astype(np.uint32)
+    total = int(wl.bufs[0].numel())
+    alg = int(lens.astype(np.int64).sum()) + 2 * n
+    pin = xsum.PinnedBuffer(total + 64)
+    res = {"workload": f"config 3 from pinned host memory: {n} packets, {alg / 1e9:.2f} GB algorithmic"}
+    try:
+        xsum._check(xsum.lib().tasx_memcpy_d2h(pin.addr, wl.bufs[0].data_ptr(), total), "tasx_memcpy_d2h")
+        ref = wl.loop()
+        ref(0, 1)
+        torch.cuda.synchronize()
+        exp = wl.outs[0].cpu().numpy().view(np.uint16).copy()
+        del wl, ref
+        torch.cuda.empty_cache()
+        out = np.empty(n, np.uint16)
+        xsum.ctx_init(1, torch.cuda.current_device(), 64 << 20)
+        try:
+            res["staged"] = timed_host_batch(
+                lambda: xsum.raw_cksum_batch_host_offs(1, pin.addr, offs, n, lengths=lens, out=out), alg, reps, ws,
+                pcie_h2d_bytes=int(((lens.astype(np.int64) + 15) // 16 * 16).sum()) + 12 * n,
+                what="tasx_raw_cksum_batch_host_offs (staged gather)")
+            res["staged"]["matches_device"] = bool(np.array_equal(out, exp))
+            out[:] = 0
+            res["zero_copy"] = timed_host_batch(
+                lambda: xsum.raw_cksum_batch_host_offs(1, pin.addr, offs, n, lengths=lens, out=out, zerocopy=True),
+                alg, reps, ws, pcie_h2d_bytes=alg + 12 * n, what="tasx_raw_cksum_batch_host_offs (zero-copy)")
+            res["zero_copy"]["matches_device"] = bool(np.array_equal(out, exp))
+        finally:
+            xsum.ctx_destroy(1)
+    finally:
+        pin.free()
+    return res
+
+
+def e2e_tso_leg(ws: int, rank: int, reps: int = 3) -> dict:
+    """Config 5 from host memory: 16,384 TSO segments (ip.len 65535) in pinned
+    memory at 65,552 B strides, through tasx_tcp4_cksum_batch_host_offs:
+    staged (the CPU gathers header + L4 of each segment, H2D, one stride-mode
+    launch per chunk, D2H) and zero-copy (frame lengths as hints, the kernel
+    reads the segments in place).  Checked against the device-resident kernel."""
+    wl = tso_workload(rank)
+    n, stride = wl.n, wl.stride
+    alg = n * (wl.ip_total + 4)
+    pin = xsum.PinnedBuffer(n * stride + 64)
+    res = {"workload": f"config 5 from pinned host memory: {n} TSO segments, {alg / 1e9:.2f} GB algorithmic"}
+    try:
+        xsum._check(xsum.lib().tasx_memcpy_d2h(pin.addr, wl.bufs[0].data_ptr(), n * stride), "tasx_memcpy_d2h")
+        wl.loop(HINT)(0, 1)
+        torch.cuda.synchronize()
+        exp = wl.outs[0].cpu().numpy().view(np.uint16).copy()
+        del wl
+        torch.cuda.empty_cache()
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        flen = np.full(n, pktgen.ETH_LEN + 65535, np.uint32)
+        out = np.empty(2 * n, np.uint16)
+        xsum.ctx_init(1, torch.cuda.current_device(), 64 << 20)
+        try:
+            res["staged"] = timed_host_batch(
+                lambda: xsum.tcp4_cksum_batch_host_offs(1, pin.addr, offs, n, out=out), alg, reps, ws,
+                pcie_h2d_bytes=n * 65552, what="tasx_tcp4_cksum_batch_host_offs (staged gather)")
+            res["staged"]["matches_device"] = bool(np.array_equal(out, exp))
+            out[:] = 0
+            res["zero_copy"] = timed_host_batch(
+                lambda: xsum.tcp4_cksum_batch_host_offs(1, pin.addr, offs, n, out=out, frame_len=flen, zerocopy=True),
+                alg, reps, ws, pcie_h2d_bytes=n * 65536 + 12 * n, what="tasx_tcp4_cksum_batch_host_offs (zero-copy)")
+            res["zero_copy"]["matches_device"] = bool(np.array_equal(out, exp))
+        finally:
+            xsum.ctx_destroy(1)
+    finally:
+        pin.free()
+    return res
 
 
 def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
@@ -889,10 +998,18 @@ def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
             res["flush32_note"] = ("32 x tasx_defer_tcp4 + tasx_flush via ctypes (Python call overhead "
                                    "included); tools/flush_bench.c has the C-side numbers")
             f32.free()
+        # the same frames as scattered mbufs: the CPU gathers only the summed
+        # bytes (tasx_tcp4_cksum_batch_host_offs, staged)
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(STRIDE)
+        res["staged_gather"] = timed_host_batch(
+            lambda: xsum.tcp4_cksum_batch_host_offs(0, pin.addr, offs, n, out=out), alg, reps, ws,
+            pcie_h2d_bytes=n * 1536 + 12 * n, what="tasx_tcp4_cksum_batch_host_offs (staged gather)")
         res["tx_segment_host"] = txseg_host_leg(ws, rank, 2 * reps)
     finally:
         xsum.ctx_destroy(0)
         pin.free()
+    res["mixed"] = e2e_mixed_leg(ws, rank)
+    res["tso"] = e2e_tso_leg(ws, rank)
     res["value"] = res["staged"]["value"]
     res["unit"] = "GiB/s"
     res["host_threads"] = f"one per GPU ({ws}), each pinned to its GPU's NUMA node"
@@ -924,47 +1041,58 @@ def cpu_model() -> str:
 
 
 # The box's CPU share for one GPU: worker pools stay within it (the machine's
-# other cores serve the other GPUs' jobs)
+# other cores serve the other GPUs' jobs; OMP_NUM_THREADS is 16 there)
 CPU_SHARE = 16
+CPU_SWEEP = (1, 2, 4, 8, 16)
+
+
+def cpu_sweep(bench_fn, alg_bytes: int, budget_s: float) -> tuple[dict, dict]:
+    """The oracle over the WHOLE batch at 1, 2, 4, 8 and 16 pinned threads (the
+    ones this rank may use, up to the GPU's CPU share); bench_fn(threads, reps)
+    returns the median seconds per pass.  Returns ({threads: GiB/s}, {threads:
+    passes})."""
+    allowed = len(os.sched_getaffinity(0))
+    ths = [t for t in CPU_SWEEP if t <= min(CPU_SHARE, allowed)] or [1]
+    rate, reps_used = {}, {}
+    for t in ths:
+        t1 = bench_fn(t, 1)
+        reps = max(3, min(2000, int(budget_s / len(ths) / max(t1, 1e-6))))
+        rate[t] = alg_bytes / bench_fn(t, reps) / GIB
+        reps_used[t] = reps
+    return rate, reps_used
+
+
+def cpu_record(rate: dict, reps: dict, sample: str, kind_note: str, parity: bool) -> dict:
+    top = max(rate)
+    allowed = len(os.sched_getaffinity(0))
+    return {
+        "value": rate[top], "unit": "GiB/s", "cores": top, "kind": "port",
+        "sample": f"{sample}; median of {reps[top]} passes on {top} pinned threads; {kind_note}; CPU {cpu_model()}",
+        "single_core_value": rate[min(rate)],
+        "thread_sweep": {str(t): round(v, 3) for t, v in rate.items()},
+        "sweep_passes": {str(t): v for t, v in reps.items()},
+        "host_cpus": os.cpu_count(), "cpus_this_rank": allowed, "cpu_model": cpu_model(),
+        "cores_note": (f"measured at 1..{top} threads over the whole batch; {CPU_SHARE} is the box's CPU share for "
+                       f"one GPU (worker pools stay within it: the host's other {(os.cpu_count() or 0) - CPU_SHARE} "
+                       "CPUs serve the other GPUs' jobs), so no run uses more"),
+        "parity_vs_gpu": "bit-exact" if parity else "MISMATCH",
+    }
 
 
 def cpu_baseline_leg(wl: Tcp4Workload, gpu_out: np.ndarray, budget_s: float) -> dict:
     """The oracle (C restatement of the reference path, per-frame calls) timed on
-    this box's host cores, on a bounded sample of the same workload: 1 thread
-    and the GPU's CPU share (threads pinned to the cores this rank may use)."""
+    this box's host cores over the whole headline batch, at 1..16 threads
+    (threads pinned to the cores this rank may use)."""
     orc, kind_note, tmp = host_oracle()
     frames = wl.host.copy()
     n = wl.n
     exp = orc.tcp4_batch(frames.copy(), n, stride=STRIDE)
     parity = bool(np.array_equal(exp, gpu_out))
-    allowed = len(os.sched_getaffinity(0))
-    threads = min(CPU_SHARE, allowed)
-    t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=1)
-    reps1 = max(3, min(200, int(budget_s * 0.4 / max(t1, 1e-6))))
-    t1 = orc.bench(1, frames, n, stride=STRIDE, threads=1, reps=reps1)
-    tn = orc.bench(1, frames, n, stride=STRIDE, threads=threads, reps=1)
-    repsn = max(3, min(2000, int(budget_s * 0.4 / max(tn, 1e-6))))
-    tn = orc.bench(1, frames, n, stride=STRIDE, threads=threads, reps=repsn)
     alg = n * (IP_TOTAL + 4)
+    rate, reps = cpu_sweep(lambda t, r: orc.bench(1, frames, n, stride=STRIDE, threads=t, reps=r), alg, budget_s)
     shutil.rmtree(tmp, ignore_errors=True)
-    return {
-        "value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"the 64K-frame TCP4 batch (98.6 MB algorithmic), per-frame oracle_tcp_checksums "
-                  f"(DPDK 19.11 restatement), median of {repsn} passes on {threads} pinned threads; "
-                  f"1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}; CPU {cpu_model()}",
-        "single_core_value": alg / t1 / GIB,
-        "host_cpus": os.cpu_count(), "cpus_this_rank": allowed,
-        "cores_note": (f"{threads} threads = the box's CPU share for one GPU; the host's other "
-                       f"{(os.cpu_count() or 0) - threads} CPUs serve the other GPUs' jobs and are not used"),
-        # BASELINE.md asks for all host cores too; running them would take the
-        # other GPUs' CPU shares, so the figure is the measured per-thread rate
-        # at `threads` scaled linearly to every host CPU: an upper bound (the
-        # host's DRAM bandwidth caps it long before), never a measurement
-        "all_cores_estimate": {"value": alg / tn / GIB / threads * (os.cpu_count() or threads),
-                               "unit": "GiB/s", "cores": os.cpu_count(), "measured": False,
-                               "how": f"{threads}-thread rate / {threads} x host CPUs (linear upper bound)"},
-        "parity_vs_gpu": "bit-exact" if parity else "MISMATCH",
-    }
+    return cpu_record(rate, reps, "the whole 64K-frame TCP4 batch (98.6 MB algorithmic), per-frame "
+                      "oracle_tcp_checksums (DPDK 19.11 restatement)", kind_note, parity)
 
 
 def pmc_leg(mode: str, kernel_name: str, launches: int) -> dict | None:
@@ -1020,7 +1148,7 @@ def pmc_child(mode: str, steps: int):
     elif mode == "shard8m":
         run = shard8m_workload(1, 0).loop()
     else:
-        run = mixed_workload(0).loop()
+        run = mixed_workload().loop()
     run(0, steps)
     torch.cuda.synchronize()
 
@@ -1028,22 +1156,35 @@ def pmc_child(mode: str, steps: int):
 # ---------------------------------------------------------------------------
 # other BASELINE.json configs (--workload)
 
-def mixed_workload(rank: int) -> RawWorkload:
+MIXED_N = 1 << 20
+
+
+def mixed_workload(ws: int = 1, rank: int = 0) -> RawWorkload:
     """Config 3: 1,048,576 RAW packets, sizes uniform over {64,576,1500,9000} B in
-    random order, packed at 16-byte aligned offsets."""
-    n = 1 << 20
-    lens = pktgen.mixed_lengths(n, seed=pktgen.SEED + rank).astype(np.int64)
+    random order, packed at 16-byte aligned offsets.  Over N ranks the one batch
+    is split into contiguous byte-balanced shards (tas_amd/shard.py); rank r
+    holds its shard's packets (random bytes of its own)."""
+    lens_all = pktgen.mixed_lengths(MIXED_N, seed=pktgen.SEED).astype(np.int64)
+    a, b = shard.shard_ranges(lens_all, ws)[rank]
+    lens = lens_all[a:b]
     slot = (lens + 15) // 16 * 16
-    offs = np.zeros(n, np.int64)
+    offs = np.zeros(len(lens), np.int64)
     np.cumsum(slot[:-1], out=offs[1:])
-    return RawWorkload(1, pktgen.SEED + rank, n=n, offsets=offs, lengths=lens,
-                       total_bytes=int(offs[-1] + slot[-1]))
+    wl = RawWorkload(1, pktgen.SEED + rank, n=len(lens), offsets=offs, lengths=lens,
+                     total_bytes=int(offs[-1] + slot[-1]))
+    wl.shard = (a, b)
+    return wl
+
+
+SHARD8M_N = 8 * (1 << 20)
 
 
 def shard8m_workload(ws: int, rank: int) -> RawWorkload:
     """Config 4: 8,388,608 x 1500 B split over the ranks (1,048,576 per GPU at 8)."""
-    a, b = shard.shard_ranges(8 * (1 << 20), ws)[rank]
-    return RawWorkload(1, pktgen.SEED + rank, n=b - a, length=RAW_LEN)
+    a, b = shard.shard_ranges(SHARD8M_N, ws)[rank]
+    wl = RawWorkload(1, pktgen.SEED + rank, n=b - a, length=RAW_LEN)
+    wl.shard = (a, b)
+    return wl
 
 
 def tso_workload(rank: int) -> Tcp4Workload:
@@ -1060,16 +1201,23 @@ def other_workload(args, ws, rank, info):
         desc = f"8,388,608 x 1500 B payloads sharded over {ws} GPU(s): {wl.n} packets on this rank"
         scaling = "strong"
     elif name == "mixed":
-        wl = mixed_workload(rank)
+        wl = mixed_workload(ws, rank)
         run, kernel = wl.loop(), "raw_wave_kernel"
-        desc = "1,048,576 RAW packets per GPU, sizes uniform over {64,576,1500,9000} B in random order"
-        scaling = "weak"
+        desc = (f"1,048,576 RAW packets, sizes uniform over {{64,576,1500,9000}} B in random order, split by bytes "
+                f"over {ws} GPU(s): {wl.n} packets on this rank")
+        scaling = "strong"
     else:  # tso
         wl = tso_workload(rank)
         run, kernel = wl.loop(HINT), "tcp4_tas_kernel"
         desc = "16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B), tcp_checksums() flag-off, hinted"
         scaling = "weak"
     r = leg(run, wl.bytes_per_step, args, ws, desc, kernel)
+    # per-rank accounting: packets, algorithmic bytes, seconds for the K steps
+    shards = {"packets": [int(v) for v in gather_over_ranks(float(wl.n), ws)],
+              "bytes_per_step": [int(v) for v in gather_over_ranks(float(wl.bytes_per_step), ws)],
+              "first_packet": [int(v) for v in gather_over_ranks(float(getattr(wl, "shard", (0, 0))[0]), ws)],
+              "seconds": gather_over_ranks(r["seconds"], ws)}
+    rehearse = bool(info.get("rehearse"))
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         torch.cuda.synchronize()
@@ -1088,54 +1236,43 @@ def other_workload(args, ws, rank, info):
                           "data": "synthetic (device-generated random bytes)",
                           "config": {"workload": desc, "parallelism": f"shard{ws}"},
                           "roofline": r["roofline"], "kernel": kernel,
-                          "frac_of_n_hbm": round(r["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
+                          # ranks sharing one GPU (--rehearse) make no HBM-fraction claim
+                          "frac_of_n_hbm": None if rehearse else round(r["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
                           **({"per_rank_value": r["per_rank_value"]} if "per_rank_value" in r else {}),
-                          "ranks": info.get("all_bus_ids"), "cpu_baseline": cpu,
-                          **({"pmc": pmc} if pmc else {})}), flush=True)
+                          "shards": shards,
+                          "ranks": {"bus_ids": info.get("all_bus_ids", [info.get("pci_bus_id")]), "rehearse": rehearse},
+                          "cpu_baseline": cpu, **({"pmc": pmc} if pmc else {})}), flush=True)
 
 
 def other_cpu_baseline(name: str, wl, budget_s: float) -> dict:
-    """The oracle on a bounded sample of the other configs (BASELINE.md's CPU
-    plan: the same generator, per-packet calls, 1 thread and the CPU share),
-    checked against the GPU's results for the same packets."""
+    """The oracle over the WHOLE batch of the other configs (BASELINE.md's CPU
+    plan: the same generator, per-packet calls), at 1..16 threads, checked
+    against the GPU's results for the same packets."""
     orc, kind_note, tmp = host_oracle()
-    threads = min(CPU_SHARE, len(os.sched_getaffinity(0)))
+    m = wl.n
     if name == "tso":
-        m, stride = 4096, wl.stride  # 268 MB: beyond the 16 threads' share of L3
-        host = wl.bufs[0][:m * stride].cpu().numpy().copy()
+        stride = wl.stride
+        host = wl.bufs[0].cpu().numpy().copy()
         gpu = wl.outs[0][:2 * m].cpu().numpy().view(np.uint16)
         parity = np.array_equal(orc.tcp4_batch(host.copy(), m, stride=stride), gpu)
         kw = dict(stride=stride)
         mode, alg = 1, m * (wl.ip_total + 4)
-        sample = f"the first {m} TSO segments (ip.len {wl.ip_total}), per-segment oracle_tcp_checksums in place"
+        sample = f"all {m} TSO segments (ip.len {wl.ip_total}), per-segment oracle_tcp_checksums"
     else:
-        m = 65536 if wl.off is not None else 262144  # 182 / 393 MB: streamed, not L3-resident
         gpu = wl.outs[0][:m].cpu().numpy().view(np.uint16)
+        host = wl.bufs[0].cpu().numpy()
         if wl.off is None:
-            host = wl.bufs[0][:m * wl.len0].cpu().numpy()
             kw = dict(stride=wl.len0, len0=wl.len0)
             alg = m * (wl.len0 + 2)
         else:
-            offs = wl.off[:m].cpu().numpy().astype(np.uint64)
-            lens = wl.lens[:m].cpu().numpy().astype(np.uint32)
-            host = wl.bufs[0][:int(offs[-1]) + int(lens[-1])].cpu().numpy()
-            kw = dict(offsets=offs, lengths=lens)
-            alg = int(lens.astype(np.int64).sum()) + 2 * m
+            kw = dict(offsets=wl.off.cpu().numpy().astype(np.uint64), lengths=wl.lens.cpu().numpy().astype(np.uint32))
+            alg = int(kw["lengths"].astype(np.int64).sum()) + 2 * m
         parity = np.array_equal(orc.raw_batch(host, m, **kw), gpu)
         mode = 0
-        sample = f"the first {m} packets of the batch, per-packet oracle_raw_cksum (rte_raw_cksum restatement)"
-    t1 = orc.bench(mode, host, m, threads=1, reps=1, **kw)
-    reps1 = max(3, min(200, int(budget_s * 0.4 / max(t1, 1e-6))))
-    t1 = orc.bench(mode, host, m, threads=1, reps=reps1, **kw)
-    tn = orc.bench(mode, host, m, threads=threads, reps=1, **kw)
-    repsn = max(3, min(2000, int(budget_s * 0.4 / max(tn, 1e-6))))
-    tn = orc.bench(mode, host, m, threads=threads, reps=repsn, **kw)
+        sample = f"all {m} packets of this rank's batch, per-packet oracle_raw_cksum (rte_raw_cksum restatement)"
+    rate, reps = cpu_sweep(lambda t, r: orc.bench(mode, host, m, threads=t, reps=r, **kw), alg, budget_s)
     shutil.rmtree(tmp, ignore_errors=True)
-    return {"value": alg / tn / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} ({alg / 1e6:.1f} MB algorithmic), median of {repsn} passes on {threads} "
-                      f"pinned threads; 1 thread: {alg / t1 / GIB:.2f} GiB/s (median of {reps1}); {kind_note}",
-            "single_core_value": alg / t1 / GIB,
-            "parity_vs_gpu": "bit-exact" if parity else "MISMATCH"}
+    return cpu_record(rate, reps, f"{sample} ({alg / 1e6:.1f} MB algorithmic)", kind_note, parity)
 
 
 # ---------------------------------------------------------------------------
@@ -1207,7 +1344,11 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     rot = max(1, args.rotate)
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
     head = leg(wl.loop(HINT), wl.bytes_per_step, args, ws, Tcp4Workload.desc, "tcp4_tas14_kernel<hint>")
-    head["roofline"]["pattern_ceiling"] = tcp4_pattern_ceiling(wl, head["roofline"]["launch_avg_us"])
+    rehearse = bool(info.get("rehearse"))
+    if rehearse:  # ranks share the GPU: another rank's launches overlap this one's
+        head["roofline"]["pattern_ceiling"] = None
+    else:
+        head["roofline"]["pattern_ceiling"] = tcp4_pattern_ceiling(wl, head["roofline"]["launch_avg_us"])
     ctx2 = None
     if not args.no_contexts:
         streams = [torch.cuda.Stream() for _ in range(2)]
@@ -1362,7 +1503,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                        "parallelism": f"shard{ws} (independent per-GPU batches, no collective)"},
             "roofline": head["roofline"],
             "kernel": head["kernel"],
-            "frac_of_n_hbm": round(head["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
+            "frac_of_n_hbm": None if rehearse else round(head["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
             "per_rank_value": head.get("per_rank_value", [round(head["value"], 2)]),
             "ranks": {"bus_ids": info.get("all_bus_ids", [info.get("pci_bus_id")]),
                       "numa_node_rank0": info.get("numa_node"), "rehearse": info.get("rehearse")},
@@ -1386,6 +1527,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             line["e2e"] = extra["e2e"]
         if "pmc" in extra:
             line["pmc"] = extra["pmc"]
+        if rehearse:
+            line = drop_rehearsal_fractions(line)
         print(json.dumps(line), flush=True)
 
 

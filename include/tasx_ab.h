@@ -64,6 +64,10 @@ int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t
  * lane -- the TX segment build's ceiling, timed by bench.py. */
 int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream);
 
+/* Test hook: restart a context's flush tickets at `start` (nothing pending or
+ * in flight, no feeder), so a test can run flushes across the 2^32 wrap. */
+int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,10 +44,13 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 4
+#define TASX_ABI_VERSION 5
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
+/* host batches over offsets (ABI 5): read the packets where they lie, in
+ * pinned or registered memory, over PCIe instead of gathering them */
+#define TASX_F_ZEROCOPY 0x2u
 
 /* largest RAW packet: DPDK's 32-bit accumulator cannot wrap below this
  * (65536 words * 0xffff + 0xff < 2^32), so results stay bit-exact. */
@@ -276,6 +279,38 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
 int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     uint64_t stride, uint32_t len0, uint32_t n, uint16_t *out);
 
+/* Host-memory batches over scattered packets (ABI 5; SURVEY.md section 8b:
+ * "(base, offsets[], lengths[], n) -> u16[n] ... host-pointer variants").
+ * TAS's frames are mbufs scattered over a per-core mempool
+ * (tas/fast/network.c:320-330) and leave through tx_flush
+ * (tas/fast/fastemu.c:544-566); these are the end-to-end forms of the _dev
+ * batches for such frames.  Packet i starts at base + off[i], or at the
+ * address off[i] when base == NULL (staged form only).  off, len, flen and out
+ * are host arrays; results are as the _dev forms'.
+ *   staged (flags without TASX_F_ZEROCOPY): the calling thread gathers only
+ *     the bytes that are summed (RAW: len_i bytes; TCP4: the 20-byte IPv4
+ *     header and max(total_length - 20, 18) L4 bytes) into the context's
+ *     pinned staging, one hipMemcpyAsync H2D per chunk, the kernel from HBM,
+ *     one D2H of the results; the gather of chunk k + 1 overlaps the GPU's
+ *     work on chunk k.
+ *   zero-copy (TASX_F_ZEROCOPY): base is pinned (tasx_host_alloc) or
+ *     registered (tasx_host_register / tasx_ctx_register_frames) memory and
+ *     the kernel reads the packets in place over PCIe, only the 16-byte
+ *     aligned chunks that hold summed bytes (so up to 15 bytes past a packet
+ *     must be readable); TCP4 with TASX_F_INPLACE stores both fields into the
+ *     frames from the GPU.
+ * RAW: len[i] (or len0 for all when len == NULL) <= TASX_RAW_MAX_LEN.
+ * TCP4: flen (optional) holds frame lengths from the frame start (the mbuf
+ * data_len); the zero-copy kernel takes them as per-frame read geometry, as
+ * tasx_tcp4_cksum_batch_dev_hint does; results follow ip.total_length.  out
+ * (4-byte aligned) may be NULL with TASX_F_INPLACE. */
+int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base,
+    const uint64_t *off, const uint32_t *flen, uint32_t n, uint32_t ip_off,
+    uint32_t l4_off, uint16_t *out, uint32_t flags);
+int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base,
+    const uint64_t *off, const uint32_t *len, uint32_t len0, uint32_t n,
+    uint16_t *out, uint32_t flags);
+
 /* The calling thread's context: TAS runs one dataplane_context per fast-path
  * thread (dataplane_loop, tas/fast/fastemu.c:142), so the thread that will call
  * tcp_checksums() binds its context once, and the per-frame calls pass
@@ -313,17 +348,18 @@ int tasx_flush(unsigned ctx_id);
  * far more than a core's CPU checksums of one tx_flush batch (DESIGN.md
  * section 5.1); split, a fast-path core submits a batch, keeps polling its
  * queues, and hands the batch's frames to the NIC once its ticket completes,
- * with up to 3 batches in flight per context.
+ * with up to 4 batches in flight per context.
  *   tasx_flush_submit: launches every recorded frame (one or more flushes) and
  *     returns in *ticket the ticket of the last one (the last submitted ticket
  *     when nothing was recorded; 0 before the first flush).  Blocks only when
- *     3 flushes are already in flight (it completes the oldest).
+ *     4 flushes are already in flight (it completes the oldest).
  *   tasx_flush_poll: 1 when flush `ticket` and every earlier one are complete
  *     (both checksum fields stored in their frames), 0 if not yet; never
  *     blocks.  Completes flushes in ticket order.
  *   tasx_flush_wait: spins until flush `ticket` is complete.
  * Frames must stay valid and unmodified until their ticket completes.
- * Tickets count up from 1 and wrap at 2^32 (comparisons are wrap-safe). */
+ * Tickets count up from 1 and wrap at 2^32 (comparisons are wrap-safe; after
+ * the wrap 0 is an ordinary ticket, and flush t always uses slot t % 4). */
 int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket);
 int tasx_flush_poll(unsigned ctx_id, uint32_t ticket);
 int tasx_flush_wait(unsigned ctx_id, uint32_t ticket);

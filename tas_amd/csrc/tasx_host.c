@@ -21,7 +21,9 @@
 
 #include "tasx_kernels.h"
 
-#define NSLOT 3
+/* pipeline slots per context: flush t uses slot t % NSLOT, so NSLOT divides
+ * 2^32 and the mapping stays consistent when tickets wrap */
+#define NSLOT 4
 #define DEFAULT_SLOT_BYTES (64u << 20)
 #define DEFER_MAX_FRAME 65536u /* ip_off + 65535-byte datagram */
 
@@ -116,6 +118,17 @@ int tasx_raw_cksum_batch_dev(const void *base, const uint64_t *off,
   if (r != 0)
     return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
   return 0;
+}
+
+/* RX: a uniform received length beyond the frame's room or stride slot is not
+ * trusted for reads (the kernels cap per-frame lengths the same way) */
+static uint32_t rx_cap_flen0(uint32_t flen0, uint32_t room, uint64_t stride, const uint64_t *off)
+{
+  if (room && flen0 > room)
+    return room;
+  if (!room && !off && stride && flen0 > stride)
+    return stride < 0xffffffffull ? (uint32_t) stride : flen0;
+  return flen0;
 }
 
 /* a room must hold the headers a row always reads and may not reach into the
@@ -243,6 +256,7 @@ int tasx_tcp4_verify_batch_dev_room(const void *base, const uint64_t *off,
     return set_err(-EINVAL, "tcp4 verify: NULL base/flags");
   if ((r = check_room(room, stride, off, ip_off, l4_off, "tcp4 verify")) != 0)
     return r;
+  flen0 = rx_cap_flen0(flen0, room, stride, off);
   memset(&p, 0, sizeof(p));
   p.base = (uint8_t *) base;
   p.off = off;
@@ -309,6 +323,7 @@ int tasx_rx_batch_dev(const void *base, const uint64_t *off, uint64_t stride,
     return set_err(-EINVAL, "rx batch: NULL base/flags");
   if ((r = check_room(room, stride, off, ip_off, l4_off, "rx batch")) != 0)
     return r;
+  flen0 = rx_cap_flen0(flen0, room, stride, off);
   if (!flowht || !flowst || !fid_out)
     return set_err(-EINVAL, "rx batch: NULL flowht/flowst/fid_out");
   if (ht_entries == 0 || fs_num == 0)
@@ -404,6 +419,7 @@ struct tasx_ctx {
   uint8_t *d_buf[NSLOT];
   uint64_t *d_off[NSLOT];
   uint16_t *d_out[NSLOT];
+  uint32_t *d_len[NSLOT]; /* per-packet lengths / hints of a host batch chunk */
   uint8_t *h_stage[NSLOT];
   uint64_t *h_off[NSLOT];
   uint16_t *h_out[NSLOT];
@@ -487,6 +503,8 @@ static void ctx_release(struct tasx_ctx *c)
       hipFree(c->d_off[s]);
     if (c->d_out[s])
       hipFree(c->d_out[s]);
+    if (c->d_len[s])
+      hipFree(c->d_len[s]);
     if (c->h_stage[s])
       hipHostFree(c->h_stage[s]);
     if (c->h_off[s])
@@ -541,6 +559,7 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
         (e = hipMalloc((void **) &c->d_buf[s], c->slot_bytes)) != hipSuccess ||
         (e = hipMalloc((void **) &c->d_off[s], (size_t) c->slot_frames * 8)) != hipSuccess ||
         (e = hipMalloc((void **) &c->d_out[s], (size_t) c->slot_frames * 4)) != hipSuccess ||
+        (e = hipMalloc((void **) &c->d_len[s], (size_t) c->slot_frames * 4)) != hipSuccess ||
         (e = hipHostMalloc((void **) &c->h_stage[s], c->slot_bytes, 0)) != hipSuccess ||
         (e = hipHostMalloc((void **) &c->h_off[s], (size_t) c->slot_frames * 8, 0)) != hipSuccess ||
         (e = hipHostMalloc((void **) &c->h_out[s], (size_t) c->slot_frames * 4, 0)) != hipSuccess ||
@@ -739,6 +758,273 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
 }
 
 /* ---------------------------------------------------------------------- */
+/* end-to-end host batches over scattered packets: (base, off[], len[]) -> u16
+ * (TAS's frames are mbufs scattered over a per-core
+ * mempool, tas/fast/network.c:320-330).
+ *   staged: the CPU gathers only the bytes summed into the slot's pinned
+ *     staging (16-byte aligned records), one hipMemcpyAsync H2D of the records
+ *     and their descriptors, the kernel from HBM, one D2H of the results;
+ *     while the GPU works on chunk k the CPU gathers chunk k + 1.
+ *   zero-copy (TASX_F_ZEROCOPY): the packets stay where they are, in pinned or
+ *     registered memory; the kernel reads them over PCIe (only the chunks
+ *     holding summed bytes) at base's device address + off[i], descriptors and
+ *     results through the slot's mapped pinned buffers. */
+
+static uint32_t staged_l4(uint32_t tl);
+static size_t staged_rec(uint32_t tl);
+
+static uint8_t *host_pkt(const void *base, const uint64_t *off, uint32_t i)
+{
+  return (uint8_t *) (base ? (uintptr_t) base + off[i] : (uintptr_t) off[i]);
+}
+
+/* the device's address of pinned / registered host memory at base */
+static int zc_base(const void *base, uint8_t **dev, const char *what)
+{
+  void *d = NULL;
+  if (!base)
+    return set_err(-EINVAL, "%s: zero-copy needs a base in pinned or registered memory", what);
+  if (hipHostGetDevicePointer(&d, (void *) base, 0) != hipSuccess) {
+    (void) hipGetLastError();
+    return set_err(-EINVAL, "%s: base %p is not pinned or registered memory", what, base);
+  }
+  *dev = (uint8_t *) d;
+  return 0;
+}
+
+struct host_job {
+  uint32_t first, cnt;
+};
+
+/* results of chunk j in slot s: to out (and into the frames, TCP4 in place) */
+static void finish_tcp4_offs(struct tasx_ctx *c, int s, const struct host_job *j, void *base,
+    const uint64_t *off, uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags)
+{
+  const uint16_t *r = c->h_out[s];
+  if (out)
+    memcpy(out + 2 * (size_t) j->first, r, (size_t) j->cnt * 4);
+  if ((flags & TASX_F_INPLACE) && !(flags & TASX_F_ZEROCOPY)) { /* zero-copy kernels store in place */
+    for (uint32_t k = 0; k < j->cnt; k++) {
+      uint8_t *f = host_pkt(base, off, j->first + k);
+      memcpy(f + ip_off + 10, &r[2 * k], 2);
+      memcpy(f + l4_off + 16, &r[2 * k + 1], 2);
+    }
+  }
+}
+
+int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t *off,
+    const uint32_t *flen, uint32_t n, uint32_t ip_off, uint32_t l4_off, uint16_t *out,
+    uint32_t flags)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  struct host_job jobs[NSLOT];
+  const int zc = (flags & TASX_F_ZEROCOPY) != 0;
+  uint8_t *dbase = NULL;
+  uint32_t first = 0, k = 0;
+  int rc;
+
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (n == 0)
+    return 0;
+  if (!off || (!out && !(flags & TASX_F_INPLACE)) || ((uintptr_t) out & 3u))
+    return set_err(-EINVAL, "tcp4 host offs batch: NULL off/out, or out not 4-byte aligned");
+  if (flags & ~(TASX_F_INPLACE | TASX_F_ZEROCOPY))
+    return set_err(-EINVAL, "tcp4 host offs batch: unknown flags 0x%x", flags);
+  if (l4_off < ip_off + 20u || l4_off > 0xffffu)
+    return set_err(-EINVAL, "tcp4 host offs batch: need ip_off + 20 <= l4_off <= 65535");
+  HIPCHK(hipSetDevice(c->device));
+  if (zc && (rc = zc_base(base, &dbase, "tcp4 host offs batch")) != 0)
+    return rc;
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
+  while (first < n) {
+    const int s = (int) (k % NSLOT);
+    struct flush_slot *f = &c->fl[s];
+    tasx_tcp4_params p;
+    uint32_t cnt = 0;
+    if (k >= NSLOT) {
+      HIPCHK(hipStreamSynchronize(c->st[s]));
+      finish_tcp4_offs(c, s, &jobs[s], base, off, ip_off, l4_off, out, flags);
+    }
+    memset(&p, 0, sizeof(p));
+    p.l4_off = l4_off;
+    if (zc) {
+      /* descriptors into the slot's mapped pinned memory; the kernel reads
+       * the frames where they are and writes the results to h_out */
+      cnt = n - first < c->slot_frames ? n - first : c->slot_frames;
+      memcpy(c->h_off[s], off + first, (size_t) cnt * 8);
+      if (flen)
+        memcpy(f->h_flen, flen + first, (size_t) cnt * 4);
+      p.base = dbase;
+      p.off = f->d_off;
+      p.flen = flen ? f->d_flen : NULL;
+      p.out = f->d_out;
+      p.ip_off = ip_off;
+      p.flags = flags & TASX_F_INPLACE;
+    } else {
+      /* TAS-layout records as the staged flush builds them: 14 unread lead
+       * bytes, the 20-byte IPv4 header at 14 mod 16, the L4 segment after it
+       * (the sums are relative to the header / segment start) */
+      size_t pos = 0;
+      uint32_t rec0 = 0, tl0 = 0, uniform = 1;
+      while (first + cnt < n && cnt < c->slot_frames) {
+        const uint8_t *fr = host_pkt(base, off, first + cnt);
+        const uint8_t *ip = fr + ip_off;
+        const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+        const size_t rec = staged_rec(tl);
+        if (pos + rec > c->slot_bytes)
+          break;
+        memcpy(c->h_stage[s] + pos + TASX_TAS_IP_OFF, ip, 20);
+        memcpy(c->h_stage[s] + pos + TASX_TAS_IP_OFF + 20, fr + l4_off, staged_l4(tl));
+        c->h_off[s][cnt] = pos;
+        f->h_flen[cnt] = TASX_TAS_IP_OFF + (tl < 20 ? 20 : tl);
+        if (cnt == 0) {
+          rec0 = (uint32_t) rec;
+          tl0 = tl;
+        } else if (rec != rec0 || tl != tl0) {
+          uniform = 0;
+        }
+        pos += rec;
+        cnt++;
+      }
+      if (cnt == 0)
+        return set_err(-EINVAL, "tcp4 host offs batch: frame %u does not fit a %zu-byte slot", first,
+            c->slot_bytes);
+      HIPCHK(hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]));
+      p.base = c->d_buf[s];
+      if (uniform && tl0 >= 20) {
+        /* one record size: stride mode with a uniform hint (the headline and
+         * TSO kernels) */
+        p.stride = rec0;
+        p.flen0 = f->h_flen[0];
+      } else {
+        HIPCHK(hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
+        HIPCHK(hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]));
+        p.off = c->d_off[s];
+        p.flen = c->d_len[s];
+      }
+      p.out = c->d_out[s];
+      p.ip_off = TASX_TAS_IP_OFF;
+      p.l4_off = TASX_TAS_L4_OFF;
+    }
+    p.n = cnt;
+    if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
+      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
+    if (!zc)
+      HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4, hipMemcpyDeviceToHost, c->st[s]));
+    jobs[s].first = first;
+    jobs[s].cnt = cnt;
+    first += cnt;
+    k++;
+  }
+  for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
+    const int s = (int) (d % NSLOT);
+    HIPCHK(hipStreamSynchronize(c->st[s]));
+    finish_tcp4_offs(c, s, &jobs[s], base, off, ip_off, l4_off, out, flags);
+  }
+  return 0;
+}
+
+int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base, const uint64_t *off,
+    const uint32_t *len, uint32_t len0, uint32_t n, uint16_t *out, uint32_t flags)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  struct host_job jobs[NSLOT];
+  const int zc = (flags & TASX_F_ZEROCOPY) != 0;
+  uint8_t *dbase = NULL;
+  uint32_t first = 0, k = 0;
+  int rc;
+
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (n == 0)
+    return 0;
+  if (!off || !out)
+    return set_err(-EINVAL, "raw host offs batch: NULL off/out");
+  if (flags & ~TASX_F_ZEROCOPY)
+    return set_err(-EINVAL, "raw host offs batch: unknown flags 0x%x", flags);
+  if (!len && len0 > TASX_RAW_MAX_LEN)
+    return set_err(-EINVAL, "raw host offs batch: len0 %u > %u", len0, TASX_RAW_MAX_LEN);
+  for (uint32_t i = 0; len && i < n; i++)
+    if (len[i] > TASX_RAW_MAX_LEN)
+      return set_err(-EINVAL, "raw host offs batch: len[%u] = %u > %u", i, len[i], TASX_RAW_MAX_LEN);
+  HIPCHK(hipSetDevice(c->device));
+  if (zc && (rc = zc_base(base, &dbase, "raw host offs batch")) != 0)
+    return rc;
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
+  while (first < n) {
+    const int s = (int) (k % NSLOT);
+    struct flush_slot *f = &c->fl[s];
+    tasx_raw_params p;
+    uint32_t cnt = 0;
+    if (k >= NSLOT) {
+      HIPCHK(hipStreamSynchronize(c->st[s]));
+      memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
+    }
+    memset(&p, 0, sizeof(p));
+    if (zc) {
+      cnt = n - first < c->slot_frames ? n - first : c->slot_frames;
+      memcpy(c->h_off[s], off + first, (size_t) cnt * 8);
+      if (len)
+        memcpy(f->h_flen, len + first, (size_t) cnt * 4);
+      p.base = dbase;
+      p.off = f->d_off;
+      p.len = len ? f->d_flen : NULL;
+      p.len0 = len0;
+      p.out = f->d_out;
+    } else {
+      /* only the summed bytes, each packet at a 16-byte aligned record (the
+       * sum of a buffer does not depend on its address) */
+      size_t pos = 0;
+      while (first + cnt < n && cnt < c->slot_frames) {
+        const uint32_t l = len ? len[first + cnt] : len0;
+        const size_t rec = ((size_t) l + 15) & ~(size_t) 15;
+        if (pos + rec > c->slot_bytes)
+          break;
+        memcpy(c->h_stage[s] + pos, host_pkt(base, off, first + cnt), l);
+        c->h_off[s][cnt] = pos;
+        f->h_flen[cnt] = l;
+        pos += rec;
+        cnt++;
+      }
+      if (cnt == 0)
+        return set_err(-EINVAL, "raw host offs batch: packet %u does not fit a %zu-byte slot", first,
+            c->slot_bytes);
+      if (pos)
+        HIPCHK(hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]));
+      p.base = c->d_buf[s];
+      if (len) {
+        HIPCHK(hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
+        HIPCHK(hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]));
+        p.off = c->d_off[s];
+        p.len = c->d_len[s];
+      } else { /* uniform length: stride mode over the records */
+        p.stride = len0 ? ((uint64_t) len0 + 15) & ~(uint64_t) 15 : 16;
+        p.len0 = len0;
+      }
+      p.out = c->d_out[s];
+    }
+    p.n = cnt;
+    if (tasx_launch_raw(&p, g_variant, c->st[s]) != 0)
+      return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
+    if (!zc)
+      HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 2, hipMemcpyDeviceToHost, c->st[s]));
+    jobs[s].first = first;
+    jobs[s].cnt = cnt;
+    first += cnt;
+    k++;
+  }
+  for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
+    const int s = (int) (d % NSLOT);
+    HIPCHK(hipStreamSynchronize(c->st[s]));
+    memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
 /* deferred per-frame surface */
 
 int tasx_defer_tcp4(unsigned ctx_id, void *frame, uint16_t ip_off, uint16_t l4_off)
@@ -824,6 +1110,24 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
     *staged_flushes = c->n_staged_flushes;
   return 0;
 }
+
+#ifdef TASX_AB
+/* A/B test hook: restart the context's tickets at `start` (nothing in flight),
+ * so a test can run flushes across the 2^32 wrap.  Every completion word holds
+ * `start`, which no upcoming ticket equals (as 0 does after tasx_ctx_init). */
+int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (c->npend || c->fd || !ticket_le(c->next_ticket, c->done_ticket))
+    return set_err(-EBUSY, "ctx %u has frames pending, flushes in flight or a feeder", ctx_id);
+  for (int s = 0; s < NSLOT; s++)
+    __atomic_store_n(c->h_done + DONE_STRIDE * (uint32_t) s, start, __ATOMIC_RELEASE);
+  c->next_ticket = c->done_ticket = c->local_last = c->fd_done = start;
+  return 0;
+}
+#endif
 
 /* Complete every flush up to `upto` whose completion word has arrived, oldest
  * first (the staged path copies its results into the frames); returns 1 when
@@ -1169,9 +1473,16 @@ static int feeder_ok(const struct tasx_ctx *c, uint32_t n)
  * context's feeder tickets complete, the local path takes them) */
 static int feeder_submit(struct tasx_ctx *c)
 {
+  int rc;
   while (c->npend > 0) {
     if (!feeder_ok(c, c->npend))
       return flush_wait(c, c->next_ticket); /* in ticket order before the local flushes */
+    /* A flush this context launched itself (a batch outside the region) must
+     * complete first: the feeder's completion of a later ticket moves
+     * done_ticket past it (flush_reap), which would skip copying its staged
+     * results into its frames and free its slot while the GPU still uses it. */
+    if (!ticket_le(c->local_last, c->done_ticket) && (rc = flush_wait(c, c->local_last)) != 0)
+      return rc;
     const uint32_t cnt = c->npend < FB_MAX ? c->npend : FB_MAX;
     uint32_t k = 0;
     while (c->fq_head - __atomic_load_n(&c->fq_tail, __ATOMIC_ACQUIRE) >= FQ) {

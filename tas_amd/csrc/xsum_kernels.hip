@@ -389,19 +389,26 @@ __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
   }
 }
 
-// Receive-side read bound of a frame, in bytes from its start: the received
-// frame length (the hint: the mbuf data_len), else the batch's room, else the
-// stride slot; ~0 when nothing bounds it (offsets without hints or room: the
-// buffer must then hold ip_off + total_length bytes, as DPDK assumes).
-__device__ __forceinline__ uint32_t rx_bound(const tasx_tcp4_params &p, uint32_t hint)
+// The bytes a frame owns from its start: the batch's room, else its stride
+// slot (stride mode); ~0 when nothing bounds it.
+__device__ __forceinline__ uint32_t slot_bound(const tasx_tcp4_params &p)
 {
-  if (hint)
-    return hint;
   if (p.room)
     return p.room;
   if (!p.off && p.stride)
     return p.stride < 0xffffffffull ? (uint32_t) p.stride : 0xffffffffu;
   return 0xffffffffu;
+}
+
+// Receive-side read bound of a frame, in bytes from its start: the received
+// frame length (the hint: the mbuf data_len) capped at the frame's room or
+// stride slot (a hint beyond them is not trusted for reads), else the room /
+// slot; ~0 when nothing bounds it (offsets without hints or room: the buffer
+// must then hold ip_off + total_length bytes, as DPDK assumes).
+__device__ __forceinline__ uint32_t rx_bound(const tasx_tcp4_params &p, uint32_t hint)
+{
+  const uint32_t b = slot_bound(p);
+  return hint ? min(hint, b) : b;
 }
 
 // TCP4, any frame layout: header words and the checksum-field bytes by byte
@@ -1129,7 +1136,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // it against total_length afterwards, as kHint does for a uniform hint
     const uint32_t h = ldg(p.flen, i);
     const uint32_t hl = h > p.ip_off ? h - p.ip_off : 0u;
-    in_range = row_ok && hl >= 38u && hl <= 1522u && (!p.room || h <= p.room); // reads stay inside the room
+    in_range = row_ok && hl >= 38u && hl <= 1522u && h <= slot_bound(p); // reads stay inside the room / slot
     hend = in_range ? hl : (row_ok ? 20u : 1u);
     const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
 #pragma unroll
@@ -1144,7 +1151,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
   } else if constexpr (MODE == kHintArrS) {
     const uint32_t hl = hs > p.ip_off ? hs - p.ip_off : 0u;
-    in_range = row_ok && hl >= 38u && hl <= 1522u && (!p.room || hs <= p.room);
+    in_range = row_ok && hl >= 38u && hl <= 1522u && hs <= slot_bound(p);
     hend = in_range ? hl : (row_ok ? 20u : 1u);
     const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
     v[0] = ld16nt_off(fb, min(lo, lastoff));

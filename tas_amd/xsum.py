@@ -33,6 +33,7 @@ _lib = None
 _loaded: dict = {}
 
 TASX_F_INPLACE = 0x1
+TASX_F_ZEROCOPY = 0x2  # host batches over offsets: the GPU reads the packets in place
 TXSEG_SCRATCH = 0x80000000  # tasx_tx_seg.room flag: bytes past the frame are scratch
 TAS_IP_OFF = 14
 TAS_L4_OFF = 34
@@ -68,6 +69,8 @@ SIGNATURES = {
     "tasx_ctx_destroy": (_c_int, [_uns]),
     "tasx_tcp4_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
     "tasx_raw_cksum_batch_host": (_c_int, [_uns, _vp, _c_u64, _c_u32, _c_u32, _vp]),
+    "tasx_tcp4_cksum_batch_host_offs": (_c_int, [_uns, _vp, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _c_u32]),
+    "tasx_raw_cksum_batch_host_offs": (_c_int, [_uns, _vp, _vp, _vp, _c_u32, _c_u32, _vp, _c_u32]),
     "tasx_set_thread_ctx": (_c_int, [_uns]),
     "tasx_thread_ctx": (_c_int, []),
     "tasx_tcp_checksums": (_c_int, [_uns, _vp, _vp, _c_u32, _c_u32, _c_u16]),
@@ -108,6 +111,7 @@ AB_SIGNATURES = {
                                       _vp]),
     "tasx_ab_tcp4_pattern": (_c_int, [_vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ab_stream_copy": (_c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "tasx_ab_ctx_set_tickets": (_c_int, [_uns, _c_u32]),
 }
 
 
@@ -478,6 +482,55 @@ def raw_cksum_batch_host(ctx_id: int, base_addr: int, stride: int, len0: int, n:
                          out_addr: int) -> None:
     _check(lib().tasx_raw_cksum_batch_host(ctx_id, base_addr, stride, len0, n, out_addr),
            "tasx_raw_cksum_batch_host")
+
+
+def _np_ptr(a, dtype):
+    """Host address of a contiguous numpy array of `dtype` (None passes through)."""
+    import numpy as np
+    if a is None:
+        return None
+    assert isinstance(a, np.ndarray) and a.dtype == dtype and a.flags["C_CONTIGUOUS"], (a.dtype, dtype)
+    return a.ctypes.data
+
+
+def tcp4_cksum_batch_host_offs(ctx_id: int, base_addr: int | None, offsets, n: int, out=None, *,
+                               frame_len=None, ip_off: int = TAS_IP_OFF, l4_off: int = TAS_L4_OFF,
+                               inplace: bool = False, zerocopy: bool = False):
+    """tcp_checksums() of n frames in host memory at base_addr + offsets[i]
+    (numpy uint64; base_addr None: offsets are addresses), end to end
+    (tasx_tcp4_cksum_batch_host_offs).  out: numpy uint16 array of 2n, or None
+    to allocate (skipped with inplace and out=False).  frame_len: numpy uint32
+    frame lengths (the mbuf data_len), optional.  zerocopy: the GPU reads the
+    frames in place (base_addr pinned or registered)."""
+    import numpy as np
+    if out is None:
+        out = np.empty(2 * n, dtype=np.uint16)
+    elif out is False:
+        out = None
+    assert offsets.size >= n and (frame_len is None or frame_len.size >= n)
+    assert out is None or out.size >= 2 * n
+    flags = (TASX_F_INPLACE if inplace else 0) | (TASX_F_ZEROCOPY if zerocopy else 0)
+    _check(lib().tasx_tcp4_cksum_batch_host_offs(ctx_id, base_addr, _np_ptr(offsets, np.uint64),
+                                                 _np_ptr(frame_len, np.uint32), n, ip_off, l4_off,
+                                                 _np_ptr(out, np.uint16), flags),
+           "tasx_tcp4_cksum_batch_host_offs")
+    return out
+
+
+def raw_cksum_batch_host_offs(ctx_id: int, base_addr: int | None, offsets, n: int, *, lengths=None,
+                              len0: int = 0, out=None, zerocopy: bool = False):
+    """rte_raw_cksum of n packets in host memory at base_addr + offsets[i]
+    (lengths[i], numpy uint32, or len0 for all), end to end
+    (tasx_raw_cksum_batch_host_offs).  Returns numpy uint16."""
+    import numpy as np
+    if out is None:
+        out = np.empty(n, dtype=np.uint16)
+    assert offsets.size >= n and out.size >= n and (lengths is None or lengths.size >= n)
+    _check(lib().tasx_raw_cksum_batch_host_offs(ctx_id, base_addr, _np_ptr(offsets, np.uint64),
+                                                _np_ptr(lengths, np.uint32), len0, n, _np_ptr(out, np.uint16),
+                                                TASX_F_ZEROCOPY if zerocopy else 0),
+           "tasx_raw_cksum_batch_host_offs")
+    return out
 
 
 def set_kernel_variant(variant: int = 0) -> None:

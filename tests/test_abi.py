@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 4
+    assert L.tasx_abi_version() == 5
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -91,6 +91,10 @@ def test_abi_version_and_errors_without_gpu(L):
     assert L.tasx_flush(3) == -errno.EINVAL
     assert L.tasx_pending(99) == -errno.EINVAL
     assert L.tasx_ctx_destroy(0) == -errno.EINVAL
+    # host batches over offsets: the context is checked first, n == 0 is a no-op
+    assert L.tasx_tcp4_cksum_batch_host_offs(5, None, None, None, 4, 14, 34, None, 0) == -errno.EINVAL
+    assert L.tasx_raw_cksum_batch_host_offs(5, None, None, None, 0, 4, None, 0) == -errno.EINVAL
+    assert b"not initialised" in L.tasx_last_error()
 
 
 def test_python_wrapper_raises(L):

@@ -96,10 +96,14 @@ def test_bench_rx_mix(oracle):
     assert np.all(got == 3)
 
 
-def test_bench_config3_mixed_mtu(oracle):
+@pytest.mark.parametrize("ws,rank", [(1, 0), (4, 3)])
+def test_bench_config3_mixed_mtu(oracle, ws, rank):
     """Config 3: 1,048,576 RAW packets, {64, 576, 1500, 9000} B in random order,
-    per-packet offsets and lengths (tasx_raw_cksum_batch_dev)."""
-    wl = bench.mixed_workload(0)
+    per-packet offsets and lengths (tasx_raw_cksum_batch_dev); and rank 3's
+    byte-balanced shard of it at N = 4."""
+    wl = bench.mixed_workload(ws, rank)
+    if ws == 1:
+        assert wl.n == 1 << 20
     wl.loop()(0, 1)
     assert xsum.last_kernel() == "raw_wave_kernel"
     offs = host(wl.off).astype(np.uint64)

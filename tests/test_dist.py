@@ -142,3 +142,55 @@ def test_bench_two_ranks_on_the_gpu_rehearsal():
     assert line["n_gpus"] == 2 and len(line["per_rank_value"]) == 2 and line["ranks"]["rehearse"] is True
     assert line["kernel"] == "tcp4_tas14_kernel<hint>" and line["value"] > 0
     assert line["rx_verify"]["all_frames_verified"] is True
+    # ranks sharing the GPU claim no pattern-ceiling or N x HBM fraction
+    assert line["frac_of_n_hbm"] is None and line["roofline"]["pattern_ceiling"] is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["shard8m", "mixed"])
+def test_bench_four_ranks_strong_scaling_rehearsal(workload):
+    """The strong-scaling configs at N = 4 on the one-GPU box (`--rehearse`:
+    four ranks share the GPU over gloo): the shards' packets and bytes add up
+    to the config, contiguously; the mixed batch's shards are byte-balanced
+    within one 9,000 B packet; `value` is all ranks' bytes over the slowest
+    rank's time; and the rehearsal line claims no fraction above 1."""
+    import json
+    import bench
+    ws = 4
+    r = _bench("--gpus", str(ws), "--rehearse", "--workload", workload, "--steps", "5", "--warmup", "2",
+               "--no-cpu-baseline", "--no-pmc", timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == ws and line["ranks"]["rehearse"] is True and line["scaling"] == "strong"
+    sh = line["shards"]
+    if workload == "shard8m":
+        total_n = bench.SHARD8M_N
+        alg = [p * (bench.RAW_LEN + 2) for p in sh["packets"]]
+        lens = None
+    else:
+        total_n = bench.MIXED_N
+        lens = pktgen.mixed_lengths(total_n, seed=pktgen.SEED).astype(np.int64)
+        ranges = shard.shard_ranges(lens, ws)
+        alg = [int(lens[a:b].sum()) + 2 * (b - a) for a, b in ranges]
+        ideal = lens.sum() / ws
+        assert max(abs(int(lens[a:b].sum()) - ideal) for a, b in ranges) <= 9000
+    assert sum(sh["packets"]) == total_n
+    assert sh["first_packet"] == [int(v) for v in np.cumsum([0] + sh["packets"][:-1])]
+    assert sh["bytes_per_step"] == alg
+    # value: every rank's bytes over the slowest rank's K steps
+    steps = line["steps"]
+    exp = sum(alg) * steps / max(sh["seconds"]) / float(1 << 30)
+    assert abs(line["value"] - exp) <= 0.01 * exp + 0.02
+
+    def fracs(o):
+        if isinstance(o, dict):
+            for k, v in o.items():
+                if "frac" in k and isinstance(v, (int, float)):
+                    yield k, v
+                yield from fracs(v)
+        elif isinstance(o, list):
+            for v in o:
+                yield from fracs(v)
+    assert line["frac_of_n_hbm"] is None
+    assert all(v <= 1 for _, v in fracs(line)), list(fracs(line))
+
