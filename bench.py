@@ -1413,7 +1413,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         del wl.bufs[1:], wl.outs[1:]
         torch.cuda.empty_cache()
         tw = TxSegWorkload(rot, pktgen.SEED + 2000 + rank)
-        txseg = leg(tw.loop(), tw.bytes_per_step, args, ws, TxSegWorkload.desc, "tx_segment_tas_kernel")
+        txseg = leg(tw.loop(), tw.bytes_per_step, args, ws, TxSegWorkload.desc, "tx_segment_lds_kernel")
         txseg["algorithmic_bytes_per_segment"] = tw.bytes_per_seg
         txseg["block_floor"] = dict(tw.block_floor)
         # bytes each way of the 128-byte block floor (the kernel's reads and writes)

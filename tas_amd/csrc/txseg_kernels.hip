@@ -854,6 +854,260 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 }
 
 // ---------------------------------------------------------------------------
+// tx_segment_lds_kernel (round 3, the product for TAS's layout): the same
+// segment build, one 16-lane row per segment, with the payload read by
+// ALIGNED, L2-allocating 16-byte loads and realigned through a per-row LDS
+// slice instead of one unaligned non-temporal window load per frame chunk.
+//   For the frame's (at most 96) chunks the row loads the aligned source chunks that
+//   cover the payload windows: piece A (before the circular buffer
+//   wraps) from its 128-byte line on, so that lanes own whole lines, then piece
+//   B (after the wrap).  Lane gl, slot u loads virtual chunk gl + 16u (7 slots:
+//   112 chunks, enough for 96 frame chunks at any shift) and writes it to slot
+//   1 + gl + 16u of the slice.  Each lane then reads its frame chunk's 16-byte
+//   window back at its byte offset as five dwords and funnel-shifts them
+//   (v_alignbyte_b32); the chunk that straddles the wrap splices a piece-B
+//   window in.  Header chunks 0..3 (read from the frame) and chunk 4 (header
+//   bytes 64-65 + payload [0, 14)) go out in round 0's store instructions with
+//   stale checksum fields, every store non-temporal and covering whole 256-byte
+//   blocks (lanes own frame chunks by address); the two 16-bit fields are
+//   stored at the end by the lane holding chunk 1, after the row total has
+//   reached it by DPP row rotations.
+//   Why: an unaligned window shares its first and last 128-byte lines with the
+//   neighbouring windows, and with non-temporal loads those lines were fetched
+//   again; aligned temporal loads let L2 merge them.  On the bench's pattern
+//   (tools/txseg_lds_probe.hip, profiles/r03/r03c-r03d): 43.3 us for the
+//   unaligned non-temporal windows, 39.4 us for the same windows temporal,
+//   34.2-34.9 us for this scheme.
+//   Aligned loads never leave the pages of the bytes they hold, and each load
+//   address is clamped to the aligned chunks that touch the shm region, so no
+//   load faults; bytes outside what a window needs are masked away.
+//   Rows that are not TAS data segments (hdrs_len != 66, a frame off 16-byte
+//   alignment, total_length != 52 + payload, a rejected descriptor) go to the
+//   general body (txseg_row), as before.
+// SLOTS load slots per lane: 6 (96 aligned chunks: piece A from its 16-byte
+// chunk on, 25.3 KiB of LDS per block, 6 blocks per CU) or 7 (112: piece A from
+// its 128-byte line on, so lanes own whole lines; 29.4 KiB, 5 blocks per CU).
+// A window's bytes [o, o + 16) lie in the loaded chunks; its fifth dword, read
+// past them, lies in the same aligned chunk as byte o + 15.
+constexpr int kLdsLead = 64; // lead bytes: chunk 0's window (payload index -66) stays in the slice
+template <int SLOTS>
+constexpr int lds_slice() { return kLdsLead + 16 * 16 * SLOTS + 32; } // lead, the slots, tail slack
+
+// 16 bytes at a dword-aligned LDS address shifted by r bytes: five dwords and a funnel shift
+__device__ __forceinline__ u32x4 lds_window_at(const uint8_t *wp, uint32_t r)
+{
+  const uint32_t *w = (const uint32_t *) wp;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+               __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
+}
+
+// 16 bytes at LDS byte offset o of the slice: five dwords and a funnel shift
+__device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
+{
+  const uint32_t *w = (const uint32_t *) (sl + (o & ~3u));
+  const uint32_t r = o & 3u;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
+               __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
+}
+
+// OPT (A/B, timing only: results wrong): 1 = no general-body fallback compiled
+// in, 2 = wraps ignored (piece A only)
+template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
+{
+  constexpr int kLdsSlots = SLOTS, kLdsSlice = lds_slice<SLOTS>();
+  constexpr uintptr_t kAlignA = SLOTS >= 7 ? 127u : 15u;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[(kBlock / 16) * kLdsSlice];
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return; // whole 16-lane group leaves together
+  uint8_t *const sl = lds + (threadIdx.x / 16) * kLdsSlice;
+  const u32x4 d0 = ld16((const u32x4 *) p.segs, 2 * i), d1 = ld16((const u32x4 *) p.segs, 2 * i + 1);
+  const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
+  const uint64_t tx_base = d0.z | ((uint64_t) d0.w << 32);
+  const uint32_t tx_len = d1.x, pos = d1.y, pay_ = d1.z & 0xffffu, hl_ = d1.z >> 16;
+  const bool ok = (pay_ == 0 || pos < tx_len) && pay_ <= tx_len && tx_base <= p.shm_len &&
+                  tx_len <= p.shm_len - tx_base && hl_ >= p.l4_off + 20;
+  uint8_t *const f = p.frames + frame_off;
+  // one round of 96 frame chunks: frames up to 1536 bytes (TAS's data
+  // segments are at most 66 + TCP_MSS = 1514, fast_flows.c:37, :887-888);
+  // larger ones go to the general body
+  bool fast = ok && hl_ == 66u && ((uintptr_t) f & 15u) == 0 && pay_ <= 1536u - 66u;
+  if (fast) {
+    const int pay = (int) pay_, fend = 66 + pay;
+    const int K = (fend + 15) >> 4;
+    // the room: the last chunk written whole (its bytes past the frame with
+    // their own values), or -- scratch -- the frame's last 128-byte block
+    // written whole with zeros past the frame (no read, no partial line; within
+    // the round's 96 chunks)
+    const uint32_t room = d1.w & ~TASX_TXSEG_SCRATCH;
+    const bool scratch = (d1.w & TASX_TXSEG_SCRATCH) != 0u && room >= 16u * (uint32_t) K;
+    const bool whole = room >= 16u * (uint32_t) K;
+    int kend = K; // chunks [K, kend): scratch zeros up to the block's end
+    if (scratch) {
+      const uint64_t be = (frame_off + (uint64_t) fend + 127u) & ~127ull;
+      kend = max(K, min(min((int) ((be - frame_off + 15u) >> 4), (int) (room >> 4)), 96));
+    }
+    const int aoff = (int) (((uintptr_t) f >> 4) & 15u);
+    const int kh = (gl - aoff) & 15; // this lane's chunk in every 16-chunk group of the frame
+    // loads at 32-bit offsets from the region's first aligned chunk (an SGPR
+    // base; shm_len < 4 GiB), clamped to the aligned chunks that touch the region
+    const uintptr_t sb = (uintptr_t) p.shm;
+    const uint8_t *const sbase = (const uint8_t *) (sb & ~(uintptr_t) 15);
+    const uint32_t hi_ok = (uint32_t) (((sb + p.shm_len - 1u) & ~(uintptr_t) 15) - (sb & ~(uintptr_t) 15));
+    const int64_t s1 = (int64_t) (tx_base + pos);
+    const int wrap = (int) tx_len - (int) pos;
+    const int wrapc = (pay > 0 && wrap < pay && !(OPT & 2)) ? wrap : 0x7fffffff; // payload index where piece B starts
+    const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4)); // header chunks 0..4
+    uint32_t acc = 0;
+    u32x4 vlast = hv; // the frame's last chunk when it is partial (its lane: kh == (K - 1) & 15)
+    const int hlast = fend - 16 * (K - 1); // bytes of the frame in its last chunk, 1..16
+    {
+      // payload windows of chunks [4, K): payload [jlo, jhi)
+      const int jlo = -2, jhi = 16 * K - 66;
+      const int aend = min(jhi, wrapc);
+      // piece A: payload [jlo, aend) at s1 + j, from its 16-byte chunk (7 slots:
+      // its 128-byte line) on
+      const uintptr_t bA = sb + (uintptr_t) (s1 + jlo);
+      const uintptr_t cA = bA & ~kAlignA;
+      const int nA = aend > jlo ? (int) ((((bA + (uintptr_t) (aend - jlo) + 15u) & ~(uintptr_t) 15) - cA) >> 4) : 0;
+      // piece B: payload [max(jlo, wrapc), jhi) at tx_base + j - wrapc
+      const int jb = max(jlo, wrapc);
+      const uintptr_t bB = sb + (uintptr_t) tx_base + (uintptr_t) (jb > wrapc ? jb - wrapc : 0);
+      const uintptr_t cB = bB & ~(uintptr_t) 15;
+      const int nB = jhi > wrapc ? (int) ((((bB + (uintptr_t) (jhi - jb) + 15u) & ~(uintptr_t) 15) - cB) >> 4) : 0;
+      // 32-bit offsets from sbase (shm_len < 4 GiB): virtual chunk v is piece
+      // A's chunk v, else piece B's chunk v - nA; past the end the last one again
+      // (an L2 hit); every offset clamped to the aligned chunks that touch the region
+      const int rA = (int) (int64_t) (cA - (uintptr_t) sbase), rB = (int) (int64_t) (cB - (uintptr_t) sbase);
+      const int nAB = max(nA + nB, 1);
+      const int dB = nB > 0 ? rB - rA - 16 * nA : 0;
+      u32x4 a[kLdsSlots];
+#pragma unroll
+      for (int u = 0; u < kLdsSlots; ++u) {
+        const int v = min(gl + 16 * u, nAB - 1);
+        const int ro = rA + 16 * v + (v >= nA ? dB : 0);
+        a[u] = ld16_off(sbase, (uint32_t) min(max(ro, 0), (int) hi_ok));
+      }
+#pragma unroll
+      for (int u = 0; u < kLdsSlots; ++u)
+        *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // LDS byte offsets: payload index 0 in piece A, piece B's first byte;
+      // window u at o0 + 256u (+ dW for a window in piece B)
+      const int oA = kLdsLead + (int) (sb + (uintptr_t) s1 - cA);
+      const int oB = kLdsLead + 16 * nA + (int) (sb + (uintptr_t) tx_base - cB);
+      const int o0 = oA + 16 * kh - 66; // >= 0: the lead covers chunk 0's window
+      const int dW = wrapc < pay ? oB - oA - wrapc : 0;
+      u32x4 w[6]; // the windows of frame chunks 16u + kh
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+        const int j0 = 16 * (16 * u + kh) - 66;
+        const int o = min(o0 + 256 * u + (j0 >= wrapc ? dW : 0), kLdsSlice - 20);
+        w[u] = lds_window(sl, (uint32_t) o);
+      }
+      // the chunk holding the wrap (a row whose payload wraps off a chunk
+      // boundary): its bytes from wrapc - j0 on are piece B's
+      const int ks = wrapc < pay ? (66 + wrapc) >> 4 : -1;
+      const bool strad = ks >= 0 && ((66 + wrapc) & 15) != 0 && kh == (ks & 15);
+      if (__builtin_amdgcn_ballot_w64(strad) != 0ull) {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int j0 = 16 * (16 * u + kh) - 66;
+          if (strad && u == (ks >> 4))
+            w[u] = splice(w[u], lds_window(sl, (uint32_t) min(max(oB + j0 - wrapc, 0), kLdsSlice - 20)), wrapc - j0, 16);
+        }
+      }
+      // slot 0: header chunks 0..3 as read, chunk 4 = header bytes 64-65 +
+      // payload [0, 14); L4 sums from chunk 2's byte 2 on (TCP starts at 34),
+      // chunk 3 without tcp.chksum (bytes 2-3).  Slot 0 (the frame's first two
+      // lines, both checksum fields) is stored L2-allocating so that the fields
+      // stored at the end merge there; the rest non-temporal.
+      if (kh < 4)
+        w[0] = hv;
+      else if (kh == 4)
+        w[0] = splice(hv, w[0], 2, 16);
+      const uint32_t mx = kh == 2 ? 0xffff0000u : (kh == 3 ? 0x0000ffffu : kh < 2 ? 0u : 0xffffffffu);
+      const uint32_t mr = kh < 2 ? 0u : 0xffffffffu;
+      if (__builtin_amdgcn_ballot_w64(K < 81) == 0ull) {
+        // every row of the wave holds at least 81 chunks: slots 0..4 are whole
+        // frame chunks, only slot 5 holds the frame's end
+        acc = sad4(u32x4{w[0].x & mx, w[0].y & mr, w[0].z & mr, w[0].w & mr}, acc);
+        *(__attribute__((address_space(1))) u32x4 *) (f + 16 * kh) = w[0];
+#pragma unroll
+        for (int u = 1; u < 5; ++u) {
+          acc = sad4(w[u], acc);
+          __builtin_nontemporal_store(w[u], (__attribute__((address_space(1))) u32x4 *) (f + 16 * (16 * u + kh)));
+        }
+        const int k = 80 + kh;
+        const bool full = k < K - 1 || (k == K - 1 && hlast == 16);
+        const uint32_t t = sad4(w[5], acc);
+        acc = full ? t : acc;
+        vlast = k == K - 1 ? w[5] : vlast;
+        if (full || (k >= K && k < kend))
+          __builtin_nontemporal_store(k < K ? w[5] : u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
+      } else {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+          const int k = 16 * u + kh;
+          const u32x4 v = w[u];
+          // whole chunks here, the partial last one after the loop
+          const bool full = k < K - 1 || (k == K - 1 && hlast == 16);
+          const uint32_t t = u == 0 ? sad4(u32x4{v.x & mx, v.y & mr, v.z & mr, v.w & mr}, acc) : sad4(v, acc);
+          acc = full ? t : acc;
+          vlast = k == K - 1 ? v : vlast;
+          // whole chunks, and scratch zeros past the frame to its block's end
+          if (full || (k >= K && k < kend)) {
+            const u32x4 sv = k < K ? v : u32x4{0u, 0u, 0u, 0u};
+            if (u == 0)
+              *(__attribute__((address_space(1))) u32x4 *) (f + 16 * k) = sv;
+            else
+              __builtin_nontemporal_store(sv, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
+          }
+        }
+      }
+    }
+    if (hlast < 16 && kh == ((K - 1) & 15)) { // the frame's partial last chunk (one lane)
+      acc += sad_below(vlast, (uint32_t) hlast);
+      uint8_t *const cp = f + 16 * (K - 1);
+      if (whole) // its bytes past the frame with their own values (scratch: zeros)
+        __builtin_nontemporal_store(splice(scratch ? u32x4{0u, 0u, 0u, 0u} : ld16((const u32x4 *) cp, 0u), vlast, 0, hlast),
+                                    (__attribute__((address_space(1))) u32x4 *) cp);
+      else
+        store_range(cp, vlast, 0, hlast, false);
+    }
+    // IPv4 and pseudo-header channels from header chunks 0..2 (tcp4_tas14_kernel's map)
+    const uint32_t c0d3 = row_ror<1>(hv.w), c2d0 = row_ror<15>(hv.x);
+    const uint32_t addrs = sadw(hv.z & 0xffff0000u, sadw(hv.w, sadw(c2d0 & 0xffffu, 0u)));
+    const uint32_t ph = sadw(hv.y & 0xff000000u, addrs);
+    const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(hv.x, sadw(hv.y, addrs)));
+    const int l1 = (int) ((threadIdx.x & 63u) & ~15u) + ((1 + aoff) & 15); // lane holding chunk 1
+    acc += row_ror<8>(acc);
+    acc += row_ror<4>(acc);
+    acc += row_ror<2>(acc);
+    acc += row_ror<1>(acc);
+    const bool ok1 = kh == 1 && bswap16(hv.x & 0xffffu) == 52u + (uint32_t) pay;
+    fast = (__builtin_amdgcn_ballot_w64(ok1) >> l1) & 1ull; // otherwise the general body redoes the segment
+    if (ok1) {
+      const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
+      const uint32_t tcpc = inv_result(
+          residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph) + bswap16(32u + (uint32_t) pay))));
+      if (p.out)
+        stg(p.out, i, ipc | (tcpc << 16));
+      *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
+      *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
+    }
+  }
+  if (!(OPT & 1) && !fast)
+    txseg_row<3, NTS>(p, i, gl);
+}
+
+// ---------------------------------------------------------------------------
 // tx_segment_wave_kernel: the TAS-layout build with ONE segment per wave.  The
 // segment's geometry is wave-uniform, so the descriptor comes in by scalar
 // loads and every branch on it is uniform.  The payload is read by ALIGNED
@@ -1116,6 +1370,23 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 27: tasx_note_kernel("tx_segment_tas_kernel<no_fields>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoFields>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 28: tasx_note_kernel("tx_segment_tas_kernel<no_sums>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxHeaderFirst | kTxDppTail | kTxNoSums>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   case 29: if (tas) { tasx_note_kernel("tx_segment_wave_kernel"); hipLaunchKernelGGL((tx_segment_wave_kernel<true>), dim3((uint32_t) ((p->n + 3u) / 4u)), block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 31: the product with 7 load slots (lanes own whole 128-byte source lines)
+  case 31: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<slots7>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 7>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 32-34: timing-only ablations of the product: no fallback / no wraps / both
+  case 32: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 33: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 34: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb,nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 3>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU
+  case 35: case 36: case 37: case 38: if (tas) {
+    constexpr uint32_t st = (kBlock / 16) * (uint32_t) lds_slice<6>(); // the kernel's static LDS
+    static const uint32_t extra[4] = {163840u / 5u - st - 64u, 163840u / 4u - st - 64u, 163840u / 3u - st - 64u,
+                                      163840u / 2u - st - 64u};
+    static const char *const names[4] = {"tx_segment_lds_kernel<5blk>", "tx_segment_lds_kernel<4blk>", "tx_segment_lds_kernel<3blk>", "tx_segment_lds_kernel<2blk>"};
+    tasx_note_kernel(names[p->dbg - 35]);
+    hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6>), grid, block, extra[p->dbg - 35], s, *p);
+    return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 30: the round-2 product (unaligned non-temporal window loads, header-first, DPP tail)
+  case 30: if (tas) { tasx_note_kernel("tx_segment_tas_kernel"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 16: tasx_note_kernel("tx_segment_tas_kernel<fields_only>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxFieldsOnly>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
   // 9..14: ablations (timing only)
   case 9: tasx_note_kernel("tx_segment_tas_kernel<abl1>"); hipLaunchKernelGGL((tx_segment_tas_kernel<6, true, 1, kTxNoScratch>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1135,8 +1406,11 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   }
 #endif
   if (tas) {
-    tasx_note_kernel("tx_segment_tas_kernel");
-    hipLaunchKernelGGL((tx_segment_tas_kernel<6, true>), grid, block, 0, s, *p);
+    // aligned L2-allocating loads realigned through LDS (34-35 us against 43 us
+    // for the round-2 form's unaligned windows on the bench's pattern;
+    // tools/txseg_lds_probe.hip)
+    tasx_note_kernel("tx_segment_lds_kernel");
+    hipLaunchKernelGGL((tx_segment_lds_kernel<true>), grid, block, 0, s, *p);
   } else {
     tasx_note_kernel("tx_segment_u_kernel");
     hipLaunchKernelGGL((tx_segment_u_kernel<6, true>), grid, block, 0, s, *p);

@@ -36,6 +36,8 @@ __device__ __forceinline__ u32x4 ld16nt_off(const uint8_t *base, uint32_t off)
 {
   return __builtin_nontemporal_load((gcu4 *) (base + off));
 }
+// the same, L2-allocating (lines that neighbouring loads share are fetched once)
+__device__ __forceinline__ u32x4 ld16_off(const uint8_t *base, uint32_t off) { return *(gcu4 *) (base + off); }
 __device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return *(gcu8 *) p; }
 __device__ __forceinline__ void st8(uint8_t *p, uint32_t v) { *(gu8 *) p = (uint8_t) v; }
 template <typename T>

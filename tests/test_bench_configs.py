@@ -155,7 +155,7 @@ def test_bench_tx_segment_leg():
     the built frames against the oracle's flow_tx_read + tcp_checksums."""
     tw = bench.TxSegWorkload(1, pktgen.SEED + 2000)
     tw.loop()(0, 1)
-    assert xsum.last_kernel() == "tx_segment_tas_kernel"
+    assert xsum.last_kernel() == "tx_segment_lds_kernel"
     assert tw.cpu_check(0.05)["parity_vs_gpu"] == "bit-exact"
 
 

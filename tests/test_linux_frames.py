@@ -167,7 +167,7 @@ def test_gpu_txseg_rebuilds_linux_frames():
     dsegs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
     out = xsum.tx_segment_batch(dshm, dfr, dsegs, len(segs), shm_len=sl)
     torch.cuda.synchronize()
-    assert xsum.last_kernel() == "tx_segment_tas_kernel"
+    assert xsum.last_kernel() == "tx_segment_lds_kernel"
     np.testing.assert_array_equal(dfr.cpu().numpy().reshape(want.shape), want)
     o = out.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(o & 0xFFFF, want[:, 24:26].copy().view(np.uint16).ravel())

@@ -70,9 +70,10 @@ def test_generator_wraps_and_flows():
 # ---------------------------------------------------------------------------
 # GPU parity
 
-# "wave": the one-segment-per-wave build (A/B variant TASX_TXSEG_DEBUG=29 of
-# libtasx_ab.so) on the same cases as the product
-IMPLS = ["product", "wave"]
+# "r2": the round-2 product, tx_segment_tas_kernel (unaligned non-temporal
+# window loads; A/B variant TASX_TXSEG_DEBUG=30 of libtasx_ab.so), on the same
+# cases as the product (tx_segment_lds_kernel)
+IMPLS = ["product", "r2"]
 
 
 def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):
@@ -80,12 +81,12 @@ def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, im
     from tas_amd import xsum
     if impl == "product":
         return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
-    os.environ["TASX_TXSEG_DEBUG"] = "29"
+    os.environ["TASX_TXSEG_DEBUG"] = "30"
     try:
         with xsum.using_library(xsum.AB_LIB_PATH):
             r = _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
             if ip_off == 14 and l4_off == 34:
-                assert xsum.last_kernel() == "tx_segment_wave_kernel", xsum.last_kernel()
+                assert xsum.last_kernel() == "tx_segment_tas_kernel", xsum.last_kernel()
             return r
     finally:
         del os.environ["TASX_TXSEG_DEBUG"]
@@ -274,7 +275,7 @@ def test_gpu_txseg_host_memory(oracle, where):
             dsegs = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
         out = xsum.tx_segment_batch(hs.dev_addr, frames, dsegs, n, shm_len=sl)
         torch.cuda.synchronize()
-        assert xsum.last_kernel() == "tx_segment_tas_kernel"
+        assert xsum.last_kernel() == "tx_segment_lds_kernel"
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
         got = dfr.cpu().numpy() if where == "shm" else pins[1].array.copy()
         np.testing.assert_array_equal(got, exp_fr)
