@@ -948,17 +948,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const bool whole = room >= 16u * (uint32_t) K;
     int kend = K; // chunks [K, kend): scratch zeros up to the block's end
     if (scratch) {
-      const uint64_t be = (frame_off + (uint64_t) fend + 127u) & ~127ull;
-      kend = max(K, min(min((int) ((be - frame_off + 15u) >> 4), (int) (room >> 4)), 96));
+      const uint32_t fo7 = (uint32_t) frame_off & 127u;
+      kend = max(K, min(min((int) ((((fo7 + (uint32_t) fend + 127u) & ~127u) - fo7 + 15u) >> 4), (int) (room >> 4)), 96));
     }
     const int aoff = (int) (((uintptr_t) f >> 4) & 15u);
     const int kh = (gl - aoff) & 15; // this lane's chunk in every 16-chunk group of the frame
-    // loads at 32-bit offsets from the region's first aligned chunk (an SGPR
-    // base; shm_len < 4 GiB), clamped to the aligned chunks that touch the region
+    // Shm positions as 32-bit offsets from the region's first aligned chunk
+    // sbase (an SGPR base; shm_len < 4 GiB, checked by the host), modulo 2^32:
+    // loads are clamped to the aligned chunks that touch the region, so an
+    // offset that wrapped below the region (payload index -2 of a buffer at its
+    // start: chunk 4's don't-care bytes) reads some chunk of the region.
     const uintptr_t sb = (uintptr_t) p.shm;
     const uint8_t *const sbase = (const uint8_t *) (sb & ~(uintptr_t) 15);
-    const uint32_t hi_ok = (uint32_t) (((sb + p.shm_len - 1u) & ~(uintptr_t) 15) - (sb & ~(uintptr_t) 15));
-    const int64_t s1 = (int64_t) (tx_base + pos);
+    const uint32_t sh0 = (uint32_t) (sb & 15u);
+    const uint32_t hi_ok = (uint32_t) ((sb + p.shm_len - 1u) & ~(uintptr_t) 15) - (uint32_t) (sb & ~(uintptr_t) 15);
+    const uint32_t t0 = sh0 + (uint32_t) tx_base, s1 = t0 + pos; // ring start, payload index 0
     const int wrap = (int) tx_len - (int) pos;
     const int wrapc = (pay > 0 && wrap < pay && !(OPT & 2)) ? wrap : 0x7fffffff; // payload index where piece B starts
     const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4)); // header chunks 0..4
@@ -971,26 +975,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       const int aend = min(jhi, wrapc);
       // piece A: payload [jlo, aend) at s1 + j, from its 16-byte chunk (7 slots:
       // its 128-byte line) on
-      const uintptr_t bA = sb + (uintptr_t) (s1 + jlo);
-      const uintptr_t cA = bA & ~kAlignA;
-      const int nA = aend > jlo ? (int) ((((bA + (uintptr_t) (aend - jlo) + 15u) & ~(uintptr_t) 15) - cA) >> 4) : 0;
-      // piece B: payload [max(jlo, wrapc), jhi) at tx_base + j - wrapc
+      const uint32_t bA = s1 + (uint32_t) jlo, cA = bA & ~(uint32_t) kAlignA;
+      const int nA = aend > jlo ? (int) ((((bA + (uint32_t) (aend - jlo) + 15u) & ~15u) - cA) >> 4) : 0;
+      // piece B: payload [max(jlo, wrapc), jhi) at the ring start + j - wrapc
       const int jb = max(jlo, wrapc);
-      const uintptr_t bB = sb + (uintptr_t) tx_base + (uintptr_t) (jb > wrapc ? jb - wrapc : 0);
-      const uintptr_t cB = bB & ~(uintptr_t) 15;
-      const int nB = jhi > wrapc ? (int) ((((bB + (uintptr_t) (jhi - jb) + 15u) & ~(uintptr_t) 15) - cB) >> 4) : 0;
-      // 32-bit offsets from sbase (shm_len < 4 GiB): virtual chunk v is piece
-      // A's chunk v, else piece B's chunk v - nA; past the end the last one again
-      // (an L2 hit); every offset clamped to the aligned chunks that touch the region
-      const int rA = (int) (int64_t) (cA - (uintptr_t) sbase), rB = (int) (int64_t) (cB - (uintptr_t) sbase);
+      const uint32_t bB = t0 + (uint32_t) (jb > wrapc ? jb - wrapc : 0), cB = bB & ~15u;
+      const int nB = jhi > wrapc ? (int) ((((bB + (uint32_t) (jhi - jb) + 15u) & ~15u) - cB) >> 4) : 0;
+      // virtual chunk v is piece A's chunk v, else piece B's chunk v - nA; past
+      // the end the last one again (an L2 hit)
       const int nAB = max(nA + nB, 1);
-      const int dB = nB > 0 ? rB - rA - 16 * nA : 0;
+      const uint32_t dB = nB > 0 ? cB - cA - 16u * (uint32_t) nA : 0u;
       u32x4 a[kLdsSlots];
 #pragma unroll
       for (int u = 0; u < kLdsSlots; ++u) {
         const int v = min(gl + 16 * u, nAB - 1);
-        const int ro = rA + 16 * v + (v >= nA ? dB : 0);
-        a[u] = ld16_off(sbase, (uint32_t) min(max(ro, 0), (int) hi_ok));
+        const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
+        a[u] = ld16_off(sbase, min(ro, hi_ok));
       }
 #pragma unroll
       for (int u = 0; u < kLdsSlots; ++u)
@@ -1000,8 +1000,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // LDS byte offsets: payload index 0 in piece A, piece B's first byte;
       // window u at o0 + 256u (+ dW for a window in piece B)
-      const int oA = kLdsLead + (int) (sb + (uintptr_t) s1 - cA);
-      const int oB = kLdsLead + 16 * nA + (int) (sb + (uintptr_t) tx_base - cB);
+      const int oA = kLdsLead + (int) (s1 - cA);
+      const int oB = kLdsLead + 16 * nA + (int) (t0 - cB);
       const int o0 = oA + 16 * kh - 66; // >= 0: the lead covers chunk 0's window
       const int dW = wrapc < pay ? oB - oA - wrapc : 0;
       u32x4 w[6]; // the windows of frame chunks 16u + kh
