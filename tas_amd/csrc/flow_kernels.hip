@@ -21,29 +21,7 @@
 
 namespace {
 
-constexpr uint32_t kPoly = 0x82f63b78u; // CRC32C (Castagnoli), reflected
-
-// slice-by-4 tables: t[k][x] = CRC of byte x followed by k zero bytes (init 0)
-struct CrcTables {
-  uint32_t t[4][256];
-};
-
-constexpr CrcTables make_crc_tables()
-{
-  CrcTables T{};
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k)
-      c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
-    T.t[0][i] = c;
-  }
-  for (int k = 1; k < 4; ++k)
-    for (uint32_t i = 0; i < 256; ++i)
-      T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xffu];
-  return T;
-}
-
-__constant__ CrcTables kCrc = make_crc_tables();
+// CRC32C slice-by-4 tables: CrcTables / make_crc_tables / kCrc (xsum_device.h)
 
 // byte-position tables for the whole 12-byte key: CRC32C from state 0 is
 // linear, so flow_hash = XOR over key byte positions p of b[p][key[p]], with
@@ -72,13 +50,9 @@ __constant__ CrcKeyTables kCrcKey = make_crc_key_tables();
 template <bool TAB>
 __device__ __forceinline__ uint32_t crc32c_word(const uint32_t (*t)[256], uint32_t crc, uint32_t w)
 {
-  crc ^= w;
   if constexpr (TAB)
-    return t[3][crc & 0xffu] ^ t[2][(crc >> 8) & 0xffu] ^ t[1][(crc >> 16) & 0xffu] ^ t[0][crc >> 24];
-#pragma unroll
-  for (int k = 0; k < 32; ++k)
-    crc = (crc >> 1) ^ (kPoly & (0u - (crc & 1u)));
-  return crc;
+    return crc32c_u32_tab(t, crc, w);
+  return crc32c_u32(crc, w);
 }
 
 __device__ __forceinline__ uint32_t ld32b(const uint8_t *p)

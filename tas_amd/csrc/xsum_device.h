@@ -363,6 +363,38 @@ __device__ __forceinline__ uint32_t tas_flow_hash(uint32_t lip, uint32_t rip, ui
   return crc32c_u32(crc32c_u32(crc32c_u32(0u, lip), rip), ports);
 }
 
+// slice-by-4 tables (built at compile time): t[k][x] = CRC of byte x followed
+// by k zero bytes (init 0); a word step is four independent table reads
+constexpr uint32_t kPoly = 0x82f63b78u; // CRC32C (Castagnoli), reflected
+struct CrcTables {
+  uint32_t t[4][256];
+};
+constexpr CrcTables make_crc_tables()
+{
+  CrcTables T{};
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k)
+      c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
+    T.t[0][i] = c;
+  }
+  for (int k = 1; k < 4; ++k)
+    for (uint32_t i = 0; i < 256; ++i)
+      T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xffu];
+  return T;
+}
+__constant__ CrcTables kCrc = make_crc_tables();
+
+// SSE4.2 crc32 on one 32-bit little-endian word from a (LDS) copy of kCrc
+__device__ __forceinline__ uint32_t crc32c_u32_tab(const uint32_t (*t)[256], uint32_t crc, uint32_t w)
+{
+  crc ^= w;
+  return t[3][crc & 0xffu] ^ t[2][(crc >> 8) & 0xffu] ^ t[1][(crc >> 16) & 0xffu] ^ t[0][crc >> 24];
+}
+
+template <int F, int BS, int LOPT = 0, typename P>
+__device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F]);
+
 // fast_flows_packet_fss lookups (fast_flows.c:1084-1163), F frames per lane:
 // lookup block `blk` of BS lanes takes frames blk * BS * F + f * BS + lane,
 // TAS's header layout (l4_off == ip_off + 20: the 12 key bytes in one
@@ -370,24 +402,51 @@ __device__ __forceinline__ uint32_t tas_flow_hash(uint32_t lip, uint32_t rip, ui
 // before any is used.  The split-grid blocks of tcp4_tas14_kernel<...,flow>
 // (xsum_kernels.hip) run it; flow_kernels.hip's flow_lookup_kernel is the same
 // arithmetic for any layout.  P: tasx_tcp4_params or tasx_flow_params.
-template <int F, int BS, typename P>
-__device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
+// LOPT (A/B, timing only: results wrong): 1 = no frame key load (the key made
+// from the frame index), 2 = no CRC (the key's words xor-folded), 4 = no
+// flow-state key load (the first valid hash match wins)
+template <int F, int BS, int LOPT, typename P>
+__device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F])
 {
+  static_assert(BS == 256, "one table entry per lane");
   constexpr uint32_t kNb = TASX_FLOWHT_NBSZ;
-  uint32_t i0[F], i[F], rip[F], lip[F], ports[F], h[F];
+  // the CRC32C slice-by-4 tables in LDS (4 KiB; ~300 VALU per frame less than
+  // the bitwise CRC, which cost the one-pass RX kernel 0.7 us per 64K frames)
+  __shared__ uint32_t lt[4][256];
+  uint32_t i[F], rip[F], lip[F], ports[F], h[F];
 #pragma unroll
   for (int f = 0; f < F; ++f) {
-    i0[f] = blk * (uint32_t) (BS * F) + (uint32_t) (BS * f) + threadIdx.x;
     i[f] = min(i0[f], p.n - 1u); // lanes past the batch repeat the last frame (no store)
     const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+    u32x3u k;
+    if (LOPT & 1)
+      k = u32x3u{i[f] * 2654435761u, i[f] ^ 0x5bd1e995u, i[f] * 40503u};
+    else
+      k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
     rip[f] = k.x;
     lip[f] = k.y;
     ports[f] = (k.z >> 16) | (k.z << 16); // tcp.dest | tcp.src << 16
   }
+  // the tables built while the key loads are in flight (no memory in the
+  // chain): T0 by eight bit steps, Tk[x] = T(k-1)[x] >> 8 ^ T0[T(k-1)[x] & 0xff]
+  {
+    uint32_t c = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+    lt[0][threadIdx.x] = c;
+    __syncthreads();
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      c = (c >> 8) ^ lt[0][c & 0xffu];
+      lt[k][threadIdx.x] = c;
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int f = 0; f < F; ++f)
-    h[f] = tas_flow_hash(lip[f], rip[f], ports[f]);
+    h[f] = (LOPT & 2) ? lip[f] ^ rip[f] ^ ports[f]
+                      : crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, lip[f]), rip[f]), ports[f]);
   uint64_t e[F][kNb];
 #pragma unroll
   for (int f = 0; f < F; ++f)
@@ -404,8 +463,11 @@ __device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
       const uint32_t ef = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
       fid[f][j] = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
       cand[f][j] = (ef & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
-      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
-          p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
+      if (LOPT & 4)
+        key[f][j] = u32x3{lip[f], rip[f], ports[f]};
+      else
+        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
+            p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
     }
 #pragma unroll
   for (int f = 0; f < F; ++f) {
@@ -420,6 +482,17 @@ __device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
         stg(p.hash_out, i[f], h[f]);
     }
   }
+}
+
+// lookup block `blk` of BS lanes: frames blk * BS * F + f * BS + lane
+template <int F, int BS, int LOPT = 0, typename P>
+__device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
+{
+  uint32_t i0[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f)
+    i0[f] = blk * (uint32_t) (BS * F) + (uint32_t) (BS * f) + threadIdx.x;
+  flow_lookup_lanes_at<F, BS, LOPT>(p, i0);
 }
 
 } // namespace

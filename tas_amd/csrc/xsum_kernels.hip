@@ -1031,12 +1031,20 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //  kFlowSplit / kFlowSplit1: two / one frames per lookup lane -- two for
 //   uniform-length (data) bursts, one for the row forms (data/ACK mixes),
 //   the other choice as A/B variant 27.
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3 };
+//  kFlowInter (round 3): groups of 128 verify blocks followed by 8 lookup
+//   blocks (136 = 17 x 8 blocks, so every block keeps blockIdx % 8: its XCD
+//   under round-robin placement).  Lookup block x of a group takes the 256
+//   frames of the group's verify blocks on its own XCD (x, x + 8, ...), one per
+//   lane, after them; those rows load their first 256 bytes L2-allocating, so
+//   the lookup reads each frame's 12-byte key from that XCD's L2 instead of
+//   fetching the line again.
+enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4 };
+constexpr uint32_t kInterV = 128u, kInterL = 8u; // verify / lookup blocks per group
 // frames per lane of a split grid's lookup blocks
 template <int FLOW>
 constexpr uint32_t split_frames() { return FLOW == kFlowSplit1 ? 1u : 2u; }
 template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
-          int FLOW = kFlowNone>
+          int FLOW = kFlowNone, int LOPT = 0>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
@@ -1045,6 +1053,25 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1) || !DONE, "split grids post no completion word");
   const int gl = threadIdx.x & 15;
   uint32_t vb = blockIdx.x; // this block's verify block
+  // kFlowRow: CRC32C from slice-by-4 tables the block builds in LDS first (before
+  // any row leaves: every wave reaches the barriers; the bitwise CRC cost every
+  // verify wave ~300 VALU)
+  __shared__ uint32_t lt[FLOW == kFlowRow ? 4 : 1][256];
+  if constexpr (FLOW == kFlowRow) {
+    static_assert(BS == 256, "one table entry per thread");
+    uint32_t c = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
+    lt[0][threadIdx.x] = c;
+    __syncthreads();
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      c = (c >> 8) ^ lt[0][c & 0xffu];
+      lt[k][threadIdx.x] = c;
+    }
+    __syncthreads();
+  }
   if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1) {
     // the lookup blocks first: their dependent chains are the long ones, so
     // they start at once and overlap the verify blocks instead of forming the
@@ -1052,10 +1079,22 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     constexpr uint32_t kF = split_frames<FLOW>(); // frames per lookup lane (flow_kernels.hip: kFlowFramesPerLane)
     const uint32_t nl = (p.n + BS * kF - 1u) / (BS * kF);
     if (blockIdx.x < nl) {
-      flow_lookup_lanes<kF, BS>(p, blockIdx.x);
+      flow_lookup_lanes<kF, BS, LOPT>(p, blockIdx.x);
       return;
     }
     vb = blockIdx.x - nl;
+  }
+  if constexpr (FLOW == kFlowInter) {
+    static_assert(BS == 256, "16 verify rows per block, one lookup lane per frame of 16 blocks");
+    const uint32_t g = blockIdx.x / (kInterV + kInterL), r = blockIdx.x % (kInterV + kInterL);
+    if (r >= kInterV) {
+      // lane t: row t % 16 of the group's verify block x + 8 (t / 16)
+      const uint32_t x = r - kInterV;
+      const uint32_t i0[1] = {(g * kInterV + x + kInterL * (threadIdx.x / 16u)) * (BS / 16) + (threadIdx.x & 15u)};
+      flow_lookup_lanes_at<1, BS, LOPT>(p, i0);
+      return;
+    }
+    vb = g * kInterV + r;
   }
   uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
   uint32_t hs = 0; // kHintArrS: the row's hint
@@ -1107,6 +1146,20 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const uint32_t b = rx_bound(p, MODE == kHintArrS ? hs : p.flen ? ldg(p.flen, i) : p.flen0);
     have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
   }
+  // FLOW (kFlowRow): the key arrived with the hint, so the hash and the bucket
+  // probe go out BEFORE the chunk loads (vector loads complete in order: a
+  // bucket issued after the chunks could be used only once they all landed)
+  uint32_t fh = 0;
+  uint64_t fe = 0;
+  if constexpr (FLOW == kFlowRow) {
+    if (gl < kNb) {
+      fh = crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, fkey.y), fkey.x), (fkey.z >> 16) | (fkey.z << 16));
+      const uint32_t ht = p.ht_entries;
+      const uint32_t hb = (ht & (ht - 1u)) == 0u ? (fh & (ht - 1u)) : fh % ht; // the bucket's first entry
+      const uint32_t ej = hb + (uint32_t) gl;
+      fe = ldg((const uint64_t *) p.flowht, ej >= ht ? ej - ht : ej);
+    }
+  }
   // the datagram [ip, ip + hend): uniform from the hint, or per row from the
   // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
   const uint32_t lo = a0 + 16u * (uint32_t) gl;
@@ -1145,6 +1198,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         v[u] = u32x4{0u, 0u, 0u, 0u};
         if ((uint32_t) gl + 16u * u <= last) // the tail comes from v[last / 16] on lane last % 16
           v[u] = ld16nt_off(fb, lo + 256u * u);
+      } else if (FLOW == kFlowInter && u == 0) { // the key's line stays in L2 for the lookup block
+        v[u] = ld16_off(fb, min(lo, lastoff));
       } else {
         v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
       }
@@ -1191,15 +1246,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
-  // FLOW: the hash and the bucket probe go out while the chunks are in flight
-  uint32_t fh = 0, ffid = 0;
+  // FLOW: the flow-state key load goes out while the chunks are in flight (the
+  // bucket, issued before them, has returned first)
+  uint32_t ffid = 0;
   u32x3 ck = {0u, 0u, 0u};
   bool fcand = false;
   if constexpr (FLOW == kFlowRow) {
     if (gl < kNb) {
-      fh = tas_flow_hash(fkey.y, fkey.x, (fkey.z >> 16) | (fkey.z << 16));
-      const uint64_t e = ldg((const uint64_t *) p.flowht, (fh + (uint32_t) gl) % p.ht_entries);
-      const uint32_t ef = (uint32_t) e, eh = (uint32_t) (e >> 32);
+      const uint32_t ef = (uint32_t) fe, eh = (uint32_t) (fe >> 32);
       ffid = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
       fcand = (ef & TASX_FLOWHTE_VALID) && eh == fh && ffid < p.fs_num;
       ck = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
@@ -1700,6 +1754,22 @@ static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hip
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the grid of tcp4_tas14_kernel<..., kFlowInter>: per group of kInterV verify
+// blocks, kInterL lookup blocks after them
+template <typename K>
+static int launch_inter(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
+{
+  const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
+  const uint64_t groups = (nv + kInterV - 1) / kInterV, blocks = groups * (kInterV + kInterL);
+  if (nv == 0)
+    return 0;
+  if (blocks > 0x7fffffffull)
+    return -2;
+  t_last_kernel = name;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <bool OFFS, int MODE, int FLOW>
 static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
@@ -1730,6 +1800,21 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 27) // A/B: two frames per lookup lane
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
+  if (variant == 28 && mode == kHintArr && !OFFS) // A/B: lookup blocks after their verify blocks, same XCD
+    return launch_inter("tcp4_tas14_kernel<hints,verify,flow_inter>",
+                        tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowInter>, p, s, lds);
+  // 29 / 30 / 31: timing-only ablations of the lookup blocks (results wrong):
+  // no frame key load / no CRC / no flow-state key load
+  if (variant >= 29 && variant <= 31 && mode == kHintArr && !OFFS) {
+    static const char *const nm[3] = {"tcp4_tas14_kernel<hints,verify,flow,nokey>", "tcp4_tas14_kernel<hints,verify,flow,nocrc>",
+                                      "tcp4_tas14_kernel<hints,verify,flow,nofskey>"};
+    const char *name = nm[variant - 29];
+    if (variant == 29)
+      return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 1>, p, s, lds);
+    if (variant == 30)
+      return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 2>, p, s, lds);
+    return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 4>, p, s, lds);
+  }
 #else
   (void) variant;
 #endif

@@ -22,7 +22,7 @@ this script (10.77.0.2, speaking TCP by hand through the TUN fd):
 Each packet is stored as a TAS frame (14 zero Ethernet bytes, IPv4 at 14, TCP
 at 34) in a 2048-byte mbuf room, with its length and origin.  The tests take
 the checksum fields out and recompute them with the oracle and the GPU kernels
-(tests/test_golden.py, tests/test_gpu_parity.py).  Needs root and /dev/net/tun
+(tests/test_linux_frames.py).  Needs root and /dev/net/tun
 (this build container, not the GPU box); sequence numbers and timestamps differ
 per run, so the committed file is one run's capture.
 

@@ -44,6 +44,9 @@ def make(leg: str, rotate: int = 16):
     if leg == "rx":
         w = bench.RxPassWorkload(bench.FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000)
         return w.loop(benchloop.RX_FUSED), w.bytes_per_step
+    if leg == "rx_separate":
+        w = bench.RxPassWorkload(bench.FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000)
+        return w.loop(benchloop.RX_SEPARATE), w.bytes_per_step
     if leg == "rx_verify":
         w = bench.RxPassWorkload(bench.FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000)
         return benchloop.Loop("tcp4", [a.v for a in w.loop(benchloop.RX_FUSED).arr], [
@@ -64,9 +67,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default="")
     ap.add_argument("--rotate", type=int, default=16, help="txseg: rotating input sets")
+    ap.add_argument("--variant", type=int, default=0, help="tasx_set_kernel_variant (A/B variants need TASX_LIB)")
     a = ap.parse_args()
     xsum.lib()
     run, nbytes = make(a.leg, a.rotate)
+    xsum.set_kernel_variant(a.variant)
     bench.prewarm(run)
     for r in range(a.reps):
         run(0, 20)
@@ -79,7 +84,7 @@ def main():
         us = e0.elapsed_time(e1) * 1e3 / a.steps
         print(json.dumps({"leg": a.leg, "tag": a.tag, "rep": r, "us": round(us, 3), "kernel": xsum.last_kernel(),
                           "frac": round(nbytes / us / 1e3 / bench.HBM_PEAK_GBS, 4),
-                          "lib": Path(xsum.library_path()).name,
+                          "lib": Path(xsum.library_path()).name, "variant": a.variant,
                           "env": {k: v for k, v in os.environ.items() if k.startswith("TASX_")}}), flush=True)
 
 
