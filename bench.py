@@ -651,6 +651,59 @@ def tcp4_pattern_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200)
                       "residency, words xor-folded instead of summed"}
 
 
+def mix_bounds(mw: "FlushMixWorkload", launches: int = 200) -> dict:
+    """The data/ACK mix's latency roofline, measured live
+    with the A/B build's tasx_ab_tcp4_mix_pattern over the flush_mix frames:
+    `chain_us` -- each row's dependent chain alone (hint -> the chunk holding
+    the frame's end -> result store, 8 waves per SIMD as the product: almost no
+    bytes), `pattern_us` -- the product's exact loads and stores with the words
+    xor-folded.  The roofline is the larger of the chain and the HBM time of
+    the algorithmic bytes at 8 TB/s; the chain over its generations of
+    resident rows gives the loaded latency per dependent load."""
+    ab = xsum._load(xsum.AB_LIB_PATH)
+    s = torch.cuda.current_stream().cuda_stream
+    R = len(mw.bufs)
+    outs = [torch.empty(mw.n, dtype=torch.int32, device="cuda") for _ in range(2)]  # not the checked results
+
+    def timed(chain: int) -> float:
+        def pat(k):
+            rc = ab.tasx_ab_tcp4_mix_pattern(mw.bufs[k % R].data_ptr(), mw.stride, mw.n, mw.flen.data_ptr(), IP_OFF,
+                                             chain, outs[k % 2].data_ptr(), s)
+            if rc:
+                raise xsum.TasxError(rc, "tasx_ab_tcp4_mix_pattern")
+        for k in range(20):
+            pat(k)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for k in range(launches):
+            pat(k)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / launches
+
+    pattern_us, chain_us = timed(0), timed(1)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rows_in_flight = cus * 4 * 8 * 4  # CUs x SIMDs x 8 waves x 4 rows of 16 lanes
+    gens = -(-mw.n // rows_in_flight)
+    return {"pattern_us": round(pattern_us, 3), "chain_us": round(chain_us, 3),
+            "rows": mw.n, "rows_in_flight": rows_in_flight, "generations": gens, "dependent_loads_per_row": 2,
+            "loaded_latency_us": round(chain_us / (gens * 2), 3),
+            "kernel": "tcp4_mix_pattern_kernel<chain> / tcp4_mix_pattern_kernel (libtasx_ab.so)"}
+
+
+def price_mix(leg_: dict, mb: dict, alg_bytes: int) -> None:
+    """Attach the latency roofline (mix_bounds) to a data/ACK mix leg's roofline."""
+    avg = leg_["roofline"]["launch_avg_us"]
+    hbm_us = alg_bytes / HBM_PEAK_GBS / 1e3
+    bound_us = max(mb["chain_us"], hbm_us)
+    leg_["roofline"]["latency"] = dict(mb, **{
+        "bound": "max(dependent chain, HBM)", "hbm_us": round(hbm_us, 3), "bound_us": round(bound_us, 3),
+        "frac": round(bound_us / avg, 4), "frac_of_pattern": round(mb["pattern_us"] / avg, 4),
+        "model": "chain_us = generations x dependent_loads_per_row x loaded_latency_us; "
+                 "frac = max(chain_us, bytes / 8 TB/s) / launch"})
+
+
 def copy_ceiling(nbytes: int, copies: int = 50, rotate: int = 4) -> dict:
     """The device's read+write streaming rate, measured live: a grid-stride
     copy kernel (one non-temporal 16-byte load and store per lane;
@@ -1393,11 +1446,16 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         mw = FlushMixWorkload(min(rot, 12), pktgen.SEED + 500 + rank)
         mix = leg(mw.loop(), mw.bytes_per_step, args, ws, FlushMixWorkload.desc, "tcp4_tas14_kernel<hints>")
         mix["parity"] = "tests/test_bench_configs.py::test_bench_flush_mix"
+        mb = None if rehearse else mix_bounds(mw)  # before the RX form checksums the frames in place
+        if mb is not None:
+            price_mix(mix, mb, mw.bytes_per_step)
         rm = RxMixWorkload(mw)
         rx_mix = leg(rm.loop(), rm.bytes_per_step, args, ws, RxMixWorkload.desc, "tcp4_tas14_kernel<hints,verify>")
         torch.cuda.synchronize()
         rx_mix["all_frames_verified"] = bool(all((f == 3).all().item() for f in rm.flags))
         rx_mix["parity"] = "tests/test_bench_configs.py::test_bench_rx_mix"
+        if mb is not None:  # the same frames and rows: the same chain and pattern
+            price_mix(rx_mix, mb, rm.bytes_per_step)
         del mw, rm
         torch.cuda.empty_cache()
     raw = None
@@ -1486,8 +1544,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                 if pm and "hbm_bytes_per_launch" in pm:
                     mix["roofline"]["traffic"] = int(pm["hbm_bytes_per_launch"])
                 mix["pmc"] = pm
-            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplit1 = 3>)
-                prx = pmc_leg("rx", "256, false, 3>", 48)
+            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplit1 = 3, LOPT 0>)
+                prx = pmc_leg("rx", "256, false, 3, 0>", 48)
                 if prx and "hbm_bytes_per_launch" in prx:
                     rx_pass["roofline"]["traffic"] = int(prx["hbm_bytes_per_launch"])
                 rx_pass["pmc"] = prx

@@ -59,6 +59,16 @@ int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t
 int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
     uint32_t *out, void *stream);
 
+/* The data/ACK mix's access pattern (tcp4_tas14_kernel<hints>, per-frame hints
+ * as the row geometry) with no checksum logic: chain = 0 reads what the
+ * product reads, chain = 1 only each row's hint and the chunk holding its
+ * frame's end (the row's dependent chain, almost no bytes).  bench.py prices
+ * the flush_mix and rx_verify_mix legs against them (their latency roofline).
+ * Stride-mode TAS batches (ip_off 14 mod 16, 16-byte aligned rooms >= 1536 B,
+ * n * stride < 4 GiB; -EINVAL otherwise); out[i] is not a checksum. */
+int tasx_ab_tcp4_mix_pattern(const void *base, uint64_t stride, uint32_t n, const uint32_t *flen,
+    uint32_t ip_off, int chain, uint32_t *out, void *stream);
+
 /* The device's read+write streaming rate: a grid-stride copy of `bytes` (16-byte
  * multiple, 16-byte aligned), one non-temporal 16-byte load and store per
  * lane -- the TX segment build's ceiling, timed by bench.py. */

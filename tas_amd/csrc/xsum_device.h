@@ -404,7 +404,8 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
 // arithmetic for any layout.  P: tasx_tcp4_params or tasx_flow_params.
 // LOPT (A/B, timing only: results wrong): 1 = no frame key load (the key made
 // from the frame index), 2 = no CRC (the key's words xor-folded), 4 = no
-// flow-state key load (the first valid hash match wins)
+// flow-state key load (the first valid hash match wins), 8 = no bucket loads
+// (entry j made valid with the frame's hash, flow id (h + j) % fs_num)
 template <int F, int BS, int LOPT, typename P>
 __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F])
 {
@@ -452,7 +453,8 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
   for (int f = 0; f < F; ++f)
 #pragma unroll
     for (uint32_t j = 0; j < kNb; ++j)
-      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
+      e[f][j] = (LOPT & 8) ? (((uint64_t) h[f] << 32) | TASX_FLOWHTE_VALID | ((h[f] + j) % p.fs_num))
+                           : ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
   bool cand[F][kNb];
   uint32_t fid[F][kNb];
   u32x3 key[F][kNb];

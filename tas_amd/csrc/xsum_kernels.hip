@@ -1038,7 +1038,16 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   lane, after them; those rows load their first 256 bytes L2-allocating, so
 //   the lookup reads each frame's 12-byte key from that XCD's L2 instead of
 //   fetching the line again.
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4 };
+//  kFlowSplitX (round 3): the split grid with the lookup blocks first, one
+//   frame per lane, each lookup block taking the frames of the 16 verify blocks
+//   that land on its own XCD (blocks are placed round-robin over the 8 XCDs
+//   by blockIdx; the lookup block count is a multiple of 8, so verify block vb
+//   keeps vb % 8).  The lookup's plain key load leaves the frame's first line in
+//   that XCD's L2, where the verify row's chunk-0 load then finds it.
+enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5 };
+// lookup blocks of a kFlowSplitX grid over nv verify blocks of BS / 16 rows
+template <int BS>
+__host__ __device__ constexpr uint32_t splitx_lookup_blocks(uint32_t nv) { return ((nv + 15u) / 16u + 7u) & ~7u; }
 constexpr uint32_t kInterV = 128u, kInterL = 8u; // verify / lookup blocks per group
 // frames per lane of a split grid's lookup blocks
 template <int FLOW>
@@ -1050,7 +1059,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
   static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
-  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1) || !DONE, "split grids post no completion word");
+  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX) || !DONE,
+                "split grids post no completion word");
   const int gl = threadIdx.x & 15;
   uint32_t vb = blockIdx.x; // this block's verify block
   // kFlowRow: CRC32C from slice-by-4 tables the block builds in LDS first (before
@@ -1080,6 +1090,18 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const uint32_t nl = (p.n + BS * kF - 1u) / (BS * kF);
     if (blockIdx.x < nl) {
       flow_lookup_lanes<kF, BS, LOPT>(p, blockIdx.x);
+      return;
+    }
+    vb = blockIdx.x - nl;
+  }
+  if constexpr (FLOW == kFlowSplitX) {
+    static_assert(BS == 256, "16 verify rows per block, one lookup lane per frame of 16 blocks");
+    const uint32_t nl = splitx_lookup_blocks<BS>((p.n + BS / 16 - 1u) / (BS / 16));
+    if (blockIdx.x < nl) {
+      // lane t: row t % 16 of verify block 8 (16 (b / 8) + t / 16) + b % 8 (lanes past the batch: no store)
+      const uint32_t b = blockIdx.x;
+      const uint32_t i0[1] = {(8u * (16u * (b / 8u) + threadIdx.x / 16u) + (b & 7u)) * (BS / 16) + (threadIdx.x & 15u)};
+      flow_lookup_lanes_at<1, BS, LOPT>(p, i0);
       return;
     }
     vb = blockIdx.x - nl;
@@ -1664,7 +1686,65 @@ __global__ __launch_bounds__(kBlock) void tcp4_pattern_kernel(tasx_tcp4_params p
   if (gl == 15)
     stg((uint32_t *) p.out, i, x);
 }
+
+// The data/ACK mix's access pattern (tcp4_tas14_kernel<hints>, the flush_mix
+// leg) with no checksum logic, for its latency roofline (bench.py
+// mix_bounds): each row reads its hint, then (CHAIN = 0) the same clamped
+// chunk loads as the product, xor-folded, or (CHAIN = 1) only the chunk
+// holding the frame's end on lane 15 -- the row's dependent chain (hint ->
+// frame -> result store) with almost no bytes behind it; 8 waves per SIMD as
+// the product.
+template <int CHAIN>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void tcp4_mix_pattern_kernel(tasx_tcp4_params p)
+{
+  const int gl = threadIdx.x & 15;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if (i >= p.n)
+    return;
+  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
+  const uint32_t h = ldg(p.flen, i);
+  const uint32_t hl = h > p.ip_off + 20u ? min(h - p.ip_off, 1522u) : 20u;
+  const uint32_t lastoff = a0 + 16u * ((14u + hl - 1u) >> 4), lo = a0 + 16u * (uint32_t) gl;
+  uint32_t x = 0;
+  if constexpr (CHAIN) {
+    if (gl == 15) {
+      const u32x4 t = ld16nt_off(p.base, lastoff);
+      x = t.x ^ t.y ^ t.z ^ t.w;
+    }
+  } else {
+    u32x4 v[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+      v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+      x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  x = row_sum16(x);
+  if (gl == 15)
+    stg((uint32_t *) p.out, i, x);
+}
 } // namespace
+
+extern "C" int tasx_ab_tcp4_mix_pattern(const void *base, uint64_t stride, uint32_t n, const uint32_t *flen,
+                                        uint32_t ip_off, int chain, uint32_t *out, void *stream)
+{
+  tasx_tcp4_params p;
+  memset(&p, 0, sizeof(p));
+  p.base = (uint8_t *) base;
+  p.stride = stride;
+  p.n = n;
+  p.flen = flen;
+  p.ip_off = ip_off;
+  p.l4_off = ip_off + 20u;
+  p.out = (uint16_t *) out;
+  // the product's own geometry checks: 16-byte aligned rooms of at least 1536 bytes, 32-bit offsets
+  if (!out || !flen || !base || (ip_off & 15u) != 14u || (stride & 15u) || stride < 1536u ||
+      (uint64_t) n * stride > 0xffffffffull || ((uintptr_t) base & 15u))
+    return -EINVAL;
+  return chain ? launch_groups("tcp4_mix_pattern_kernel<chain>", tcp4_mix_pattern_kernel<1>, p, (hipStream_t) stream, 0u)
+               : launch_groups("tcp4_mix_pattern_kernel", tcp4_mix_pattern_kernel<0>, p, (hipStream_t) stream, 0u);
+}
 
 extern "C" int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
                                     uint32_t *out, void *stream)
@@ -1770,6 +1850,21 @@ static int launch_inter(const char *name, K kern, const tasx_tcp4_params &p, hip
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// the grid of tcp4_tas14_kernel<..., kFlowSplitX>: the XCD-matched lookup blocks, then the verify blocks
+template <typename K>
+static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
+{
+  const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
+  if (nv == 0)
+    return 0;
+  const uint64_t blocks = nv + splitx_lookup_blocks<kBlock>((uint32_t) nv);
+  if (blocks > 0x7fffffffull)
+    return -2;
+  t_last_kernel = name;
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <bool OFFS, int MODE, int FLOW>
 static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
@@ -1803,6 +1898,15 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 28 && mode == kHintArr && !OFFS) // A/B: lookup blocks after their verify blocks, same XCD
     return launch_inter("tcp4_tas14_kernel<hints,verify,flow_inter>",
                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowInter>, p, s, lds);
+  if (variant == 32 && mode == kHintArr && !OFFS) // A/B: lookup blocks first, each on its verify blocks' XCD
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow_xcd>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX>, p, s, lds);
+  if (variant == 33 && mode == kHintArr && !OFFS) // timing only (results wrong): no bucket loads
+    return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,nobucket>",
+                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 8>, p, s, lds);
+  if (variant == 34 && mode == kHintArr && !OFFS) // timing only (results wrong): no loads past the frame key
+    return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,keyonly>",
+                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 12>, p, s, lds);
   // 29 / 30 / 31: timing-only ablations of the lookup blocks (results wrong):
   // no frame key load / no CRC / no flow-state key load
   if (variant >= 29 && variant <= 31 && mode == kHintArr && !OFFS) {
