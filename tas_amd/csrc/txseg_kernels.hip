@@ -912,8 +912,9 @@ __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
                __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
 }
 
-// OPT (A/B, timing only: results wrong): 1 = no general-body fallback compiled
-// in, 2 = wraps ignored (piece A only)
+// OPT (A/B): 1 = no general-body fallback compiled in, 2 = wraps ignored
+// (piece A only) -- both timing only, results wrong -- 4 = the first block
+// stored non-temporal too (correct)
 template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
@@ -1038,7 +1039,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         // every row of the wave holds at least 81 chunks: slots 0..4 are whole
         // frame chunks, only slot 5 holds the frame's end
         acc = sad4(u32x4{w[0].x & mx, w[0].y & mr, w[0].z & mr, w[0].w & mr}, acc);
-        *(__attribute__((address_space(1))) u32x4 *) (f + 16 * kh) = w[0];
+        if (OPT & 4)
+          __builtin_nontemporal_store(w[0], (__attribute__((address_space(1))) u32x4 *) (f + 16 * kh));
+        else
+          *(__attribute__((address_space(1))) u32x4 *) (f + 16 * kh) = w[0];
 #pragma unroll
         for (int u = 1; u < 5; ++u) {
           acc = sad4(w[u], acc);
@@ -1064,7 +1068,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           // whole chunks, and scratch zeros past the frame to its block's end
           if (full || (k >= K && k < kend)) {
             const u32x4 sv = k < K ? v : u32x4{0u, 0u, 0u, 0u};
-            if (u == 0)
+            if (u == 0 && !(OPT & 4))
               *(__attribute__((address_space(1))) u32x4 *) (f + 16 * k) = sv;
             else
               __builtin_nontemporal_store(sv, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
@@ -1376,6 +1380,7 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 32: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 33: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 34: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb,nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 3>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU
   case 35: case 36: case 37: case 38: if (tas) {
     constexpr uint32_t st = (kBlock / 16) * (uint32_t) lds_slice<6>(); // the kernel's static LDS

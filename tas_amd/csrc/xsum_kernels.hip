@@ -1044,10 +1044,12 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   by blockIdx; the lookup block count is a multiple of 8, so verify block vb
 //   keeps vb % 8).  The lookup's plain key load leaves the frame's first line in
 //   that XCD's L2, where the verify row's chunk-0 load then finds it.
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5 };
-// lookup blocks of a kFlowSplitX grid over nv verify blocks of BS / 16 rows
-template <int BS>
-__host__ __device__ constexpr uint32_t splitx_lookup_blocks(uint32_t nv) { return ((nv + 15u) / 16u + 7u) & ~7u; }
+//   kFlowSplitX2: the same with two frames per lookup lane (32 verify blocks
+//   per lookup block).
+enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
+// lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
+template <uint32_t F>
+__host__ __device__ constexpr uint32_t splitx_lookup_blocks(uint32_t nv) { return ((nv + 16u * F - 1u) / (16u * F) + 7u) & ~7u; }
 constexpr uint32_t kInterV = 128u, kInterL = 8u; // verify / lookup blocks per group
 // frames per lane of a split grid's lookup blocks
 template <int FLOW>
@@ -1059,7 +1061,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
   static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
-  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX) || !DONE,
+  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX && FLOW != kFlowSplitX2) || !DONE,
                 "split grids post no completion word");
   const int gl = threadIdx.x & 15;
   uint32_t vb = blockIdx.x; // this block's verify block
@@ -1094,14 +1096,18 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     vb = blockIdx.x - nl;
   }
-  if constexpr (FLOW == kFlowSplitX) {
-    static_assert(BS == 256, "16 verify rows per block, one lookup lane per frame of 16 blocks");
-    const uint32_t nl = splitx_lookup_blocks<BS>((p.n + BS / 16 - 1u) / (BS / 16));
+  if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2) {
+    static_assert(BS == 256, "16 verify rows per block, one lookup lane per row of 16 blocks");
+    constexpr uint32_t kF = FLOW == kFlowSplitX2 ? 2u : 1u;
+    const uint32_t nl = splitx_lookup_blocks<kF>((p.n + BS / 16 - 1u) / (BS / 16));
     if (blockIdx.x < nl) {
-      // lane t: row t % 16 of verify block 8 (16 (b / 8) + t / 16) + b % 8 (lanes past the batch: no store)
+      // lane t, frame f: row t % 16 of verify block 8 (16 F (b / 8) + 16 f + t / 16) + b % 8 (past the batch: no store)
       const uint32_t b = blockIdx.x;
-      const uint32_t i0[1] = {(8u * (16u * (b / 8u) + threadIdx.x / 16u) + (b & 7u)) * (BS / 16) + (threadIdx.x & 15u)};
-      flow_lookup_lanes_at<1, BS, LOPT>(p, i0);
+      uint32_t i0[kF];
+#pragma unroll
+      for (uint32_t f = 0; f < kF; ++f)
+        i0[f] = (8u * (16u * kF * (b / 8u) + 16u * f + threadIdx.x / 16u) + (b & 7u)) * (BS / 16) + (threadIdx.x & 15u);
+      flow_lookup_lanes_at<kF, BS, LOPT>(p, i0);
       return;
     }
     vb = blockIdx.x - nl;
@@ -1850,14 +1856,14 @@ static int launch_inter(const char *name, K kern, const tasx_tcp4_params &p, hip
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// the grid of tcp4_tas14_kernel<..., kFlowSplitX>: the XCD-matched lookup blocks, then the verify blocks
-template <typename K>
+// the grid of tcp4_tas14_kernel<..., kFlowSplitX*>: the XCD-matched lookup blocks, then the verify blocks
+template <uint32_t F = 1, typename K>
 static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
   const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
   if (nv == 0)
     return 0;
-  const uint64_t blocks = nv + splitx_lookup_blocks<kBlock>((uint32_t) nv);
+  const uint64_t blocks = nv + splitx_lookup_blocks<F>((uint32_t) nv);
   if (blocks > 0x7fffffffull)
     return -2;
   t_last_kernel = name;
@@ -1901,6 +1907,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 32 && mode == kHintArr && !OFFS) // A/B: lookup blocks first, each on its verify blocks' XCD
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow_xcd>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX>, p, s, lds);
+  if (variant == 35 && mode == kHintArr && !OFFS) // A/B: the same with two frames per lookup lane
+    return launch_splitx<2>("tcp4_tas14_kernel<hints,verify,flow_xcd2>",
+                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX2>, p, s, lds);
   if (variant == 33 && mode == kHintArr && !OFFS) // timing only (results wrong): no bucket loads
     return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,nobucket>",
                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 8>, p, s, lds);
@@ -1946,6 +1955,12 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
     if (variant == 27)
       return launch_split<1>("tcp4_tas14_kernel<hint,verify,flow_f1>",
                              tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit1>, *p, s, lds);
+    if (variant == 32)
+      return launch_splitx<1>("tcp4_tas14_kernel<hint,verify,flow_xcd>",
+                              tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX>, *p, s, lds);
+    if (variant == 35)
+      return launch_splitx<2>("tcp4_tas14_kernel<hint,verify,flow_xcd2>",
+                              tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, lds);
 #endif
     // a uniform received length is a data burst: two frames per lookup lane
     // (17.6 against 18.1 us with one; profiles/r02/r02cc)

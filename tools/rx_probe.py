@@ -3,9 +3,11 @@
 RX bursts of TAS frames in 2048 B mbufs (data segments and pure ACKs in random
 order, the ACK fraction swept), flow keys from bench.py's TAS-sized flow table,
 each frame's received length as its hint.  Times, per case, the product's
-split grid (variant 0: lookup blocks ahead of the verify blocks), the lookup
-inside the verify rows (A/B variant 26; needs
-TASX_LIB=tas_amd/_lib/libtasx_ab.so) and the two kernels in turn, every
+split grid (variant 0: lookup blocks ahead of the verify blocks), the A/B
+variants --variants names (26: the lookup inside the verify rows, 27: the other
+frames-per-lane choice, 32 / 35: lookup blocks on their verify blocks' XCD with
+one / two frames per lane; needs TASX_LIB=tas_amd/_lib/libtasx_ab.so) and the
+two kernels in turn, every
 result checked against the first run's, interleaved over --rounds.  One JSON
 line per case.  Launches come from C (tas_amd/benchsrc/bench_loop.c).
 
@@ -43,6 +45,7 @@ def main():
     ap.add_argument("--rotate", type=int, default=8)
     ap.add_argument("--fracs", default="u,0,0.5,1")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--variants", default="26,27", help="A/B variants timed beside the product (A/B build)")
     a = ap.parse_args()
     ab = xsum.library_path().name == "libtasx_ab.so"
     fw = bench.FlowLookupWorkload(1, pktgen.SEED + 3000)
@@ -53,7 +56,7 @@ def main():
         rp = bench.RxPassWorkload(fw, a.rotate, pktgen.SEED + 4000, ack_frac=frac)
         cases = [("product", benchloop.RX_FUSED, 0), ("separate", benchloop.RX_SEPARATE, 0)]
         if ab:
-            cases += [("row", benchloop.RX_FUSED, 26), ("split_other_f", benchloop.RX_FUSED, 27)]
+            cases += [(f"v{v}", benchloop.RX_FUSED, int(v)) for v in a.variants.split(",") if v]
         ref = None
         res = {k: [] for k, _, _ in cases}
         for _ in range(a.rounds):
