@@ -449,6 +449,45 @@ class TxSegWorkload:
                 "parity_vs_gpu": "bit-exact" if np.array_equal(frames, gpu_frames) else "MISMATCH"}
 
 
+def txseg_pattern_ceiling(tw: "TxSegWorkload", avg_us: float, launches: int = 100) -> dict:
+    """The TX segment build's access pattern alone, timed live over the same
+    rotation: the product kernel with TASX_TXSEG_DEBUG=40 (A/B build) -- the
+    same descriptor, header and aligned source loads, the same frame stores,
+    the loaded chunks stored as they are (no LDS realignment, no splice)."""
+    ab = xsum._load(xsum.AB_LIB_PATH)
+    s = torch.cuda.current_stream().cuda_stream
+    R = len(tw.shms)
+    old = os.environ.get("TASX_TXSEG_DEBUG")
+    os.environ["TASX_TXSEG_DEBUG"] = "40"  # read by the A/B build at each call
+    frames = [b.clone() for b in tw.bufs[:2]]  # the pattern stores unrealigned bytes: not the checked frames
+
+    def pat(k):
+        rc = ab.tasx_tx_segment_batch_dev(tw.shms[k % R].data_ptr(), tw.shm_len, frames[k % 2].data_ptr(),
+                                          tw.segs.data_ptr(), tw.n, IP_OFF, L4_OFF, tw.outs[k % 2].data_ptr(), s)
+        if rc:
+            raise xsum.TasxError(rc, "tasx_tx_segment_batch_dev (pattern)")
+    try:
+        for k in range(10):
+            pat(k)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for k in range(launches):
+            pat(k)
+        e1.record()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("TASX_TXSEG_DEBUG", None)
+        else:
+            os.environ["TASX_TXSEG_DEBUG"] = old
+    us = e0.elapsed_time(e1) * 1e3 / launches
+    del frames
+    return {"bound": "the access pattern", "us": round(us, 3), "frac": round(us / avg_us, 4),
+            "kernel": "tx_segment_lds_kernel<pattern> (libtasx_ab.so): the product's loads and stores, "
+                      "no realignment through LDS"}
+
+
 def txseg_block_floor(segs, block: int = 128) -> dict:
     """HBM bytes the TX segment build cannot avoid at the memory side's 128-byte
     request granularity (calibrated: tools/fetch_calib.hip): the blocks each
@@ -1478,6 +1517,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         cc = copy_ceiling(int(tw.block_floor["bytes"]) // 2)
         cc["alg_frac_of_copy"] = round(txseg["roofline"]["achieved"] / cc["GBps"], 4)
         txseg["copy_ceiling"] = cc
+        if not rehearse:
+            txseg["pattern_ceiling"] = txseg_pattern_ceiling(tw, txseg["roofline"]["launch_avg_us"])
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             txseg["cpu_baseline"] = tw.cpu_check(3.0)
         del tw
@@ -1544,8 +1585,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                 if pm and "hbm_bytes_per_launch" in pm:
                     mix["roofline"]["traffic"] = int(pm["hbm_bytes_per_launch"])
                 mix["pmc"] = pm
-            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplit1 = 3, LOPT 0>)
-                prx = pmc_leg("rx", "256, false, 3, 0>", 48)
+            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplitX = 5, LOPT 0>)
+                prx = pmc_leg("rx", "256, false, 5, 0>", 48)
                 if prx and "hbm_bytes_per_launch" in prx:
                     rx_pass["roofline"]["traffic"] = int(prx["hbm_bytes_per_launch"])
                 rx_pass["pmc"] = prx

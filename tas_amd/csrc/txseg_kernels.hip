@@ -914,7 +914,9 @@ __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
 
 // OPT (A/B): 1 = no general-body fallback compiled in, 2 = wraps ignored
 // (piece A only) -- both timing only, results wrong -- 4 = the first block
-// stored non-temporal too (correct)
+// stored non-temporal too (correct), 8 = the access pattern alone (timing
+// only: the aligned source chunks stored as loaded, no LDS realignment or
+// splice; bench.py's tx_segment pattern_ceiling)
 template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
@@ -993,12 +995,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
         a[u] = ld16_off(sbase, min(ro, hi_ok));
       }
+      if constexpr (!(OPT & 8)) {
 #pragma unroll
-      for (int u = 0; u < kLdsSlots; ++u)
-        *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int u = 0; u < kLdsSlots; ++u)
+          *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
       // LDS byte offsets: payload index 0 in piece A, piece B's first byte;
       // window u at o0 + 256u (+ dW for a window in piece B)
       const int oA = kLdsLead + (int) (s1 - cA);
@@ -1010,12 +1014,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       for (int u = 0; u < 6; ++u) {
         const int j0 = 16 * (16 * u + kh) - 66;
         const int o = min(o0 + 256 * u + (j0 >= wrapc ? dW : 0), kLdsSlice - 20);
-        w[u] = lds_window(sl, (uint32_t) o);
+        w[u] = (OPT & 8) ? a[u] : lds_window(sl, (uint32_t) o);
       }
       // the chunk holding the wrap (a row whose payload wraps off a chunk
       // boundary): its bytes from wrapc - j0 on are piece B's
       const int ks = wrapc < pay ? (66 + wrapc) >> 4 : -1;
-      const bool strad = ks >= 0 && ((66 + wrapc) & 15) != 0 && kh == (ks & 15);
+      const bool strad = !(OPT & 8) && ks >= 0 && ((66 + wrapc) & 15) != 0 && kh == (ks & 15);
       if (__builtin_amdgcn_ballot_w64(strad) != 0ull) {
 #pragma unroll
         for (int u = 0; u < 6; ++u) {
@@ -1380,6 +1384,7 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 32: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 33: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 34: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb,nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 3>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 40: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU
   case 35: case 36: case 37: case 38: if (tas) {

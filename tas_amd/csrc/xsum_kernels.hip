@@ -1013,12 +1013,12 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 
 // FLOW (RX, with VERIFY): the frames' flow lookup (fast_flows_packet_fss,
 // tas/fast/fast_flows.c:1084-1163) in the same launch.
-//  kFlowSplit* (the product): the grid's first blocks run flow_lookup_lanes,
-//   F frames per lane (F BS frames per block), the rest are the verify blocks.  The
-//   lookup's dependent chain (key -> bucket -> flow key) is the long one, so
-//   its blocks start first and overlap the verify rows instead of forming the
-//   grid's tail.  64K received frames: 1.24-1.40x the two kernels in turn
-//   (DESIGN.md section 5.2).
+//  kFlowSplit / kFlowSplit1 (the round-2 product, A/B 36 / 27): the grid's first blocks run
+//   flow_lookup_lanes, F frames per lane (F BS consecutive frames per block),
+//   the rest are the verify blocks.  The lookup's dependent chain (key ->
+//   bucket -> flow key) is the long one, so its blocks start first and
+//   overlap the verify rows instead of forming the grid's tail.  64K received
+//   frames: 1.24-1.40x the two kernels in turn.
 //  kFlowRow (A/B variant 26): lanes 0..3 of each verify row load the 12-byte
 //   key before the chunk loads, hash it, probe bucket entry h + lane and load
 //   that candidate's key while the chunks land.  Each wave of 4 rows pays a
@@ -1038,7 +1038,8 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   lane, after them; those rows load their first 256 bytes L2-allocating, so
 //   the lookup reads each frame's 12-byte key from that XCD's L2 instead of
 //   fetching the line again.
-//  kFlowSplitX (round 3): the split grid with the lookup blocks first, one
+//  kFlowSplitX (round 3, the product for the row forms; kFlowSplitX2 for a
+//   uniform received length): the split grid with the lookup blocks first, one
 //   frame per lane, each lookup block taking the frames of the 16 verify blocks
 //   that land on its own XCD (blocks are placed round-robin over the 8 XCDs
 //   by blockIdx; the lookup block count is a multiple of 8, so verify block vb
@@ -1874,19 +1875,29 @@ static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hi
 template <bool OFFS, int MODE, int FLOW>
 static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
 {
-  static const char *const names[2][2][4] = {
-      {{"", "tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,flow>"},
-       {"", "tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,offs,flow>"}},
-      {{"", "tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,flow>"},
-       {"", "tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,offs,flow>"}}};
-  const char *name = names[MODE == kHintArr][OFFS][FLOW];
+  // kernel names by FLOW: kFlowRow, kFlowSplit, kFlowSplit1, kFlowSplitX (the product), kFlowSplitX2
+  static const char *const names[2][2][5] = {
+      {{"tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow_f2>",
+        "tcp4_tas14_kernel<tl_first,verify,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,flow>",
+        "tcp4_tas14_kernel<tl_first,verify,flow_xcd2>"},
+       {"tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow_f2>",
+        "tcp4_tas14_kernel<tl_first,verify,offs,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>",
+        "tcp4_tas14_kernel<tl_first,verify,offs,flow_xcd2>"}},
+      {{"tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow_f2>",
+        "tcp4_tas14_kernel<hints,verify,flow_split1>", "tcp4_tas14_kernel<hints,verify,flow>",
+        "tcp4_tas14_kernel<hints,verify,flow_xcd2>"},
+       {"tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow_f2>",
+        "tcp4_tas14_kernel<hints,verify,offs,flow_split1>", "tcp4_tas14_kernel<hints,verify,offs,flow>",
+        "tcp4_tas14_kernel<hints,verify,offs,flow_xcd2>"}}};
+  static_assert(FLOW == kFlowRow || FLOW == kFlowSplit || FLOW == kFlowSplit1 || FLOW == kFlowSplitX ||
+                    FLOW == kFlowSplitX2, "a row form of the RX pass");
+  const int fi = FLOW == kFlowRow ? 0 : FLOW == kFlowSplit ? 1 : FLOW == kFlowSplit1 ? 2 : FLOW == kFlowSplitX ? 3 : 4;
+  const char *name = names[MODE == kHintArr][OFFS][fi];
   auto kern = tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kBlock, false, FLOW>;
   if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1)
     return launch_split<split_frames<FLOW>()>(name, kern, p, s, lds);
+  if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2)
+    return launch_splitx<FLOW == kFlowSplitX2 ? 2u : 1u>(name, kern, p, s, lds);
   return launch_groups(name, kern, p, s, lds);
 }
 
@@ -1898,26 +1909,27 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 26) // A/B: the lookup inside the rows
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowRow>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowRow>(p, s, lds);
-  if (variant == 27) // A/B: two frames per lookup lane
+  if (variant == 27) // A/B: two frames per lookup lane, lookup blocks over consecutive frames
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
+  if (variant == 35) // A/B: XCD-matched lookup blocks with two frames per lane
+    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX2>(p, s, lds)
+                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX2>(p, s, lds);
+  if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
+    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
+                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
   if (variant == 28 && mode == kHintArr && !OFFS) // A/B: lookup blocks after their verify blocks, same XCD
     return launch_inter("tcp4_tas14_kernel<hints,verify,flow_inter>",
                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowInter>, p, s, lds);
-  if (variant == 32 && mode == kHintArr && !OFFS) // A/B: lookup blocks first, each on its verify blocks' XCD
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow_xcd>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX>, p, s, lds);
-  if (variant == 35 && mode == kHintArr && !OFFS) // A/B: the same with two frames per lookup lane
-    return launch_splitx<2>("tcp4_tas14_kernel<hints,verify,flow_xcd2>",
-                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX2>, p, s, lds);
-  if (variant == 33 && mode == kHintArr && !OFFS) // timing only (results wrong): no bucket loads
+  // timing-only ablations of the round-2 product's lookup blocks (results
+  // wrong): 29 no frame key load, 30 no CRC, 31 no flow-state key load, 33 no
+  // bucket loads, 34 the frame key only
+  if (variant == 33 && mode == kHintArr && !OFFS)
     return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,nobucket>",
                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 8>, p, s, lds);
-  if (variant == 34 && mode == kHintArr && !OFFS) // timing only (results wrong): no loads past the frame key
+  if (variant == 34 && mode == kHintArr && !OFFS)
     return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,keyonly>",
                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 12>, p, s, lds);
-  // 29 / 30 / 31: timing-only ablations of the lookup blocks (results wrong):
-  // no frame key load / no CRC / no flow-state key load
   if (variant >= 29 && variant <= 31 && mode == kHintArr && !OFFS) {
     static const char *const nm[3] = {"tcp4_tas14_kernel<hints,verify,flow,nokey>", "tcp4_tas14_kernel<hints,verify,flow,nocrc>",
                                       "tcp4_tas14_kernel<hints,verify,flow,nofskey>"};
@@ -1932,10 +1944,13 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   (void) variant;
 #endif
   // RX bursts without a uniform length are data/ACK mixes: one frame per
-  // lookup lane (64K frames, half / all ACKs 12.8 / 8.7 us against 13.6 / 9.3
-  // with two; profiles/r02/r02cc)
-  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
-                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  // lookup lane, each lookup block over the frames of the 16 verify blocks on
+  // its own XCD, so that the verify rows find the frames' first lines in L2
+  // (64K frames, 0 / 50 / 100 % ACKs: 17.4 / 12.1 / 7.7-7.9 us against 18.3-18.6
+  // / 12.8-12.9 / 8.8-9.0 for lookup blocks over consecutive frames, and 16.9 /
+  // 13.0 / 7.1-7.3 with two frames per lane; profiles/r03/INDEX.md r03b)
+  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX>(p, s, lds)
+                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX>(p, s, lds);
 }
 
 // RX verification + flow lookup: the row kernels' selection (as
@@ -1958,14 +1973,16 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
     if (variant == 32)
       return launch_splitx<1>("tcp4_tas14_kernel<hint,verify,flow_xcd>",
                               tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX>, *p, s, lds);
-    if (variant == 35)
-      return launch_splitx<2>("tcp4_tas14_kernel<hint,verify,flow_xcd2>",
-                              tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, lds);
+    if (variant == 36) // the round-2 product: lookup blocks over consecutive frames
+      return launch_split<2>("tcp4_tas14_kernel<hint,verify,flow_split2>",
+                             tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit>, *p, s, lds);
 #endif
-    // a uniform received length is a data burst: two frames per lookup lane
-    // (17.6 against 18.1 us with one; profiles/r02/r02cc)
-    return launch_split("tcp4_tas14_kernel<hint,verify,flow>",
-                        tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit>, *p, s, lds);
+    // a uniform received length is a data burst: two frames per lookup lane,
+    // each lookup block over the frames of the 32 verify blocks on its own XCD
+    // (64K frames: 16.8 against 17.1 us with one frame per lane and 17.6-17.9
+    // with lookup blocks over consecutive frames; profiles/r03/INDEX.md r03b)
+    return launch_splitx<2>("tcp4_tas14_kernel<hint,verify,flow>",
+                            tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, lds);
   }
   if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
     const int mode = p->flen ? kHintArr : kTlFirst;

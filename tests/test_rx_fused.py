@@ -164,32 +164,33 @@ def test_rx_fused_row_variant_ab(oracle, form):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 26, 27, 28, 32, 35])
+@pytest.mark.parametrize("variant", [0, 26, 27, 28, 35, 36])
 def test_rx_fused_batch_edges(oracle, variant):
     """Batch sizes around row, block and lookup-block boundaries (16 frames
-    per verify block, 256 / 512 frames per lookup block, 128-block groups, 8 XCDs): every frame
-    verified and looked up once, in the product's split grid, the row form (A/B
-    26), the split grid with two frames per lookup lane (A/B 27), lookup blocks
-    after their verify blocks (A/B 28) and lookup blocks on their verify blocks'
-    XCD with one / two frames per lane (A/B 32 / 35)."""
+    per verify block, 256 / 512 frames per lookup block, 2048 / 4096 frames per
+    8 XCD-matched lookup blocks or per 128-block group): every frame verified
+    and looked up once, in the product's split grid (lookup blocks first, each
+    over the frames of the verify blocks on its own XCD), the row form (A/B
+    26), lookup blocks over consecutive frames with two / one frames per lane
+    (A/B 27, and 36 = the round-2 product), lookup blocks after their verify
+    blocks (A/B 28) and the product's grid with two frames per lookup lane (A/B
+    35)."""
     import contextlib
     import torch
     from tas_amd import xsum
-    frames, rcv, ht, fs, nflows, _ = _burst(oracle, 4200 if variant >= 28 else 1300, 2048, seed=911)
+    frames, rcv, ht, fs, nflows, _ = _burst(oracle, 4200, 2048, seed=911)
     dev = "cuda:0"
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     fr = t(frames)
     ctx = xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()
     kernel = {0: "tcp4_tas14_kernel<hints,verify,flow>", 26: "tcp4_tas14_kernel<hints,verify,flow_row>",
               27: "tcp4_tas14_kernel<hints,verify,flow_f2>", 28: "tcp4_tas14_kernel<hints,verify,flow_inter>",
-              32: "tcp4_tas14_kernel<hints,verify,flow_xcd>", 35: "tcp4_tas14_kernel<hints,verify,flow_xcd2>"}[variant]
+              35: "tcp4_tas14_kernel<hints,verify,flow_xcd2>", 36: "tcp4_tas14_kernel<hints,verify,flow_split1>"}[variant]
     with ctx:
         xsum.set_kernel_variant(variant)
         try:
-            ns = (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300)
-            if variant >= 28:  # 2048 frames per group of 128 verify blocks / of 8 XCD-matched lookup blocks
-                ns += (2047, 2048, 2049, 2100, 4095, 4096, 4097, 4200)
-            for n in ns:
+            for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096,
+                      4097, 4200):
                 exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
                 exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, rcv[:n].astype(np.uint32), stride=2048)
                 flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048,
