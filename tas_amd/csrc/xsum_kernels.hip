@@ -1047,6 +1047,11 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 //   that XCD's L2, where the verify row's chunk-0 load then finds it.
 //   kFlowSplitX2: the same with two frames per lookup lane (32 verify blocks
 //   per lookup block).
+// LOPT bit of tcp4_tas14_kernel<kHintArr> (A/B): prefetch the hint line one
+// generation ahead; a generation = 256 CUs x 8 blocks of 16 rows (gfx950 at 8
+// waves per SIMD)
+constexpr int kHintPrefetch = 16;
+constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
 enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
 template <uint32_t F>
@@ -1275,6 +1280,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
+  // LOPT & kHintPrefetch (A/B, kHintArr): after its chunk loads, one lane per
+  // hint line (32 rows) loads the line of the row one generation of resident
+  // rows later, so that row's first load (its hint) is an L2 hit (block b and
+  // block b + kPrefetchRows / 16 run on the same XCD)
+  uint32_t pf = 0;
+  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS) {
+    const uint32_t j = i + kPrefetchRows;
+    if (gl == 0 && (i & 31u) == 0u && j < p.n)
+      pf = ldg(p.flen, j);
+  }
   // FLOW: the flow-state key load goes out while the chunks are in flight (the
   // bucket, issued before them, has returned first)
   uint32_t ffid = 0;
@@ -1291,6 +1306,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
   }
   tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
+  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS)
+    asm volatile("" ::"v"(pf)); // the prefetch is not dead code
   if constexpr (FLOW == kFlowRow) {
     const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16);
     const bool match = gl < kNb && fcand && ck.x == fkey.y && ck.y == fkey.x && ck.z == ports;
@@ -1918,6 +1935,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 37 && mode == kHintArr && !OFFS) // A/B: the product with the next generation's hint lines prefetched
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prefetch>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kHintPrefetch>, p, s, lds);
   if (variant == 28 && mode == kHintArr && !OFFS) // A/B: lookup blocks after their verify blocks, same XCD
     return launch_inter("tcp4_tas14_kernel<hints,verify,flow_inter>",
                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowInter>, p, s, lds);
@@ -2032,6 +2052,10 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
 #ifdef TASX_AB
     if (variant == 9) // A/B: total_length first whatever the call carries
       mode = kTlFirst;
+    if (variant == 37 && mode == kHintArr && !p->off) // next generation's hint lines prefetched
+      return launch_groups("tcp4_tas14_kernel<hints,verify,prefetch>",
+                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
+                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
 #endif
     return p->off ? launch_tas14_verify<true>(*p, mode, s) : launch_tas14_verify<false>(*p, mode, s);
   }
@@ -2133,6 +2157,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   // 64 / 128 / 512 / 1024 threads instead of 256
   // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
   // in blocks of 64 / 128 / 512 / 1024 threads
+  if (variant == 37 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, next generation's hint lines prefetched
+    return launch_groups("tcp4_tas14_kernel<hints,prefetch>",
+                         tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
+                         TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
   if (variant >= 22 && variant <= 25 && p->flen && tas14_nohint_ok(*p)) {
     switch (variant) {
     case 22: return launch_groups<16, 64>("tcp4_tas14_kernel<hints,bs64>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 64>, *p, s);
