@@ -78,7 +78,7 @@ int tasx_set_diag_buffer(void *dev_buf)
   g_diag = (uint64_t *) dev_buf;
   return 0;
 }
-#define TASX_MAX_VARIANT 40
+#define TASX_MAX_VARIANT 48
 #else
 #define TASX_MAX_VARIANT 7
 #endif

@@ -903,11 +903,21 @@ __device__ __forceinline__ u32x4 lds_window_at(const uint8_t *wp, uint32_t r)
 }
 
 // 16 bytes at LDS byte offset o of the slice: five dwords and a funnel shift
+// (B128: the first four by one ds_read_b128 at the dword-aligned address --
+// A/B only: it relies on the LDS running in unaligned mode)
+template <bool B128 = false>
 __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
 {
   const uint32_t *w = (const uint32_t *) (sl + (o & ~3u));
   const uint32_t r = o & 3u;
-  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  uint32_t w0, w1, w2, w3;
+  if constexpr (B128) {
+    const u32x4 q = *(const u32x4 *) w;
+    w0 = q.x, w1 = q.y, w2 = q.z, w3 = q.w;
+  } else {
+    w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  }
+  const uint32_t w4 = w[4];
   return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
                __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
 }
@@ -916,7 +926,8 @@ __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
 // (piece A only) -- both timing only, results wrong -- 4 = the first block
 // stored non-temporal too (correct), 8 = the access pattern alone (timing
 // only: the aligned source chunks stored as loaded, no LDS realignment or
-// splice; bench.py's tx_segment pattern_ceiling)
+// splice; bench.py's tx_segment pattern_ceiling), 16 = windows read back by
+// ds_read_b128 + ds_read_b32 (correct where the LDS runs in unaligned mode)
 template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
@@ -1014,7 +1025,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       for (int u = 0; u < 6; ++u) {
         const int j0 = 16 * (16 * u + kh) - 66;
         const int o = min(o0 + 256 * u + (j0 >= wrapc ? dW : 0), kLdsSlice - 20);
-        w[u] = (OPT & 8) ? a[u] : lds_window(sl, (uint32_t) o);
+        w[u] = (OPT & 8) ? a[u] : lds_window<(OPT & 16) != 0>(sl, (uint32_t) o);
       }
       // the chunk holding the wrap (a row whose payload wraps off a chunk
       // boundary): its bytes from wrapc - j0 on are piece B's
@@ -1025,7 +1036,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         for (int u = 0; u < 6; ++u) {
           const int j0 = 16 * (16 * u + kh) - 66;
           if (strad && u == (ks >> 4))
-            w[u] = splice(w[u], lds_window(sl, (uint32_t) min(max(oB + j0 - wrapc, 0), kLdsSlice - 20)), wrapc - j0, 16);
+            w[u] = splice(w[u], lds_window<(OPT & 16) != 0>(sl, (uint32_t) min(max(oB + j0 - wrapc, 0), kLdsSlice - 20)),
+                          wrapc - j0, 16);
         }
       }
       // slot 0: header chunks 0..3 as read, chunk 4 = header bytes 64-65 +
@@ -1384,6 +1396,7 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 32: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 33: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 34: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb,nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 3>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 41: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<b128>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 40: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU

@@ -70,10 +70,12 @@ def test_generator_wraps_and_flows():
 # ---------------------------------------------------------------------------
 # GPU parity
 
-# "r2": the round-2 product, tx_segment_tas_kernel (unaligned non-temporal
-# window loads; A/B variant TASX_TXSEG_DEBUG=30 of libtasx_ab.so), on the same
-# cases as the product (tx_segment_lds_kernel)
-IMPLS = ["product", "r2"]
+# A/B variants of libtasx_ab.so (TASX_TXSEG_DEBUG) run on the same cases as
+# the product (tx_segment_lds_kernel): "r2" = 30, the round-2 product
+# tx_segment_tas_kernel (unaligned non-temporal window loads); "b128" = 41,
+# the product with its LDS windows read back by ds_read_b128
+IMPLS = ["product", "r2", "b128"]
+AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel"), "b128": ("41", "tx_segment_lds_kernel<b128>")}
 
 
 def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):
@@ -81,12 +83,13 @@ def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, im
     from tas_amd import xsum
     if impl == "product":
         return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
-    os.environ["TASX_TXSEG_DEBUG"] = "30"
+    dbg, kernel = AB_IMPLS[impl]
+    os.environ["TASX_TXSEG_DEBUG"] = dbg
     try:
         with xsum.using_library(xsum.AB_LIB_PATH):
             r = _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
             if ip_off == 14 and l4_off == 34:
-                assert xsum.last_kernel() == "tx_segment_tas_kernel", xsum.last_kernel()
+                assert xsum.last_kernel() == kernel, xsum.last_kernel()
             return r
     finally:
         del os.environ["TASX_TXSEG_DEBUG"]

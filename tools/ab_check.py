@@ -32,7 +32,7 @@ def main():
                 xsum.tcp4_cksum_batch(fr, mw.n, stride=mw.stride, frame_len=mw.flen, room=mw.stride, inplace=True,
                                       want_out=False)
                 flags = torch.full((mw.n,), 0x5a, dtype=torch.uint8, device="cuda")
-                xsum.tcp4_verify_batch(fr, mw.n, stride=mw.stride, frame_len=mw.flen, flags=flags)
+                xsum.tcp4_verify_batch(fr, mw.n, stride=mw.stride, frame_len=mw.flen, out=flags)
                 torch.cuda.synchronize()
                 res[var] = (out.cpu(), flags.cpu(), k_tx, xsum.last_kernel())
             finally:
