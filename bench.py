@@ -459,11 +459,12 @@ def txseg_pattern_ceiling(tw: "TxSegWorkload", avg_us: float, launches: int = 10
     R = len(tw.shms)
     old = os.environ.get("TASX_TXSEG_DEBUG")
     os.environ["TASX_TXSEG_DEBUG"] = "40"  # read by the A/B build at each call
-    frames = [b.clone() for b in tw.bufs[:2]]  # the pattern stores unrealigned bytes: not the checked frames
 
+    # the same rotation of shm regions and frame buffers as the leg (the
+    # pattern stores unrealigned bytes: the leg's frames are not checked after it)
     def pat(k):
-        rc = ab.tasx_tx_segment_batch_dev(tw.shms[k % R].data_ptr(), tw.shm_len, frames[k % 2].data_ptr(),
-                                          tw.segs.data_ptr(), tw.n, IP_OFF, L4_OFF, tw.outs[k % 2].data_ptr(), s)
+        rc = ab.tasx_tx_segment_batch_dev(tw.shms[k % R].data_ptr(), tw.shm_len, tw.bufs[k % R].data_ptr(),
+                                          tw.segs.data_ptr(), tw.n, IP_OFF, L4_OFF, tw.outs[k % R].data_ptr(), s)
         if rc:
             raise xsum.TasxError(rc, "tasx_tx_segment_batch_dev (pattern)")
     try:
@@ -482,7 +483,6 @@ def txseg_pattern_ceiling(tw: "TxSegWorkload", avg_us: float, launches: int = 10
         else:
             os.environ["TASX_TXSEG_DEBUG"] = old
     us = e0.elapsed_time(e1) * 1e3 / launches
-    del frames
     return {"bound": "the access pattern", "us": round(us, 3), "frac": round(us / avg_us, 4),
             "kernel": "tx_segment_lds_kernel<pattern> (libtasx_ab.so): the product's loads and stores, "
                       "no realignment through LDS"}
@@ -1517,10 +1517,10 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         cc = copy_ceiling(int(tw.block_floor["bytes"]) // 2)
         cc["alg_frac_of_copy"] = round(txseg["roofline"]["achieved"] / cc["GBps"], 4)
         txseg["copy_ceiling"] = cc
-        if not rehearse:
-            txseg["pattern_ceiling"] = txseg_pattern_ceiling(tw, txseg["roofline"]["launch_avg_us"])
         if rank == 0 and ws == 1 and not args.no_cpu_baseline:
             txseg["cpu_baseline"] = tw.cpu_check(3.0)
+        if not rehearse:  # last: it overwrites the leg's frames
+            txseg["pattern_ceiling"] = txseg_pattern_ceiling(tw, txseg["roofline"]["launch_avg_us"])
         del tw
         torch.cuda.empty_cache()
 

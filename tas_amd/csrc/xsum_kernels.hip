@@ -1723,6 +1723,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
 {
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  if constexpr (CHAIN == 2) {
+    // two frames per row, i and i + n / 2 (rounded up): both hints, then both
+    // frames' chunk loads, one generation of resident rows for 64K frames
+    const uint32_t half = (p.n + 1u) / 2u;
+    if (i >= half)
+      return;
+    const uint32_t i2 = min(i + half, p.n - 1u);
+    const uint32_t h1 = ldg(p.flen, i), h2 = ldg(p.flen, i2);
+    uint32_t x1 = 0, x2 = 0;
+    u32x4 v1[6], v2[6];
+    {
+      const uint32_t a1 = i * (uint32_t) p.stride + (p.ip_off & ~15u), a2 = i2 * (uint32_t) p.stride + (p.ip_off & ~15u);
+      const uint32_t hl1 = h1 > p.ip_off + 20u ? min(h1 - p.ip_off, 1522u) : 20u;
+      const uint32_t hl2 = h2 > p.ip_off + 20u ? min(h2 - p.ip_off, 1522u) : 20u;
+      const uint32_t l1 = a1 + 16u * ((14u + hl1 - 1u) >> 4), l2 = a2 + 16u * ((14u + hl2 - 1u) >> 4);
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+        v1[u] = ld16nt_off(p.base, min(a1 + 16u * (uint32_t) gl + 256u * u, l1));
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+        v2[u] = ld16nt_off(p.base, min(a2 + 16u * (uint32_t) gl + 256u * u, l2));
+    }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      x1 ^= v1[u].x ^ v1[u].y ^ v1[u].z ^ v1[u].w;
+      x2 ^= v2[u].x ^ v2[u].y ^ v2[u].z ^ v2[u].w;
+    }
+    x1 = row_sum16(x1);
+    x2 = row_sum16(x2);
+    if (gl == 15) {
+      stg((uint32_t *) p.out, i, x1);
+      if (i + half < p.n)
+        stg((uint32_t *) p.out, i2, x2);
+    }
+    return;
+  }
   if (i >= p.n)
     return;
   const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
@@ -1766,6 +1802,16 @@ extern "C" int tasx_ab_tcp4_mix_pattern(const void *base, uint64_t stride, uint3
   if (!out || !flen || !base || (ip_off & 15u) != 14u || (stride & 15u) || stride < 1536u ||
       (uint64_t) n * stride > 0xffffffffull || ((uintptr_t) base & 15u))
     return -EINVAL;
+  if (chain == 2) { // two frames per row: half the rows
+    tasx_tcp4_params q = p;
+    q.n = (n + 1u) / 2u;
+    const uint64_t blocks = ((uint64_t) q.n + kBlock / 16 - 1) / (kBlock / 16);
+    if (blocks == 0)
+      return 0;
+    t_last_kernel = "tcp4_mix_pattern_kernel<pair>";
+    hipLaunchKernelGGL(tcp4_mix_pattern_kernel<2>, dim3((uint32_t) blocks), dim3(kBlock), 0, (hipStream_t) stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
   return chain ? launch_groups("tcp4_mix_pattern_kernel<chain>", tcp4_mix_pattern_kernel<1>, p, (hipStream_t) stream, 0u)
                : launch_groups("tcp4_mix_pattern_kernel", tcp4_mix_pattern_kernel<0>, p, (hipStream_t) stream, 0u);
 }
