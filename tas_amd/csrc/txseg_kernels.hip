@@ -1396,6 +1396,9 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 32: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 1>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 33: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 2>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 34: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nofb,nowrap>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 3>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 42 / 43: the access pattern alone (40) at 8 / 6 waves per SIMD (the pattern uses no LDS)
+  case 42: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern,wpe8>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 8, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  case 43: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern,wpe6>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 6, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 41: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<b128>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 40: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
