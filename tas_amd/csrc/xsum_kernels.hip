@@ -897,7 +897,7 @@ enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
 // the general body for a row the fast path cannot take.
-template <int U, int MODE, bool VERIFY, bool OFFS, bool FALLBACK = true>
+template <int U, int MODE, bool VERIFY, bool OFFS, bool FALLBACK = true, bool ROWFB = false>
 __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t i, int gl, const uint8_t *fb,
                                              uint32_t a0, uint32_t hend, bool in_range, const u32x4 (&v)[U])
 {
@@ -979,7 +979,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
     const int gbase = (threadIdx.x & 63) & ~15;
     const bool rbad = (MODE == kHint || kArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
     if (rbad) {
-      if constexpr (OFFS)
+      if constexpr (OFFS || ROWFB) // ROWFB (A/B): the any-layout row body in stride mode too
         tcp4_frame_row<3, VERIFY>(p, i, gl);
       else
         tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
@@ -1051,6 +1051,10 @@ __device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
 // generation ahead; a generation = 256 CUs x 8 blocks of 16 rows (gfx950 at 8
 // waves per SIMD)
 constexpr int kHintPrefetch = 16;
+// LOPT bit (A/B): a stride-mode row the fast path cannot take is redone by the
+// any-layout row body (tcp4_frame_row, as the OFFS forms) instead of
+// tcp4_tas_frame, whose registers spill at 8 waves per SIMD
+constexpr int kRowFallback = 32;
 constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
 enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
@@ -1305,7 +1309,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                               p.fs_key_off);
     }
   }
-  tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
+  tas14_finish<U, MODE, VERIFY, OFFS, true, (LOPT & kRowFallback) != 0>(p, i, gl, fb, a0, hend, in_range, v);
   if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS)
     asm volatile("" ::"v"(pf)); // the prefetch is not dead code
   if constexpr (FLOW == kFlowRow) {
@@ -1981,6 +1985,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 38 && mode == kHintArr && !OFFS) // A/B: the product with the row-body fallback
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,rowfb>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kRowFallback>, p, s, lds);
   if (variant == 37 && mode == kHintArr && !OFFS) // A/B: the product with the next generation's hint lines prefetched
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prefetch>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kHintPrefetch>, p, s, lds);
@@ -2098,6 +2105,10 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
 #ifdef TASX_AB
     if (variant == 9) // A/B: total_length first whatever the call carries
       mode = kTlFirst;
+    if (variant == 38 && mode == kHintArr && !p->off) // the row-body fallback
+      return launch_groups("tcp4_tas14_kernel<hints,verify,rowfb>",
+                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
+                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
     if (variant == 37 && mode == kHintArr && !p->off) // next generation's hint lines prefetched
       return launch_groups("tcp4_tas14_kernel<hints,verify,prefetch>",
                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
@@ -2203,6 +2214,10 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   // 64 / 128 / 512 / 1024 threads instead of 256
   // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
   // in blocks of 64 / 128 / 512 / 1024 threads
+  if (variant == 38 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, the row-body fallback
+    return launch_groups("tcp4_tas14_kernel<hints,rowfb>",
+                         tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
+                         TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
   if (variant == 37 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, next generation's hint lines prefetched
     return launch_groups("tcp4_tas14_kernel<hints,prefetch>",
                          tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
