@@ -1055,6 +1055,10 @@ constexpr int kHintPrefetch = 16;
 // any-layout row body (tcp4_frame_row, as the OFFS forms) instead of
 // tcp4_tas_frame, whose registers spill at 8 waves per SIMD
 constexpr int kRowFallback = 32;
+// LOPT bit (A/B, timing only): a split grid's verify blocks exit at once
+constexpr int kLookupOnly = 64;
+// LOPT bit (A/B, timing only): a split grid's lookup blocks exit at once
+constexpr int kVerifyOnly = 128;
 constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
 enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
@@ -1111,6 +1115,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     constexpr uint32_t kF = FLOW == kFlowSplitX2 ? 2u : 1u;
     const uint32_t nl = splitx_lookup_blocks<kF>((p.n + BS / 16 - 1u) / (BS / 16));
     if (blockIdx.x < nl) {
+      if constexpr ((LOPT & kVerifyOnly) != 0)
+        return; // A/B timing: the verify blocks alone
       // lane t, frame f: row t % 16 of verify block 8 (16 F (b / 8) + 16 f + t / 16) + b % 8 (past the batch: no store)
       const uint32_t b = blockIdx.x;
       uint32_t i0[kF];
@@ -1120,6 +1126,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       flow_lookup_lanes_at<kF, BS, LOPT>(p, i0);
       return;
     }
+    if constexpr ((LOPT & kLookupOnly) != 0)
+      return; // A/B timing: the lookup blocks alone
     vb = blockIdx.x - nl;
   }
   if constexpr (FLOW == kFlowInter) {
@@ -1985,6 +1993,12 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 40 && mode == kHintArr && !OFFS) // A/B timing: the product's verify blocks alone (results wrong)
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,verify_only>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kVerifyOnly>, p, s, lds);
+  if (variant == 39 && mode == kHintArr && !OFFS) // A/B timing: the product's lookup blocks alone (results wrong)
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,lookup_only>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLookupOnly>, p, s, lds);
   if (variant == 38 && mode == kHintArr && !OFFS) // A/B: the product with the row-body fallback
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,rowfb>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kRowFallback>, p, s, lds);
