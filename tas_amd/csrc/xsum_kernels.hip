@@ -1059,6 +1059,8 @@ constexpr int kRowFallback = 32;
 constexpr int kLookupOnly = 64;
 // LOPT bit (A/B, timing only): a split grid's lookup blocks exit at once
 constexpr int kVerifyOnly = 128;
+// LOPT bit (A/B): a split grid's lookup waves run at the highest issue priority
+constexpr int kLookupPrio = 256;
 constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
 enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
@@ -1117,6 +1119,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (blockIdx.x < nl) {
       if constexpr ((LOPT & kVerifyOnly) != 0)
         return; // A/B timing: the verify blocks alone
+      if constexpr ((LOPT & kLookupPrio) != 0)
+        __builtin_amdgcn_s_setprio(3); // A/B: the lookup waves' instructions issue first
       // lane t, frame f: row t % 16 of verify block 8 (16 F (b / 8) + 16 f + t / 16) + b % 8 (past the batch: no store)
       const uint32_t b = blockIdx.x;
       uint32_t i0[kF];
@@ -1993,6 +1997,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 41 && mode == kHintArr && !OFFS) // A/B: the product with the lookup waves at issue priority 3
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prio>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLookupPrio>, p, s, lds);
   if (variant == 40 && mode == kHintArr && !OFFS) // A/B timing: the product's verify blocks alone (results wrong)
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,verify_only>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kVerifyOnly>, p, s, lds);
