@@ -1105,7 +1105,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // they start at once and overlap the verify blocks instead of forming the
     // grid's tail (interleaved one per BS frames they did: DESIGN.md 5.2)
     constexpr uint32_t kF = split_frames<FLOW>(); // frames per lookup lane (flow_kernels.hip: kFlowFramesPerLane)
-    const uint32_t nl = (p.n + BS * kF - 1u) / (BS * kF);
+    const uint32_t nl = (uint32_t) (((uint64_t) p.n + BS * kF - 1u) / (BS * kF)); // 64-bit: n near 2^32
     if (blockIdx.x < nl) {
       flow_lookup_lanes<kF, BS, LOPT>(p, blockIdx.x);
       return;
@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2) {
     static_assert(BS == 256, "16 verify rows per block, one lookup lane per row of 16 blocks");
     constexpr uint32_t kF = FLOW == kFlowSplitX2 ? 2u : 1u;
-    const uint32_t nl = splitx_lookup_blocks<kF>((p.n + BS / 16 - 1u) / (BS / 16));
+    const uint32_t nl = splitx_lookup_blocks<kF>((uint32_t) (((uint64_t) p.n + BS / 16 - 1u) / (BS / 16)));
     if (blockIdx.x < nl) {
       if constexpr ((LOPT & kVerifyOnly) != 0)
         return; // A/B timing: the verify blocks alone
