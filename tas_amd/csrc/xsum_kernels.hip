@@ -1061,6 +1061,24 @@ constexpr int kLookupOnly = 64;
 constexpr int kVerifyOnly = 128;
 // LOPT bit (A/B): a split grid's lookup waves run at the highest issue priority
 constexpr int kLookupPrio = 256;
+// LOPT bit (A/B, kHintArr): rows of the second generation of resident blocks
+// take the other half of the hint lines the first generation read (block b
+// and block b + kGenBlocks, same XCD), so their hint loads hit L2 -- no extra
+// instruction, unlike kHintPrefetch.  A generation = 256 CUs x 8 blocks.
+constexpr int kLinePair = 512;
+constexpr uint32_t kGenBlocks = 256u * 8u;
+// frame of row `row` (of 16) in verify block vb of nblk, kLinePair order:
+// blocks 2kG + r and (2k + 1)G + r share hint line kG + r (32 frames); blocks
+// past the last whole pair of generations keep the identity order
+__device__ __forceinline__ uint32_t line_pair_frame(uint32_t vb, uint32_t row, uint32_t nblk)
+{
+  constexpr uint32_t G = kGenBlocks;
+  const uint32_t P = nblk / (2u * G);
+  if (vb >= 2u * G * P)
+    return vb * 16u + row;
+  const uint32_t g = vb / G, r = vb % G;
+  return 32u * ((g / 2u) * G + r) + 16u * (g & 1u) + row;
+}
 constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
 enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
@@ -1125,8 +1143,12 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const uint32_t b = blockIdx.x;
       uint32_t i0[kF];
 #pragma unroll
-      for (uint32_t f = 0; f < kF; ++f)
-        i0[f] = (8u * (16u * kF * (b / 8u) + 16u * f + threadIdx.x / 16u) + (b & 7u)) * (BS / 16) + (threadIdx.x & 15u);
+      for (uint32_t f = 0; f < kF; ++f) {
+        const uint32_t vbk = 8u * (16u * kF * (b / 8u) + 16u * f + threadIdx.x / 16u) + (b & 7u);
+        i0[f] = vbk * (BS / 16) + (threadIdx.x & 15u);
+        if constexpr ((LOPT & kLinePair) != 0) // the verify rows' frame order (past the batch: still >= n)
+          i0[f] = line_pair_frame(vbk, threadIdx.x & 15u, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
+      }
       flow_lookup_lanes_at<kF, BS, LOPT>(p, i0);
       return;
     }
@@ -1147,6 +1169,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     vb = g * kInterV + r;
   }
   uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
+  if constexpr ((LOPT & kLinePair) != 0 && MODE == kHintArr && BS == 256)
+    i = line_pair_frame(vb, threadIdx.x / 16, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
   uint32_t hs = 0; // kHintArrS: the row's hint
   if constexpr (MODE == kHintArrS) {
     // The block's rows take its frames long ones first (stable), so that the
@@ -1997,6 +2021,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 42 && mode == kHintArr && !OFFS) // A/B: the product with line-paired generations
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,linepair>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLinePair>, p, s, lds);
   if (variant == 41 && mode == kHintArr && !OFFS) // A/B: the product with the lookup waves at issue priority 3
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prio>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLookupPrio>, p, s, lds);
@@ -2126,6 +2153,10 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
 #ifdef TASX_AB
     if (variant == 9) // A/B: total_length first whatever the call carries
       mode = kTlFirst;
+    if (variant == 42 && mode == kHintArr && !p->off) // line-paired generations
+      return launch_groups("tcp4_tas14_kernel<hints,verify,linepair>",
+                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kLinePair>, *p, s,
+                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
     if (variant == 38 && mode == kHintArr && !p->off) // the row-body fallback
       return launch_groups("tcp4_tas14_kernel<hints,verify,rowfb>",
                            tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
@@ -2235,6 +2266,13 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   // 64 / 128 / 512 / 1024 threads instead of 256
   // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
   // in blocks of 64 / 128 / 512 / 1024 threads
+  if (variant == 42 && p->flen && !tas14_ok(*p) && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) // hints, line-paired generations
+    return p->off ? launch_groups("tcp4_tas14_kernel<hints,offs,linepair>",
+                                  tcp4_tas14_kernel<6, kHintArr, false, 8, true, kBlock, false, kFlowNone, kLinePair>, *p, s,
+                                  TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u))
+                  : launch_groups("tcp4_tas14_kernel<hints,linepair>",
+                                  tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kLinePair>, *p, s,
+                                  TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
   if (variant == 38 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, the row-body fallback
     return launch_groups("tcp4_tas14_kernel<hints,rowfb>",
                          tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
