@@ -722,7 +722,7 @@ def mix_bounds(mw: "FlushMixWorkload", launches: int = 200) -> dict:
         return e0.elapsed_time(e1) * 1e3 / launches
 
     pattern_us, chain_us = timed(0), timed(1)
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     rows_in_flight = cus * 4 * 8 * 4  # CUs x SIMDs x 8 waves x 4 rows of 16 lanes
     gens = -(-mw.n // rows_in_flight)
     return {"pattern_us": round(pattern_us, 3), "chain_us": round(chain_us, 3),
