@@ -8,17 +8,22 @@ for path in sys.argv[1:]:
     print(f"== {path}: value {d['value']} GiB/s, ms_per_step {d['ms_per_step'] * 1e3:.3f} us, "
           f"launch_avg {d['roofline']['launch_avg_us']} us, frac {d['roofline']['frac']}, "
           f"traffic {d['roofline'].get('traffic')}, kernel {d.get('kernel')}, "
-          f"pattern_ceiling {d['roofline'].get('pattern_ceiling', {}).get('us')} us")
-    for k in ("tcp4_nohint", "tcp4_frames_only", "rx_verify", "flush_mix", "rx_verify_mix", "raw", "tx_segment", "flow_lookup"):
+          f"pattern_ceiling {(d['roofline'].get('pattern_ceiling') or {}).get('us')} us")
+    for k in ("tcp4_nohint", "tcp4_frames_only", "rx_verify", "flush_mix", "rx_verify_mix", "raw", "tx_segment", "flow_lookup",
+              "rx_pass"):
         v = d.get(k)
         if not v:
             continue
         r = v["roofline"]
         extra = ""
-        if k == "tx_segment" and v.get("pmc"):
+        if k in ("tx_segment", "rx_pass") and r.get("traffic"):
             extra = f" traffic/alg {r['traffic'] / r['algorithmic_bytes_per_launch']:.3f}"
         if k == "tx_segment" and v.get("copy_ceiling"):
-            extra += f" copy_ceiling {v['copy_ceiling']}"
+            extra += f" copy_ceiling {v['copy_ceiling'].get('us')} us"
+        if k == "tx_segment" and v.get("pattern_ceiling"):
+            extra += f" pattern_ceiling {v['pattern_ceiling'].get('us')} us"
+        if k in ("flush_mix", "rx_verify_mix") and r.get("latency"):
+            extra = f" latency-roofline frac {r['latency'].get('frac')} of-pattern {r['latency'].get('frac_of_pattern')}"
         if k == "flow_lookup":
             extra = f" line {v.get('line_roofline', {}).get('frac')} ceiling {v.get('pattern_ceiling')}"
         print(f"  {k:17s} {v['value']:8.1f} GiB/s  step {v['ms_per_step'] * 1e3:7.3f} us  launch {r['launch_avg_us']:7.3f} us"
