@@ -4,7 +4,8 @@
 # side read requests by size (one counter group per rocprofv3 run), and the
 # XCD-matched split grid checked bit-exact against the product
 # (tools/rx_check.py).  Usage: bash tools/rx_split.sh TAG VARIANT...
-#   0 product, 32 lookup blocks on their verify blocks' XCD, 28 lookup blocks
+#   0 product (since r03c: lookup blocks on their verify blocks' XCD, then
+#   A/B 32; 36 = the round-2 product), 28 lookup blocks
 #   after their verify blocks, 29 no frame key load, 31 no flow-state key load,
 #   33 no bucket loads, 34 the frame key only
 set -u
@@ -13,7 +14,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp TASX_LIB=$PWD/tas_amd/_lib/libtasx_ab.so
 O=$PWD/gpurun_out/$TAG
 mkdir -p "$O"
-for v in 32 28; do
+for v in 36 28; do
   timeout -k 10 120 python tools/rx_check.py $v >> "$O/check.log" 2>&1 || { echo "check $v failed"; exit 1; }
 done
 cat "$O/check.log"
