@@ -2266,6 +2266,15 @@ extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *st
   // 64 / 128 / 512 / 1024 threads instead of 256
   // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
   // in blocks of 64 / 128 / 512 / 1024 threads
+  // 43 / 44: the whole-room / total_length-first rows with the headline's
+  // residency (no waves-per-EU floor, the 30 KiB LDS cap) instead of 8 waves per SIMD
+  if ((variant == 43 || variant == 44) && !p->flen && !tas14_ok(*p) && tas14_nohint_ok(*p)) {
+    const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
+    if (variant == 43 && from_a0 >= 1536u)
+      return launch_groups("tcp4_tas14_kernel<room,occ>", tcp4_tas14_kernel<6, kRoom, false, 1>, *p, s, kOccLds);
+    if (variant == 44)
+      return launch_groups("tcp4_tas14_kernel<tl_first,occ>", tcp4_tas14_kernel<6, kTlFirst, false, 1>, *p, s, kOccLds);
+  }
   if (variant == 42 && p->flen && !tas14_ok(*p) && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) // hints, line-paired generations
     return p->off ? launch_groups("tcp4_tas14_kernel<hints,offs,linepair>",
                                   tcp4_tas14_kernel<6, kHintArr, false, 8, true, kBlock, false, kFlowNone, kLinePair>, *p, s,

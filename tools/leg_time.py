@@ -57,6 +57,12 @@ def make(leg: str, rotate: int = 16):
     if leg == "tcp4":
         w = bench.Tcp4Workload(16, pktgen.SEED)
         return w.loop(bench.HINT), w.bytes_per_step
+    if leg == "tcp4_nohint":  # bench.py's tcp4_nohint leg: no hint, room = the mbuf data room
+        w = bench.Tcp4Workload(16, pktgen.SEED)
+        return w.loop(bench.ROOM, flen0=0, room=bench.STRIDE), w.bytes_per_step
+    if leg == "tcp4_frames_only":  # bench.py's tcp4_frames_only leg
+        w = bench.Tcp4Workload(16, pktgen.SEED)
+        return w.loop(bench.DEV, flen0=0), w.bytes_per_step
     raise SystemExit(f"unknown leg {leg}")
 
 
