@@ -405,7 +405,8 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
 // LOPT (A/B, timing only: results wrong): 1 = no frame key load (the key made
 // from the frame index), 2 = no CRC (the key's words xor-folded), 4 = no
 // flow-state key load (the first valid hash match wins), 8 = no bucket loads
-// (entry j made valid with the frame's hash, flow id (h + j) % fs_num)
+// (entry j made valid with the frame's hash, flow id (h + j) % fs_num); 1024
+// (correct) = the flow-state key loads non-temporal
 template <int F, int BS, int LOPT, typename P>
 __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F])
 {
@@ -465,11 +466,13 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
       const uint32_t ef = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
       fid[f][j] = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
       cand[f][j] = (ef & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
+      const uint8_t *fsk = p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off;
       if (LOPT & 4)
         key[f][j] = u32x3{lip[f], rip[f], ports[f]};
+      else if (LOPT & 1024) // A/B: the flow-state key lines streamed (evicted first), the buckets kept
+        key[f][j] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x3 *) fsk);
       else
-        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
-            p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
+        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) fsk;
     }
 #pragma unroll
   for (int f = 0; f < F; ++f) {

@@ -2021,6 +2021,9 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, i
   if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
     return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
                             : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
+  if (variant == 43 && mode == kHintArr && !OFFS) // A/B: the product with non-temporal flow-state key loads
+    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,fsnt>",
+                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, 1024>, p, s, lds);
   if (variant == 42 && mode == kHintArr && !OFFS) // A/B: the product with line-paired generations
     return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,linepair>",
                          tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLinePair>, p, s, lds);
