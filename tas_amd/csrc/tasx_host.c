@@ -1419,7 +1419,8 @@ int tasx_flush(unsigned ctx_id)
 #define FB_MAX 1024u     /* frames per queued batch */
 #define SWEEP_MAX 32768u /* frames per launch */
 #define SWEEP_REC 256u   /* (context, ticket) records per sweep */
-#define NSWEEP 2u
+#define NSWEEP 2u     /* sweeps in flight (the A/B build: TASX_FEEDER_SWEEPS = 2 or 4) */
+#define NSWEEP_MAX 4u /* a power of two: sweep s uses buffer s % nsweep across the uint32 wrap */
 #define MAX_DEVICES 64
 
 struct fbatch {
@@ -1445,7 +1446,8 @@ struct feeder {
   hipStream_t st;
   uint32_t *h_done, *d_done; /* one completion word per sweep buffer */
   uint32_t *d_count;         /* per sweep buffer: blocks finished (device memory) */
-  struct fsweep sw[NSWEEP];
+  uint32_t nsweep;           /* NSWEEP, or 4 (A/B) */
+  struct fsweep sw[NSWEEP_MAX];
   uint64_t sweeps, frames;   /* statistics */
 };
 
@@ -1546,10 +1548,10 @@ static int feeder_launch(struct feeder *F, struct fsweep *w, uint32_t seq)
   p.ip_off = TASX_TAS_IP_OFF;
   p.l4_off = TASX_TAS_L4_OFF;
   p.flags = TASX_F_INPLACE;
-  fused_done(&p, F->d_done + DONE_STRIDE * (seq % NSWEEP), F->d_count + DONE_STRIDE * (seq % NSWEEP), seq);
+  fused_done(&p, F->d_done + DONE_STRIDE * (seq % F->nsweep), F->d_count + DONE_STRIDE * (seq % F->nsweep), seq);
   if (tasx_launch_tcp4(&p, 0, F->st) != 0)
     return -1;
-  return tasx_last_launch_posted_done() ? 0 : post_done(F->d_done + DONE_STRIDE * (seq % NSWEEP), seq, F->st);
+  return tasx_last_launch_posted_done() ? 0 : post_done(F->d_done + DONE_STRIDE * (seq % F->nsweep), seq, F->st);
 }
 
 static void *feeder_main(void *arg)
@@ -1565,8 +1567,8 @@ static void *feeder_main(void *arg)
     /* publish completed sweeps, oldest first */
     while (published != launched) {
       const uint32_t s = published + 1;
-      struct fsweep *w = &F->sw[s % NSWEEP];
-      if (__atomic_load_n(F->h_done + DONE_STRIDE * (s % NSWEEP), __ATOMIC_ACQUIRE) != s)
+      struct fsweep *w = &F->sw[s % F->nsweep];
+      if (__atomic_load_n(F->h_done + DONE_STRIDE * (s % F->nsweep), __ATOMIC_ACQUIRE) != s)
         break;
       for (uint32_t r = 0; r < w->nrec; r++)
         __atomic_store_n(&g_ctx[w->rec_ctx[r]].fd_done, w->rec_ticket[r], __ATOMIC_RELEASE);
@@ -1577,8 +1579,8 @@ static void *feeder_main(void *arg)
       did = 1;
     }
     /* gather into a free sweep buffer and launch it */
-    if (launched - published < NSWEEP) {
-      struct fsweep *w = &F->sw[(launched + 1) % NSWEEP];
+    if (launched - published < F->nsweep) {
+      struct fsweep *w = &F->sw[(launched + 1) % F->nsweep];
       feeder_gather(F, w);
       __atomic_fetch_add(&F->gathers, 1u, __ATOMIC_RELEASE);
       if (w->nrec > 0) {
@@ -1612,7 +1614,7 @@ static void *feeder_main(void *arg)
 
 static void feeder_free(struct feeder *F)
 {
-  for (unsigned k = 0; k < NSWEEP; k++) {
+  for (unsigned k = 0; k < NSWEEP_MAX; k++) {
     if (F->sw[k].h_off)
       hipHostFree(F->sw[k].h_off);
     if (F->sw[k].h_flen)
@@ -1649,14 +1651,22 @@ int tasx_feeder_start(int device)
   }
   F->device = device;
   F->running = 1;
+  F->nsweep = NSWEEP;
+#ifdef TASX_AB
+  {
+    const char *e = getenv("TASX_FEEDER_SWEEPS"); /* A/B: 4 sweeps in flight */
+    if (e && atoi(e) == 4)
+      F->nsweep = 4u;
+  }
+#endif
   if ((e = hipSetDevice(device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&F->st, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP, hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP_MAX, hipHostMallocCoherent)) != hipSuccess ||
       (e = hipHostGetDevicePointer((void **) &F->d_done, F->h_done, 0)) != hipSuccess ||
-      (e = hipMalloc((void **) &F->d_count, 4u * DONE_STRIDE * NSWEEP)) != hipSuccess ||
-      (e = hipMemset(F->d_count, 0, 4u * DONE_STRIDE * NSWEEP)) != hipSuccess)
+      (e = hipMalloc((void **) &F->d_count, 4u * DONE_STRIDE * NSWEEP_MAX)) != hipSuccess ||
+      (e = hipMemset(F->d_count, 0, 4u * DONE_STRIDE * NSWEEP_MAX)) != hipSuccess)
     rc = hip_err(e, "feeder allocation");
-  for (unsigned k = 0; !rc && k < NSWEEP; k++) {
+  for (unsigned k = 0; !rc && k < F->nsweep; k++) {
     struct fsweep *w = &F->sw[k];
     if ((e = hipHostMalloc((void **) &w->h_off, 8u * SWEEP_MAX, 0)) != hipSuccess ||
         (e = hipHostMalloc((void **) &w->h_flen, 4u * SWEEP_MAX, 0)) != hipSuccess ||
@@ -1665,7 +1675,7 @@ int tasx_feeder_start(int device)
       rc = hip_err(e, "feeder sweep buffers");
   }
   if (!rc) {
-    memset(F->h_done, 0, 4u * DONE_STRIDE * NSWEEP);
+    memset(F->h_done, 0, 4u * DONE_STRIDE * NSWEEP_MAX);
     if (pthread_create(&F->thr, NULL, feeder_main, F) != 0)
       rc = set_err(-ENOMEM, "feeder: pthread_create failed");
   }
