@@ -8,13 +8,14 @@
 // launch, and total / K back-to-back) for several launch shapes.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o tools/bin/hbm_ceiling tools/hbm_ceiling.hip
-//   tools/bin/hbm_ceiling [bytes_per_launch] [rotations] [launches]
+//   tools/bin/hbm_ceiling [bytes_per_launch] [rotations] [launches] [all|glds|blk]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
 #include <algorithm>
+#include <string.h>
 
 #define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -77,6 +78,66 @@ __global__ __launch_bounds__(BS) void stream_blk(const u32x4 *p, uint64_t nchunk
   if (r == 0x12345678u) out[0] = r;
 }
 
+// LDS-DMA (round 4): gfx950's 16-byte global_load_lds_dwordx4
+// lands each lane's 16 bytes in LDS with no VGPR destination; one wave-instruction
+// writes 1 KiB linearly at M0.  Each wave owns a ring of D 1-KiB slots; group j
+// (64 consecutive chunks) goes to slot j % D.  The wave waits for its own oldest
+// DMA with a counted vmcnt (same-wave ordering needs no barrier), folds the slot
+// with ds_read_b128 + v_sad_u16, then refills it with group j + D.  FOLD = false
+// skips the LDS read (pure DMA issue rate).
+template <bool NT>
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr)
+{
+  uint32_t keep;
+  if constexpr (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+}
+
+template <int D, int BS, bool NT, bool FOLD>
+__global__ __launch_bounds__(BS) void stream_glds(const u32x4 *p, uint64_t ngroups, uint32_t *out)
+{
+  __shared__ u32x4 ring[BS / 64][D][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t) (uintptr_t) &ring[wave][0][0]);
+  const uint64_t W = (uint64_t) gridDim.x * (BS / 64);
+  const uint64_t g0 = __builtin_amdgcn_readfirstlane((uint32_t) (blockIdx.x * (BS / 64) + wave));
+  // groups g0, g0 + W, ...: n_it of them for this wave
+  const uint64_t n_it = g0 < ngroups ? (ngroups - g0 + W - 1) / W : 0;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < n_it) glds16<NT>(p + (g0 + d * W) * 64 + lane, lbase + d * 1024);
+  uint64_t it = 0;
+  for (; it + D < n_it; ++it) {
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D - 1) : "memory");
+    const int slot = (int) (it % D);
+    if constexpr (FOLD) {
+      u32x4 v = ring[wave][slot][lane];
+      acc = __builtin_amdgcn_sad_u16(v.x, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.y, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.z, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.w, 0, acc);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    glds16<NT>(p + (g0 + (it + D) * W) * 64 + lane, lbase + slot * 1024);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (; it < n_it; ++it) {
+    if constexpr (FOLD) {
+      u32x4 v = ring[wave][it % D][lane];
+      acc = __builtin_amdgcn_sad_u16(v.x, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.y, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.z, 0, acc);
+      acc = __builtin_amdgcn_sad_u16(v.w, 0, acc);
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 struct Res { double ev_us, wall_us; };
 
 template <typename F>
@@ -129,6 +190,16 @@ void blk_case(std::vector<u32x4 *> &buf, uint64_t nch, uint32_t *out, int R, int
   report(nm, run([&](int r) { hipLaunchKernelGGL((stream_blk<U, BS, NT>), dim3(grid), dim3(BS), 0, s, buf[r], nch, per_block, out); }, R, K, s));
 }
 
+template <int D, int BS, bool NT, bool FOLD>
+void glds_case(std::vector<u32x4 *> &buf, uint64_t nch, uint32_t *out, int R, int K, hipStream_t s, int ncu, int bpc)
+{
+  const uint64_t ngroups = nch / 64;  // whole 1-KiB groups (the tail < 1 KiB is not read)
+  int grid = ncu * bpc;
+  char nm[96];
+  snprintf(nm, sizeof nm, "glds D=%d BS=%d %s%s %d blk/CU", D, BS, NT ? "nt" : "  ", FOLD ? "" : " nofold", bpc);
+  report(nm, run([&](int r) { hipLaunchKernelGGL((stream_glds<D, BS, NT, FOLD>), dim3(grid), dim3(BS), 0, s, buf[r], ngroups, out); }, R, K, s));
+}
+
 int main(int argc, char **argv)
 {
   B = argc > 1 ? strtoull(argv[1], 0, 0) : 98304000ull;
@@ -146,6 +217,35 @@ int main(int argc, char **argv)
   hipDeviceProp_t prop; CHK(hipGetDeviceProperties(&prop, 0));
   int ncu = prop.multiProcessorCount;
   printf("CUs %d, %llu B per launch, %d rotating buffers, %d launches\n", ncu, (unsigned long long) B, R, K);
+  const char *mode = argc > 4 ? argv[4] : "all";
+  if (!strcmp(mode, "glds") || !strcmp(mode, "all")) {
+    // register-load references first, then LDS-DMA rings at several depths / residencies
+    gs_case<8, 256, false>(buf, nch, out, R, K, s, ncu, 8);
+    gs_case<8, 256, true>(buf, nch, out, R, K, s, ncu, 8);
+    gs_case<4, 256, false>(buf, nch, out, R, K, s, ncu, 16);
+    for (int bpc : {2, 4, 8}) {
+      glds_case<4, 256, false, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<4, 256, true, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<8, 256, false, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<8, 256, true, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<8, 256, true, false>(buf, nch, out, R, K, s, ncu, bpc);
+    }
+    for (int bpc : {1, 2, 4}) {
+      glds_case<16, 256, false, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<16, 256, true, true>(buf, nch, out, R, K, s, ncu, bpc);
+      glds_case<16, 512, true, true>(buf, nch, out, R, K, s, ncu, bpc);
+    }
+    glds_case<4, 1024, true, true>(buf, nch, out, R, K, s, ncu, 1);
+    glds_case<4, 1024, true, true>(buf, nch, out, R, K, s, ncu, 2);
+    if (!strcmp(mode, "glds")) return 0;
+  }
+  if (!strcmp(mode, "blk")) {  // the fastest register-load shapes only
+    for (uint64_t kib : {8, 16, 32}) {
+      blk_case<8, 256, true>(buf, nch, out, R, K, s, kib * 64);
+      blk_case<4, 256, true>(buf, nch, out, R, K, s, kib * 64);
+    }
+    return 0;
+  }
   for (int bpc : {2, 4, 8, 16}) {
     gs_case<4, 256, false>(buf, nch, out, R, K, s, ncu, bpc);
     gs_case<8, 256, false>(buf, nch, out, R, K, s, ncu, bpc);
