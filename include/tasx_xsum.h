@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 5
+#define TASX_ABI_VERSION 6
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -398,6 +398,39 @@ int tasx_feeder_stop(int device);
 int tasx_feeder_stats(int device, uint64_t *sweeps, uint64_t *frames);
 int tasx_ctx_use_feeder(unsigned ctx_id, int on);
 int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
+
+/* Flush server (ABI 6): a persistent kernel per GPU takes the flushes of
+ * every attached context from pinned host memory, so a fast-path core's
+ * tasx_flush_submit() makes NO HIP call and the GPU pays no launch per batch.
+ * Each context has a ring of TASX_SRV_RING (8) descriptor slots, up to 64
+ * frames each: submit writes the frames' offsets in the context's registered
+ * region and their ip.total_length into the next slot, the header last, and
+ * returns; workgroup (context id) of the server kernel polls that ring over
+ * PCIe, sums the frames in place and stores both checksum fields into them,
+ * then posts the ring's progress, which tasx_flush_poll/_wait read (ticket
+ * order as before; submit spins only when 8 batches are in flight).  Frames
+ * the server does not take -- outside the registered region, not TAS layout,
+ * a frame start (ip - 14) not 16-byte aligned, or total_length outside
+ * [38, 1522] -- are flushed by the context itself after its server tickets.
+ * Frames must stay unmodified until their ticket completes; a frame whose
+ * total_length changed meanwhile is left alone and the context's next
+ * poll/wait returns -EIO.  The TAS path this replaces: tx_flush
+ * (tas/fast/fastemu.c:544-566) after tcp_checksums (fast_flows.c:1058-1069).
+ *   tasx_server_start(device): launch the server kernel (TASX_MAX_CTX
+ *     workgroups of 1024 threads) and its keepalive thread; the kernel also
+ *     leaves by itself 2 s after the process stops refreshing it
+ *   tasx_server_stop(device): -EBUSY while contexts are attached; waits up
+ *     to 5 s for the kernel to leave, else -EIO
+ *   tasx_ctx_use_server(ctx, 1 / 0): attach (needs a running server and a
+ *     registered frame region below 4 GiB; not together with the feeder) /
+ *     detach (waits for the context's tickets)
+ *   tasx_server_stats: batches and frames submitted since start
+ *   tasx_ctx_server_flushes: batches the context handed to the server */
+int tasx_server_start(int device);
+int tasx_server_stop(int device);
+int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames);
+int tasx_ctx_use_server(unsigned ctx_id, int on);
+int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for tests and A/B runs.  Per calling thread (TAS runs one

@@ -23,7 +23,7 @@ LIB_AB = OUT_DIR / "libtasx_ab.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
-HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip", "flow_kernels.hip"]
+HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip", "flow_kernels.hip", "server_kernels.hip"]
 C_SRCS = ["tasx_host.c"]
 
 

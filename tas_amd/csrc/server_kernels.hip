@@ -1,0 +1,221 @@
+// server_kernels.hip -- the persistent flush server (round 4): one long-running
+// kernel per GPU that takes TAS's tx_flush batches (tas/fast/fastemu.c:544-566,
+// at most TXBUF_SIZE = 32 frames per core per loop, tas/include/fastpath.h:38)
+// straight from pinned host memory, with no HIP call on the fast-path core.
+//
+// Every deferred flush so far paid a kernel launch plus a completion round
+// trip (~13 us), more than one core's CPU checksums of
+// the same 32 frames.  Here the fast-path core writes a descriptor slot into
+// its context's ring in coherent pinned memory (frame offsets in its
+// registered mbuf region, each with its ip.total_length) and the header last;
+// workgroup r of this grid polls ring r, sums the frames in place over PCIe
+// and stores both checksum fields into them, then posts the ring's consumed
+// count.  Layout and protocol: tasx_kernels.h (TASX_SRV_*), tasx_host.c
+// (server_submit).
+//
+// Coherence without fences on the data path (MI355X_MICROARCH.md, hand-off
+// rules): every word the host writes is read with system-scope (sc0 sc1)
+// loads, so no cache level can return an older copy; frames are read by
+// sc0 sc1 nt buffer loads (a ring position reuses mbufs, so a line cached by
+// an earlier batch must never be served) and the two checksum fields are
+// written by sc0 sc1 stores (write-through to host memory).  Each wave waits
+// for its stores (vmcnt(0)), the workgroup meets at a barrier, and only then
+// does one lane store the consumed count, also sc0 sc1: the host sees the
+// count after the fields.  Descriptor words carry the 16-bit tag of their ring
+// position, so a slot read over PCIe while the host was still writing it is
+// recognised (a word with an older tag) and read again -- no separate
+// doorbell round trip.
+//
+// Exit: every wave of every workgroup leaves when the host sets the stop word,
+// or when the lease word has not changed for lease_ticks of the GPU's wall
+// clock (the host's keepalive thread bumps it every 50 ms while the server is
+// started, so this only ends a server whose process is gone).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tasx_kernels.h"
+
+#include "xsum_device.h"
+
+namespace {
+
+constexpr int kSrvBlock = 1024;           // 64 rows of 16 lanes: one frame per row
+constexpr int kSys = 1 | 16;              // cache policy sc0 sc1: system scope
+constexpr int kSysNt = kSys | 2;          // ... and non-temporal
+constexpr uint32_t kRsrcWord3 = 0x00020000u; // gfx9 buffer resource dword 3
+
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
+{
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys32(uint32_t *p, uint32_t v)
+{
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t rlane64(uint64_t x, int l)
+{
+  const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) x, l);
+  const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (x >> 32), l);
+  return ((uint64_t) hi << 32) | lo;
+}
+
+// One TAS TX frame per 16-lane row: frame start at byte fo of the region
+// (16-byte aligned; IPv4 at +14, TCP at +34), datagram length tl in
+// [38, 1522] (the host checks both).  The arithmetic of tcp4_tas14_kernel's
+// rows (xsum_kernels.hip tas14_finish, TX): lane gl holds chunks gl + 16u;
+// chunk 2's first two bytes and tcp.chksum (chunk 3, bytes 2-3) masked, lane 1
+// forms the IPv4 and pseudo-header channels with chunk 0's and chunk 2's
+// dwords moved in by DPP, bytes past the datagram come off on lane 15 (its
+// last load is the last chunk).  Returns false (no store) when the frame's own
+// total_length is not tl: the frame changed after it was submitted.
+__device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, uint32_t tl, int gl)
+{
+  constexpr int U = 6;
+  const uint32_t last = (14u + tl - 1u) >> 4, lastoff = fo + 16u * last;
+  const uint32_t lo = fo + 16u * (uint32_t) gl;
+  u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, min(lo + 256u * u, lastoff), 0, kSysNt);
+  const uint32_t tail = 14u + tl - 16u * last; // bytes of the last chunk inside, 1..16
+  const u32x4 h = v[0];
+  const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 ? 0x0000ffffu : 0xffffffffu);
+  uint32_t acc = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
+  acc = (gl < 2 || (uint32_t) gl > last) ? 0u : acc;
+  const uint32_t c0d3 = row_shr<1>(h.w), c2d0 = row_shl<1>(h.x);
+  const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u))); // src, dst
+  const uint32_t ph = sadw(h.y & 0xff000000u, addrs);                                    // + proto
+  const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));         // ip.chksum left out
+  const uint32_t tlw = h.x & 0xffffu;
+#pragma unroll
+  for (int u = 1; u < U; ++u) {
+    const uint32_t s = sad4(v[u], acc);
+    acc = ((uint32_t) gl + 16u * u <= last) ? s : acc;
+  }
+  {
+    uint32_t gm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = tail > 4u * j ? min(tail - 4u * j, 4u) : 0u;
+      gm[j] = (uint32_t) (~0ull << (8u * k));
+    }
+    const u32x4 t = v[U - 1];
+    const uint32_t g = sad4(u32x4{t.x & gm[0], t.y & gm[1], t.z & gm[2], t.w & gm[3]}, 0u);
+    acc -= gl == 15 ? g : 0u;
+  }
+  acc = row_sum16(acc);
+  const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
+  const bool ok = tl15 == tl;
+  if (gl == 15 && ok) {
+    const uint32_t ipc = inv_result(residue(fold32_to_16(ip15)));
+    const uint32_t r = fold32_to_16(acc) + fold32_to_16(ph15) + bswap16(tl - 20u);
+    const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short) ipc, rs, fo + 24u, 0, kSys);  // ip.chksum
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short) tcpc, rs, fo + 50u, 0, kSys); // tcp.chksum
+  }
+  return ok;
+}
+
+// Workgroup r serves ring r (context r).  Wave 0 polls the ring's next slot:
+// lanes read the 64 entry words, lanes 0-1 the two header words, lane 2 the
+// control word, all system scope, in one round trip; a slot is taken when the
+// header and every entry carry the position's tag.  The other 15 waves wait at
+// the barrier meanwhile (no issue slots).  Then row k sums frame k, and
+// thread 0 posts consumed = position + 1 after every wave's stores completed.
+__global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
+{
+  __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
+  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_p;
+  __shared__ uint64_t s_base;
+  const uint32_t r = blockIdx.x;
+  const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
+  uint8_t *const mem = P.mem;
+  uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
+  if (threadIdx.x == 0) {
+    s_p = (uint32_t) ld_sys64((const uint64_t *) dline); // consumed (low word): a restart continues there
+    s_bad = 0u;
+  }
+  __syncthreads();
+  uint32_t p = s_p;
+  uint64_t t_act = wall_clock64(), t_lease = t_act;
+  uint32_t lease = 0u;
+  for (;;) {
+    if (threadIdx.x < 64) {
+      for (;;) {
+        const uint8_t *slot = mem + TASX_SRV_SLOTP(r, p);
+        const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
+        const uint64_t e = ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane);
+        const uint64_t hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
+                                     : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
+        const uint64_t h0 = rlane64(hw, 0), h1 = rlane64(hw, 1), c = rlane64(hw, 2);
+        const uint32_t n = (uint32_t) (h0 & 0xffffu);
+        const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
+        if (hdr && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (e >> 48) != tag) == 0ull) {
+          if ((uint32_t) lane < n) {
+            s_off[lane] = (uint32_t) e;
+            s_tl[lane] = (uint32_t) (e >> 32) & 0xffffu;
+          }
+          if (lane == 0) {
+            s_n = n;
+            s_bytes = (uint32_t) (h0 >> 16);
+            s_base = h1 & 0xffffffffffffull;
+            s_cmd = 0u;
+          }
+          t_act = wall_clock64();
+          break;
+        }
+        // nothing yet (or the header landed before some of its entries: read
+        // the slot again at once)
+        const uint64_t now = wall_clock64();
+        if ((uint32_t) c != 0u) { // stop
+          if (lane == 0)
+            s_cmd = 1u;
+          break;
+        }
+        if ((uint32_t) (c >> 32) != lease) {
+          lease = (uint32_t) (c >> 32);
+          t_lease = now;
+        } else if (now - t_lease > P.lease_ticks) { // no keepalive: the host process is gone
+          if (lane == 0)
+            s_cmd = 2u;
+          break;
+        }
+        if (hdr)
+          continue;
+        if (now - t_act < P.hot_ticks)
+          __builtin_amdgcn_s_sleep(1);
+        else
+          __builtin_amdgcn_s_sleep(32);
+      }
+    }
+    __syncthreads();
+    if (s_cmd != 0u)
+      break;
+    const uint32_t row = threadIdx.x >> 4;
+    if (row < s_n) {
+      const uint64_t base = s_base;
+      __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (uintptr_t) base, 0, (int) s_bytes,
+                                                                    (int) kRsrcWord3);
+      const uint32_t fo = s_off[row], tl = s_tl[row];
+      const bool ok = (fo & 15u) == 0u && tl >= 38u && tl <= 1522u && srv_row(rs, fo, tl, gl);
+      if (gl == 15 && !ok)
+        atomicOr(&s_bad, 1u);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (s_bad)
+        st_sys32(dline + 1, 1u); // sticky: a frame changed after submission (or a malformed slot)
+      st_sys32(dline, p + 1u);
+    }
+    ++p;
+  }
+}
+
+} // namespace
+
+extern "C" int tasx_launch_server(const tasx_srv_params *p, void *stream)
+{
+  hipLaunchKernelGGL(flush_server_kernel, dim3(TASX_MAX_CTX), dim3(kSrvBlock), 0, (hipStream_t) stream, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

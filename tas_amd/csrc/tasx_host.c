@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -453,6 +454,13 @@ struct tasx_ctx {
   uint32_t fd_done;   /* the last of its tickets the feeder has completed (release) */
   uint32_t local_last; /* the last ticket this thread launched itself */
   uint32_t n_feeder_flushes;
+  /* flush server (tasx_ctx_use_server): batches go to ring (context id) of the
+   * GPU's persistent server kernel; no HIP call on submit */
+  struct fserver *sv;
+  uint32_t sv_pos;      /* next ring position to fill */
+  uint32_t sv_done_pos; /* positions the server has finished (as last seen) */
+  uint32_t sv_ticket[TASX_SRV_RING]; /* ticket of the batch at each ring position */
+  uint32_t n_server_flushes;
 };
 
 #define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
@@ -609,6 +617,8 @@ int tasx_ctx_destroy(unsigned ctx_id)
   hipSetDevice(c->device);
   if (c->fd)
     (void) tasx_ctx_use_feeder(ctx_id, 0);
+  if (c->sv)
+    (void) tasx_ctx_use_server(ctx_id, 0);
   (void) flush_wait(c, c->next_ticket);
   for (int s = 0; s < NSLOT; s++)
     hipStreamSynchronize(c->st[s]);
@@ -1132,8 +1142,12 @@ int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start)
 /* Complete every flush up to `upto` whose completion word has arrived, oldest
  * first (the staged path copies its results into the frames); returns 1 when
  * `upto` is complete, 0 if not yet. */
+static void server_reap(struct tasx_ctx *c);
+
 static int flush_reap(struct tasx_ctx *c, uint32_t upto)
 {
+  if (c->sv)
+    server_reap(c);
   if (c->fd) { /* tickets the feeder completed (all of its tickets before them too) */
     const uint32_t fdone = __atomic_load_n(&c->fd_done, __ATOMIC_ACQUIRE);
     if (!ticket_le(fdone, c->done_ticket))
@@ -1162,13 +1176,20 @@ static int flush_reap(struct tasx_ctx *c, uint32_t upto)
  * polls (a few microseconds) the stream is queried, so an error or a lost word
  * ends the wait instead of spinning on. */
 static int feeder_error(const struct tasx_ctx *c);
+static int server_health(const struct tasx_ctx *c);
 
 static int flush_wait(struct tasx_ctx *c, uint32_t ticket)
 {
   uint32_t k = 0;
+  int rc;
   while (!flush_reap(c, ticket)) {
     if ((++k & 4095u) == 0 && c->fd && feeder_error(c))
       return set_err(-EIO, "flush: the feeder thread failed");
+    if ((k & 4095u) == 0 && c->sv && (rc = server_health(c)) != 0)
+      return rc;
+    /* only server tickets outstanding: this context's stream has nothing to do */
+    if ((k & 4095u) == 0 && c->sv && ticket_le(c->local_last, c->done_ticket))
+      continue;
     /* only feeder tickets outstanding: this context's stream has nothing to do */
     if ((k & 4095u) == 0 && c->fd && ticket_le(c->local_last, c->done_ticket))
       continue;
@@ -1346,6 +1367,7 @@ static uint32_t staged_fit(const struct tasx_ctx *c, size_t *need)
 }
 
 static int feeder_submit(struct tasx_ctx *c);
+static int server_submit(struct tasx_ctx *c);
 
 int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket)
 {
@@ -1354,6 +1376,8 @@ int tasx_flush_submit(unsigned ctx_id, uint32_t *ticket)
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   if (c->fd && (rc = feeder_submit(c)) != 0)
+    return rc;
+  if (c->sv && (rc = server_submit(c)) != 0)
     return rc;
   if (c->npend > 0)
     HIPCHK(hipSetDevice(c->device));
@@ -1382,7 +1406,13 @@ int tasx_flush_poll(unsigned ctx_id, uint32_t ticket)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   if (!ticket_le(ticket, c->next_ticket))
     return set_err(-EINVAL, "flush ticket %u not submitted (last %u)", ticket, c->next_ticket);
-  return flush_reap(c, ticket);
+  const int done = flush_reap(c, ticket);
+  if (!done && c->sv) {
+    const int rc = server_health(c);
+    if (rc)
+      return rc;
+  }
+  return done;
 }
 
 int tasx_flush_wait(unsigned ctx_id, uint32_t ticket)
@@ -1789,6 +1819,322 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   if (feeder_flushes)
     *feeder_flushes = c->n_feeder_flushes;
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Flush server (ABI 6): one persistent kernel per GPU (server_kernels.hip)
+ * serves every attached context.  A context's tasx_flush_submit() writes each
+ * batch of up to TASX_SRV_FB frames into the next slot of its own ring in
+ * coherent pinned memory -- the entries (frame offset in its registered
+ * region | ip.total_length | tag), then the region word, then the header
+ * (release) -- and returns: no HIP call, no lock, no launch.  Workgroup r of
+ * the kernel polls ring r, checksums the frames in place over PCIe and posts
+ * the ring's consumed count, which tasx_flush_poll/_wait read.  A keepalive
+ * thread bumps the lease word every 10 ms; the kernel leaves on the stop word
+ * or, when the lease has not moved for 2 s, on its own (the process is gone). */
+
+#define SRV_LEASE_S 2u
+#define SRV_HOT_US 200u
+#define SRV_STOP_WAIT_MS 5000u
+
+struct fserver {
+  int device;
+  hipStream_t st;
+  uint8_t *h_mem, *d_mem; /* coherent pinned block (tasx_kernels.h TASX_SRV_*) */
+  uint32_t attached;      /* bit r: ring r serves a context */
+  int keep_run;
+  pthread_t keep;
+  uint64_t batches, frames; /* submitted (statistics) */
+};
+
+static struct fserver *g_server[MAX_DEVICES];
+static pthread_mutex_t g_server_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static uint32_t *srv_dline(const struct fserver *S, unsigned r)
+{
+  return (uint32_t *) (S->h_mem + TASX_SRV_DONE(r));
+}
+
+static void *server_keepalive(void *arg)
+{
+  struct fserver *S = arg;
+  uint32_t *lease = (uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1;
+  uint32_t k = 1;
+  const struct timespec ts = {0, 10 * 1000 * 1000};
+  while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
+    __atomic_store_n(lease, k++, __ATOMIC_RELEASE);
+    nanosleep(&ts, NULL);
+  }
+  return NULL;
+}
+
+/* process exit with a server still started: stop the kernel first (the
+ * runtime's own teardown would otherwise wait for it until the lease ran out) */
+static void server_atexit(void)
+{
+  for (int d = 0; d < MAX_DEVICES; d++) {
+    struct fserver *S = g_server[d];
+    if (S) {
+      __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
+      __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+    }
+  }
+}
+
+static void server_free(struct fserver *S)
+{
+  if (S->h_mem)
+    hipHostFree(S->h_mem);
+  if (S->st)
+    hipStreamDestroy(S->st);
+  free(S);
+}
+
+/* 0 while the server kernel runs and has flagged no error */
+static int server_health(const struct tasx_ctx *c)
+{
+  const unsigned id = (unsigned) (c - g_ctx);
+  if (__atomic_load_n(srv_dline(c->sv, id) + 1, __ATOMIC_ACQUIRE) != 0)
+    return set_err(-EIO, "flush server: a frame of ring %u changed after submission (or a malformed slot)", id);
+  const hipError_t e = hipStreamQuery(c->sv->st);
+  if (e == hipErrorNotReady)
+    return 0;
+  if (e == hipSuccess)
+    return set_err(-EIO, "flush server: the kernel has exited (stopped, or its lease ran out)");
+  return hip_err(e, "flush server: hipStreamQuery");
+}
+
+static void server_reap(struct tasx_ctx *c)
+{
+  const unsigned id = (unsigned) (c - g_ctx);
+  const uint32_t cons = __atomic_load_n(srv_dline(c->sv, id), __ATOMIC_ACQUIRE);
+  if (cons == c->sv_done_pos)
+    return;
+  const uint32_t t = c->sv_ticket[(cons - 1u) % TASX_SRV_RING];
+  c->sv_done_pos = cons;
+  if (!ticket_le(t, c->done_ticket))
+    c->done_ticket = t;
+}
+
+/* every frame of the open batch is one the server takes: TAS layout in the
+ * registered region, 16-byte aligned frame start (ip - 14), total_length in
+ * [38, 1522], and the whole chunks it reads inside the region */
+static int server_ok(const struct tasx_ctx *c, uint32_t n)
+{
+  const uintptr_t dend = (uintptr_t) c->zc_dev + c->zc_bytes;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t *ip = c->pend_ip[i];
+    if (c->pend_l4[i] != ip + 20 || ip < c->zc_host + TASX_TAS_IP_OFF ||
+        ip + 20 > c->zc_host + c->zc_bytes)
+      return 0;
+    const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+    const uintptr_t fdev = (uintptr_t) (c->zc_dev + (ip - TASX_TAS_IP_OFF - c->zc_host));
+    /* the row reads the chunks of [frame, frame + 14 + tl) */
+    if (tl < 38u || tl > 1522u || (fdev & 15u) != 0 || fdev + ((14u + tl + 15u) & ~15u) > dend)
+      return 0;
+  }
+  return 1;
+}
+
+static int server_submit(struct tasx_ctx *c)
+{
+  const unsigned id = (unsigned) (c - g_ctx);
+  struct fserver *S = c->sv;
+  int rc;
+  while (c->npend > 0) {
+    if (!server_ok(c, c->npend))
+      return flush_wait(c, c->next_ticket); /* the local path takes it, after the server's tickets */
+    /* a flush this context launched itself completes first (as feeder_submit) */
+    if (!ticket_le(c->local_last, c->done_ticket) && (rc = flush_wait(c, c->local_last)) != 0)
+      return rc;
+    const uint32_t cnt = c->npend < TASX_SRV_FB ? c->npend : TASX_SRV_FB;
+    /* the slot's previous batch (position sv_pos - RING) must be finished */
+    uint32_t k = 0;
+    while (c->sv_pos - __atomic_load_n(srv_dline(S, id), __ATOMIC_ACQUIRE) >= TASX_SRV_RING) {
+      if ((++k & 4095u) == 0 && (rc = server_health(c)) != 0)
+        return rc;
+    }
+    const uint32_t pos = c->sv_pos;
+    const uint64_t tag = (uint64_t) ((pos + 1u) & 0xffffu) << 48;
+    uint64_t *slot = (uint64_t *) (S->h_mem + TASX_SRV_SLOTP(id, pos));
+    const uintptr_t b16 = (uintptr_t) c->zc_dev & ~(uintptr_t) 15;
+    const uint8_t *h16 = c->zc_host - ((uintptr_t) c->zc_dev & 15u); /* host view of b16 */
+    const uint64_t bytes = c->zc_bytes + ((uintptr_t) c->zc_dev & 15u);
+    for (uint32_t i = 0; i < cnt; i++) {
+      const uint8_t *ip = c->pend_ip[i];
+      const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+      const uint64_t fo = (uint64_t) (ip - TASX_TAS_IP_OFF - h16);
+      slot[TASX_SRV_HDR / 8 + i] = fo | (uint64_t) tl << 32 | tag;
+    }
+    __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
+    __atomic_store_n(&slot[0], (uint64_t) cnt | (bytes > 0xffffffffull ? 0xffffffffull : bytes) << 16 | tag,
+                     __ATOMIC_RELEASE);
+    c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
+    c->sv_pos = pos + 1u;
+    c->n_server_flushes++;
+    __atomic_fetch_add(&S->batches, (uint64_t) 1, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&S->frames, (uint64_t) cnt, __ATOMIC_RELAXED);
+    if (cnt < c->npend) {
+      memmove(c->pend_ip, c->pend_ip + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_ip));
+      memmove(c->pend_l4, c->pend_l4 + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_l4));
+    }
+    c->npend -= cnt;
+  }
+  return 0;
+}
+
+int tasx_server_start(int device)
+{
+  int ndev = 0, khz = 0, rc = 0;
+  hipError_t e;
+  static int atexit_set = 0;
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "server: device %d out of range", device);
+  if ((e = hipGetDeviceCount(&ndev)) != hipSuccess)
+    return hip_err(e, "hipGetDeviceCount");
+  if (device >= ndev)
+    return set_err(-ENODEV, "device %d not present (%d GPUs)", device, ndev);
+  pthread_mutex_lock(&g_server_mu);
+  if (g_server[device]) {
+    pthread_mutex_unlock(&g_server_mu);
+    return set_err(-EINVAL, "flush server for device %d already running", device);
+  }
+  struct fserver *S = calloc(1, sizeof(*S));
+  if (!S) {
+    pthread_mutex_unlock(&g_server_mu);
+    return set_err(-ENOMEM, "server: out of host memory");
+  }
+  S->device = device;
+  if ((e = hipSetDevice(device)) != hipSuccess ||
+      (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipHostMalloc((void **) &S->h_mem, TASX_SRV_BYTES, hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void **) &S->d_mem, S->h_mem, 0)) != hipSuccess)
+    rc = hip_err(e, "server allocation");
+  if (!rc && khz <= 0)
+    rc = set_err(-ENODEV, "server: device %d reports no wall clock", device);
+  if (!rc) {
+    memset(S->h_mem, 0, TASX_SRV_BYTES);
+    tasx_srv_params prm;
+    prm.mem = S->d_mem;
+    prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
+    prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
+    S->keep_run = 1;
+    __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
+    if (pthread_create(&S->keep, NULL, server_keepalive, S) != 0) {
+      S->keep_run = 0;
+      rc = set_err(-ENOMEM, "server: pthread_create failed");
+    } else if (tasx_launch_server(&prm, S->st) != 0) {
+      rc = hip_err(hipGetLastError(), "server kernel launch");
+      __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
+      pthread_join(S->keep, NULL);
+    }
+  }
+  if (rc) {
+    server_free(S);
+    pthread_mutex_unlock(&g_server_mu);
+    return rc;
+  }
+  if (!atexit_set) {
+    atexit(server_atexit);
+    atexit_set = 1;
+  }
+  g_server[device] = S;
+  pthread_mutex_unlock(&g_server_mu);
+  return 0;
+}
+
+int tasx_server_stop(int device)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "server: device %d out of range", device);
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = g_server[device];
+  if (!S) {
+    pthread_mutex_unlock(&g_server_mu);
+    return set_err(-EINVAL, "no flush server running for device %d", device);
+  }
+  if (__atomic_load_n(&S->attached, __ATOMIC_ACQUIRE) != 0) {
+    pthread_mutex_unlock(&g_server_mu);
+    return set_err(-EBUSY, "flush server for device %d still serves contexts", device);
+  }
+  __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+  __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
+  pthread_join(S->keep, NULL);
+  /* bounded wait for every workgroup to leave */
+  hipError_t e = hipErrorNotReady;
+  const struct timespec ts = {0, 100 * 1000};
+  for (uint32_t t = 0; t < SRV_STOP_WAIT_MS * 10u && (e = hipStreamQuery(S->st)) == hipErrorNotReady; t++)
+    nanosleep(&ts, NULL);
+  g_server[device] = NULL;
+  pthread_mutex_unlock(&g_server_mu);
+  if (e == hipErrorNotReady) /* still running: leave its memory mapped (leaked), never free under it */
+    return set_err(-EIO, "flush server for device %d did not stop within %u ms", device, SRV_STOP_WAIT_MS);
+  server_free(S);
+  return e == hipSuccess ? 0 : hip_err(e, "flush server kernel");
+}
+
+int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-EINVAL, "no flush server running for device %d", device);
+  pthread_mutex_lock(&g_server_mu);
+  const struct fserver *S = g_server[device];
+  if (S) {
+    if (batches)
+      *batches = __atomic_load_n(&S->batches, __ATOMIC_RELAXED);
+    if (frames)
+      *frames = __atomic_load_n(&S->frames, __ATOMIC_RELAXED);
+  }
+  pthread_mutex_unlock(&g_server_mu);
+  return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
+}
+
+int tasx_ctx_use_server(unsigned ctx_id, int on)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  int rc;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  const unsigned id = (unsigned) (c - g_ctx);
+  if (on) {
+    if (c->sv)
+      return 0;
+    if (c->fd)
+      return set_err(-EBUSY, "ctx %u uses the shared feeder (tasx_ctx_use_feeder 0 first)", ctx_id);
+    if (!c->zc_host)
+      return set_err(-EINVAL, "ctx %u has no frame region (tasx_ctx_register_frames)", ctx_id);
+    if (c->zc_bytes + 16u > 0xffffffffull || (uint64_t) (uintptr_t) c->zc_dev + c->zc_bytes >= (1ull << 48))
+      return set_err(-EINVAL, "ctx %u: frame region beyond the server's 32-bit offsets / 48-bit addresses", ctx_id);
+    if ((rc = flush_wait(c, c->next_ticket)) != 0)
+      return rc;
+    pthread_mutex_lock(&g_server_mu);
+    struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
+    if (S) {
+      c->sv_pos = c->sv_done_pos = __atomic_load_n(srv_dline(S, id), __ATOMIC_ACQUIRE);
+      c->sv = S;
+      __atomic_or_fetch(&S->attached, 1u << id, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&g_server_mu);
+    return S ? 0 : set_err(-EINVAL, "no flush server running for device %d (tasx_server_start)", c->device);
+  }
+  if (!c->sv)
+    return 0;
+  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+    return rc;
+  __atomic_and_fetch(&c->sv->attached, ~(1u << id), __ATOMIC_RELEASE);
+  c->sv = NULL;
+  return 0;
+}
+
+int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (server_flushes)
+    *server_flushes = c->n_server_flushes;
   return 0;
 }
 

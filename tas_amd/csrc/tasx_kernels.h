@@ -87,6 +87,33 @@ typedef struct tasx_flow_params {
   uint32_t fs_key_off;
 } tasx_flow_params;
 
+/* The persistent flush server (server_kernels.hip): one block of coherent
+ * pinned host memory per GPU, host-written lines apart from GPU-written ones.
+ *   [TASX_SRV_CTL]     u64: stop (low word, host) | lease (high word, host keepalive)
+ *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 consumed (positions
+ *                      taken and finished), u32 error (sticky)
+ *   [TASX_SRV_SLOTP(r, p)] ring r, position p: a 1 KiB descriptor slot,
+ *     u64 h0 = n | min(region bytes, 2^32 - 1) << 16 | tag << 48,
+ *     u64 h1 = region device address (48 bits) | tag << 48,
+ *     then n <= TASX_SRV_FB entries u64 = frame offset in the region (32
+ *     bits) | ip.total_length << 32 | tag << 48,
+ *   tag = (p + 1) mod 2^16; the host writes the entries, then h1, then h0. */
+#define TASX_SRV_RING 8u   /* slots per ring */
+#define TASX_SRV_FB 64u    /* frames per slot */
+#define TASX_SRV_SLOT 1024u
+#define TASX_SRV_HDR 16u
+#define TASX_SRV_CTL 0u
+#define TASX_SRV_DONE(r) (64u * (1u + (r)))
+#define TASX_SRV_RINGS 2048u
+#define TASX_SRV_SLOTP(r, p) (TASX_SRV_RINGS + ((r) * TASX_SRV_RING + (p) % TASX_SRV_RING) * TASX_SRV_SLOT)
+#define TASX_SRV_BYTES (TASX_SRV_RINGS + TASX_MAX_CTX * TASX_SRV_RING * TASX_SRV_SLOT)
+
+typedef struct tasx_srv_params {
+  uint8_t *mem;          /* device view of the server's pinned block */
+  uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
+  uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
+} tasx_srv_params;
+
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 TASX_INTERNAL int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);
 TASX_INTERNAL int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream);
@@ -107,6 +134,8 @@ TASX_INTERNAL int tasx_last_launch_posted_done(void);
 TASX_INTERNAL int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 TASX_INTERNAL int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
+/* the flush server: TASX_MAX_CTX workgroups, workgroup r serves ring r */
+TASX_INTERNAL int tasx_launch_server(const tasx_srv_params *p, void *stream);
 /* record the name of the kernel the calling thread launches (tasx_last_kernel) */
 TASX_INTERNAL void tasx_note_kernel(const char *name);
 

@@ -89,6 +89,11 @@ SIGNATURES = {
     "tasx_feeder_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
     "tasx_ctx_use_feeder": (_c_int, [_uns, _c_int]),
     "tasx_ctx_feeder_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
+    "tasx_server_start": (_c_int, [_c_int]),
+    "tasx_server_stop": (_c_int, [_c_int]),
+    "tasx_server_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
+    "tasx_ctx_use_server": (_c_int, [_uns, _c_int]),
+    "tasx_ctx_server_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_last_kernel": (ctypes.c_char_p, []),
     "tasx_host_alloc": (_vp, [_sz]),
@@ -468,6 +473,32 @@ def use_feeder(ctx_id: int, on: bool = True) -> None:
 def feeder_flushes(ctx_id: int) -> int:
     n = ctypes.c_uint32()
     _check(lib().tasx_ctx_feeder_flushes(ctx_id, ctypes.byref(n)), "tasx_ctx_feeder_flushes")
+    return n.value
+
+
+def server_start(device: int = 0) -> None:
+    """The persistent flush-server kernel for `device` (tasx_server_start)."""
+    _check(lib().tasx_server_start(device), "tasx_server_start")
+
+
+def server_stop(device: int = 0) -> None:
+    _check(lib().tasx_server_stop(device), "tasx_server_stop")
+
+
+def server_stats(device: int = 0) -> tuple[int, int]:
+    b, fr = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().tasx_server_stats(device, ctypes.byref(b), ctypes.byref(fr)), "tasx_server_stats")
+    return b.value, fr.value
+
+
+def use_server(ctx_id: int, on: bool = True) -> None:
+    """Attach the context to (or detach it from) its GPU's flush server."""
+    _check(lib().tasx_ctx_use_server(ctx_id, 1 if on else 0), "tasx_ctx_use_server")
+
+
+def server_flushes(ctx_id: int) -> int:
+    n = ctypes.c_uint32()
+    _check(lib().tasx_ctx_server_flushes(ctx_id, ctypes.byref(n)), "tasx_ctx_server_flushes")
     return n.value
 
 

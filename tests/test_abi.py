@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 5
+    assert L.tasx_abi_version() == 6
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -95,6 +95,14 @@ def test_abi_version_and_errors_without_gpu(L):
     assert L.tasx_tcp4_cksum_batch_host_offs(5, None, None, None, 4, 14, 34, None, 0) == -errno.EINVAL
     assert L.tasx_raw_cksum_batch_host_offs(5, None, None, None, 0, 4, None, 0) == -errno.EINVAL
     assert b"not initialised" in L.tasx_last_error()
+    # flush server (ABI 6): nothing running, no context
+    assert L.tasx_server_stop(0) == -errno.EINVAL
+    assert L.tasx_server_stats(0, None, None) == -errno.EINVAL
+    assert L.tasx_server_stop(-1) == -errno.ENODEV
+    assert L.tasx_ctx_use_server(3, 1) == -errno.EINVAL
+    assert L.tasx_ctx_server_flushes(3, None) == -errno.EINVAL
+    if L.tasx_device_count() <= 0:  # no GPU in this container: start fails, nothing launched
+        assert L.tasx_server_start(0) in (-errno.EIO, -errno.ENODEV)
 
 
 def test_python_wrapper_raises(L):

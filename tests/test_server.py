@@ -1,0 +1,267 @@
+"""The persistent flush server (ABI 6; tas_amd/csrc/server_kernels.hip): TAS's
+tx_flush batches (tas/fast/fastemu.c:544-566, at most TXBUF_SIZE = 32 frames,
+tas/include/fastpath.h:38) handed to one long-running kernel per GPU through
+descriptor rings in pinned memory -- no HIP call on the submitting thread.
+Every test checks the frames bit for bit against the C oracle's
+tcp_checksums (fast_flows.c:1058-1069) over the same frames.
+
+Run on the MI355X box:  python -m pytest tests/test_server.py -m gpu -x -q
+"""
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from tas_amd import pktgen, xsum
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    xsum.lib()
+    yield
+    try:  # never leave a server running past the module
+        xsum.server_stop(0)
+    except xsum.TasxError:
+        pass
+
+
+def _frames(nframes: int, seed: int, short: bool = True):
+    """tx_flush-shaped frames (data segments of 0..1448 B, pure ACKs) at a
+    2048 B mbuf stride in a pinned region, checksum fields stale."""
+    pay = np.where(np.arange(nframes) % 3 == 0, 0, (np.arange(nframes) * 53 + seed) % 1449)
+    frames = pktgen.tcp4_frames(nframes, payload=pay, stride=2048, seed=seed)
+    if short:  # total_length < 38: a batch holding one goes through the context itself
+        f = frames.reshape(nframes, 2048)
+        bad = np.arange(5, nframes, 97)
+        f[bad, 16], f[bad, 17] = 0, (np.arange(len(bad)) * 7) % 38
+    pin = xsum.PinnedBuffer(frames.size + 4096)
+    pin.array[:] = 0
+    pin.array[:frames.size] = frames
+    return pin, frames
+
+
+def _ref(oracle, frames, n):
+    ref = frames.copy()
+    oracle.tcp4_batch(ref, n, stride=2048, inplace=True)
+    return ref
+
+
+class _Ctxs:
+    def __init__(self, ids, per_ctx_bytes=1 << 20):
+        self.ids, self.pins = list(ids), []
+        for c in self.ids:
+            xsum.ctx_init(c, 0, per_ctx_bytes)
+
+    def close(self):
+        for c in self.ids:
+            try:
+                xsum.ctx_destroy(c)
+            except xsum.TasxError:
+                pass
+        for p in self.pins:
+            p.free()
+
+
+def test_server_interleaved_contexts(oracle):
+    """Three contexts on one server, batches submitted interleaved, 32 frames
+    each, completions in each context's ticket order; the batches holding a
+    frame the server does not take (total_length < 38) are flushed by their
+    context after its server tickets; stop refuses while contexts are attached."""
+    ids, nb, n = (2, 7, 15), 12, 32
+    xsum.server_start(0)
+    cx = _Ctxs(ids)
+    try:
+        with pytest.raises(xsum.TasxError):
+            xsum.server_start(0)                     # one server per GPU
+        refs = []
+        for k, c in enumerate(ids):
+            pin, frames = _frames(nb * n, 300 + k)
+            cx.pins.append(pin)
+            refs.append(_ref(oracle, frames, nb * n))
+            with pytest.raises(xsum.TasxError):
+                xsum.use_server(c)                   # no frame region yet
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_server(c)
+        tickets = {c: [] for c in ids}
+        for b in range(nb):
+            for k, c in enumerate(ids):
+                for i in range(n):
+                    xsum.tcp_checksums(c, cx.pins[k].addr + (b * n + i) * 2048)
+                tickets[c].append(xsum.flush_submit(c))
+        for k, c in enumerate(ids):
+            assert tickets[c] == list(range(1, nb + 1))
+            xsum.flush_wait(c, tickets[c][-1])
+            assert all(xsum.flush_poll(c, t) for t in tickets[c])
+            np.testing.assert_array_equal(cx.pins[k].array[:refs[k].size], refs[k])
+            local = sum(1 for b in range(nb) if any((b * n + i) % 97 == 5 and b * n + i >= 5 for i in range(n)))
+            assert xsum.server_flushes(c) == nb - local
+            assert xsum.ctx_stats(c)[0] == local     # those went zero-copy through the context
+        batches, frames_done = xsum.server_stats(0)
+        assert batches == sum(xsum.server_flushes(c) for c in ids)
+        with pytest.raises(xsum.TasxError):
+            xsum.server_stop(0)                      # contexts attached
+        for c in ids:
+            xsum.use_server(c, False)
+        xsum.server_stop(0)
+        with pytest.raises(xsum.TasxError):
+            xsum.server_stop(0)                      # not running
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
+
+
+def test_server_reused_mbufs_and_large_flush(oracle):
+    """The same mbufs refilled with new frames between flushes (a line read by
+    an earlier batch must never be served again), one flush of 200 frames
+    (split over four ring slots: 64 per slot), and back-to-back synchronous
+    tasx_flush calls."""
+    xsum.server_start(0)
+    cx = _Ctxs([4])
+    try:
+        n = 200
+        pin = xsum.PinnedBuffer(n * 2048 + 4096)
+        cx.pins.append(pin)
+        xsum.register_frames(4, pin.addr, pin.nbytes)
+        xsum.use_server(4)
+        for rnd in range(6):
+            pay = (np.arange(n) * (37 + rnd) + 11 * rnd) % 1449
+            pay[rnd::5] = 0
+            frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=700 + rnd)
+            pin.array[:frames.size] = frames
+            ref = _ref(oracle, frames, n)
+            m = n if rnd % 2 == 0 else 32
+            for i in range(m):
+                xsum.tcp_checksums(4, pin.addr + i * 2048)
+            xsum.tx_flush(4)
+            np.testing.assert_array_equal(pin.array[:m * 2048], ref[:m * 2048])
+        assert xsum.server_flushes(4) == 3 * 4 + 3 * 1 and xsum.ctx_stats(4) == (0, 0)
+        xsum.use_server(4, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_ring_wrap_and_tag_wrap(oracle):
+    """70,000 one-frame flushes with up to 8 in flight: the 8-slot ring wraps
+    8,750 times and the 16-bit slot tags wrap (position 65,535 -> 0) with the
+    server reading every slot fresh; every frame right."""
+    xsum.server_start(0)
+    cx = _Ctxs([9])
+    try:
+        nf = 64
+        pin, frames = _frames(nf, 901, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nf)
+        xsum.register_frames(9, pin.addr, pin.nbytes)
+        xsum.use_server(9)
+        total, inflight = 70000, []
+        for k in range(total):
+            xsum.tcp_checksums(9, pin.addr + (k % nf) * 2048)
+            inflight.append(xsum.flush_submit(9))
+            if len(inflight) >= 8:
+                xsum.flush_wait(9, inflight.pop(0))
+        xsum.flush_wait(9, inflight[-1])
+        np.testing.assert_array_equal(pin.array[:frames.size], ref)
+        assert xsum.server_flushes(9) == total
+        xsum.use_server(9, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_threads(oracle):
+    """Eight fast-path threads, each with its own context bound
+    (tasx_set_thread_ctx) and attached to the server, 60 tx_flush batches
+    each with up to 7 in flight (poll, then wait for the oldest): every frame
+    of every thread checksummed exactly."""
+    ids, nb, n = tuple(range(1, 9)), 60, 32
+    xsum.server_start(0)
+    cx = _Ctxs(ids)
+    errs, refs = [], []
+    try:
+        for k, c in enumerate(ids):
+            pin, frames = _frames(nb * n, 500 + k, short=False)
+            cx.pins.append(pin)
+            refs.append(_ref(oracle, frames, nb * n))
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_server(c)
+
+        def core(k, c):
+            try:
+                xsum.set_thread_ctx(c)
+                inflight = []
+                for b in range(nb):
+                    for i in range(n):
+                        xsum.tcp_checksums(xsum.CTX_SELF, cx.pins[k].addr + (b * n + i) * 2048)
+                    inflight.append(xsum.flush_submit(xsum.CTX_SELF))
+                    while inflight and xsum.flush_poll(xsum.CTX_SELF, inflight[0]):
+                        inflight.pop(0)
+                    if len(inflight) >= 7:
+                        xsum.flush_wait(xsum.CTX_SELF, inflight.pop(0))
+                if inflight:
+                    xsum.flush_wait(xsum.CTX_SELF, inflight[-1])
+                xsum.set_thread_ctx(xsum.CTX_SELF)
+            except Exception as e:  # reported below
+                errs.append(e)
+        th = [threading.Thread(target=core, args=(k, c)) for k, c in enumerate(ids)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not errs, errs
+        for k, c in enumerate(ids):
+            np.testing.assert_array_equal(cx.pins[k].array[:refs[k].size], refs[k])
+            assert xsum.server_flushes(c) == nb
+        for c in ids:
+            xsum.use_server(c, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_stop_is_bounded_and_restarts(oracle):
+    """Stop returns promptly (the kernel polls the stop word between batches),
+    a new server starts in its place, a context re-attaches and its flushes
+    are right; the feeder and the server are exclusive per context."""
+    cx = _Ctxs([12])
+    try:
+        pin, frames = _frames(64, 77, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, 64)
+        xsum.register_frames(12, pin.addr, pin.nbytes)
+        for rnd in range(3):
+            xsum.server_start(0)
+            xsum.use_server(12)
+            pin.array[:frames.size] = frames
+            for i in range(64):
+                xsum.tcp_checksums(12, pin.addr + i * 2048)
+            xsum.tx_flush(12)
+            np.testing.assert_array_equal(pin.array[:frames.size], ref)
+            xsum.use_server(12, False)
+            t0 = time.perf_counter()
+            xsum.server_stop(0)
+            assert time.perf_counter() - t0 < 0.5
+        xsum.feeder_start(0)
+        try:
+            xsum.use_feeder(12)
+            xsum.server_start(0)
+            with pytest.raises(xsum.TasxError):
+                xsum.use_server(12)                  # attached to the feeder
+            xsum.use_feeder(12, False)
+            xsum.server_stop(0)
+        finally:
+            xsum.feeder_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass

@@ -21,6 +21,7 @@
  *       -o tools/bin/feeder_bench -Ltas_amd/_lib -ltasx -Loracle/build -loracle \
  *       -Wl,-rpath,/root/repo/tas_amd/_lib -Wl,-rpath,/root/repo/oracle/build
  *   tools/bin/feeder_bench [flushes_per_thread] [in_flight (1..7, default 3)]
+ *                          [modes: bit 0 per-context, 1 feeder, 2 server; default 7]
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -152,6 +153,7 @@ int main(int argc, char **argv)
   if (INFLIGHT < 1 || INFLIGHT > MAXQ - 1)
     INFLIGHT = 3;
   DSLOT = INFLIGHT + 1;
+  const int modes = argc > 3 ? atoi(argv[3]) : 7;
   const int nthreads[] = {1, 2, 4, 8};
   const size_t pool_bytes = (size_t) DSLOT * BATCH * STRIDE;
   struct thr T[MAXT];
@@ -194,26 +196,39 @@ int main(int argc, char **argv)
     fprintf(stderr, "feeder: %s\n", tasx_last_error());
     return 1;
   }
-  for (int mode = 0; mode < 2; mode++) {
+  static const char *const mname[3] = {"per_context", "feeder", "server"};
+  for (int mode = 0; mode < 3; mode++) {
+    if (!(modes & (1 << mode)))
+      continue;
+    if (mode == 2 && tasx_server_start(0) != 0) {
+      fprintf(stderr, "server: %s\n", tasx_last_error());
+      return 1;
+    }
     for (unsigned ni = 0; ni < sizeof(nthreads) / sizeof(nthreads[0]); ni++) {
       const int n = nthreads[ni];
       pthread_t th[MAXT];
       uint64_t sw0 = 0, sw1 = 0, fr0, fr1;
       for (int k = 0; k < n; k++) {
         T[k].flushes = flushes, T[k].use_feeder = mode, T[k].stall = 0, T[k].nlat = 0, T[k].err = 0;
-        if (tasx_ctx_use_feeder((unsigned) k, mode) != 0) {
-          fprintf(stderr, "use_feeder: %s\n", tasx_last_error());
+        if (tasx_ctx_use_feeder((unsigned) k, mode == 1) != 0 || tasx_ctx_use_server((unsigned) k, mode == 2) != 0) {
+          fprintf(stderr, "use_feeder / use_server: %s\n", tasx_last_error());
           return 1;
         }
       }
-      tasx_feeder_stats(0, &sw0, &fr0);
+      if (mode == 2)
+        tasx_server_stats(0, &sw0, &fr0);
+      else
+        tasx_feeder_stats(0, &sw0, &fr0);
       const double t0 = now_us();
       for (int k = 0; k < n; k++)
         pthread_create(&th[k], NULL, run, &T[k]);
       for (int k = 0; k < n; k++)
         pthread_join(th[k], NULL);
       const double wall = now_us() - t0;
-      tasx_feeder_stats(0, &sw1, &fr1);
+      if (mode == 2)
+        tasx_server_stats(0, &sw1, &fr1);
+      else
+        tasx_feeder_stats(0, &sw1, &fr1);
       double core_all[MAXT], stall = 0, lat_all[MAXT];
       for (int k = 0; k < n; k++) {
         if (T[k].err) {
@@ -227,10 +242,18 @@ int main(int argc, char **argv)
       printf("{\"mode\": \"%s\", \"threads\": %d, \"in_flight\": %u, \"flushes_per_thread\": %d, \"frames_per_flush\": %u, "
              "\"core_us_per_flush\": %.3f, \"stall_us_per_flush\": %.3f, \"latency_us\": %.2f, "
              "\"frames_per_s\": %.0f, \"sweeps\": %llu, \"frames_per_sweep\": %.1f}\n",
-             mode ? "feeder" : "per_context", n, INFLIGHT, flushes, BATCH, median(core_all, n), stall / n, median(lat_all, n),
+             mname[mode], n, INFLIGHT, flushes, BATCH, median(core_all, n), stall / n, median(lat_all, n),
              (double) n * flushes * BATCH / (wall * 1e-6), (unsigned long long) (sw1 - sw0),
              sw1 > sw0 ? (double) (fr1 - fr0) / (double) (sw1 - sw0) : 0.0);
       fflush(stdout);
+    }
+    if (mode == 2) {
+      for (int k = 0; k < MAXT; k++)
+        tasx_ctx_use_server((unsigned) k, 0);
+      if (tasx_server_stop(0) != 0) {
+        fprintf(stderr, "server stop: %s\n", tasx_last_error());
+        return 1;
+      }
     }
   }
   /* every thread's last batches against the oracle */
