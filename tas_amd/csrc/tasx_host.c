@@ -635,6 +635,25 @@ struct chunk_job {
   uint32_t first, cnt;
 };
 
+/* An error after the first chunk's launch leaves earlier chunks running on
+ * the slot streams, reading and writing the slots' pinned buffers: wait for
+ * them all before returning, so no later call (or flush) reuses a buffer a
+ * stale chunk still uses.  Returns rc. */
+static int host_offs_fail(struct tasx_ctx *c, int rc)
+{
+  for (int s = 0; s < NSLOT; s++)
+    (void) hipStreamSynchronize(c->st[s]);
+  (void) hipGetLastError();
+  return rc;
+}
+#define HIPCHK_DRAIN(c, call)                          \
+  do {                                                 \
+    hipError_t e_ = (call);                            \
+    if (e_ != hipSuccess)                              \
+      return host_offs_fail((c), hip_err(e_, #call));  \
+  } while (0)
+
+
 static void finish_tcp4_chunk(struct tasx_ctx *c, int s, const struct chunk_job *j,
     uint8_t *base, uint64_t stride, uint32_t ip_off, uint32_t l4_off,
     uint16_t *out, uint32_t flags)
@@ -680,12 +699,12 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     const int s = (int) (k % NSLOT);
     tasx_tcp4_params p;
     if (k >= NSLOT) {
-      HIPCHK(hipStreamSynchronize(c->st[s]));
+      HIPCHK_DRAIN(c, hipStreamSynchronize(c->st[s]));
       finish_tcp4_chunk(c, s, &jobs[s], (uint8_t *) base, stride, ip_off, l4_off, out, flags);
     }
     jobs[s].first = first;
     jobs[s].cnt = (n - first < per) ? n - first : per;
-    HIPCHK(hipMemcpyAsync(c->d_buf[s], (uint8_t *) base + (uint64_t) first * stride,
+    HIPCHK_DRAIN(c, hipMemcpyAsync(c->d_buf[s], (uint8_t *) base + (uint64_t) first * stride,
         (size_t) jobs[s].cnt * stride, hipMemcpyHostToDevice, c->st[s]));
     memset(&p, 0, sizeof(p));
     p.base = c->d_buf[s];
@@ -700,14 +719,14 @@ int tasx_tcp4_cksum_batch_host(unsigned ctx_id, void *base, uint64_t stride,
     p.room = stride <= 0xffffffffull ? (uint32_t) stride : 0u;
 
     if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
-      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 4,
+      return host_offs_fail(c, hip_err(hipGetLastError(), "tcp4_cksum_kernel launch"));
+    HIPCHK_DRAIN(c, hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 4,
         hipMemcpyDeviceToHost, c->st[s]));
   }
   /* drain: the last min(k, NSLOT) chunks, in submission order */
   for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
     const int s = (int) (d % NSLOT);
-    HIPCHK(hipStreamSynchronize(c->st[s]));
+    HIPCHK_DRAIN(c, hipStreamSynchronize(c->st[s]));
     finish_tcp4_chunk(c, s, &jobs[s], (uint8_t *) base, stride, ip_off, l4_off, out, flags);
   }
   return rc;
@@ -739,13 +758,15 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     const int s = (int) (k % NSLOT);
     tasx_raw_params p;
     if (k >= NSLOT) {
-      HIPCHK(hipStreamSynchronize(c->st[s]));
+      const hipError_t e = hipStreamSynchronize(c->st[s]);
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
       memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
     }
     jobs[s].first = first;
     jobs[s].cnt = (n - first < per) ? n - first : per;
     /* the last packet of a chunk only needs len0 bytes */
-    HIPCHK(hipMemcpyAsync(c->d_buf[s], (const uint8_t *) base + (uint64_t) first * stride,
+    HIPCHK_DRAIN(c, hipMemcpyAsync(c->d_buf[s], (const uint8_t *) base + (uint64_t) first * stride,
         (size_t) (jobs[s].cnt - 1) * stride + len0, hipMemcpyHostToDevice, c->st[s]));
     p.base = c->d_buf[s];
     p.off = NULL;
@@ -755,13 +776,15 @@ int tasx_raw_cksum_batch_host(unsigned ctx_id, const void *base,
     p.len0 = len0;
     p.n = jobs[s].cnt;
     if (tasx_launch_raw(&p, g_variant, c->st[s]) != 0)
-      return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
-    HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 2,
+      return host_offs_fail(c, hip_err(hipGetLastError(), "raw_cksum_kernel launch"));
+    HIPCHK_DRAIN(c, hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) jobs[s].cnt * 2,
         hipMemcpyDeviceToHost, c->st[s]));
   }
   for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
     const int s = (int) (d % NSLOT);
-    HIPCHK(hipStreamSynchronize(c->st[s]));
+    const hipError_t e = hipStreamSynchronize(c->st[s]);
+    if (e != hipSuccess)
+      return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
     memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
   }
   return 0;
@@ -806,6 +829,26 @@ struct host_job {
   uint32_t first, cnt;
 };
 
+/* Zero-copy reads stay inside the allocation base lies in (or the
+ * context's registered frame region): [base + lo, base + hi) must fit it.
+ * Unknown extents (memory the runtime does not describe) are not checked. */
+static int zc_extent_ok(const struct tasx_ctx *c, const void *base, uint64_t hi, const char *what)
+{
+  void *ab = NULL;
+  size_t asz = 0;
+  const uint8_t *b = (const uint8_t *) base;
+  if (hipMemGetAddressRange((hipDeviceptr_t *) &ab, &asz, (hipDeviceptr_t) base) == hipSuccess && ab && asz) {
+    if ((const uint8_t *) ab <= b && b + hi <= (const uint8_t *) ab + asz)
+      return 0;
+    return set_err(-EINVAL, "%s: packets reach %llu bytes past base, beyond its %zu-byte allocation", what,
+                   (unsigned long long) hi, asz);
+  }
+  (void) hipGetLastError();
+  if (c->zc_host && b >= c->zc_host && b < c->zc_host + c->zc_bytes && b + hi > c->zc_host + c->zc_bytes)
+    return set_err(-EINVAL, "%s: packets reach past the registered frame region", what);
+  return 0;
+}
+
 /* results of chunk j in slot s: to out (and into the frames, TCP4 in place) */
 static void finish_tcp4_offs(struct tasx_ctx *c, int s, const struct host_job *j, void *base,
     const uint64_t *off, uint32_t ip_off, uint32_t l4_off, uint16_t *out, uint32_t flags)
@@ -846,6 +889,31 @@ int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t 
   HIPCHK(hipSetDevice(c->device));
   if (zc && (rc = zc_base(base, &dbase, "tcp4 host offs batch")) != 0)
     return rc;
+  if (zc) {
+    /* the kernels read a frame's whole 16-byte chunks up to its hint (or its
+     * header when no hint is given; TX frames' total_length is trusted, as
+     * in the _dev forms) */
+    uint64_t hi = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint64_t e = off[i] + (flen && flen[i] > ip_off + 20u ? flen[i] : ip_off + 20u) + 15u;
+      hi = e > hi ? e : hi;
+    }
+    if ((rc = zc_extent_ok(c, base, hi, "tcp4 host offs batch")) != 0)
+      return rc;
+  } else {
+    /* before anything is launched: every record fits a slot, and with frame
+     * lengths given, every datagram lies inside its frame (the gather copies
+     * ip_off + total_length bytes) */
+    for (uint32_t i = 0; i < n; i++) {
+      const uint8_t *ip = host_pkt(base, off, i) + ip_off;
+      const uint32_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+      if (staged_rec(tl) > c->slot_bytes)
+        return set_err(-EINVAL, "tcp4 host offs batch: frame %u does not fit a %zu-byte slot", i, c->slot_bytes);
+      if (flen && (uint64_t) ip_off + (tl > 20u ? tl : 20u) > flen[i])
+        return set_err(-EINVAL, "tcp4 host offs batch: frame %u: ip_off + total_length %u exceeds its length %u", i,
+                       tl, flen[i]);
+    }
+  }
   if ((rc = flush_wait(c, c->next_ticket)) != 0)
     return rc;
   while (first < n) {
@@ -854,7 +922,9 @@ int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t 
     tasx_tcp4_params p;
     uint32_t cnt = 0;
     if (k >= NSLOT) {
-      HIPCHK(hipStreamSynchronize(c->st[s]));
+      const hipError_t e = hipStreamSynchronize(c->st[s]);
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
       finish_tcp4_offs(c, s, &jobs[s], base, off, ip_off, l4_off, out, flags);
     }
     memset(&p, 0, sizeof(p));
@@ -898,10 +968,10 @@ int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t 
         pos += rec;
         cnt++;
       }
-      if (cnt == 0)
-        return set_err(-EINVAL, "tcp4 host offs batch: frame %u does not fit a %zu-byte slot", first,
-            c->slot_bytes);
-      HIPCHK(hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]));
+      if (cnt == 0) /* checked up front; kept as a guard */
+        return host_offs_fail(c, set_err(-EINVAL, "tcp4 host offs batch: frame %u does not fit a %zu-byte slot",
+                                         first, c->slot_bytes));
+      hipError_t e = hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]);
       p.base = c->d_buf[s];
       if (uniform && tl0 >= 20) {
         /* one record size: stride mode with a uniform hint (the headline and
@@ -909,20 +979,27 @@ int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t 
         p.stride = rec0;
         p.flen0 = f->h_flen[0];
       } else {
-        HIPCHK(hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
-        HIPCHK(hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]));
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]);
         p.off = c->d_off[s];
         p.flen = c->d_len[s];
       }
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipMemcpyAsync"));
       p.out = c->d_out[s];
       p.ip_off = TASX_TAS_IP_OFF;
       p.l4_off = TASX_TAS_L4_OFF;
     }
     p.n = cnt;
     if (tasx_launch_tcp4(&p, g_variant, c->st[s]) != 0)
-      return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-    if (!zc)
-      HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4, hipMemcpyDeviceToHost, c->st[s]));
+      return host_offs_fail(c, hip_err(hipGetLastError(), "tcp4_cksum_kernel launch"));
+    if (!zc) {
+      const hipError_t e = hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 4, hipMemcpyDeviceToHost, c->st[s]);
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipMemcpyAsync"));
+    }
     jobs[s].first = first;
     jobs[s].cnt = cnt;
     first += cnt;
@@ -930,7 +1007,9 @@ int tasx_tcp4_cksum_batch_host_offs(unsigned ctx_id, void *base, const uint64_t 
   }
   for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
     const int s = (int) (d % NSLOT);
-    HIPCHK(hipStreamSynchronize(c->st[s]));
+    const hipError_t e = hipStreamSynchronize(c->st[s]);
+    if (e != hipSuccess)
+      return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
     finish_tcp4_offs(c, s, &jobs[s], base, off, ip_off, l4_off, out, flags);
   }
   return 0;
@@ -962,6 +1041,20 @@ int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base, const uint
   HIPCHK(hipSetDevice(c->device));
   if (zc && (rc = zc_base(base, &dbase, "raw host offs batch")) != 0)
     return rc;
+  {
+    /* before anything is launched: every record fits a slot (staged), every
+     * packet's chunks inside base's allocation (zero-copy) */
+    uint64_t hi = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t l = len ? len[i] : len0;
+      if (!zc && (((size_t) l + 15) & ~(size_t) 15) > c->slot_bytes)
+        return set_err(-EINVAL, "raw host offs batch: packet %u does not fit a %zu-byte slot", i, c->slot_bytes);
+      const uint64_t e = off[i] + l + 15u;
+      hi = e > hi ? e : hi;
+    }
+    if (zc && (rc = zc_extent_ok(c, base, hi, "raw host offs batch")) != 0)
+      return rc;
+  }
   if ((rc = flush_wait(c, c->next_ticket)) != 0)
     return rc;
   while (first < n) {
@@ -970,7 +1063,9 @@ int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base, const uint
     tasx_raw_params p;
     uint32_t cnt = 0;
     if (k >= NSLOT) {
-      HIPCHK(hipStreamSynchronize(c->st[s]));
+      const hipError_t e = hipStreamSynchronize(c->st[s]);
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
       memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
     }
     memset(&p, 0, sizeof(p));
@@ -999,28 +1094,36 @@ int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base, const uint
         pos += rec;
         cnt++;
       }
-      if (cnt == 0)
-        return set_err(-EINVAL, "raw host offs batch: packet %u does not fit a %zu-byte slot", first,
-            c->slot_bytes);
+      if (cnt == 0) /* checked up front; kept as a guard */
+        return host_offs_fail(c, set_err(-EINVAL, "raw host offs batch: packet %u does not fit a %zu-byte slot",
+                                         first, c->slot_bytes));
+      hipError_t e = hipSuccess;
       if (pos)
-        HIPCHK(hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]));
+        e = hipMemcpyAsync(c->d_buf[s], c->h_stage[s], pos, hipMemcpyHostToDevice, c->st[s]);
       p.base = c->d_buf[s];
       if (len) {
-        HIPCHK(hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]));
-        HIPCHK(hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]));
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(c->d_off[s], c->h_off[s], (size_t) cnt * 8, hipMemcpyHostToDevice, c->st[s]);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(c->d_len[s], f->h_flen, (size_t) cnt * 4, hipMemcpyHostToDevice, c->st[s]);
         p.off = c->d_off[s];
         p.len = c->d_len[s];
       } else { /* uniform length: stride mode over the records */
         p.stride = len0 ? ((uint64_t) len0 + 15) & ~(uint64_t) 15 : 16;
         p.len0 = len0;
       }
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipMemcpyAsync"));
       p.out = c->d_out[s];
     }
     p.n = cnt;
     if (tasx_launch_raw(&p, g_variant, c->st[s]) != 0)
-      return hip_err(hipGetLastError(), "raw_cksum_kernel launch");
-    if (!zc)
-      HIPCHK(hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 2, hipMemcpyDeviceToHost, c->st[s]));
+      return host_offs_fail(c, hip_err(hipGetLastError(), "raw_cksum_kernel launch"));
+    if (!zc) {
+      const hipError_t e = hipMemcpyAsync(c->h_out[s], c->d_out[s], (size_t) cnt * 2, hipMemcpyDeviceToHost, c->st[s]);
+      if (e != hipSuccess)
+        return host_offs_fail(c, hip_err(e, "hipMemcpyAsync"));
+    }
     jobs[s].first = first;
     jobs[s].cnt = cnt;
     first += cnt;
@@ -1028,7 +1131,9 @@ int tasx_raw_cksum_batch_host_offs(unsigned ctx_id, const void *base, const uint
   }
   for (uint32_t d = (k > NSLOT) ? k - NSLOT : 0; d < k; d++) {
     const int s = (int) (d % NSLOT);
-    HIPCHK(hipStreamSynchronize(c->st[s]));
+    const hipError_t e = hipStreamSynchronize(c->st[s]);
+    if (e != hipSuccess)
+      return host_offs_fail(c, hip_err(e, "hipStreamSynchronize"));
     memcpy(out + jobs[s].first, c->h_out[s], (size_t) jobs[s].cnt * 2);
   }
   return 0;

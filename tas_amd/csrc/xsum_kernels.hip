@@ -1231,7 +1231,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const uint32_t ht = p.ht_entries;
       const uint32_t hb = (ht & (ht - 1u)) == 0u ? (fh & (ht - 1u)) : fh % ht; // the bucket's first entry
       const uint32_t ej = hb + (uint32_t) gl;
-      fe = ldg((const uint64_t *) p.flowht, ej >= ht ? ej - ht : ej);
+      // one subtraction wraps ej < ht + kNb; tables smaller than a bucket take the modulo
+      fe = ldg((const uint64_t *) p.flowht, ht >= (uint32_t) kNb ? (ej >= ht ? ej - ht : ej) : ej % ht);
     }
   }
   // the datagram [ip, ip + hend): uniform from the hint, or per row from the

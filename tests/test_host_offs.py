@@ -9,7 +9,10 @@
 * the feeder ordering rule: a batch the context flushes
   itself, then a feeder batch, with no poll in between;
 * flush tickets across the 2^32 wrap (ADVICE r2, medium; A/B test hook);
-* RX received lengths beyond the stride slot.
+* RX received lengths beyond the stride slot (ADVICE r2, low);
+* (round 4) errors found before any chunk is launched leave the
+  context usable; forged total_length and zero-copy extents refused; other
+  header layouts through all three forms.
 """
 import numpy as np
 import pytest
@@ -167,6 +170,112 @@ def test_host_offs_errors():
             xsum.tcp4_cksum_batch_host_offs(ctx, big.ctypes.data, offs, 1)
     finally:
         xsum.ctx_destroy(ctx)
+
+
+def test_host_offs_error_leaves_context_usable(oracle):
+    """a batch whose LAST frame does not fit a slot is
+    refused before anything is launched (staged TCP4 and RAW), and the same
+    context then runs a normal multi-chunk batch and a flush bit-exact."""
+    ctx = 6
+    xsum.ctx_init(ctx, 0, 1 << 16)                      # 43 MTU records per 64 KiB slot
+    try:
+        n = 200
+        frames = pktgen.tcp4_frames(n, payload=(np.arange(n) * 31) % 1449, stride=2048, seed=61)
+        big = pktgen.tcp4_frames(1, payload=0, stride=65552, ip_total_len=65535)
+        buf = np.concatenate([frames, big])
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(2048)
+        offs[-1] = frames.size                           # frame n - 1 is the TSO frame: 65,552 B records
+        with pytest.raises(xsum.TasxError):
+            xsum.tcp4_cksum_batch_host_offs(ctx, buf.ctypes.data, offs, n)
+        lens = np.full(n, 1500, np.uint32)
+        lens[-1] = 70000
+        with pytest.raises(xsum.TasxError):
+            xsum.raw_cksum_batch_host_offs(ctx, buf.ctypes.data, offs, n, lengths=lens)
+        good = np.arange(n, dtype=np.uint64) * np.uint64(2048)
+        ref = frames.copy()
+        exp = oracle.tcp4_batch(ref, n, offsets=good, inplace=True)
+        got = xsum.tcp4_cksum_batch_host_offs(ctx, frames.ctypes.data, good, n)
+        np.testing.assert_array_equal(got, exp)
+        exp_raw = oracle.raw_batch(frames, n, offsets=good, lengths=np.full(n, 1500, np.uint32))
+        np.testing.assert_array_equal(
+            xsum.raw_cksum_batch_host_offs(ctx, frames.ctypes.data, good, n, len0=1500), exp_raw)
+        for i in range(32):
+            xsum.tcp_checksums(ctx, frames.ctypes.data + i * 2048)
+        xsum.tx_flush(ctx)
+        np.testing.assert_array_equal(frames[:32 * 2048], ref[:32 * 2048])
+    finally:
+        xsum.ctx_destroy(ctx)
+
+
+def test_host_offs_forged_total_length_and_extents():
+    """with frame lengths given, a staged frame whose
+    ip_off + total_length exceeds its length is refused (the gather would read
+    past the mbuf); a zero-copy batch whose packets reach past the pinned
+    allocation (or the registered region) is refused instead of faulting."""
+    ctx = 8
+    xsum.ctx_init(ctx, 0, 1 << 20)
+    pin = xsum.PinnedBuffer(64 * 2048)
+    try:
+        frames = pktgen.tcp4_frames(64, payload=100, stride=2048, seed=71)
+        pin.array[:] = frames
+        offs = np.arange(64, dtype=np.uint64) * np.uint64(2048)
+        flen = np.full(64, 14 + 52 + 100, np.uint32)
+        xsum.tcp4_cksum_batch_host_offs(ctx, pin.addr, offs, 64, frame_len=flen)
+        forged = frames.copy()
+        forged[9 * 2048 + 16], forged[9 * 2048 + 17] = 0xFF, 0xF0          # total_length 65,520
+        with pytest.raises(xsum.TasxError):
+            xsum.tcp4_cksum_batch_host_offs(ctx, forged.ctypes.data, offs, 64, frame_len=flen)
+        xsum.register_frames(ctx, pin.addr, pin.nbytes)
+        far = offs.copy()
+        far[-1] = np.uint64(pin.nbytes + (1 << 20))
+        with pytest.raises(xsum.TasxError):
+            xsum.tcp4_cksum_batch_host_offs(ctx, pin.addr, far, 64, frame_len=flen, zerocopy=True)
+        with pytest.raises(xsum.TasxError):
+            xsum.raw_cksum_batch_host_offs(ctx, pin.addr, far, 64, len0=1500, zerocopy=True)
+        # the context still works
+        xsum.tcp4_cksum_batch_host_offs(ctx, pin.addr, offs, 64, frame_len=flen, zerocopy=True)
+    finally:
+        xsum.ctx_destroy(ctx)
+        pin.free()
+
+
+@pytest.mark.parametrize("ip_off,l4_off", [(18, 42), (0, 24), (22, 46)])
+def test_host_offs_other_layouts(oracle, ip_off, l4_off):
+    """staged, zero-copy and the device-resident batch agree
+    with the oracle for ip_off != 14 and l4_off = ip_off + 24 (IP options),
+    data and short segments, out of place and in place."""
+    n, stride = 700, 2048
+    rng = np.random.default_rng(ip_off * 7 + l4_off)
+    buf0 = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    f = buf0.reshape(n, stride)
+    tl = rng.integers(20, 1500, n)
+    tl[::9] = rng.integers(0, 20, len(tl[::9]))               # total_length < 20: tcp.chksum 0
+    f[:, ip_off + 2], f[:, ip_off + 3] = tl >> 8, tl & 0xFF
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    ref = buf0.copy()
+    exp = oracle.tcp4_batch(ref, n, offsets=offs, ip_off=ip_off, l4_off=l4_off, inplace=True)
+    ctx = 10
+    xsum.ctx_init(ctx, 0, 256 << 10)
+    pin = xsum.PinnedBuffer(buf0.size)
+    try:
+        for zc in (False, True):
+            b = buf0.copy() if not zc else None
+            if zc:
+                pin.array[:] = buf0
+            base = pin.addr if zc else b.ctypes.data
+            got = xsum.tcp4_cksum_batch_host_offs(ctx, base, offs, n, ip_off=ip_off, l4_off=l4_off, zerocopy=zc)
+            np.testing.assert_array_equal(got, exp)
+            xsum.tcp4_cksum_batch_host_offs(ctx, base, offs, n, out=False, inplace=True, ip_off=ip_off,
+                                            l4_off=l4_off, zerocopy=zc)
+            np.testing.assert_array_equal(pin.array if zc else b, ref)
+        d = torch.from_numpy(buf0.copy()).to(DEV)
+        got = xsum.tcp4_cksum_batch(d, n, offsets=torch.from_numpy(offs.astype(np.int64)).to(DEV), ip_off=ip_off,
+                                    l4_off=l4_off)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint16), exp)
+    finally:
+        xsum.ctx_destroy(ctx)
+        pin.free()
 
 
 # ---------------------------------------------------------------------------

@@ -164,6 +164,72 @@ def test_rx_fused_row_variant_ab(oracle, form):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("ent", [1, 2, 3, 5])
+def test_rx_fused_row_variant_tiny_tables(oracle, ent):
+    """A/B 26 probes bucket entries (h + j) % ht_entries in
+    the verify rows; tables smaller than a bucket (1-3 entries) wrap more
+    than once, and every probe stays inside the table."""
+    import torch
+    from tas_amd import xsum
+    n, stride = 600, 2048
+    frames, rcv, _, fs, nflows, _ = _burst(oracle, n, stride, seed=950 + ent, nflows=8, ent=64)
+    keys = pktgen.flow_keys(8, seed=950 + ent)
+    hashes, _ = oracle.flow_lookup_batch(pktgen.rx_frames(keys, stride=128, seed=950 + ent), 8,
+                                         np.zeros(2, np.uint32), fs, fs_num=8, stride=128)
+    ht, _ = pktgen.flow_table(hashes, ent)
+    dev = "cuda:0"
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=stride)
+    exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, stride, stride=stride)
+    with xsum.using_library(xsum.AB_LIB_PATH):
+        xsum.set_kernel_variant(26)
+        try:
+            flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nflows, stride=stride)
+            torch.cuda.synchronize()
+        finally:
+            xsum.set_kernel_variant(0)
+    np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+    np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
+    assert (fid.cpu().numpy().view(np.uint32) != 0xFFFFFFFF).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 27, 32, 36])
+def test_rx_fused_uniform_batch_edges(oracle, variant):
+    """the uniform-received-length grids at the same batch
+    edges -- the product's XCD-matched lookup blocks with two frames per lane,
+    A/B 32 (XCD-matched, one frame per lookup lane), 27 and 36 (lookup blocks
+    over consecutive frames, one / two per lane)."""
+    import contextlib
+    import torch
+    from tas_amd import xsum
+    frames, rcv, ht, fs, nflows, _ = _burst(oracle, 4200, 2048, seed=913, uniform=True)
+    assert np.all(rcv == rcv[0])
+    dev = "cuda:0"
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    fr = t(frames)
+    ctx = xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()
+    kernel = {0: "tcp4_tas14_kernel<hint,verify,flow>", 27: "tcp4_tas14_kernel<hint,verify,flow_f1>",
+              32: "tcp4_tas14_kernel<hint,verify,flow_xcd>", 36: "tcp4_tas14_kernel<hint,verify,flow_split2>"}[variant]
+    with ctx:
+        xsum.set_kernel_variant(variant)
+        try:
+            for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096,
+                      4097, 4200):
+                exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
+                exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, int(rcv[0]), stride=2048)
+                flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048, frame_len=int(rcv[0]))
+                torch.cuda.synchronize()
+                assert xsum.last_kernel() == kernel
+                np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+                np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+                np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
+        finally:
+            xsum.set_kernel_variant(0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("variant", [0, 26, 27, 28, 35, 36])
 def test_rx_fused_batch_edges(oracle, variant):
     """Batch sizes around row, block and lookup-block boundaries (16 frames
