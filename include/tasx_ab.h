@@ -74,6 +74,14 @@ int tasx_ab_tcp4_mix_pattern(const void *base, uint64_t stride, uint32_t n, cons
  * lane -- the TX segment build's ceiling, timed by bench.py. */
 int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream);
 
+/* A pure streaming read of `bytes` (1 KiB multiple, 16-byte aligned) by one of
+ * the two load paths (round 4): path 0 register loads (8 KiB per block, two
+ * non-temporal 16-byte loads per lane), path 1 LDS-DMA (global_load_lds_dwordx4
+ * nt into a 4-slot ring per wave).  bench.py times both beside the headline and
+ * reports the faster as its read ceiling.  sink: a device word (never written
+ * for real data). */
+int tasx_ab_stream_read(const void *src, size_t bytes, int path, uint32_t *sink, void *stream);
+
 /* Test hook: restart a context's flush tickets at `start` (nothing pending or
  * in flight, no feeder), so a test can run flushes across the 2^32 wrap. */
 int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start);

@@ -117,6 +117,7 @@ AB_SIGNATURES = {
     "tasx_ab_tcp4_pattern": (_c_int, [_vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ab_tcp4_mix_pattern": (_c_int, [_vp, _c_u64, _c_u32, _vp, _c_u32, _c_int, _vp, _vp]),
     "tasx_ab_stream_copy": (_c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "tasx_ab_stream_read": (_c_int, [_vp, ctypes.c_size_t, _c_int, _vp, _vp]),
     "tasx_ab_ctx_set_tickets": (_c_int, [_uns, _c_u32]),
 }
 

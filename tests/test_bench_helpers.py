@@ -33,6 +33,20 @@ def test_price_mix_bound_is_the_larger_of_chain_and_hbm():
     assert leg2["roofline"]["latency"]["bound_us"] == 7.5
 
 
+def test_price_mix_disturbed_chain_claims_no_fraction():
+    """A chain kernel slower than the product's own access pattern (round 3's
+    rocprofv3 run: 10.10 us against a 10.17 us pattern would read frac 0.98)
+    is a disturbed measurement: frac is null, the raw numbers stay."""
+    mb = {"pattern_us": 10.0, "chain_us": 10.1, "rows": 65536, "rows_in_flight": 32768, "generations": 2,
+          "dependent_loads_per_row": 2, "loaded_latency_us": 2.5, "kernel": "k"}
+    leg = {"roofline": bench.roofline(51_190_000, 10.3e-3, None)}
+    bench.price_mix(leg, mb, 51_190_000)
+    lat = leg["roofline"]["latency"]
+    assert lat["frac"] is None and "note" in lat
+    assert lat["chain_us"] == 10.1 and abs(lat["frac_of_pattern"] - 10.0 / 10.3) < 1e-3
+    assert bench.MIX_BOUND_RUNS >= 3
+
+
 def test_txseg_block_floor_counts_lines():
     _, _, segs, _ = pktgen.tx_segments(64, seed=3, nflows=8, tx_len=4096, make_shm=False, room=2048)
     fl = bench.txseg_block_floor(segs)
