@@ -81,7 +81,10 @@ constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
 // level's loads of all F frames are issued together, so each lane keeps F
 // dependent chains in flight -- at 8 waves per SIMD one frame per lane leaves
 // 256K frames two generations of waves deep, each paying the whole chain.
-template <int CRC, bool CHUNK, int F = 1>
+// NTKEY (A/B variant 9, round 4): the frame-key loads non-temporal, so the
+// 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
+// table lines from the XCDs' L2s between launches
+template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
   constexpr bool TAB = CRC == kCrcSlice4;
@@ -104,7 +107,11 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
     } else if (p.l4_off == p.ip_off + 20u) {
       // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
       // unaligned dwordx3 load (gfx950 global loads take any byte address)
-      const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+      u32x3u k;
+      if constexpr (NTKEY)
+        k = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
+      else
+        k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
       rip[f] = k.x;
       lip[f] = k.y;
       l4x[f] = k.z;
@@ -267,12 +274,12 @@ extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t 
 }
 #endif
 
-template <int F>
+template <int F, bool NTKEY = false>
 static int launch_flow_f(const char *name, const tasx_flow_params *p, hipStream_t s)
 {
   const uint64_t blocks = ((uint64_t) p->n + 256u * F - 1) / (256u * F);
   tasx_note_kernel(name);
-  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -301,6 +308,7 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   case 6: return launch_flow_f<1>("flow_lookup_kernel<f1>", p, s); // 1 / 4 frames per lane
   case 7: return launch_flow_f<4>("flow_lookup_kernel<f4>", p, s);
   case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
+  case 9: return launch_flow_f<kFlowFramesPerLane, true>("flow_lookup_kernel<ntkey>", p, s);
   default: break;
   }
 #else

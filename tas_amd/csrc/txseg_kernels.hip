@@ -927,7 +927,19 @@ __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
 // stored non-temporal too (correct), 8 = the access pattern alone (timing
 // only: the aligned source chunks stored as loaded, no LDS realignment or
 // splice; bench.py's tx_segment pattern_ceiling), 16 = windows read back by
-// ds_read_b128 + ds_read_b32 (correct where the LDS runs in unaligned mode)
+// ds_read_b128 + ds_read_b32 (correct where the LDS runs in unaligned mode),
+// 32 = the source chunks land in the slice by LDS-DMA (global_load_lds_dwordx4,
+// round 4, VERDICT r03 item 4: no VGPR staging and no ds_write; one DMA per
+// row and slot, the row's lanes alone active, so that M0 -- per wave -- can
+// point at the row's own slice: the slice layout stays as it is)
+#ifdef TASX_AB
+__device__ __forceinline__ void glds16_row(const void *gsrc, uint32_t lds_addr)
+{
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+}
+#endif
 template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
@@ -1000,13 +1012,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       const int nAB = max(nA + nB, 1);
       const uint32_t dB = nB > 0 ? cB - cA - 16u * (uint32_t) nA : 0u;
       u32x4 a[kLdsSlots];
+#ifdef TASX_AB
+      if constexpr ((OPT & 32) != 0) {
+        // row q of the wave: its lanes alone write M0 + 256 q + 16 gl, so M0 =
+        // the row's slot address - 256 q puts chunk gl + 16u at slot 1 + gl + 16u
+        const uint32_t q = (threadIdx.x >> 4) & 3u;
+        const uint32_t slo = (uint32_t) (uintptr_t) (lds + (threadIdx.x / 16) * kLdsSlice + kLdsLead);
 #pragma unroll
-      for (int u = 0; u < kLdsSlots; ++u) {
-        const int v = min(gl + 16 * u, nAB - 1);
-        const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
-        a[u] = ld16_off(sbase, min(ro, hi_ok));
+        for (int u = 0; u < kLdsSlots; ++u) {
+          const int v = min(gl + 16 * u, nAB - 1);
+          const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
+          const uint8_t *src = sbase + min(ro, hi_ok);
+#pragma unroll
+          for (uint32_t qq = 0; qq < 4u; ++qq)
+            if (q == qq)
+              glds16_row(src, __builtin_amdgcn_readfirstlane(slo + 256u * (uint32_t) u - 256u * qq));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMAs have landed in LDS
+      } else
+#endif
+      {
+#pragma unroll
+        for (int u = 0; u < kLdsSlots; ++u) {
+          const int v = min(gl + 16 * u, nAB - 1);
+          const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
+          a[u] = ld16_off(sbase, min(ro, hi_ok));
+        }
       }
-      if constexpr (!(OPT & 8)) {
+      if constexpr ((OPT & 32) != 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if constexpr (!(OPT & 8)) {
 #pragma unroll
         for (int u = 0; u < kLdsSlots; ++u)
           *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
@@ -1472,6 +1509,8 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   case 43: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern,wpe6>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 6, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 41: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<b128>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 40: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
+  // 44 (round 4): the source chunks by LDS-DMA (the slice's LDS already caps residency at 6 waves per SIMD)
+  case 44: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<ldsdma>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 32>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU
   case 35: case 36: case 37: case 38: if (tas) {

@@ -73,9 +73,11 @@ def test_generator_wraps_and_flows():
 # A/B variants of libtasx_ab.so (TASX_TXSEG_DEBUG) run on the same cases as
 # the product (tx_segment_lds_kernel): "r2" = 30, the round-2 product
 # tx_segment_tas_kernel (unaligned non-temporal window loads); "b128" = 41,
-# the product with its LDS windows read back by ds_read_b128
-IMPLS = ["product", "r2", "b128"]
-AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel"), "b128": ("41", "tx_segment_lds_kernel<b128>")}
+# the product with its LDS windows read back by ds_read_b128; "ldsdma" = 44
+# (round 4), the product with its source chunks landed in the slice by LDS-DMA
+IMPLS = ["product", "r2", "b128", "ldsdma"]
+AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel"), "b128": ("41", "tx_segment_lds_kernel<b128>"),
+            "ldsdma": ("44", "tx_segment_lds_kernel<ldsdma>")}
 
 
 def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):

@@ -41,6 +41,9 @@ def make(leg: str, rotate: int = 16):
             segs["pos"] = (segs["pos"].astype(np.int64) % (16384 - 1448)).astype(np.uint32)
         w.segs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
         return w.loop(), w.bytes_per_step
+    if leg == "flow":  # bench.py's flow_lookup leg: 256K lookups in TAS-sized tables
+        w = bench.FlowLookupWorkload(4, pktgen.SEED + 3000)
+        return w.loop(), w.N * 64
     if leg == "rx":
         w = bench.RxPassWorkload(bench.FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000)
         return w.loop(benchloop.RX_FUSED), w.bytes_per_step
