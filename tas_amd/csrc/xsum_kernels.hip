@@ -197,19 +197,24 @@ __global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
 // offsets from the block's first packet (a uniform 64-bit base: 16 strides
 // from a 16-byte aligned base stay 16-byte aligned), so each load is
 // global_load_dwordx4 v, v_off, s[base] (one VGPR per address) at any batch size.
-template <int U, bool S32 = false>
+// G (A/B, round 4): lanes per packet -- 16 (the product: one DPP row), 32 or
+// 64 with U = 3 / 2 loads per lane for a 1500-byte packet: fewer loads in
+// flight per lane and more packets' worth of short-lived waves, the shape of
+// the fastest trivial streaming read at config 4's sizes (profiles/r04/INDEX.md
+// r04b); lane G - 1 holds the last chunk and the group total (group_total<G>).
+template <int U, bool S32 = false, int G = 16>
 __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
 {
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
+  const int gl = threadIdx.x & (G - 1);
+  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
   if (i >= p.n)
     return;
   const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
   const uint8_t *s = nullptr;
-  const uint8_t *const bb = p.base + (uint64_t) (blockIdx.x * (kBlock / 16)) * p.stride;
+  const uint8_t *const bb = p.base + (uint64_t) (blockIdx.x * (kBlock / G)) * p.stride;
   uint32_t o0 = 0, head, last;
   if constexpr (S32) {
-    const uint32_t so = (threadIdx.x / 16) * (uint32_t) p.stride;
+    const uint32_t so = (threadIdx.x / G) * (uint32_t) p.stride;
     o0 = so & ~15u;
     head = so & 15u;
     last = (head + len - 1u) >> 4; // valid when len > 0
@@ -222,31 +227,31 @@ __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
   uint32_t acc = 0;
   if (len) {
     u32x4 t;
-    for (uint32_t cb = 0; cb <= last; cb += 16u * U) {
+    for (uint32_t cb = 0; cb <= last; cb += (uint32_t) G * U) {
       u32x4 v[U];
       if constexpr (S32) {
         const uint32_t lb = o0 + 16u * (cb + (uint32_t) gl), lastoff = o0 + 16u * last;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          v[u] = ld16nt_off(bb, min(lb + 256u * u, lastoff));
+          v[u] = ld16nt_off(bb, min(lb + 16u * G * u, lastoff));
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          v[u] = ld16nt(c0p, min(cb + (uint32_t) gl + 16u * u, last));
+          v[u] = ld16nt(c0p, min(cb + (uint32_t) gl + (uint32_t) G * u, last));
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t a = sad4(v[u], acc);
-        acc = cb + (uint32_t) gl + 16u * u <= last ? a : acc;
+        acc = cb + (uint32_t) gl + (uint32_t) G * u <= last ? a : acc;
       }
       if (cb == 0)
         acc -= gl == 0 ? sad_below(v[0], head) : 0u;
       t = v[U - 1];
     }
-    acc -= gl == 15 ? sad_from(t, head + len - 16u * last) : 0u;
+    acc -= gl == G - 1 ? sad_from(t, head + len - 16u * last) : 0u;
   }
-  acc = row_sum16(acc);
-  if (gl == 15) {
+  acc = group_total<G>(acc);
+  if (gl == G - 1) {
     uint32_t f = fold32_to_16(acc);
     if (head & 1)
       f = bswap16(f);
@@ -1902,6 +1907,22 @@ extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stre
 #endif
   case 7:
     return launch_groups("raw_wave_kernel", raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
+#ifdef TASX_AB
+  // round 4 (stride mode from a 16-byte aligned base, else automatic): 45 / 46
+  // = 32 / 64 lanes per packet with 3 / 2 loads per lane, no residency cap; 47 =
+  // the product's 16-lane rows without the cap; 48 = 32 lanes with the cap
+  case 45: case 46: case 47: case 48:
+    if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
+        (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32)) {
+      switch (variant) {
+      case 45: return launch_groups<32>("raw_sad_kernel<s32,g32>", raw_sad_kernel<3, true, 32>, *p, s, 0u);
+      case 46: return launch_groups<64>("raw_sad_kernel<s32,g64>", raw_sad_kernel<2, true, 64>, *p, s, 0u);
+      case 47: return launch_groups("raw_sad_kernel<s32,nocap>", raw_sad_kernel<6, true>, *p, s, 0u);
+      default: return launch_groups<32>("raw_sad_kernel<s32,g32,cap>", raw_sad_kernel<3, true, 32>, *p, s, kOccLds);
+      }
+    }
+    return tasx_launch_raw(p, 0, stream);
+#endif
   case 0:
   case 3:
   case 6:

@@ -28,7 +28,7 @@ def _lib():
 
 
 # variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = set(range(8, 26)) | {1, 4, 5}
+AB_VARIANTS = set(range(8, 26)) | {1, 4, 5} | set(range(45, 49))
 
 
 @contextlib.contextmanager
@@ -423,6 +423,28 @@ def test_raw_all_variants(oracle, variant):
         got = u16(xsum.raw_cksum_batch(to_dev(buf), n, offsets=to_dev(offs.astype(np.int64)),
                                        lengths=to_dev(lens.astype(np.int32))))
         np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("variant", [45, 46, 47, 48])
+def test_raw_stride_lane_groups(oracle, variant):
+    """A/B 45-48 (round 4): RAW stride mode with 32 / 64 lanes per packet (3 /
+    2 loads per lane) and without the residency cap -- odd strides and lengths,
+    packets longer than one round (9000 B: several rounds of G*U chunks),
+    empty packets, and config 2's 64K x 1500 B batch."""
+    for L, stride in ((1500, 1500), (1499, 1501), (0, 16), (1, 17), (9000, 9000), (4097, 4112)):
+        n = 2500
+        buf = pktgen.random_bytes(L * 3 + stride + variant, n * stride + 16)
+        exp = oracle.raw_batch(buf, n, stride=stride, len0=L)
+        with kernel_variant(variant):
+            got = u16(xsum.raw_cksum_batch(to_dev(buf), n, stride=stride, len0=L))
+            assert xsum.last_kernel().startswith("raw_sad_kernel<s32,"), xsum.last_kernel()
+        np.testing.assert_array_equal(got, exp, err_msg=f"L={L} stride={stride}")
+    n, L = 65536, 1500
+    d = dev_random(n * L, 2)
+    exp = oracle.raw_batch(d.cpu().numpy(), n, stride=L, len0=L)
+    with kernel_variant(variant):
+        got = u16(xsum.raw_cksum_batch(d, n, stride=L, len0=L))
+    np.testing.assert_array_equal(got, exp)
 
 
 @pytest.mark.parametrize("variant", [0, 5])

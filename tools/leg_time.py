@@ -41,6 +41,12 @@ def make(leg: str, rotate: int = 16):
             segs["pos"] = (segs["pos"].astype(np.int64) % (16384 - 1448)).astype(np.uint32)
         w.segs = torch.from_numpy(segs.view(np.uint8).copy()).cuda()
         return w.loop(), w.bytes_per_step
+    if leg == "raw":  # bench.py's raw leg: 64K x 1500 B packed payloads
+        w = bench.RawWorkload(rotate, pktgen.SEED + 1000)
+        return w.loop(), w.bytes_per_step
+    if leg in ("shard8m", "shard1m"):  # config 4 at N = 1 (12.6 GB) / its per-GPU shard at N = 8 (1.57 GB)
+        w = bench.shard8m_workload(1 if leg == "shard8m" else 8, 0)
+        return w.loop(), w.bytes_per_step
     if leg == "flow":  # bench.py's flow_lookup leg: 256K lookups in TAS-sized tables
         w = bench.FlowLookupWorkload(4, pktgen.SEED + 3000)
         return w.loop(), w.N * 64
