@@ -82,6 +82,12 @@ int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream);
  * for real data). */
 int tasx_ab_stream_read(const void *src, size_t bytes, int path, uint32_t *sink, void *stream);
 
+/* The flush server's timing sums for ring r (TASX_SRV_DIAG=1 in the
+ * environment at tasx_server_start), in us: out[0] detection -> frames
+ * loaded, out[1] frames loaded -> stores acknowledged, out[2] completion ->
+ * next detection, over out[3] batches; out[4] empty polls. */
+int tasx_ab_server_diag(int device, unsigned r, double *out);
+
 /* Test hook: restart a context's flush tickets at `start` (nothing pending or
  * in flight, no feeder), so a test can run flushes across the 2^32 wrap. */
 int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start);

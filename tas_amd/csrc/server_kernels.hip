@@ -52,6 +52,10 @@ __device__ __forceinline__ void st_sys32(uint32_t *p, uint32_t v)
 {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void st_sys64(uint64_t *p, uint64_t v)
+{
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ uint64_t rlane64(uint64_t x, int l)
 {
   const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) x, l);
@@ -139,6 +143,14 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint32_t p = s_p;
   uint64_t t_act = wall_clock64(), t_lease = t_act;
   uint32_t lease = 0u;
+#ifdef TASX_AB
+  // A/B diagnostics (P.diag): per ring, running sums of the detection -> frames
+  // loaded and frames loaded -> stores acknowledged times, the gap between a
+  // batch's completion and the next detection, and the empty polls, in the
+  // ring's done line after every batch (tasx_ab_server_diag)
+  uint64_t d_load = 0, d_ack = 0, d_gap = 0, d_n = 0, d_empty = 0, t_end = t_act;
+  const bool diag = P.diag != 0u;
+#endif
   for (;;) {
     if (threadIdx.x < 64) {
       for (;;) {
@@ -148,6 +160,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         const uint64_t hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
                                      : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
         const uint64_t h0 = rlane64(hw, 0), h1 = rlane64(hw, 1), c = rlane64(hw, 2);
+#ifdef TASX_AB
+        if (diag)
+          d_empty++;
+#endif
         const uint32_t n = (uint32_t) (h0 & 0xffffu);
         const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
         if (hdr && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (e >> 48) != tag) == 0ull) {
@@ -201,12 +217,32 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       if (gl == 15 && !ok)
         atomicOr(&s_bad, 1u);
     }
+#ifdef TASX_AB
+    const uint64_t t_loaded = diag ? wall_clock64() : 0ull; // thread 0: its row's loads are in (its sums used them)
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
       if (s_bad)
         st_sys32(dline + 1, 1u); // sticky: a frame changed after submission (or a malformed slot)
       st_sys32(dline, p + 1u);
+#ifdef TASX_AB
+      if (diag) {
+        const uint64_t t_acked = wall_clock64();
+        d_load += t_loaded - t_act;
+        d_ack += t_acked - t_loaded;
+        d_gap += t_act - t_end;
+        d_n++;
+        d_empty--; // the poll that found the batch
+        t_end = t_acked;
+        uint64_t *dd = (uint64_t *) (dline + 2);
+        st_sys64(dd, d_load);
+        st_sys64(dd + 1, d_ack);
+        st_sys64(dd + 2, d_gap);
+        st_sys64(dd + 3, d_n);
+        st_sys64(dd + 4, d_empty);
+      }
+#endif
     }
     ++p;
   }

@@ -1951,6 +1951,7 @@ struct fserver {
   int keep_run;
   pthread_t keep;
   uint64_t batches, frames; /* submitted (statistics) */
+  uint32_t khz;             /* wall clock rate (A/B diagnostics) */
 };
 
 static struct fserver *g_server[MAX_DEVICES];
@@ -2125,6 +2126,11 @@ int tasx_server_start(int device)
     prm.mem = S->d_mem;
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
+    prm.diag = 0;
+#ifdef TASX_AB
+    prm.diag = getenv("TASX_SRV_DIAG") != NULL;
+    S->khz = (uint32_t) khz;
+#endif
     S->keep_run = 1;
     __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
     if (pthread_create(&S->keep, NULL, server_keepalive, S) != 0) {
@@ -2195,6 +2201,29 @@ int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
   pthread_mutex_unlock(&g_server_mu);
   return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
 }
+
+#ifdef TASX_AB
+/* A/B: ring r's timing sums (TASX_SRV_DIAG=1 at tasx_server_start), in us:
+ * out[0] detection -> frames loaded, [1] frames loaded -> stores
+ * acknowledged, [2] completion -> next detection, summed over out[3] batches;
+ * out[4] empty polls */
+int tasx_ab_server_diag(int device, unsigned r, double *out)
+{
+  if (device < 0 || device >= MAX_DEVICES || r >= TASX_MAX_CTX || !out)
+    return set_err(-EINVAL, "server diag: bad argument");
+  pthread_mutex_lock(&g_server_mu);
+  const struct fserver *S = g_server[device];
+  if (S) {
+    const uint64_t *dd = (const uint64_t *) (srv_dline(S, r) + 2);
+    for (int k = 0; k < 5; k++) {
+      const uint64_t v = __atomic_load_n(dd + k, __ATOMIC_ACQUIRE);
+      out[k] = (k < 3 && S->khz) ? (double) v * 1000.0 / S->khz : (double) v;
+    }
+  }
+  pthread_mutex_unlock(&g_server_mu);
+  return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
+}
+#endif
 
 int tasx_ctx_use_server(unsigned ctx_id, int on)
 {

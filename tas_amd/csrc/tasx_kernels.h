@@ -91,7 +91,8 @@ typedef struct tasx_flow_params {
  * pinned host memory per GPU, host-written lines apart from GPU-written ones.
  *   [TASX_SRV_CTL]     u64: stop (low word, host) | lease (high word, host keepalive)
  *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 consumed (positions
- *                      taken and finished), u32 error (sticky)
+ *                      taken and finished), u32 error (sticky); A/B builds:
+ *                      then 5 u64 timing sums (tasx_ab_server_diag)
  *   [TASX_SRV_SLOTP(r, p)] ring r, position p: a 1 KiB descriptor slot,
  *     u64 h0 = n | min(region bytes, 2^32 - 1) << 16 | tag << 48,
  *     u64 h1 = region device address (48 bits) | tag << 48,
@@ -112,6 +113,7 @@ typedef struct tasx_srv_params {
   uint8_t *mem;          /* device view of the server's pinned block */
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
+  uint32_t diag;         /* A/B builds: timing sums in the done lines (tasx_ab_server_diag) */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
