@@ -151,62 +151,98 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint64_t d_load = 0, d_ack = 0, d_gap = 0, d_n = 0, d_empty = 0, t_end = t_act;
   const bool diag = P.diag != 0u;
 #endif
+  // The poller's reads of ring r's slot at position pp: its entry word (every
+  // lane), the two header words (lanes 0-1) and the control word (lane 2).
+  struct SlotRead {
+    uint64_t e, hw;
+  };
+  auto read_slot = [&](uint32_t pp) {
+    const uint8_t *slot = mem + TASX_SRV_SLOTP(r, pp);
+    SlotRead v;
+    v.e = ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane);
+    v.hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
+                    : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
+    return v;
+  };
+  // A read of position p: 1 = the batch is complete (taken: its descriptors
+  // into LDS), 0 = nothing yet, 2 = the header landed before some of its
+  // entries (read again at once), 3 = stop, 4 = the lease ran out
+  auto judge = [&](const SlotRead &v) -> int {
+    const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
+    const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
+    const uint32_t n = (uint32_t) (h0 & 0xffffu);
+    const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
+    if (hdr && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (v.e >> 48) != tag) == 0ull) {
+      if ((uint32_t) lane < n) {
+        s_off[lane] = (uint32_t) v.e;
+        s_tl[lane] = (uint32_t) (v.e >> 32) & 0xffffu;
+      }
+      if (lane == 0) {
+        s_n = n;
+        s_bytes = (uint32_t) (h0 >> 16);
+        s_base = h1 & 0xffffffffffffull;
+      }
+      t_act = wall_clock64();
+      return 1;
+    }
+#ifdef TASX_AB
+    if (diag)
+      d_empty++;
+#endif
+    const uint64_t now = wall_clock64();
+    if ((uint32_t) c != 0u)
+      return 3;
+    if ((uint32_t) (c >> 32) != lease) {
+      lease = (uint32_t) (c >> 32);
+      t_lease = now;
+    } else if (now - t_lease > P.lease_ticks) { // no keepalive: the host process is gone
+      return 4;
+    }
+    return hdr ? 2 : 0;
+  };
+  // poll modes (P.poll): bit 0 = read the next position's slot while the rows
+  // work on this one (a queued batch is taken without a round trip); bit 1 =
+  // two reads of the slot in flight, half a round trip apart (a batch is seen
+  // sooner after the host publishes it)
+  const bool prefetch = (P.poll & 1u) != 0u, two = (P.poll & 2u) != 0u;
+  SlotRead pre = {0ull, 0ull};
+  bool have_pre = false;
   for (;;) {
     if (threadIdx.x < 64) {
-      for (;;) {
-        const uint8_t *slot = mem + TASX_SRV_SLOTP(r, p);
-        const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
-        const uint64_t e = ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane);
-        const uint64_t hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
-                                     : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
-        const uint64_t h0 = rlane64(hw, 0), h1 = rlane64(hw, 1), c = rlane64(hw, 2);
-#ifdef TASX_AB
-        if (diag)
-          d_empty++;
-#endif
-        const uint32_t n = (uint32_t) (h0 & 0xffffu);
-        const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
-        if (hdr && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (e >> 48) != tag) == 0ull) {
-          if ((uint32_t) lane < n) {
-            s_off[lane] = (uint32_t) e;
-            s_tl[lane] = (uint32_t) (e >> 32) & 0xffffu;
-          }
-          if (lane == 0) {
-            s_n = n;
-            s_bytes = (uint32_t) (h0 >> 16);
-            s_base = h1 & 0xffffffffffffull;
-            s_cmd = 0u;
-          }
-          t_act = wall_clock64();
-          break;
-        }
-        // nothing yet (or the header landed before some of its entries: read
-        // the slot again at once)
-        const uint64_t now = wall_clock64();
-        if ((uint32_t) c != 0u) { // stop
-          if (lane == 0)
-            s_cmd = 1u;
-          break;
-        }
-        if ((uint32_t) (c >> 32) != lease) {
-          lease = (uint32_t) (c >> 32);
-          t_lease = now;
-        } else if (now - t_lease > P.lease_ticks) { // no keepalive: the host process is gone
-          if (lane == 0)
-            s_cmd = 2u;
-          break;
-        }
-        if (hdr)
-          continue;
-        if (now - t_act < P.hot_ticks)
-          __builtin_amdgcn_s_sleep(1);
-        else
-          __builtin_amdgcn_s_sleep(32);
+      SlotRead a = have_pre ? pre : read_slot(p), b = {0ull, 0ull};
+      if (two) {
+        if (!have_pre)
+          __builtin_amdgcn_s_sleep(24);
+        b = read_slot(p);
       }
+      int st;
+      for (;;) {
+        st = judge(a);
+        if (st == 1 || st >= 3)
+          break;
+        a = read_slot(p);
+        if (two) {
+          st = judge(b);
+          if (st == 1 || st >= 3)
+            break;
+          b = read_slot(p);
+        }
+        if (st == 2)
+          continue; // the header without all its entries: read again at once
+        if (wall_clock64() - t_act >= P.hot_ticks)
+          __builtin_amdgcn_s_sleep(32);
+        else if (!two)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0)
+        s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
     }
     __syncthreads();
     if (s_cmd != 0u)
       break;
+    have_pre = prefetch && threadIdx.x < 64;
+    if (have_pre) // the next position's slot, read while this batch is summed
+      pre = read_slot(p + 1u);
     const uint32_t row = threadIdx.x >> 4;
     if (row < s_n) {
       const uint64_t base = s_base;
@@ -233,7 +269,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         d_ack += t_acked - t_loaded;
         d_gap += t_act - t_end;
         d_n++;
-        d_empty--; // the poll that found the batch
         t_end = t_acked;
         uint64_t *dd = (uint64_t *) (dline + 2);
         st_sys64(dd, d_load);

@@ -1942,6 +1942,7 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
 #define SRV_LEASE_S 2u
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
+#define SRV_POLL 0u /* the kernel's poll mode (tasx_srv_params.poll) */
 
 struct fserver {
   int device;
@@ -2127,8 +2128,11 @@ int tasx_server_start(int device)
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.diag = 0;
+    prm.poll = SRV_POLL;
 #ifdef TASX_AB
     prm.diag = getenv("TASX_SRV_DIAG") != NULL;
+    if (getenv("TASX_SRV_POLL")) /* A/B: the poll modes (server_kernels.hip) */
+      prm.poll = (uint32_t) atoi(getenv("TASX_SRV_POLL")) & 3u;
     S->khz = (uint32_t) khz;
 #endif
     S->keep_run = 1;

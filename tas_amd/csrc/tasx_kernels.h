@@ -114,6 +114,7 @@ typedef struct tasx_srv_params {
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint32_t diag;         /* A/B builds: timing sums in the done lines (tasx_ab_server_diag) */
+  uint32_t poll;         /* bit 0: read the next slot during a batch; bit 1: two reads in flight */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
