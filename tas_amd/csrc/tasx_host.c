@@ -461,6 +461,7 @@ struct tasx_ctx {
   uint32_t sv_done_pos; /* positions the server has finished (as last seen) */
   uint32_t sv_ticket[TASX_SRV_RING]; /* ticket of the batch at each ring position */
   uint32_t n_server_flushes;
+  uint64_t sv_batches, sv_frames; /* since attach (this thread's own counters: no shared line per flush) */
 };
 
 #define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
@@ -1951,7 +1952,7 @@ struct fserver {
   uint32_t attached;      /* bit r: ring r serves a context */
   int keep_run;
   pthread_t keep;
-  uint64_t batches, frames; /* submitted (statistics) */
+  uint64_t batches, frames; /* submitted by contexts since detached (statistics) */
   uint32_t khz;             /* wall clock rate (A/B diagnostics) */
 };
 
@@ -2080,8 +2081,8 @@ static int server_submit(struct tasx_ctx *c)
     c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
     c->sv_pos = pos + 1u;
     c->n_server_flushes++;
-    __atomic_fetch_add(&S->batches, (uint64_t) 1, __ATOMIC_RELAXED);
-    __atomic_fetch_add(&S->frames, (uint64_t) cnt, __ATOMIC_RELAXED);
+    __atomic_store_n(&c->sv_batches, c->sv_batches + 1u, __ATOMIC_RELAXED);
+    __atomic_store_n(&c->sv_frames, c->sv_frames + cnt, __ATOMIC_RELAXED);
     if (cnt < c->npend) {
       memmove(c->pend_ip, c->pend_ip + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_ip));
       memmove(c->pend_l4, c->pend_l4 + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_l4));
@@ -2196,11 +2197,17 @@ int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
     return set_err(-EINVAL, "no flush server running for device %d", device);
   pthread_mutex_lock(&g_server_mu);
   const struct fserver *S = g_server[device];
-  if (S) {
+  if (S) { /* detached contexts' counts, plus the attached ones' so far */
+    uint64_t b = __atomic_load_n(&S->batches, __ATOMIC_RELAXED), f = __atomic_load_n(&S->frames, __ATOMIC_RELAXED);
+    for (unsigned id = 0; id < TASX_MAX_CTX; id++)
+      if (__atomic_load_n(&S->attached, __ATOMIC_ACQUIRE) & (1u << id)) {
+        b += __atomic_load_n(&g_ctx[id].sv_batches, __ATOMIC_RELAXED);
+        f += __atomic_load_n(&g_ctx[id].sv_frames, __ATOMIC_RELAXED);
+      }
     if (batches)
-      *batches = __atomic_load_n(&S->batches, __ATOMIC_RELAXED);
+      *batches = b;
     if (frames)
-      *frames = __atomic_load_n(&S->frames, __ATOMIC_RELAXED);
+      *frames = f;
   }
   pthread_mutex_unlock(&g_server_mu);
   return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
@@ -2251,6 +2258,7 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
     if (S) {
       c->sv_pos = c->sv_done_pos = __atomic_load_n(srv_dline(S, id), __ATOMIC_ACQUIRE);
+      c->sv_batches = c->sv_frames = 0;
       c->sv = S;
       __atomic_or_fetch(&S->attached, 1u << id, __ATOMIC_RELEASE);
     }
@@ -2261,7 +2269,11 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
     return 0;
   if ((rc = flush_wait(c, c->next_ticket)) != 0)
     return rc;
+  pthread_mutex_lock(&g_server_mu); /* the counts move to the server's totals atomically for tasx_server_stats */
+  __atomic_fetch_add(&c->sv->batches, c->sv_batches, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&c->sv->frames, c->sv_frames, __ATOMIC_RELAXED);
   __atomic_and_fetch(&c->sv->attached, ~(1u << id), __ATOMIC_RELEASE);
+  pthread_mutex_unlock(&g_server_mu);
   c->sv = NULL;
   return 0;
 }
