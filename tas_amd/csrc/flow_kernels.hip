@@ -81,10 +81,12 @@ constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
 // level's loads of all F frames are issued together, so each lane keeps F
 // dependent chains in flight -- at 8 waves per SIMD one frame per lane leaves
 // 256K frames two generations of waves deep, each paying the whole chain.
-// NTKEY (A/B variant 9, round 4): the frame-key loads non-temporal, so the
-// 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
-// table lines from the XCDs' L2s between launches
-template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false>
+// NTKEY (A/B variants 9 / 10, round 4): the frame-key loads non-temporal, so
+// the 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
+// table lines from the XCDs' L2s between launches; NTFS
+// (10): the flow-state key loads non-temporal too, so that the 2 MiB bucket
+// table alone competes for each XCD's 4 MiB L2
+template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false, bool NTFS = false>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
   constexpr bool TAB = CRC == kCrcSlice4;
@@ -169,8 +171,11 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
       const uint32_t ffid = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
       fid[f][j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
       cand[f][j] = (ffid & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
-      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (
-          p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
+      const uint8_t *fsk = p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off;
+      if constexpr (NTFS)
+        key[f][j] = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3 *) fsk);
+      else
+        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) fsk;
     }
 #pragma unroll
   for (int f = 0; f < F; ++f) {
@@ -274,12 +279,12 @@ extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t 
 }
 #endif
 
-template <int F, bool NTKEY = false>
+template <int F, bool NTKEY = false, bool NTFS = false>
 static int launch_flow_f(const char *name, const tasx_flow_params *p, hipStream_t s)
 {
   const uint64_t blocks = ((uint64_t) p->n + 256u * F - 1) / (256u * F);
   tasx_note_kernel(name);
-  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY, NTFS>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -309,6 +314,7 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   case 7: return launch_flow_f<4>("flow_lookup_kernel<f4>", p, s);
   case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
   case 9: return launch_flow_f<kFlowFramesPerLane, true>("flow_lookup_kernel<ntkey>", p, s);
+  case 10: return launch_flow_f<kFlowFramesPerLane, true, true>("flow_lookup_kernel<ntkey,ntfs>", p, s);
   default: break;
   }
 #else

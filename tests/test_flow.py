@@ -102,10 +102,11 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 9, 10])
 def test_gpu_flow_golden(flow_golden, variant):
     """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
-    chunks, 2 / 4 frames per lane) on the fixture."""
+    chunks, 2 / 4 frames per lane, non-temporal keys / flow-state keys) on the
+    fixture."""
     from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
@@ -123,7 +124,7 @@ def test_gpu_flow_golden(flow_golden, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 6, 7])
+@pytest.mark.parametrize("variant", [0, 6, 7, 9, 10])
 def test_gpu_flow_vs_oracle_large(oracle, variant):
     """64K flows in a TAS-sized table (2x entries), 256K frames: hits in random
     order, misses (unknown keys), hash-out off; the product and the 2 / 4

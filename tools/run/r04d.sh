@@ -10,7 +10,7 @@ for r in 1 2; do for pm in 0 1 2 3; do
   TASX_SRV_POLL=$pm TASX_SRV_DIAG=1 timeout -k 10 200 tools/bin/feeder_bench_ab 3000 7 4 > $O/srv_diag_q7_pm${pm}_r$r.jsonl 2>&1 || { echo "fb q7 failed"; exit 1; }
 done; done
 timeout -k 10 300 tools/bin/feeder_bench_ab 3000 7 2 > $O/feeder_q7.jsonl 2>&1 || { echo "feeder q7 failed"; exit 1; }
-timeout -k 10 300 python -u -m pytest tests/test_txseg.py tests/test_gpu_parity.py -k "ldsdma or lane_groups or txseg" -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "tests failed"; tail -20 $O/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_txseg.py tests/test_gpu_parity.py tests/test_flow.py -k "ldsdma or lane_groups or txseg or flow" -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "tests failed"; tail -20 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for r in 1 2; do for v in 0 44 40; do
   TASX_TXSEG_DEBUG=$v timeout -k 10 200 python tools/leg_time.py txseg --reps 2 --tag tx_d$v >> $O/time.jsonl || exit 1
@@ -22,4 +22,8 @@ done; done
 for v in 0 45 46 47; do
   timeout -k 10 200 python tools/leg_time.py shard8m --variant $v --steps 6 --reps 2 --tag shard8m_v$v >> $O/time.jsonl || exit 1
 done
+for r in 1 2; do for v in 0 9 10; do
+  timeout -k 10 200 python tools/leg_time.py flow --variant $v --reps 2 --tag flow_v$v >> $O/time.jsonl || exit 1
+done; done
+for v in 0 9 10; do VARIANT=$v GROUPS="3" bash tools/pmc_legs.sh r04d/pmc flow || exit 1; done
 echo done
