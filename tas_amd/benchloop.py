@@ -68,7 +68,10 @@ def lib() -> ctypes.CDLL:
                                       ctypes.c_int]
         L.tasxb_rx_loop.argtypes = [ctypes.c_int, ctypes.POINTER(RxArgs), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, pp, ctypes.c_int]
-        for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop, L.tasxb_rx_loop):
+        L.tasxb_flush_loop.argtypes = [ctypes.c_uint, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_double)]
+        for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop, L.tasxb_rx_loop,
+                  L.tasxb_flush_loop):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -96,3 +99,14 @@ class Loop:
             rc = self.fn(self.arr, self.R, first, K, self.streams, self.S)
         if rc:
             raise xsum.TasxError(rc, self.what)
+
+
+def flush_loop(ctx: int, base: int, stride: int, n: int, iters: int):
+    """`iters` synchronous tx_flush rounds of n deferred frames from C
+    (tasxb_flush_loop): the fast-path core's microseconds per flush."""
+    import numpy as np
+    us = np.zeros(iters, np.float64)
+    rc = lib().tasxb_flush_loop(ctx, base, stride, n, iters, us.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc:
+        raise xsum.TasxError(rc, "tasxb_flush_loop")
+    return us

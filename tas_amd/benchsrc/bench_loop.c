@@ -10,6 +10,7 @@
  * arguments, one call per step.
  */
 #include <stdint.h>
+#include <time.h>
 
 #include "tasx_xsum.h"
 
@@ -164,6 +165,39 @@ int tasxb_rx_loop(int which, const tasxb_rx *a, int R, int first, int K, void *c
     }
     if (rc)
       return rc;
+  }
+  return 0;
+}
+
+/* tx_flush at TAS's batch size from C (the fast-path core's view): `iters`
+ * synchronous flushes of the n frames at base + i * stride -- n x
+ * tasx_defer_tcp4 (the deferred tcp_checksums), tasx_flush_submit,
+ * tasx_flush_wait -- on context ctx, whatever it is attached to (nothing: its
+ * own launches; the feeder; the flush server).  us[k] = record + submit + wait
+ * of flush k (CLOCK_MONOTONIC).  0 or the first error. */
+static double tasxb_now_us(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+int tasxb_flush_loop(unsigned ctx, uint8_t *base, uint64_t stride, uint32_t n, int iters, double *us)
+{
+  for (int k = 0; k < iters; k++) {
+    const double t0 = tasxb_now_us();
+    for (uint32_t i = 0; i < n; i++) {
+      int rc = tasx_defer_tcp4(ctx, base + (uint64_t) i * stride, TASX_TAS_IP_OFF, TASX_TAS_L4_OFF);
+      if (rc)
+        return rc;
+    }
+    uint32_t t;
+    int rc = tasx_flush_submit(ctx, &t);
+    if (rc == 0)
+      rc = tasx_flush_wait(ctx, t);
+    if (rc)
+      return rc;
+    us[k] = tasxb_now_us() - t0;
   }
   return 0;
 }
