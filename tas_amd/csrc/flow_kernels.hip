@@ -81,11 +81,13 @@ constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
 // level's loads of all F frames are issued together, so each lane keeps F
 // dependent chains in flight -- at 8 waves per SIMD one frame per lane leaves
 // 256K frames two generations of waves deep, each paying the whole chain.
-// NTKEY (A/B variants 9 / 10, round 4): the frame-key loads non-temporal, so
-// the 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
-// table lines from the XCDs' L2s between launches; NTFS
-// (10): the flow-state key loads non-temporal too, so that the 2 MiB bucket
-// table alone competes for each XCD's 4 MiB L2
+// NTKEY (round 4, the product): the frame-key loads non-temporal, so the
+// 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
+// table lines from the XCDs' L2s between launches: 256K
+// lookups 11.67-11.73 us against 12.17-12.29 with L2-allocating key loads (A/B
+// 9 now), the same box (profiles/r04/INDEX.md r04d).  NTFS (A/B 10): the
+// flow-state key loads non-temporal too, so that the 2 MiB bucket table alone
+// competes for each XCD's 4 MiB L2: slower (13.33-13.37 us)
 template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false, bool NTFS = false>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
@@ -214,7 +216,8 @@ __global__ __launch_bounds__(256) void flow_pattern_kernel(tasx_flow_params p)
     i0[f] = blockIdx.x * (256u * F) + 256u * (uint32_t) f + threadIdx.x;
     i[f] = min(i0[f], p.n - 1u);
     const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+    // the product's key load (non-temporal since round 4)
+    const u32x3u k = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
     h[f] = mix32(k.x ^ k.y ^ k.z);
   }
   uint64_t e[F][TASX_FLOWHT_NBSZ];
@@ -313,14 +316,15 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   case 6: return launch_flow_f<1>("flow_lookup_kernel<f1>", p, s); // 1 / 4 frames per lane
   case 7: return launch_flow_f<4>("flow_lookup_kernel<f4>", p, s);
   case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
-  case 9: return launch_flow_f<kFlowFramesPerLane, true>("flow_lookup_kernel<ntkey>", p, s);
-  case 10: return launch_flow_f<kFlowFramesPerLane, true, true>("flow_lookup_kernel<ntkey,ntfs>", p, s);
+  case 9: return launch_flow_f<kFlowFramesPerLane, false>("flow_lookup_kernel<l2key>", p, s); // the round-3 product
+  case 10: return launch_flow_f<kFlowFramesPerLane, true, true>("flow_lookup_kernel<ntfs>", p, s);
   default: break;
   }
 #else
   (void) variant;
 #endif
   // two frames per lane: 256K lookups 11.85 us against 12.53 with one and
-  // 12.98 with four (register pressure; profiles/r02/r02ca)
-  return launch_flow_f<kFlowFramesPerLane>("flow_lookup_kernel", p, s);
+  // 12.98 with four (register pressure; profiles/r02/r02ca); the frame keys
+  // non-temporal (round 4, above)
+  return launch_flow_f<kFlowFramesPerLane, true>("flow_lookup_kernel", p, s);
 }

@@ -105,8 +105,8 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 @pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 9, 10])
 def test_gpu_flow_golden(flow_golden, variant):
     """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
-    chunks, 2 / 4 frames per lane, non-temporal keys / flow-state keys) on the
-    fixture."""
+    chunks, 2 / 4 frames per lane, L2-allocating keys (9: the round-3
+    product), non-temporal flow-state keys (10)) on the fixture."""
     from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
