@@ -8,9 +8,8 @@
 // the same 32 frames.  Here the fast-path core writes a descriptor slot into
 // its context's ring in coherent pinned memory (frame offsets in its
 // registered mbuf region, each with its ip.total_length) and the header last;
-// workgroup r of this grid polls ring r, sums the frames in place over PCIe
-// and stores both checksum fields into them, then posts the ring's consumed
-// count.  Layout and protocol: tasx_kernels.h (TASX_SRV_*), tasx_host.c
+// the workgroups of ring r poll its slots, sum the frames in place over PCIe
+// and store both checksum fields into them, then post each slot's done word.  Layout and protocol: tasx_kernels.h (TASX_SRV_*), tasx_host.c
 // (server_submit).
 //
 // Coherence without fences on the data path (MI355X_MICROARCH.md, hand-off
@@ -20,8 +19,8 @@
 // an earlier batch must never be served) and the two checksum fields are
 // written by sc0 sc1 stores (write-through to host memory).  Each wave waits
 // for its stores (vmcnt(0)), the workgroup meets at a barrier, and only then
-// does one lane store the consumed count, also sc0 sc1: the host sees the
-// count after the fields.  Descriptor words carry the 16-bit tag of their ring
+// does one lane store the slot's done word, also sc0 sc1: the host sees the
+// word after the fields.  Descriptor words carry the 16-bit tag of their ring
 // position, so a slot read over PCIe while the host was still writing it is
 // recognised (a word with an older tag) and read again -- no separate
 // doorbell round trip.
@@ -120,53 +119,62 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
   return ok;
 }
 
-// Workgroup r serves ring r (context r).  Wave 0 polls the ring's next slot:
-// lanes read the 64 entry words, lanes 0-1 the two header words, lane 2 the
-// control word, all system scope, in one round trip; a slot is taken when the
-// header and every entry carry the position's tag.  The other 15 waves wait at
-// the barrier meanwhile (no issue slots).  Then row k sums frame k, and
-// thread 0 posts consumed = position + 1 after every wave's stores completed.
+// K = P.k workgroups serve ring r (context r): workgroup k takes the ring's
+// positions p = k, k + K, k + 2K, ..., so up to K of the ring's queued batches
+// are summed at once (one workgroup per ring summed its batches one after the
+// other: 14-15 M frames/s at 8 threads x 7 in flight, profiles/r04/r04d) and
+// each posts its own slot's done word.  Wave 0 polls the workgroup's next
+// position: lanes read the 64 entry words, lanes 0-1 the two header words,
+// lane 2 the control word, all system scope, in one round trip; a slot is
+// taken when the header and every entry carry the position's tag.  After
+// P.cold_ticks without a batch only the header and control words are read
+// (16 + 8 bytes a poll instead of 528, about every 3 us): idle rings cost the
+// PCIe link almost nothing, and the first batch after the lull pays one more
+// round trip.  The other 15 waves wait at the barrier meanwhile (no issue
+// slots).  Then row j sums frame j, and thread 0 posts done[p mod RING] =
+// p + 1 after every wave's stores completed.
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
-  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_p;
+  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad;
   __shared__ uint64_t s_base;
-  const uint32_t r = blockIdx.x;
+  const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
   uint8_t *const mem = P.mem;
   uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
-  if (threadIdx.x == 0) {
-    s_p = (uint32_t) ld_sys64((const uint64_t *) dline); // consumed (low word): a restart continues there
+  if (threadIdx.x == 0)
     s_bad = 0u;
-  }
   __syncthreads();
-  uint32_t p = s_p;
+  uint32_t p = blockIdx.x % K; // the server starts on a zeroed block: every ring at position 0
   uint64_t t_act = wall_clock64(), t_lease = t_act;
   uint32_t lease = 0u;
 #ifdef TASX_AB
-  // A/B diagnostics (P.diag): per ring, running sums of the detection -> frames
-  // loaded and frames loaded -> stores acknowledged times, the gap between a
-  // batch's completion and the next detection, and the empty polls, in the
-  // ring's done line after every batch (tasx_ab_server_diag)
+  // A/B diagnostics (P.diag): per workgroup, running sums of the detection ->
+  // frames loaded and frames loaded -> stores acknowledged times, the gap
+  // between a batch's completion and the next detection, and the empty polls,
+  // in its diagnostics line after every batch (tasx_ab_server_diag)
   uint64_t d_load = 0, d_ack = 0, d_gap = 0, d_n = 0, d_empty = 0, t_end = t_act;
   const bool diag = P.diag != 0u;
+  uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
 #endif
-  // The poller's reads of ring r's slot at position pp: its entry word (every
-  // lane), the two header words (lanes 0-1) and the control word (lane 2).
+  // The poller's reads of ring r's slot at position p: the entry words (every
+  // lane; skipped when only the header is polled), the two header words
+  // (lanes 0-1) and the control word (lane 2).
   struct SlotRead {
     uint64_t e, hw;
   };
-  auto read_slot = [&](uint32_t pp) {
-    const uint8_t *slot = mem + TASX_SRV_SLOTP(r, pp);
+  auto read_slot = [&](bool entries) {
+    const uint8_t *slot = mem + TASX_SRV_SLOTP(r, p);
     SlotRead v;
-    v.e = ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane);
+    v.e = entries ? ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane) : 0ull;
     v.hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
                     : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
     return v;
   };
   // A read of position p: 1 = the batch is complete (taken: its descriptors
-  // into LDS), 0 = nothing yet, 2 = the header landed before some of its
-  // entries (read again at once), 3 = stop, 4 = the lease ran out
+  // into LDS), 0 = nothing yet, 2 = the header without all its entries (the
+  // host still writing them, or a header-only poll: read the whole slot at
+  // once), 3 = stop, 4 = the lease ran out
   auto judge = [&](const SlotRead &v) -> int {
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
@@ -200,39 +208,26 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     }
     return hdr ? 2 : 0;
   };
-  // poll modes (P.poll): bit 0 = read the next position's slot while the rows
-  // work on this one (a queued batch is taken without a round trip); bit 1 =
-  // two reads of the slot in flight, half a round trip apart (a batch is seen
-  // sooner after the host publishes it)
-  const bool prefetch = (P.poll & 1u) != 0u, two = (P.poll & 2u) != 0u;
-  SlotRead pre = {0ull, 0ull};
-  bool have_pre = false;
   for (;;) {
     if (threadIdx.x < 64) {
-      SlotRead a = have_pre ? pre : read_slot(p), b = {0ull, 0ull};
-      if (two) {
-        if (!have_pre)
-          __builtin_amdgcn_s_sleep(24);
-        b = read_slot(p);
-      }
+      bool entries = true;
       int st;
       for (;;) {
-        st = judge(a);
+        st = judge(read_slot(entries));
         if (st == 1 || st >= 3)
           break;
-        a = read_slot(p);
-        if (two) {
-          st = judge(b);
-          if (st == 1 || st >= 3)
-            break;
-          b = read_slot(p);
-        }
+        entries = true;
         if (st == 2)
-          continue; // the header without all its entries: read again at once
-        if (wall_clock64() - t_act >= P.hot_ticks)
+          continue; // the header is in: read the whole slot again at once
+        const uint64_t idle = wall_clock64() - t_act;
+        if (idle >= P.cold_ticks) {
+          entries = false;
+          __builtin_amdgcn_s_sleep(127);
+        } else if (idle >= P.hot_ticks) {
           __builtin_amdgcn_s_sleep(32);
-        else if (!two)
+        } else {
           __builtin_amdgcn_s_sleep(1);
+        }
       }
       if (lane == 0)
         s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
@@ -240,9 +235,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     __syncthreads();
     if (s_cmd != 0u)
       break;
-    have_pre = prefetch && threadIdx.x < 64;
-    if (have_pre) // the next position's slot, read while this batch is summed
-      pre = read_slot(p + 1u);
     const uint32_t row = threadIdx.x >> 4;
     if (row < s_n) {
       const uint64_t base = s_base;
@@ -260,8 +252,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     __syncthreads();
     if (threadIdx.x == 0) {
       if (s_bad)
-        st_sys32(dline + 1, 1u); // sticky: a frame changed after submission (or a malformed slot)
-      st_sys32(dline, p + 1u);
+        st_sys32(dline + TASX_SRV_ERRW, 1u); // sticky: a frame changed after submission (or a malformed slot)
+      st_sys32(dline + p % TASX_SRV_RING, p + 1u);
 #ifdef TASX_AB
       if (diag) {
         const uint64_t t_acked = wall_clock64();
@@ -270,7 +262,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         d_gap += t_act - t_end;
         d_n++;
         t_end = t_acked;
-        uint64_t *dd = (uint64_t *) (dline + 2);
         st_sys64(dd, d_load);
         st_sys64(dd + 1, d_ack);
         st_sys64(dd + 2, d_gap);
@@ -279,7 +270,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
 #endif
     }
-    ++p;
+    p += K;
   }
 }
 
@@ -287,6 +278,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 
 extern "C" int tasx_launch_server(const tasx_srv_params *p, void *stream)
 {
-  hipLaunchKernelGGL(flush_server_kernel, dim3(TASX_MAX_CTX), dim3(kSrvBlock), 0, (hipStream_t) stream, *p);
+  if (p->k == 0u || TASX_SRV_RING % p->k != 0u || p->k > TASX_SRV_KMAX)
+    return -1;
+  hipLaunchKernelGGL(flush_server_kernel, dim3(TASX_MAX_CTX * p->k), dim3(kSrvBlock), 0, (hipStream_t) stream, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

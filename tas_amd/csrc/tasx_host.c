@@ -1934,16 +1934,18 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
  * batch of up to TASX_SRV_FB frames into the next slot of its own ring in
  * coherent pinned memory -- the entries (frame offset in its registered
  * region | ip.total_length | tag), then the region word, then the header
- * (release) -- and returns: no HIP call, no lock, no launch.  Workgroup r of
- * the kernel polls ring r, checksums the frames in place over PCIe and posts
- * the ring's consumed count, which tasx_flush_poll/_wait read.  A keepalive
+ * (release) -- and returns: no HIP call, no lock, no launch.  SRV_K
+ * workgroups of the kernel poll ring r (workgroup k the positions k mod
+ * SRV_K), checksum the frames in place over PCIe and post each slot's done
+ * word; tasx_flush_poll/_wait reap those in position order.  A keepalive
  * thread bumps the lease word every 10 ms; the kernel leaves on the stop word
  * or, when the lease has not moved for 2 s, on its own (the process is gone). */
 
 #define SRV_LEASE_S 2u
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
-#define SRV_POLL 0u /* the kernel's poll mode (tasx_srv_params.poll) */
+#define SRV_COLD_US 2000u /* idle time from which a ring's header alone is polled */
+#define SRV_K 4u          /* workgroups per ring (tasx_srv_params.k) */
 
 struct fserver {
   int device;
@@ -1954,6 +1956,8 @@ struct fserver {
   pthread_t keep;
   uint64_t batches, frames; /* submitted by contexts since detached (statistics) */
   uint32_t khz;             /* wall clock rate (A/B diagnostics) */
+  uint32_t k;               /* workgroups per ring */
+  uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
 };
 
 static struct fserver *g_server[MAX_DEVICES];
@@ -2003,7 +2007,7 @@ static void server_free(struct fserver *S)
 static int server_health(const struct tasx_ctx *c)
 {
   const unsigned id = (unsigned) (c - g_ctx);
-  if (__atomic_load_n(srv_dline(c->sv, id) + 1, __ATOMIC_ACQUIRE) != 0)
+  if (__atomic_load_n(srv_dline(c->sv, id) + TASX_SRV_ERRW, __ATOMIC_ACQUIRE) != 0)
     return set_err(-EIO, "flush server: a frame of ring %u changed after submission (or a malformed slot)", id);
   const hipError_t e = hipStreamQuery(c->sv->st);
   if (e == hipErrorNotReady)
@@ -2013,14 +2017,19 @@ static int server_health(const struct tasx_ctx *c)
   return hip_err(e, "flush server: hipStreamQuery");
 }
 
+/* the positions finished in order from sv_done_pos (the ring's workgroups
+ * finish theirs out of order) */
 static void server_reap(struct tasx_ctx *c)
 {
   const unsigned id = (unsigned) (c - g_ctx);
-  const uint32_t cons = __atomic_load_n(srv_dline(c->sv, id), __ATOMIC_ACQUIRE);
-  if (cons == c->sv_done_pos)
+  const uint32_t *done = srv_dline(c->sv, id);
+  uint32_t d = c->sv_done_pos;
+  while (d != c->sv_pos && __atomic_load_n(&done[d % TASX_SRV_RING], __ATOMIC_ACQUIRE) == d + 1u)
+    d++;
+  if (d == c->sv_done_pos)
     return;
-  const uint32_t t = c->sv_ticket[(cons - 1u) % TASX_SRV_RING];
-  c->sv_done_pos = cons;
+  const uint32_t t = c->sv_ticket[(d - 1u) % TASX_SRV_RING];
+  c->sv_done_pos = d;
   if (!ticket_le(t, c->done_ticket))
     c->done_ticket = t;
 }
@@ -2059,7 +2068,8 @@ static int server_submit(struct tasx_ctx *c)
     const uint32_t cnt = c->npend < TASX_SRV_FB ? c->npend : TASX_SRV_FB;
     /* the slot's previous batch (position sv_pos - RING) must be finished */
     uint32_t k = 0;
-    while (c->sv_pos - __atomic_load_n(srv_dline(S, id), __ATOMIC_ACQUIRE) >= TASX_SRV_RING) {
+    while (c->sv_pos - c->sv_done_pos >= TASX_SRV_RING) {
+      server_reap(c);
       if ((++k & 4095u) == 0 && (rc = server_health(c)) != 0)
         return rc;
     }
@@ -2122,20 +2132,26 @@ int tasx_server_start(int device)
     rc = hip_err(e, "server allocation");
   if (!rc && khz <= 0)
     rc = set_err(-ENODEV, "server: device %d reports no wall clock", device);
+  tasx_srv_params prm;
   if (!rc) {
     memset(S->h_mem, 0, TASX_SRV_BYTES);
-    tasx_srv_params prm;
     prm.mem = S->d_mem;
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
+    prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
     prm.diag = 0;
-    prm.poll = SRV_POLL;
+    prm.k = SRV_K;
 #ifdef TASX_AB
     prm.diag = getenv("TASX_SRV_DIAG") != NULL;
-    if (getenv("TASX_SRV_POLL")) /* A/B: the poll modes (server_kernels.hip) */
-      prm.poll = (uint32_t) atoi(getenv("TASX_SRV_POLL")) & 3u;
+    if (getenv("TASX_SRV_K")) /* A/B: workgroups per ring, 1/2/4/8 */
+      prm.k = (uint32_t) atoi(getenv("TASX_SRV_K"));
     S->khz = (uint32_t) khz;
 #endif
+    S->k = prm.k;
+    if (prm.k == 0u || TASX_SRV_RING % prm.k != 0u || prm.k > TASX_SRV_KMAX)
+      rc = set_err(-EINVAL, "server: %u workgroups per ring (a divisor of %u)", prm.k, TASX_SRV_RING);
+  }
+  if (!rc) {
     S->keep_run = 1;
     __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
     if (pthread_create(&S->keep, NULL, server_keepalive, S) != 0) {
@@ -2214,10 +2230,10 @@ int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
 }
 
 #ifdef TASX_AB
-/* A/B: ring r's timing sums (TASX_SRV_DIAG=1 at tasx_server_start), in us:
- * out[0] detection -> frames loaded, [1] frames loaded -> stores
- * acknowledged, [2] completion -> next detection, summed over out[3] batches;
- * out[4] empty polls */
+/* A/B: ring r's timing sums over its workgroups (TASX_SRV_DIAG=1 at
+ * tasx_server_start), in us: out[0] detection -> frames loaded, [1] frames
+ * loaded -> stores acknowledged, [2] a workgroup's completion -> its next
+ * detection, summed over out[3] batches; out[4] empty polls */
 int tasx_ab_server_diag(int device, unsigned r, double *out)
 {
   if (device < 0 || device >= MAX_DEVICES || r >= TASX_MAX_CTX || !out)
@@ -2225,10 +2241,14 @@ int tasx_ab_server_diag(int device, unsigned r, double *out)
   pthread_mutex_lock(&g_server_mu);
   const struct fserver *S = g_server[device];
   if (S) {
-    const uint64_t *dd = (const uint64_t *) (srv_dline(S, r) + 2);
-    for (int k = 0; k < 5; k++) {
-      const uint64_t v = __atomic_load_n(dd + k, __ATOMIC_ACQUIRE);
-      out[k] = (k < 3 && S->khz) ? (double) v * 1000.0 / S->khz : (double) v;
+    for (int k = 0; k < 5; k++)
+      out[k] = 0.0;
+    for (uint32_t w = 0; w < S->k; w++) {
+      const uint64_t *dd = (const uint64_t *) (S->h_mem + TASX_SRV_DIAG(r * S->k + w));
+      for (int k = 0; k < 5; k++) {
+        const uint64_t v = __atomic_load_n(dd + k, __ATOMIC_ACQUIRE);
+        out[k] += (k < 3 && S->khz) ? (double) v * 1000.0 / S->khz : (double) v;
+      }
     }
   }
   pthread_mutex_unlock(&g_server_mu);
@@ -2257,7 +2277,7 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
     pthread_mutex_lock(&g_server_mu);
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
     if (S) {
-      c->sv_pos = c->sv_done_pos = __atomic_load_n(srv_dline(S, id), __ATOMIC_ACQUIRE);
+      c->sv_pos = c->sv_done_pos = S->ring_pos[id]; /* where the ring's workgroups wait */
       c->sv_batches = c->sv_frames = 0;
       c->sv = S;
       __atomic_or_fetch(&S->attached, 1u << id, __ATOMIC_RELEASE);
@@ -2272,6 +2292,7 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
   pthread_mutex_lock(&g_server_mu); /* the counts move to the server's totals atomically for tasx_server_stats */
   __atomic_fetch_add(&c->sv->batches, c->sv_batches, __ATOMIC_RELAXED);
   __atomic_fetch_add(&c->sv->frames, c->sv_frames, __ATOMIC_RELAXED);
+  c->sv->ring_pos[id] = c->sv_pos;
   __atomic_and_fetch(&c->sv->attached, ~(1u << id), __ATOMIC_RELEASE);
   pthread_mutex_unlock(&g_server_mu);
   c->sv = NULL;

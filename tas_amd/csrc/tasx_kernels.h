@@ -90,22 +90,28 @@ typedef struct tasx_flow_params {
 /* The persistent flush server (server_kernels.hip): one block of coherent
  * pinned host memory per GPU, host-written lines apart from GPU-written ones.
  *   [TASX_SRV_CTL]     u64: stop (low word, host) | lease (high word, host keepalive)
- *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 consumed (positions
- *                      taken and finished), u32 error (sticky); A/B builds:
- *                      then 5 u64 timing sums (tasx_ab_server_diag)
+ *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 done[TASX_SRV_RING]
+ *                      (done[p mod RING] = p + 1 once position p is finished),
+ *                      u32 error at word TASX_SRV_ERRW (sticky)
+ *   [TASX_SRV_DIAG(b)] A/B builds: workgroup b's 5 u64 timing sums
+ *                      (tasx_ab_server_diag)
  *   [TASX_SRV_SLOTP(r, p)] ring r, position p: a 1 KiB descriptor slot,
  *     u64 h0 = n | min(region bytes, 2^32 - 1) << 16 | tag << 48,
  *     u64 h1 = region device address (48 bits) | tag << 48,
  *     then n <= TASX_SRV_FB entries u64 = frame offset in the region (32
  *     bits) | ip.total_length << 32 | tag << 48,
- *   tag = (p + 1) mod 2^16; the host writes the entries, then h1, then h0. */
+ *   tag = (p + 1) mod 2^16; the host writes the entries, then h1, then h0.
+ * Workgroup k of ring r's P.k takes its positions p = k mod P.k. */
 #define TASX_SRV_RING 8u   /* slots per ring */
 #define TASX_SRV_FB 64u    /* frames per slot */
+#define TASX_SRV_KMAX 8u   /* workgroups per ring, a divisor of TASX_SRV_RING */
 #define TASX_SRV_SLOT 1024u
 #define TASX_SRV_HDR 16u
 #define TASX_SRV_CTL 0u
-#define TASX_SRV_DONE(r) (64u * (1u + (r)))
-#define TASX_SRV_RINGS 2048u
+#define TASX_SRV_DONE(r) (128u * (1u + (r)))
+#define TASX_SRV_ERRW TASX_SRV_RING
+#define TASX_SRV_DIAG(b) (4096u + 64u * (b))
+#define TASX_SRV_RINGS (4096u + 64u * TASX_MAX_CTX * TASX_SRV_KMAX)
 #define TASX_SRV_SLOTP(r, p) (TASX_SRV_RINGS + ((r) * TASX_SRV_RING + (p) % TASX_SRV_RING) * TASX_SRV_SLOT)
 #define TASX_SRV_BYTES (TASX_SRV_RINGS + TASX_MAX_CTX * TASX_SRV_RING * TASX_SRV_SLOT)
 
@@ -113,8 +119,9 @@ typedef struct tasx_srv_params {
   uint8_t *mem;          /* device view of the server's pinned block */
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
-  uint32_t diag;         /* A/B builds: timing sums in the done lines (tasx_ab_server_diag) */
-  uint32_t poll;         /* bit 0: read the next slot during a batch; bit 1: two reads in flight */
+  uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
+  uint32_t diag;         /* A/B builds: timing sums (tasx_ab_server_diag) */
+  uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
@@ -137,7 +144,7 @@ TASX_INTERNAL int tasx_last_launch_posted_done(void);
 TASX_INTERNAL int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
 TASX_INTERNAL int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
-/* the flush server: TASX_MAX_CTX workgroups, workgroup r serves ring r */
+/* the flush server: TASX_MAX_CTX * p->k workgroups, p->k per ring; -1 for a bad p->k */
 TASX_INTERNAL int tasx_launch_server(const tasx_srv_params *p, void *stream);
 /* record the name of the kernel the calling thread launches (tasx_last_kernel) */
 TASX_INTERNAL void tasx_note_kernel(const char *name);

@@ -177,6 +177,49 @@ def test_server_ring_wrap_and_tag_wrap(oracle):
         cx.close()
 
 
+def test_server_reattach_keeps_ring_position(oracle):
+    """The ring's workgroups take positions k mod K and wait at the ring's next
+    one: a context detached after a number of flushes that is no multiple of K
+    (nor of the ring's 8 slots), then attached again -- also after the context
+    was destroyed and created anew under the same id -- continues at that
+    position, and every frame comes back right."""
+    xsum.server_start(0)
+    cx = _Ctxs([5])
+    try:
+        nf = 40
+        pin, frames = _frames(nf, 333, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nf)
+        xsum.register_frames(5, pin.addr, pin.nbytes)
+        k, done = 0, 0
+        for rnd, m in enumerate((3, 5, 1, 7, 11, 13)):
+            if rnd == 3:  # destroy and create the context anew under the same id
+                xsum.ctx_destroy(5)
+                xsum.ctx_init(5, 0, 1 << 20)
+                xsum.register_frames(5, pin.addr, pin.nbytes)
+            xsum.use_server(5)
+            before = xsum.server_flushes(5)
+            inflight = []
+            for _ in range(m):
+                xsum.tcp_checksums(5, pin.addr + (k % nf) * 2048)
+                k += 1
+                inflight.append(xsum.flush_submit(5))
+            xsum.flush_wait(5, inflight[-1])
+            assert xsum.server_flushes(5) - before == m
+            done += m
+            xsum.use_server(5, False)
+        assert k == done
+        np.testing.assert_array_equal(pin.array[:frames.size], ref)
+        assert xsum.server_stats(0)[0] == done
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
+
+
 def test_server_threads(oracle):
     """Eight fast-path threads, each with its own context bound
     (tasx_set_thread_ctx) and attached to the server, 60 tx_flush batches
