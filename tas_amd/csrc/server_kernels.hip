@@ -141,6 +141,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
   uint8_t *const mem = P.mem;
+  const uint8_t *const ring = P.ring;
   uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
   if (threadIdx.x == 0)
     s_bad = 0u;
@@ -164,11 +165,11 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     uint64_t e, hw;
   };
   auto read_slot = [&](bool entries) {
-    const uint8_t *slot = mem + TASX_SRV_SLOTP(r, p);
+    const uint8_t *slot = ring + TASX_SRV_SLOTP(r, p);
     SlotRead v;
     v.e = entries ? ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane) : 0ull;
     v.hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
-                    : lane == 2 ? ld_sys64((const uint64_t *) (mem + TASX_SRV_CTL)) : 0ull;
+                    : lane == 2 ? ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL)) : 0ull;
     return v;
   };
   // A read of position p: 1 = the batch is complete (taken: its descriptors

@@ -1951,6 +1951,9 @@ struct fserver {
   int device;
   hipStream_t st;
   uint8_t *h_mem, *d_mem; /* coherent pinned block (tasx_kernels.h TASX_SRV_*) */
+  uint8_t *h_ring, *d_ring; /* the host-written lines (control word, slots): h_mem / d_mem,
+                               A/B TASX_SRV_VRAM=1: uncached device memory written over the BAR */
+  void *vram;
   uint32_t attached;      /* bit r: ring r serves a context */
   int keep_run;
   pthread_t keep;
@@ -1971,7 +1974,7 @@ static uint32_t *srv_dline(const struct fserver *S, unsigned r)
 static void *server_keepalive(void *arg)
 {
   struct fserver *S = arg;
-  uint32_t *lease = (uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1;
+  uint32_t *lease = (uint32_t *) (S->h_ring + TASX_SRV_CTL) + 1;
   uint32_t k = 1;
   const struct timespec ts = {0, 10 * 1000 * 1000};
   while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
@@ -1989,7 +1992,7 @@ static void server_atexit(void)
     struct fserver *S = g_server[d];
     if (S) {
       __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
-      __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+      __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
     }
   }
 }
@@ -1998,6 +2001,8 @@ static void server_free(struct fserver *S)
 {
   if (S->h_mem)
     hipHostFree(S->h_mem);
+  if (S->vram)
+    hipFree(S->vram);
   if (S->st)
     hipStreamDestroy(S->st);
   free(S);
@@ -2075,7 +2080,7 @@ static int server_submit(struct tasx_ctx *c)
     }
     const uint32_t pos = c->sv_pos;
     const uint64_t tag = (uint64_t) ((pos + 1u) & 0xffffu) << 48;
-    uint64_t *slot = (uint64_t *) (S->h_mem + TASX_SRV_SLOTP(id, pos));
+    uint64_t *slot = (uint64_t *) (S->h_ring + TASX_SRV_SLOTP(id, pos));
     const uintptr_t b16 = (uintptr_t) c->zc_dev & ~(uintptr_t) 15;
     const uint8_t *h16 = c->zc_host - ((uintptr_t) c->zc_dev & 15u); /* host view of b16 */
     const uint64_t bytes = c->zc_bytes + ((uintptr_t) c->zc_dev & 15u);
@@ -2088,6 +2093,8 @@ static int server_submit(struct tasx_ctx *c)
     __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
     __atomic_store_n(&slot[0], (uint64_t) cnt | (bytes > 0xffffffffull ? 0xffffffffull : bytes) << 16 | tag,
                      __ATOMIC_RELEASE);
+    if (S->vram) /* A/B device-memory slots: push the stores out of the write-combining buffers */
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
     c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
     c->sv_pos = pos + 1u;
     c->n_server_flushes++;
@@ -2135,7 +2142,25 @@ int tasx_server_start(int device)
   tasx_srv_params prm;
   if (!rc) {
     memset(S->h_mem, 0, TASX_SRV_BYTES);
+    S->h_ring = S->h_mem;
+    S->d_ring = S->d_mem;
+#ifdef TASX_AB
+    if (getenv("TASX_SRV_VRAM")) { /* A/B: the slots in device memory, the host's stores posted over the BAR */
+      hipPointerAttribute_t at;
+      if ((e = hipExtMallocWithFlags(&S->vram, TASX_SRV_BYTES, hipDeviceMallocUncached)) != hipSuccess ||
+          (e = hipMemset(S->vram, 0, TASX_SRV_BYTES)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess ||
+          (e = hipPointerGetAttributes(&at, S->vram)) != hipSuccess)
+        rc = hip_err(e, "server: device-memory slots");
+      else if (!at.hostPointer && atoi(getenv("TASX_SRV_VRAM")) != 2)
+        rc = set_err(-ENOTSUP, "server: device-memory slots have no host mapping (TASX_SRV_VRAM=2 stores to the device address)");
+      else {
+        S->h_ring = at.hostPointer ? at.hostPointer : S->vram;
+        S->d_ring = S->vram;
+      }
+    }
+#endif
     prm.mem = S->d_mem;
+    prm.ring = S->d_ring;
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
@@ -2153,7 +2178,7 @@ int tasx_server_start(int device)
   }
   if (!rc) {
     S->keep_run = 1;
-    __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
     if (pthread_create(&S->keep, NULL, server_keepalive, S) != 0) {
       S->keep_run = 0;
       rc = set_err(-ENOMEM, "server: pthread_create failed");
@@ -2191,7 +2216,7 @@ int tasx_server_stop(int device)
     pthread_mutex_unlock(&g_server_mu);
     return set_err(-EBUSY, "flush server for device %d still serves contexts", device);
   }
-  __atomic_store_n((uint32_t *) (S->h_mem + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
   __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
   pthread_join(S->keep, NULL);
   /* bounded wait for every workgroup to leave */

@@ -116,7 +116,9 @@ typedef struct tasx_flow_params {
 #define TASX_SRV_BYTES (TASX_SRV_RINGS + TASX_MAX_CTX * TASX_SRV_RING * TASX_SRV_SLOT)
 
 typedef struct tasx_srv_params {
-  uint8_t *mem;          /* device view of the server's pinned block */
+  uint8_t *mem;          /* device view of the server's pinned block (the GPU-written lines) */
+  uint8_t *ring;         /* device view of the host-written lines (control word, slots): mem,
+                            or A/B builds' device-memory copy */
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */

@@ -15,4 +15,9 @@ for r in 1 2; do
   echo "round $r done"
 done
 for v in 0 9; do TASX_LIB=$PWD/tas_amd/_lib/libtasx_ab.so VARIANT=$v PMC_GROUPS="3" bash tools/pmc_legs.sh r04e/pmc flow || exit 1; done
+for vr in 1 2; do
+  TASX_SRV_VRAM=$vr TASX_SRV_DIAG=1 timeout -k 10 200 tools/bin/feeder_bench_ab 3000 1 4 > $O/srv_vram$vr.jsonl 2>&1 || { echo "vram$vr failed"; tail -3 $O/srv_vram$vr.jsonl; exit 1; }
+  TASX_SRV_VRAM=$vr TASX_SRV_DIAG=1 timeout -k 10 200 tools/bin/feeder_bench_ab 3000 7 4 >> $O/srv_vram$vr.jsonl 2>&1 || { echo "vram$vr q7 failed"; exit 1; }
+  echo "vram$vr ok"
+done
 echo done
