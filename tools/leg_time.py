@@ -50,6 +50,14 @@ def make(leg: str, rotate: int = 16):
     if leg == "flow":  # bench.py's flow_lookup leg: 256K lookups in TAS-sized tables
         w = bench.FlowLookupWorkload(4, pktgen.SEED + 3000)
         return w.loop(), w.N * 64
+    if leg in ("flow_small", "flow_tiny"):
+        # the same 256K lookups in tables that fit every XCD's L2 (small: 8192
+        # flows / 16K entries = 1 MiB + 128 KiB; tiny: 1024 / 2048 = 128 KiB +
+        # 16 KiB): what the lookup would take with the table levels served by L2
+        nf = 8192 if leg == "flow_small" else 1024
+        cls = type("SmallFlow", (bench.FlowLookupWorkload,), {"NFLOWS": nf, "ENTRIES": 2 * nf})
+        w = cls(4, pktgen.SEED + 3000)
+        return w.loop(), w.N * 64
     if leg == "rx":
         w = bench.RxPassWorkload(bench.FlowLookupWorkload(1, pktgen.SEED + 3000), 12, pktgen.SEED + 4000)
         return w.loop(benchloop.RX_FUSED), w.bytes_per_step
