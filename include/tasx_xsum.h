@@ -427,6 +427,11 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     registered frame region below 4 GiB; not together with the feeder) /
  *     detach (waits for the context's tickets; the ring's position is kept
  *     for the next context attached under that id)
+ *   While a server runs, HIP's frees would wait for its kernel: tasx_ctx_destroy
+ *     hands the context's memory to the server (released at its stop), and
+ *     tasx_host_free, tasx_host_unregister, tasx_dev_free and tasx_feeder_stop
+ *     return -EBUSY; anything else in the process that frees device or pinned
+ *     memory (e.g. torch.cuda.empty_cache) blocks until the stop
  *   tasx_server_stats: batches and frames submitted since start
  *   tasx_ctx_server_flushes: batches the context handed to the server */
 int tasx_server_start(int device);

@@ -609,6 +609,8 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
 }
 
 static int flush_wait(struct tasx_ctx *c, uint32_t ticket);
+static int server_defer_release(struct tasx_ctx *c);
+static int server_blocks_free(const char *what);
 
 int tasx_ctx_destroy(unsigned ctx_id)
 {
@@ -623,7 +625,11 @@ int tasx_ctx_destroy(unsigned ctx_id)
   (void) flush_wait(c, c->next_ticket);
   for (int s = 0; s < NSLOT; s++)
     hipStreamSynchronize(c->st[s]);
-  ctx_release(c);
+  /* hipFree / hipHostFree / hipHostUnregister wait for every stream of the
+   * device, the flush server's too: while one runs, the context's memory is
+   * handed to it and released when it stops */
+  if (!server_defer_release(c))
+    ctx_release(c);
   return 0;
 }
 
@@ -1839,6 +1845,11 @@ int tasx_feeder_stop(int device)
     pthread_mutex_unlock(&g_feeder_mu);
     return set_err(-EBUSY, "feeder for device %d still serves contexts", device);
   }
+  int rc = server_blocks_free("tasx_feeder_stop");
+  if (rc) {
+    pthread_mutex_unlock(&g_feeder_mu);
+    return rc;
+  }
   __atomic_store_n(&F->running, 0, __ATOMIC_RELEASE);
   pthread_join(F->thr, NULL);
   const int failed = F->failed;
@@ -1961,10 +1972,51 @@ struct fserver {
   uint32_t khz;             /* wall clock rate (A/B diagnostics) */
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
+  struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
+};
+
+struct grave {
+  struct tasx_ctx c;
+  struct grave *next;
 };
 
 static struct fserver *g_server[MAX_DEVICES];
 static pthread_mutex_t g_server_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* HIP's frees wait for every stream of the device, the server's kernel too:
+ * refused (-EBUSY) while any server runs, instead of waiting for its stop */
+static int server_blocks_free(const char *what)
+{
+  int d, any = 0;
+  pthread_mutex_lock(&g_server_mu);
+  for (d = 0; d < MAX_DEVICES; d++)
+    any |= g_server[d] != NULL;
+  pthread_mutex_unlock(&g_server_mu);
+  return any ? set_err(-EBUSY, "%s: a flush server is running (HIP frees wait for its kernel; tasx_server_stop first)",
+                       what)
+             : 0;
+}
+
+/* tasx_ctx_destroy with a server running on the context's device: the
+ * context's resources move to the server's list (the slot is free at once);
+ * 1 if taken */
+static int server_defer_release(struct tasx_ctx *c)
+{
+  int taken = 0;
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = c->device >= 0 && c->device < MAX_DEVICES ? g_server[c->device] : NULL;
+  struct grave *g = S ? malloc(sizeof(*g)) : NULL;
+  if (g) {
+    memcpy(&g->c, c, sizeof(*c));
+    g->next = S->graves;
+    S->graves = g;
+    memset(c, 0, sizeof(*c));
+    taken = 1;
+  }
+  pthread_mutex_unlock(&g_server_mu);
+  return taken;
+}
+
 
 static uint32_t *srv_dline(const struct fserver *S, unsigned r)
 {
@@ -2228,6 +2280,12 @@ int tasx_server_stop(int device)
   pthread_mutex_unlock(&g_server_mu);
   if (e == hipErrorNotReady) /* still running: leave its memory mapped (leaked), never free under it */
     return set_err(-EIO, "flush server for device %d did not stop within %u ms", device, SRV_STOP_WAIT_MS);
+  while (S->graves) { /* contexts destroyed while it ran */
+    struct grave *g = S->graves;
+    S->graves = g->next;
+    ctx_release(&g->c);
+    free(g);
+  }
   server_free(S);
   return e == hipSuccess ? 0 : hip_err(e, "flush server kernel");
 }
@@ -2358,6 +2416,9 @@ void *tasx_host_alloc(size_t bytes)
 
 int tasx_host_free(void *p)
 {
+  int rc = server_blocks_free("tasx_host_free");
+  if (rc)
+    return rc;
   HIPCHK(hipHostFree(p));
   return 0;
 }
@@ -2381,6 +2442,9 @@ int tasx_host_register(void *p, size_t bytes)
 
 int tasx_host_unregister(void *p)
 {
+  int rc = server_blocks_free("tasx_host_unregister");
+  if (rc)
+    return rc;
   HIPCHK(hipHostUnregister(p));
   return 0;
 }
@@ -2400,6 +2464,9 @@ void *tasx_dev_alloc(int device, size_t bytes)
 
 int tasx_dev_free(void *p)
 {
+  int rc = server_blocks_free("tasx_dev_free");
+  if (rc)
+    return rc;
   HIPCHK(hipFree(p));
   return 0;
 }

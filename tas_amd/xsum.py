@@ -586,8 +586,9 @@ class PinnedBuffer:
             raise TasxError(-errno.EIO, "tasx_host_device_pointer")
 
     def free(self) -> None:
-        if self.addr:
-            lib().tasx_host_free(self.addr)
+        # refused (-EBUSY) while a flush server runs (HIP frees wait for its
+        # kernel): the buffer stays, and a later free() releases it
+        if self.addr and lib().tasx_host_free(self.addr) == 0:
             self.addr = 0
             self.array = None
 

@@ -7,6 +7,7 @@ tcp_checksums (fast_flows.c:1058-1069) over the same frames.
 
 Run on the MI355X box:  python -m pytest tests/test_server.py -m gpu -x -q
 """
+import errno
 import threading
 import time
 
@@ -181,8 +182,9 @@ def test_server_reattach_keeps_ring_position(oracle):
     """The ring's workgroups take positions k mod K and wait at the ring's next
     one: a context detached after a number of flushes that is no multiple of K
     (nor of the ring's 8 slots), then attached again -- also after the context
-    was destroyed and created anew under the same id -- continues at that
-    position, and every frame comes back right."""
+    was destroyed and created anew under the same id while the server ran (its
+    memory released at the server's stop: HIP frees wait for the server's
+    kernel) -- continues at that position, and every frame comes back right."""
     xsum.server_start(0)
     cx = _Ctxs([5])
     try:
@@ -211,7 +213,14 @@ def test_server_reattach_keeps_ring_position(oracle):
         assert k == done
         np.testing.assert_array_equal(pin.array[:frames.size], ref)
         assert xsum.server_stats(0)[0] == done
+        # HIP frees wait for every stream of the device: refused while the
+        # server runs instead of hanging; the buffer is released after the stop
+        tmp = xsum.PinnedBuffer(4096)
+        assert xsum.lib().tasx_host_free(tmp.addr) == -errno.EBUSY
+        assert xsum.lib().tasx_feeder_stop(0) == -errno.EINVAL  # none running: checked first
         xsum.server_stop(0)
+        tmp.free()
+        assert tmp.addr == 0
     finally:
         cx.close()
         try:
