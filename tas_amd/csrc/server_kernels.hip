@@ -71,6 +71,7 @@ __device__ __forceinline__ uint64_t rlane64(uint64_t x, int l)
 // dwords moved in by DPP, bytes past the datagram come off on lane 15 (its
 // last load is the last chunk).  Returns false (no store) when the frame's own
 // total_length is not tl: the frame changed after it was submitted.
+template <int POL = kSysNt>
 __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, uint32_t tl, int gl)
 {
   constexpr int U = 6;
@@ -79,7 +80,7 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
   u32x4 v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, min(lo + 256u * u, lastoff), 0, kSysNt);
+    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, min(lo + 256u * u, lastoff), 0, POL);
   const uint32_t tail = 14u + tl - 16u * last; // bytes of the last chunk inside, 1..16
   const u32x4 h = v[0];
   const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 ? 0x0000ffffu : 0xffffffffu);
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // into LDS), 0 = nothing yet, 2 = the header without all its entries (the
   // host still writing them, or a header-only poll: read the whole slot at
   // once), 3 = stop, 4 = the lease ran out
-  auto judge = [&](const SlotRead &v) -> int {
+  auto judge = [&](const SlotRead &v, uint64_t now) -> int {
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
     const uint32_t n = (uint32_t) (h0 & 0xffffu);
@@ -198,7 +199,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     if (diag)
       d_empty++;
 #endif
-    const uint64_t now = wall_clock64();
     if ((uint32_t) c != 0u)
       return 3;
     if ((uint32_t) (c >> 32) != lease) {
@@ -213,14 +213,19 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     if (threadIdx.x < 64) {
       bool entries = true;
       int st;
-      for (;;) {
-        st = judge(read_slot(entries));
+      // the wall clock is read every 8th empty poll (s_memrealtime is a
+      // memory-path message, not a register read)
+      uint64_t now = wall_clock64();
+      for (uint32_t np = 1;; ++np) {
+        st = judge(read_slot(entries), now);
         if (st == 1 || st >= 3)
           break;
         entries = true;
         if (st == 2)
           continue; // the header is in: read the whole slot again at once
-        const uint64_t idle = wall_clock64() - t_act;
+        if ((np & 7u) == 0u)
+          now = wall_clock64();
+        const uint64_t idle = now - t_act;
         if (idle >= P.cold_ticks) {
           entries = false;
           __builtin_amdgcn_s_sleep(127);
@@ -242,7 +247,20 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (uintptr_t) base, 0, (int) s_bytes,
                                                                     (int) kRsrcWord3);
       const uint32_t fo = s_off[row], tl = s_tl[row];
-      const bool ok = (fo & 15u) == 0u && tl >= 38u && tl <= 1522u && srv_row(rs, fo, tl, gl);
+      bool ok = (fo & 15u) == 0u && tl >= 38u && tl <= 1522u;
+#ifdef TASX_AB
+      // A/B (P.fpol): the frame loads' cache policy -- 1 nt, 2 plain, 3 sc1 nt,
+      // 4 sc0 nt (the product: sc0 sc1 nt)
+      switch (P.fpol) {
+      case 1: ok = ok && srv_row<2>(rs, fo, tl, gl); break;
+      case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
+      case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
+      case 4: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break;
+      default: ok = ok && srv_row(rs, fo, tl, gl); break;
+      }
+#else
+      ok = ok && srv_row(rs, fo, tl, gl);
+#endif
       if (gl == 15 && !ok)
         atomicOr(&s_bad, 1u);
     }

@@ -2218,10 +2218,17 @@ int tasx_server_start(int device)
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
     prm.diag = 0;
     prm.k = SRV_K;
+    prm.fpol = 0;
 #ifdef TASX_AB
     prm.diag = getenv("TASX_SRV_DIAG") != NULL;
     if (getenv("TASX_SRV_K")) /* A/B: workgroups per ring, 1/2/4/8 */
       prm.k = (uint32_t) atoi(getenv("TASX_SRV_K"));
+    if (getenv("TASX_SRV_FPOL")) /* A/B: the frame loads' cache policy */
+      prm.fpol = (uint32_t) atoi(getenv("TASX_SRV_FPOL"));
+    if (getenv("TASX_SRV_HOT_US"))
+      prm.hot_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_HOT_US")) / 1000u;
+    if (getenv("TASX_SRV_COLD_US"))
+      prm.cold_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_COLD_US")) / 1000u;
     S->khz = (uint32_t) khz;
 #endif
     S->k = prm.k;

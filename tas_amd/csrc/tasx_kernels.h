@@ -124,6 +124,7 @@ typedef struct tasx_srv_params {
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
   uint32_t diag;         /* A/B builds: timing sums (tasx_ab_server_diag) */
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
+  uint32_t fpol;         /* A/B builds: the frame loads' cache policy (server_kernels.hip) */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
