@@ -237,6 +237,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
       if (lane == 0)
         s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
+#ifdef TASX_AB
+      if (st == 1 && P.fpol >= 5u) // invalidate this CU's L1 and the XCD's L2 (non-coherent lines) before the frame loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
     }
     __syncthreads();
     if (s_cmd != 0u)
@@ -255,7 +259,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       case 1: ok = ok && srv_row<2>(rs, fo, tl, gl); break;
       case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
       case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
-      case 4: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break;
+      case 4: case 5: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break; // 5: after a system acquire
+      case 6: ok = ok && srv_row<2>(rs, fo, tl, gl); break;              // 6: nt after a system acquire
       default: ok = ok && srv_row(rs, fo, tl, gl); break;
       }
 #else

@@ -150,6 +150,51 @@ def test_server_reused_mbufs_and_large_flush(oracle):
         cx.close()
 
 
+@pytest.mark.parametrize("mem", ["host_alloc", "registered"])
+def test_server_refilled_mbufs_every_flush(oracle, mem):
+    """TAS reuses an mbuf as soon as its frame has left: 300 flushes of 32
+    frames through the SAME 32 mbufs, new headers and payload every time, in
+    pinned memory from tasx_host_alloc and in plain pages pinned by
+    tasx_ctx_register_frames (hipHostRegister, as a DPDK mempool would be).
+    The ring's workgroups come back to the same mbufs every few flushes: a
+    frame line cached in an XCD's L2 by an earlier batch must never be summed."""
+    xsum.server_start(0)
+    cx = _Ctxs([6])
+    raw = None
+    try:
+        n, rounds, nbytes = 32, 300, 32 * 2048 + 4096
+        if mem == "host_alloc":
+            pin = xsum.PinnedBuffer(nbytes)
+            cx.pins.append(pin)
+            arr, addr = pin.array, pin.addr
+        else:
+            raw = np.zeros(nbytes + 4096, np.uint8)
+            off = (-raw.ctypes.data) % 4096
+            arr, addr = raw[off:off + nbytes], raw.ctypes.data + off
+        xsum.register_frames(6, addr, nbytes)
+        xsum.use_server(6)
+        for rnd in range(rounds):
+            pay = (np.arange(n) * (31 + rnd) + 7 * rnd) % 1449
+            pay[rnd % 4::4] = 0
+            frames = pktgen.tcp4_frames(n, payload=pay, stride=2048, seed=9000 + rnd)
+            arr[:frames.size] = frames
+            ref = _ref(oracle, frames, n)
+            for i in range(n):
+                xsum.tcp_checksums(6, addr + i * 2048)
+            xsum.tx_flush(6)
+            np.testing.assert_array_equal(arr[:frames.size], ref, err_msg=f"round {rnd}")
+        assert xsum.server_flushes(6) == rounds
+        xsum.use_server(6, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
+        del raw  # unregistered by the context's release (at the server's stop at the latest)
+
+
 def test_server_ring_wrap_and_tag_wrap(oracle):
     """70,000 one-frame flushes with up to 8 in flight: the 8-slot ring wraps
     8,750 times and the 16-bit slot tags wrap (position 65,535 -> 0) with the

@@ -183,7 +183,10 @@ int main(int argc, char **argv)
   for (int k = 0; k < MAXT; k++) {
     memset(&T[k], 0, sizeof(T[k]));
     T[k].id = k;
-    T[k].pool = tasx_host_alloc(pool_bytes);
+    /* FB_MALLOC=1: plain malloc'd pages, pinned by tasx_ctx_register_frames
+     * (hipHostRegister, as TAS's hugepage mempools would be) */
+    T[k].pool = getenv("FB_MALLOC") ? aligned_alloc(4096, (pool_bytes + 4095) & ~(size_t) 4095)
+                                    : tasx_host_alloc(pool_bytes);
     T[k].core = malloc(sizeof(double) * (size_t) flushes);
     T[k].lat = malloc(sizeof(double) * (size_t) flushes);
     uint64_t r2 = 100 + (uint64_t) k;
