@@ -405,9 +405,9 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * Each context has a ring of TASX_SRV_RING (8) descriptor slots, up to 64
  * frames each: submit writes the frames' offsets in the context's registered
  * region and their ip.total_length into the next slot, the header last, and
- * returns; four workgroups of the server kernel poll that ring over PCIe
- * (each every fourth position, so up to four of a context's queued batches
- * are summed at once), sum the frames in place and store both checksum fields
+ * returns; two workgroups of the server kernel poll that ring over PCIe
+ * (each every other position, so two of a context's queued batches are
+ * summed at once), sum the frames in place and store both checksum fields
  * into them, then post each slot's done word, which tasx_flush_poll/_wait
  * reap in position order (ticket order as before; submit spins only when 8
  * batches are in flight).  A ring idle for 2 ms is polled by its header alone.  Frames
@@ -418,7 +418,7 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * total_length changed meanwhile is left alone and the context's next
  * poll/wait returns -EIO.  The TAS path this replaces: tx_flush
  * (tas/fast/fastemu.c:544-566) after tcp_checksums (fast_flows.c:1058-1069).
- *   tasx_server_start(device): launch the server kernel (4 * TASX_MAX_CTX
+ *   tasx_server_start(device): launch the server kernel (2 * TASX_MAX_CTX
  *     workgroups of 1024 threads) and its keepalive thread; the kernel also
  *     leaves by itself 2 s after the process stops refreshing it
  *   tasx_server_stop(device): -EBUSY while contexts are attached; waits up

@@ -9,15 +9,22 @@
 // its context's ring in coherent pinned memory (frame offsets in its
 // registered mbuf region, each with its ip.total_length) and the header last;
 // the workgroups of ring r poll its slots, sum the frames in place over PCIe
-// and store both checksum fields into them, then post each slot's done word.  Layout and protocol: tasx_kernels.h (TASX_SRV_*), tasx_host.c
+// and store both checksum fields into them, then post each slot's done word.
+// Layout and protocol: tasx_kernels.h (TASX_SRV_*), tasx_host.c
 // (server_submit).
 //
-// Coherence without fences on the data path (MI355X_MICROARCH.md, hand-off
-// rules): every word the host writes is read with system-scope (sc0 sc1)
-// loads, so no cache level can return an older copy; frames are read by
-// sc0 sc1 nt buffer loads (a ring position reuses mbufs, so a line cached by
-// an earlier batch must never be served) and the two checksum fields are
-// written by sc0 sc1 stores (write-through to host memory).  Each wave waits
+// Coherence (MI355X_MICROARCH.md, hand-off rules): every word the host writes
+// is read with system-scope (sc0 sc1) loads, so no cache level can return an
+// older copy.  TAS reuses an mbuf as soon as its frame has left, so a frame
+// line an XCD's L2 cached for an earlier batch must never be summed: after
+// taking a batch, the polling wave issues one system-scope acquire
+// (buffer_inv sc0 sc1: this CU's L1 and the XCD's L2 drop their non-coherent
+// lines) and the rows then read the frames with nt buffer loads.  Without the
+// acquire, tests/test_server.py::test_server_refilled_mbufs_every_flush
+// fails; with system-scope frame loads instead (round 4's first server) the
+// server tops out at 14-19 M frames/s from 8 cores, against 24-28 this way
+// (profiles/r04/r04g).  The two checksum fields are written by sc0 sc1
+// stores (write-through to host memory).  Each wave waits
 // for its stores (vmcnt(0)), the workgroup meets at a barrier, and only then
 // does one lane store the slot's done word, also sc0 sc1: the host sees the
 // word after the fields.  Descriptor words carry the 16-bit tag of their ring
@@ -40,7 +47,10 @@ namespace {
 
 constexpr int kSrvBlock = 1024;           // 64 rows of 16 lanes: one frame per row
 constexpr int kSys = 1 | 16;              // cache policy sc0 sc1: system scope
-constexpr int kSysNt = kSys | 2;          // ... and non-temporal
+#ifdef TASX_AB
+constexpr int kSysNt = kSys | 2;          // ... and non-temporal (A/B 7: round 4's first frame loads)
+#endif
+constexpr int kNt = 2;                    // non-temporal (the frame loads, after an acquire)
 constexpr uint32_t kRsrcWord3 = 0x00020000u; // gfx9 buffer resource dword 3
 
 __device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p)
@@ -71,7 +81,7 @@ __device__ __forceinline__ uint64_t rlane64(uint64_t x, int l)
 // dwords moved in by DPP, bytes past the datagram come off on lane 15 (its
 // last load is the last chunk).  Returns false (no store) when the frame's own
 // total_length is not tl: the frame changed after it was submitted.
-template <int POL = kSysNt>
+template <int POL = kNt>
 __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, uint32_t tl, int gl)
 {
   constexpr int U = 6;
@@ -237,10 +247,14 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
       if (lane == 0)
         s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
+      // a batch taken: this CU's L1 and the XCD's L2 drop their non-coherent
+      // lines before any frame load (A/B: policies 1-4 and 7 without)
 #ifdef TASX_AB
-      if (st == 1 && P.fpol >= 5u) // invalidate this CU's L1 and the XCD's L2 (non-coherent lines) before the frame loads
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (st == 1 && (P.fpol == 0u || P.fpol == 5u))
+#else
+      if (st == 1)
 #endif
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     if (s_cmd != 0u)
@@ -253,14 +267,15 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       const uint32_t fo = s_off[row], tl = s_tl[row];
       bool ok = (fo & 15u) == 0u && tl >= 38u && tl <= 1522u;
 #ifdef TASX_AB
-      // A/B (P.fpol): the frame loads' cache policy -- 1 nt, 2 plain, 3 sc1 nt,
-      // 4 sc0 nt (the product: sc0 sc1 nt)
+      // A/B (P.fpol): the frame loads' cache policy -- 0 the product (nt
+      // after the acquire), 1 nt, 2 plain, 3 sc1 nt, 4 sc0 nt (1-4 without the
+      // acquire: 1, 2 and 4 serve stale lines, profiles/r04/r04g), 5 sc0 nt
+      // after the acquire, 7 sc0 sc1 nt (round 4's first server)
       switch (P.fpol) {
-      case 1: ok = ok && srv_row<2>(rs, fo, tl, gl); break;
       case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
       case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
-      case 4: case 5: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break; // 5: after a system acquire
-      case 6: ok = ok && srv_row<2>(rs, fo, tl, gl); break;              // 6: nt after a system acquire
+      case 4: case 5: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break;
+      case 7: ok = ok && srv_row<kSysNt>(rs, fo, tl, gl); break;
       default: ok = ok && srv_row(rs, fo, tl, gl); break;
       }
 #else

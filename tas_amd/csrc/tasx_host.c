@@ -1956,7 +1956,7 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
 #define SRV_COLD_US 2000u /* idle time from which a ring's header alone is polled */
-#define SRV_K 4u          /* workgroups per ring (tasx_srv_params.k) */
+#define SRV_K 2u          /* workgroups per ring (tasx_srv_params.k): profiles/r04/r04g */
 
 struct fserver {
   int device;
