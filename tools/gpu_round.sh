@@ -17,9 +17,14 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
+# PART=a: smoke, GPU tests, the default bench line; PART=b: the rest (one
+# gpurun call each; unset: both)
+if [ "${PART:-ab}" != "b" ]; then
 step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()'
 step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step bench 400 python bench.py
+fi
+[ "${PART:-ab}" = "a" ] && { echo done; exit 0; }
 # the driver's step count: ms_per_step against the event-timed launch
 step bench_k20 300 python bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline
 for w in mixed shard8m tso; do
