@@ -12,7 +12,9 @@
  *   core_us_per_flush   time inside record + submit + polls per flush (what
  *                       the fast-path core spends), median over flushes
  *   stall_us_per_flush  time blocked in tasx_flush_wait per flush (mean)
- *   latency_us          submit -> completion seen by a poll (median)
+ *   latency_us          submit returned -> completion seen by a poll (median)
+ *   latency_from_submit_us  the same from the submit call's start (a launch
+ *                       per flush pays its launch inside the call)
  *   frames_per_s        all threads' frames / wall time
  *   cpu_core_us_per_flush  the same 32 frames through oracle_tcp_checksums
  *                       on the calling core (TAS's own path)
@@ -80,7 +82,7 @@ static unsigned INFLIGHT = 3, DSLOT = 4; /* batch slots: in flight + 1 being rec
 struct thr {
   int id, flushes, use_feeder;
   uint8_t *pool;
-  double *core, *lat;
+  double *core, *lat, *lat2;
   double stall;
   int nlat, err;
 };
@@ -89,7 +91,7 @@ static void *run(void *arg)
 {
   struct thr *T = arg;
   uint32_t q[MAXQ];
-  double qt[MAXQ];
+  double qt[MAXQ], qs[MAXQ];
   unsigned qh = 0, qn = 0;
   if (tasx_set_thread_ctx((unsigned) T->id) != 0) {
     T->err = 1;
@@ -106,6 +108,7 @@ static void *run(void *arg)
       }
       const double w1 = now_us();
       T->stall += w1 - w0;
+      T->lat2[T->nlat] = w1 - qs[qh % MAXQ];
       T->lat[T->nlat++] = w1 - qt[qh % MAXQ];
       qh++, qn--;
     }
@@ -118,12 +121,13 @@ static void *run(void *arg)
       }
     }
     uint32_t tk;
+    const double tsub = now_us();
     if (tasx_flush_submit(TASX_CTX_SELF, &tk) != 0) {
       T->err = 4;
       return NULL;
     }
     const double ts = now_us();
-    q[(qh + qn) % MAXQ] = tk, qt[(qh + qn) % MAXQ] = ts, qn++;
+    q[(qh + qn) % MAXQ] = tk, qt[(qh + qn) % MAXQ] = ts, qs[(qh + qn) % MAXQ] = tsub, qn++;
     while (qn > 0) { /* completions the loop notices without blocking */
       const int r = tasx_flush_poll(TASX_CTX_SELF, q[qh % MAXQ]);
       if (r < 0) {
@@ -132,7 +136,9 @@ static void *run(void *arg)
       }
       if (r == 0)
         break;
-      T->lat[T->nlat++] = now_us() - qt[qh % MAXQ];
+      const double tc = now_us();
+      T->lat2[T->nlat] = tc - qs[qh % MAXQ];
+      T->lat[T->nlat++] = tc - qt[qh % MAXQ];
       qh++, qn--;
     }
     T->core[b] = now_us() - t0;
@@ -142,7 +148,9 @@ static void *run(void *arg)
       T->err = 6;
       return NULL;
     }
-    T->lat[T->nlat++] = now_us() - qt[qh % MAXQ];
+    const double tc = now_us();
+    T->lat2[T->nlat] = tc - qs[qh % MAXQ];
+    T->lat[T->nlat++] = tc - qt[qh % MAXQ];
     qh++, qn--;
   }
   tasx_set_thread_ctx(TASX_CTX_SELF);
@@ -189,6 +197,7 @@ int main(int argc, char **argv)
                                     : tasx_host_alloc(pool_bytes);
     T[k].core = malloc(sizeof(double) * (size_t) flushes);
     T[k].lat = malloc(sizeof(double) * (size_t) flushes);
+    T[k].lat2 = malloc(sizeof(double) * (size_t) flushes);
     uint64_t r2 = 100 + (uint64_t) k;
     for (unsigned i = 0; i < DSLOT * BATCH; i++)
       make_frame(T[k].pool + (size_t) i * STRIDE, i, &r2);
@@ -235,7 +244,7 @@ int main(int argc, char **argv)
         tasx_server_stats(0, &sw1, &fr1);
       else
         tasx_feeder_stats(0, &sw1, &fr1);
-      double core_all[MAXT], stall = 0, lat_all[MAXT];
+      double core_all[MAXT], stall = 0, lat_all[MAXT], lat2_all[MAXT];
       for (int k = 0; k < n; k++) {
         if (T[k].err) {
           fprintf(stderr, "thread %d failed (%d): %s\n", k, T[k].err, tasx_last_error());
@@ -243,6 +252,7 @@ int main(int argc, char **argv)
         }
         core_all[k] = median(T[k].core, flushes);
         lat_all[k] = median(T[k].lat, T[k].nlat);
+        lat2_all[k] = median(T[k].lat2, T[k].nlat);
         stall += T[k].stall / flushes;
       }
 #ifdef FEEDER_AB
@@ -263,9 +273,9 @@ int main(int argc, char **argv)
       }
 #endif
       printf("{\"mode\": \"%s\", \"threads\": %d, \"in_flight\": %u, \"flushes_per_thread\": %d, \"frames_per_flush\": %u, "
-             "\"core_us_per_flush\": %.3f, \"stall_us_per_flush\": %.3f, \"latency_us\": %.2f, "
+             "\"core_us_per_flush\": %.3f, \"stall_us_per_flush\": %.3f, \"latency_us\": %.2f, \"latency_from_submit_us\": %.2f, "
              "\"frames_per_s\": %.0f, \"sweeps\": %llu, \"frames_per_sweep\": %.1f}\n",
-             mname[mode], n, INFLIGHT, flushes, BATCH, median(core_all, n), stall / n, median(lat_all, n),
+             mname[mode], n, INFLIGHT, flushes, BATCH, median(core_all, n), stall / n, median(lat_all, n), median(lat2_all, n),
              (double) n * flushes * BATCH / (wall * 1e-6), (unsigned long long) (sw1 - sw0),
              sw1 > sw0 ? (double) (fr1 - fr0) / (double) (sw1 - sw0) : 0.0);
       fflush(stdout);
