@@ -1081,6 +1081,40 @@ def e2e_tso_leg(ws: int, rank: int, reps: int = 3) -> dict:
     return res
 
 
+def fastpath_mt_leg(flushes: int = 3000) -> dict:
+    """tx_flush at TAS's batch size from several fast-path threads
+    (tas/fast/fastemu.c:544-566: at most TXBUF_SIZE = 32 frames per core per
+    loop), issued from C (tasxb_fastpath_mt; INTEGRATION.md section 4b loop):
+    each thread on its own context over a pinned mempool of 32-frame slots,
+    half 1514-B data segments and half 66-B ACKs, with up to `in flight`
+    batches out.  Per-context launches, the shared feeder and the persistent
+    flush server at 1 thread x 1 in flight (latency), 8 x 3 and 8 x 7
+    (throughput).  The server's in-place fields of thread 0's last batches are
+    compared with the device-resident batch kernel on the same frames."""
+    dev = torch.cuda.current_device()
+    res = {"unit": "frames/s, us", "frames_per_flush": 32,
+           "note": "latency_us from the submit call's return, latency_from_submit_us from its start (a "
+                   "per-context launch is paid inside the call); core_us_per_flush = record 32 frames + "
+                   "submit + polls on the fast-path core; tools/feeder_bench.c adds 2 and 4 threads and the "
+                   "CPU's own per-frame cost"}
+    keep = None
+    for mode in ("per_context", "feeder", "server"):
+        for th, q in ((1, 1), (8, 3), (8, 7)):
+            kp = np.zeros((q + 1) * 32 * STRIDE, np.uint8) if (mode == "server" and th == 8 and q == 7) else None
+            r = benchloop.fastpath_mt(dev, 8, th, q, flushes, mode, kp)
+            r["frames_per_s"] = round(r["frames_per_s"])
+            res[f"{mode}_{th}x{q}"] = r
+            if kp is not None:
+                keep = kp
+    n = len(keep) // STRIDE
+    dres = xsum.tcp4_cksum_batch(torch.from_numpy(keep.copy()).cuda(), n, stride=STRIDE)
+    torch.cuda.synchronize()
+    fv = keep.reshape(n, STRIDE)
+    got = np.stack([fv[:, 24:26].copy().view(np.uint16)[:, 0], fv[:, 50:52].copy().view(np.uint16)[:, 0]], 1)
+    res["server_matches_device"] = bool(np.array_equal(got.reshape(-1), dres.cpu().numpy().view(np.uint16)))
+    return res
+
+
 def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
     """Every rank at once, each from its own NUMA-local host thread (this
     process, pinned by numa_pin before these buffers were touched):
@@ -1151,6 +1185,7 @@ def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
                                    "(tasxb_flush_loop), median us per flush: staged, zero-copy per-context launches, "
                                    "and the persistent flush server; tools/feeder_bench.c has the multi-thread numbers")
             f32.free()
+            res["fastpath_mt"] = fastpath_mt_leg()
         # the same frames as scattered mbufs: the CPU gathers only the summed
         # bytes (tasx_tcp4_cksum_batch_host_offs, staged)
         offs = np.arange(n, dtype=np.uint64) * np.uint64(STRIDE)

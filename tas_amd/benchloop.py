@@ -70,8 +70,10 @@ def lib() -> ctypes.CDLL:
                                     ctypes.c_int, pp, ctypes.c_int]
         L.tasxb_flush_loop.argtypes = [ctypes.c_uint, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_double)]
+        L.tasxb_fastpath_mt.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                        ctypes.c_int, ctypes.POINTER(ctypes.c_double), _vp, ctypes.c_size_t]
         for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop, L.tasxb_rx_loop,
-                  L.tasxb_flush_loop):
+                  L.tasxb_flush_loop, L.tasxb_fastpath_mt):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -110,3 +112,23 @@ def flush_loop(ctx: int, base: int, stride: int, n: int, iters: int):
     if rc:
         raise xsum.TasxError(rc, "tasxb_flush_loop")
     return us
+
+
+MT_MODES = {"per_context": 0, "feeder": 1, "server": 2}
+
+
+def fastpath_mt(device: int, ctx0: int, threads: int, inflight: int, flushes: int, mode: str,
+                keep: "np.ndarray | None" = None) -> dict:
+    """`threads` fast-path threads at TAS's batch size, each on its own context
+    (ctx0 + k), 32-frame tx_flush batches with up to `inflight` out
+    (tasxb_fastpath_mt): frames/s, median latencies, median core time per
+    flush.  keep: a uint8 array that receives thread 0's mempool afterwards."""
+    import numpy as np
+    out = np.zeros(4, np.float64)
+    rc = lib().tasxb_fastpath_mt(device, ctx0, threads, inflight, flushes, MT_MODES[mode],
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                 None if keep is None else keep.ctypes.data, 0 if keep is None else keep.nbytes)
+    if rc:
+        raise xsum.TasxError(rc, "tasxb_fastpath_mt")
+    return {"frames_per_s": float(out[0]), "latency_us": round(float(out[1]), 2),
+            "latency_from_submit_us": round(float(out[2]), 2), "core_us_per_flush": round(float(out[3]), 3)}

@@ -201,3 +201,232 @@ int tasxb_flush_loop(unsigned ctx, uint8_t *base, uint64_t stride, uint32_t n, i
   }
   return 0;
 }
+
+/* ---------------------------------------------------------------------- */
+/* Several fast-path threads at TAS's batch size (bench.py's `fastpath_mt`
+ * line; the same loop as tools/feeder_bench.c, without its oracle check):
+ * thread k binds context ctx0 + k (initialised here), owns a pinned mempool of
+ * slots of 32 frames at a 2 KiB stride (half 1514-B data segments, half 66-B
+ * ACKs), and runs the INTEGRATION.md section 4b loop: record 32 frames with
+ * tasx_tcp_checksums, tasx_flush_submit, poll the oldest tickets, wait for
+ * the oldest when `inflight` are out (a slot is reused only after its flush
+ * completed).  mode 0: each context launches its own flushes; 1: the shared
+ * feeder; 2: the persistent flush server.
+ *   out[0] frames/s over all threads (wall time from a common start)
+ *   out[1] median latency, submit returned -> completion seen (us)
+ *   out[2] median latency from the submit call's start (us)
+ *   out[3] median core time per flush: record + submit + polls (us)
+ * keep (optional, keep_bytes): thread 0's mempool after the run, for the
+ * caller's check against the device kernel. */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MT_BATCH 32u
+#define MT_STRIDE 2048u
+#define MT_MAXQ 8u
+#define MT_MAXT 16
+
+struct mt_thr {
+  unsigned ctx, nslot, inflight;
+  uint8_t *pool;
+  int flushes, n, err;
+  double *lat, *lat2, *core;
+  const int *go; /* 1: start, 2: leave at once */
+};
+
+static void mt_frame(uint8_t *f, unsigned k, uint64_t *rng)
+{
+  const unsigned payload = (k & 1) ? 0 : 1448, tl = 52 + payload;
+  for (unsigned i = 0; i < 66 + payload; i++) {
+    *rng = *rng * 6364136223846793005ull + 1442695040888963407ull;
+    f[i] = (uint8_t) (*rng >> 56);
+  }
+  f[12] = 0x08, f[13] = 0x00, f[14] = 0x45, f[15] = 0;
+  f[16] = (uint8_t) (tl >> 8), f[17] = (uint8_t) tl;
+  f[22] = 0xff, f[23] = 6;
+  f[34 + 12] = 0x80, f[34 + 13] = 0x18;
+}
+
+static void *mt_worker(void *arg)
+{
+  struct mt_thr *T = arg;
+  uint32_t q[MT_MAXQ];
+  double qt[MT_MAXQ], qs[MT_MAXQ];
+  unsigned qh = 0, qn = 0;
+  if (tasx_set_thread_ctx(T->ctx) != 0)
+    T->err = 1;
+  int g;
+  while ((g = __atomic_load_n(T->go, __ATOMIC_ACQUIRE)) == 0)
+    ;
+  if (g != 1)
+    T->err = 7;
+  for (int b = 0; b < T->flushes && !T->err; b++) {
+    uint8_t *slot = T->pool + (size_t) (b % T->nslot) * MT_BATCH * MT_STRIDE;
+    if (qn >= T->inflight) {
+      if (tasx_flush_wait(TASX_CTX_SELF, q[qh % MT_MAXQ]) != 0) {
+        T->err = 2;
+        break;
+      }
+      const double w1 = tasxb_now_us();
+      T->lat2[T->n] = w1 - qs[qh % MT_MAXQ];
+      T->lat[T->n++] = w1 - qt[qh % MT_MAXQ];
+      qh++, qn--;
+    }
+    const double t0 = tasxb_now_us();
+    for (unsigned i = 0; i < MT_BATCH && !T->err; i++)
+      if (tasx_tcp_checksums(TASX_CTX_SELF, NULL, slot + (size_t) i * MT_STRIDE, 0, 0, 0) != 0)
+        T->err = 3;
+    uint32_t tk;
+    const double tsub = tasxb_now_us();
+    if (T->err || tasx_flush_submit(TASX_CTX_SELF, &tk) != 0) {
+      T->err = T->err ? T->err : 4;
+      break;
+    }
+    const double ts = tasxb_now_us();
+    q[(qh + qn) % MT_MAXQ] = tk, qt[(qh + qn) % MT_MAXQ] = ts, qs[(qh + qn) % MT_MAXQ] = tsub, qn++;
+    while (qn > 0) {
+      const int r = tasx_flush_poll(TASX_CTX_SELF, q[qh % MT_MAXQ]);
+      if (r < 0)
+        T->err = 5;
+      if (r <= 0)
+        break;
+      const double tc = tasxb_now_us();
+      T->lat2[T->n] = tc - qs[qh % MT_MAXQ];
+      T->lat[T->n++] = tc - qt[qh % MT_MAXQ];
+      qh++, qn--;
+    }
+    T->core[b] = tasxb_now_us() - t0;
+  }
+  while (qn > 0 && !T->err) {
+    if (tasx_flush_wait(TASX_CTX_SELF, q[qh % MT_MAXQ]) != 0) {
+      T->err = 6;
+      break;
+    }
+    const double tc = tasxb_now_us();
+    T->lat2[T->n] = tc - qs[qh % MT_MAXQ];
+    T->lat[T->n++] = tc - qt[qh % MT_MAXQ];
+    qh++, qn--;
+  }
+  tasx_set_thread_ctx(TASX_CTX_SELF);
+  return NULL;
+}
+
+static int mt_cmp(const void *a, const void *b)
+{
+  const double x = *(const double *) a, y = *(const double *) b;
+  return (x > y) - (x < y);
+}
+
+static double mt_median(double *v, size_t n)
+{
+  if (n == 0)
+    return 0.0;
+  qsort(v, n, sizeof(double), mt_cmp);
+  return v[n / 2];
+}
+
+int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight, int flushes, int mode,
+                      double *out, uint8_t *keep, size_t keep_bytes)
+{
+  if (threads < 1 || threads > MT_MAXT || inflight < 1 || inflight > MT_MAXQ - 1 || flushes < 1 || mode < 0 ||
+      mode > 2 || ctx0 + (unsigned) threads > TASX_MAX_CTX)
+    return -22; /* -EINVAL */
+  struct mt_thr T[MT_MAXT];
+  pthread_t th[MT_MAXT];
+  int go = 0;
+  const unsigned nslot = inflight + 1;
+  const size_t pool_bytes = (size_t) nslot * MT_BATCH * MT_STRIDE;
+  int rc = 0, started = 0, nt = 0;
+  memset(T, 0, sizeof(T));
+  for (int k = 0; k < threads && !rc; k++, nt++) {
+    T[k].ctx = ctx0 + (unsigned) k, T[k].nslot = nslot, T[k].inflight = inflight, T[k].flushes = flushes;
+    T[k].pool = tasx_host_alloc(pool_bytes);
+    T[k].lat = malloc(sizeof(double) * (size_t) flushes);
+    T[k].lat2 = malloc(sizeof(double) * (size_t) flushes);
+    T[k].core = malloc(sizeof(double) * (size_t) flushes);
+    if (!T[k].pool || !T[k].lat || !T[k].lat2 || !T[k].core) {
+      rc = -12; /* -ENOMEM */
+      break;
+    }
+    uint64_t r = 100 + (uint64_t) k;
+    memset(T[k].pool, 0, pool_bytes);
+    for (unsigned i = 0; i < nslot * MT_BATCH; i++)
+      mt_frame(T[k].pool + (size_t) i * MT_STRIDE, i, &r);
+    if ((rc = tasx_ctx_init(T[k].ctx, device, 4u << 20)) != 0)
+      break;
+    if ((rc = tasx_ctx_register_frames(T[k].ctx, T[k].pool, pool_bytes)) != 0)
+      break;
+  }
+  if (!rc && mode == 1 && (rc = tasx_feeder_start(device)) == 0)
+    started = 1;
+  if (!rc && mode == 2 && (rc = tasx_server_start(device)) == 0)
+    started = 2;
+  for (int k = 0; k < threads && !rc; k++)
+    rc = mode == 1 ? tasx_ctx_use_feeder(T[k].ctx, 1) : mode == 2 ? tasx_ctx_use_server(T[k].ctx, 1) : 0;
+  double wall = 0.0;
+  if (!rc) {
+    int k;
+    for (k = 0; k < threads; k++) {
+      T[k].go = &go;
+      if (pthread_create(&th[k], NULL, mt_worker, &T[k]) != 0)
+        break;
+    }
+    const double t0 = tasxb_now_us();
+    __atomic_store_n(&go, k == threads ? 1 : 2, __ATOMIC_RELEASE); /* 2: the created ones leave */
+    for (int j = 0; j < k; j++)
+      pthread_join(th[j], NULL);
+    wall = tasxb_now_us() - t0;
+    if (k < threads)
+      rc = -11; /* -EAGAIN */
+  }
+  for (int k = 0; k < threads && !rc; k++)
+    if (T[k].err)
+      rc = -1000 - T[k].err;
+  if (!rc) {
+    size_t total = 0;
+    for (int k = 0; k < threads; k++)
+      total += (size_t) T[k].n;
+    double *all = malloc(sizeof(double) * total), *all2 = malloc(sizeof(double) * total),
+           *core = malloc(sizeof(double) * (size_t) threads * (size_t) flushes);
+    if (all && all2 && core) {
+      size_t o = 0;
+      for (int k = 0; k < threads; k++) {
+        memcpy(all + o, T[k].lat, sizeof(double) * (size_t) T[k].n);
+        memcpy(all2 + o, T[k].lat2, sizeof(double) * (size_t) T[k].n);
+        memcpy(core + (size_t) k * flushes, T[k].core, sizeof(double) * (size_t) flushes);
+        o += (size_t) T[k].n;
+      }
+      out[0] = (double) threads * flushes * MT_BATCH / (wall * 1e-6);
+      out[1] = mt_median(all, total);
+      out[2] = mt_median(all2, total);
+      out[3] = mt_median(core, (size_t) threads * (size_t) flushes);
+    } else {
+      rc = -12;
+    }
+    free(all);
+    free(all2);
+    free(core);
+    if (keep && T[0].pool)
+      memcpy(keep, T[0].pool, keep_bytes < pool_bytes ? keep_bytes : pool_bytes);
+  }
+  for (int k = 0; k < threads; k++) {
+    if (mode == 1)
+      tasx_ctx_use_feeder(T[k].ctx, 0);
+    if (mode == 2)
+      tasx_ctx_use_server(T[k].ctx, 0);
+  }
+  if (started == 1)
+    tasx_feeder_stop(device);
+  if (started == 2)
+    tasx_server_stop(device);
+  for (int k = 0; k < nt; k++) {
+    tasx_ctx_destroy(T[k].ctx);
+    if (T[k].pool)
+      tasx_host_free(T[k].pool);
+    free(T[k].lat);
+    free(T[k].lat2);
+    free(T[k].core);
+  }
+  return rc;
+}

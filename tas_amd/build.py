@@ -85,8 +85,8 @@ def build(force: bool = False, extra_hip_flags: list[str] | None = None, ab: boo
             continue
         if force or not out.exists() or out.stat().st_mtime < max(
                 BENCH_SRC.stat().st_mtime, dep.stat().st_mtime, (ROOT / "include" / "tasx_xsum.h").stat().st_mtime):
-            _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", "-shared", "-I", str(ROOT / "include"),
-                  "-o", str(out), str(BENCH_SRC), "-L", str(OUT_DIR), f"-l{name}",
+            _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", "-shared", "-pthread", "-I",
+                  str(ROOT / "include"), "-o", str(out), str(BENCH_SRC), "-L", str(OUT_DIR), f"-l{name}",
                   "-Wl,-rpath,$ORIGIN", "-Wl,--no-undefined"])
     return LIB
 
