@@ -73,3 +73,20 @@ def test_rehearsal_drops_fractions_above_one():
     assert out["frac_of_n_hbm"] is None and out["roofline"]["frac"] == 0.7
     assert out["roofline"]["pattern_ceiling"] == {"frac": None, "us": 15.0}
     assert out["legs"] == [{"frac": None}, {"frac": 0.5}] and out["value"] == 6000.0
+
+
+def test_fastpath_mt_refuses_bad_shapes_before_any_gpu_call():
+    """tasxb_fastpath_mt (bench.py's fastpath_mt line) checks its arguments
+    before it touches HIP: thread counts, in-flight depth (the 8-slot queue),
+    mode and the context-id range."""
+    import errno
+    from tas_amd import benchloop, xsum
+    bad = [(0, 1, 100, "server", 8), (17, 1, 100, "server", 0), (1, 0, 100, "feeder", 8),
+           (1, 8, 100, "feeder", 8), (1, 1, 0, "per_context", 8), (9, 1, 100, "server", 8)]
+    for th, q, fl, mode, ctx0 in bad:
+        try:
+            benchloop.fastpath_mt(0, ctx0, th, q, fl, mode)
+        except xsum.TasxError as e:
+            assert e.code == -errno.EINVAL, (th, q, fl, mode, ctx0, e.code)
+        else:
+            raise AssertionError((th, q, fl, mode, ctx0))
