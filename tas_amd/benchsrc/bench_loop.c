@@ -229,6 +229,7 @@ int tasxb_flush_loop(unsigned ctx, uint8_t *base, uint64_t stride, uint32_t n, i
 
 struct mt_thr {
   unsigned ctx, nslot, inflight;
+  int inited; /* tasx_ctx_init succeeded: destroyed at the end */
   uint8_t *pool;
   int flushes, n, err;
   double *lat, *lat2, *core;
@@ -337,9 +338,9 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
   int go = 0;
   const unsigned nslot = inflight + 1;
   const size_t pool_bytes = (size_t) nslot * MT_BATCH * MT_STRIDE;
-  int rc = 0, started = 0, nt = 0;
+  int rc = 0, started = 0;
   memset(T, 0, sizeof(T));
-  for (int k = 0; k < threads && !rc; k++, nt++) {
+  for (int k = 0; k < threads && !rc; k++) {
     T[k].ctx = ctx0 + (unsigned) k, T[k].nslot = nslot, T[k].inflight = inflight, T[k].flushes = flushes;
     T[k].pool = tasx_host_alloc(pool_bytes);
     T[k].lat = malloc(sizeof(double) * (size_t) flushes);
@@ -355,6 +356,7 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
       mt_frame(T[k].pool + (size_t) i * MT_STRIDE, i, &r);
     if ((rc = tasx_ctx_init(T[k].ctx, device, 4u << 20)) != 0)
       break;
+    T[k].inited = 1;
     if ((rc = tasx_ctx_register_frames(T[k].ctx, T[k].pool, pool_bytes)) != 0)
       break;
   }
@@ -411,17 +413,18 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
       memcpy(keep, T[0].pool, keep_bytes < pool_bytes ? keep_bytes : pool_bytes);
   }
   for (int k = 0; k < threads; k++) {
-    if (mode == 1)
+    if (mode == 1 && T[k].inited)
       tasx_ctx_use_feeder(T[k].ctx, 0);
-    if (mode == 2)
+    if (mode == 2 && T[k].inited)
       tasx_ctx_use_server(T[k].ctx, 0);
   }
   if (started == 1)
     tasx_feeder_stop(device);
   if (started == 2)
     tasx_server_stop(device);
-  for (int k = 0; k < nt; k++) {
-    tasx_ctx_destroy(T[k].ctx);
+  for (int k = 0; k < threads; k++) { /* only what this call set up */
+    if (T[k].inited)
+      tasx_ctx_destroy(T[k].ctx);
     if (T[k].pool)
       tasx_host_free(T[k].pool);
     free(T[k].lat);
