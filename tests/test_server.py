@@ -274,6 +274,51 @@ def test_server_reattach_keeps_ring_position(oracle):
             pass
 
 
+def test_server_frames_it_does_not_take(oracle):
+    """The server takes a batch only if every frame starts 16-byte aligned
+    inside the registered region and all the chunks it reads lie inside it
+    (tasx_host.c server_ok).  A frame moved 8 bytes off its mbuf start, and a
+    last frame whose final chunk would cross the region's end (the region cut
+    at the frame's last byte), send their batches through the context itself;
+    every frame right, and only the clean batch counted as a server flush."""
+    xsum.server_start(0)
+    cx = _Ctxs([11])
+    try:
+        n = 64
+        pin, frames = _frames(n, 555, short=False)
+        cx.pins.append(pin)
+        buf = pin.array
+        offs = np.arange(n, dtype=np.uint64) * 2048
+        # frame 10 moved 8 bytes into its room
+        buf[10 * 2048 + 8:10 * 2048 + 8 + 1600] = frames[10 * 2048:10 * 2048 + 1600]
+        offs[10] += 8
+        tl63 = (int(buf[63 * 2048 + 16]) << 8) | int(buf[63 * 2048 + 17])
+        region = 63 * 2048 + 14 + tl63                 # ends at frame 63's last byte
+        assert region % 16 != 0
+        ref = buf.copy()
+        oracle.tcp4_batch(ref, n, offsets=offs, inplace=True)
+        xsum.register_frames(11, pin.addr, region)
+        xsum.use_server(11)
+        batches = [[i for i in range(32) if i != 10], [10] + list(range(32, 41)), list(range(41, 64))]
+        for b in batches:
+            for i in b:
+                xsum.tcp_checksums(11, pin.addr + int(offs[i]))
+            xsum.tx_flush(11)
+        assert xsum.server_flushes(11) == 1
+        assert sum(xsum.ctx_stats(11)) == 2                # the other two went through the context
+        for i in range(n):
+            o = int(offs[i])
+            np.testing.assert_array_equal(buf[o:o + 1514], ref[o:o + 1514], err_msg=f"frame {i}")
+        xsum.use_server(11, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
+
+
 def test_server_threads(oracle):
     """Eight fast-path threads, each with its own context bound
     (tasx_set_thread_ctx) and attached to the server, 60 tx_flush batches
