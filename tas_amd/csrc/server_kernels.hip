@@ -270,12 +270,14 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // A/B (P.fpol): the frame loads' cache policy -- 0 the product (nt
       // after the acquire), 1 nt, 2 plain, 3 sc1 nt, 4 sc0 nt (1-4 without the
       // acquire: 1, 2 and 4 serve stale lines, profiles/r04/r04g), 5 sc0 nt
-      // after the acquire, 7 sc0 sc1 nt (round 4's first server)
+      // after the acquire, 7 sc0 sc1 nt (round 4's first server), 9 no frame
+      // work at all (a latency breakdown; the fields stay stale)
       switch (P.fpol) {
       case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
       case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
       case 4: case 5: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break;
       case 7: ok = ok && srv_row<kSysNt>(rs, fo, tl, gl); break;
+      case 9: break; // diagnostics only: no frame loads, no stores (wrong results)
       default: ok = ok && srv_row(rs, fo, tl, gl); break;
       }
 #else

@@ -22,6 +22,7 @@
  *   gcc -O2 -std=gnu99 -pthread -Iinclude -Ioracle tools/feeder_bench.c \
  *       -o tools/bin/feeder_bench -Ltas_amd/_lib -ltasx -Loracle/build -loracle \
  *       -Wl,-rpath,/root/repo/tas_amd/_lib -Wl,-rpath,/root/repo/oracle/build
+ *   FB_BATCH=n: n frames per flush (1..32, default 32); FB_MALLOC=1: plain pages
  *   tools/bin/feeder_bench [flushes_per_thread] [in_flight (1..7, default 3)]
  *                          [modes: bit 0 per-context, 1 feeder, 2 server; default 7]
  */
@@ -78,6 +79,7 @@ static void make_frame(uint8_t *f, unsigned k, uint64_t *rng)
 }
 
 static unsigned INFLIGHT = 3, DSLOT = 4; /* batch slots: in flight + 1 being recorded */
+static unsigned NB = BATCH;              /* frames recorded per flush (FB_BATCH, 1..32) */
 
 struct thr {
   int id, flushes, use_feeder;
@@ -113,7 +115,7 @@ static void *run(void *arg)
       qh++, qn--;
     }
     const double t0 = now_us();
-    for (unsigned i = 0; i < BATCH; i++) {
+    for (unsigned i = 0; i < NB; i++) {
       uint8_t *f = slot + (size_t) i * STRIDE;
       if (tasx_tcp_checksums(TASX_CTX_SELF, NULL, f, 0, 0, 0) != 0) {
         T->err = 3;
@@ -164,6 +166,11 @@ int main(int argc, char **argv)
   if (INFLIGHT < 1 || INFLIGHT > MAXQ - 1)
     INFLIGHT = 3;
   DSLOT = INFLIGHT + 1;
+  if (getenv("FB_BATCH")) {
+    NB = (unsigned) atoi(getenv("FB_BATCH"));
+    if (NB < 1 || NB > BATCH)
+      NB = BATCH;
+  }
   const int modes = argc > 3 ? atoi(argv[3]) : 7;
   const int nthreads[] = {1, 2, 4, 8};
   const size_t pool_bytes = (size_t) DSLOT * BATCH * STRIDE;
@@ -275,8 +282,8 @@ int main(int argc, char **argv)
       printf("{\"mode\": \"%s\", \"threads\": %d, \"in_flight\": %u, \"flushes_per_thread\": %d, \"frames_per_flush\": %u, "
              "\"core_us_per_flush\": %.3f, \"stall_us_per_flush\": %.3f, \"latency_us\": %.2f, \"latency_from_submit_us\": %.2f, "
              "\"frames_per_s\": %.0f, \"sweeps\": %llu, \"frames_per_sweep\": %.1f}\n",
-             mname[mode], n, INFLIGHT, flushes, BATCH, median(core_all, n), stall / n, median(lat_all, n), median(lat2_all, n),
-             (double) n * flushes * BATCH / (wall * 1e-6), (unsigned long long) (sw1 - sw0),
+             mname[mode], n, INFLIGHT, flushes, NB, median(core_all, n), stall / n, median(lat_all, n), median(lat2_all, n),
+             (double) n * flushes * NB / (wall * 1e-6), (unsigned long long) (sw1 - sw0),
              sw1 > sw0 ? (double) (fr1 - fr0) / (double) (sw1 - sw0) : 0.0);
       fflush(stdout);
     }

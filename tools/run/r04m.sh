@@ -1,0 +1,26 @@
+set -u
+O=gpurun_out/r04m; mkdir -p $O
+fb() { # tag env...
+  local tag=$1; shift
+  env "$@" TASX_SRV_DIAG=1 timeout -k 10 200 tools/bin/feeder_bench_ab 3000 1 4 > $O/$tag.jsonl 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "$tag rc=$rc"; tail -3 $O/$tag.jsonl; exit 1; fi
+  grep -h '"mode": "server' $O/$tag.jsonl | python3 -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l)
+    if d['threads'] != 1: continue
+    if d['mode'] == 'server_diag': print('$tag diag', d['detect_to_loaded_us'], d['loaded_to_acked_us'], d['gap_us'], d['empty_polls_per_batch'])
+    else: print('$tag', d['frames_per_flush'], d['latency_us'], d['latency_from_submit_us'], d['core_us_per_flush'])"
+}
+for r in 1 2; do
+  fb prod32_r$r
+  fb prod1_r$r FB_BATCH=1
+  fb nowork32_r$r TASX_SRV_FPOL=9
+  fb nowork1_r$r TASX_SRV_FPOL=9 FB_BATCH=1
+  fb sys32_r$r TASX_SRV_FPOL=7
+  fb noacq32_r$r TASX_SRV_FPOL=4
+  fb vram_nowork32_r$r TASX_SRV_VRAM=2 TASX_SRV_FPOL=9
+  fb k1_nowork32_r$r TASX_SRV_K=1 TASX_SRV_FPOL=9
+done
+echo done
