@@ -148,6 +148,9 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
   __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad;
+#ifdef TASX_AB
+  __shared__ uint32_t s_light;
+#endif
   __shared__ uint64_t s_base;
   const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
@@ -159,6 +162,9 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   __syncthreads();
   uint32_t p = blockIdx.x % K; // the server starts on a zeroed block: every ring at position 0
   uint64_t t_act = wall_clock64(), t_lease = t_act;
+#ifdef TASX_AB
+  uint64_t t_prev = t_act;
+#endif
   uint32_t lease = 0u;
 #ifdef TASX_AB
   // A/B diagnostics (P.diag): per workgroup, running sums of the detection ->
@@ -202,7 +208,14 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         s_bytes = (uint32_t) (h0 >> 16);
         s_base = h1 & 0xffffffffffffull;
       }
+#ifdef TASX_AB
+      t_prev = t_act;
+#endif
       t_act = wall_clock64();
+#ifdef TASX_AB
+      if (lane == 0) // A/B 10: this workgroup's previous batch was long ago (a lightly loaded ring)
+        s_light = t_act - t_prev > P.light_ticks ? 1u : 0u;
+#endif
       return 1;
     }
 #ifdef TASX_AB
@@ -250,7 +263,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // a batch taken: this CU's L1 and the XCD's L2 drop their non-coherent
       // lines before any frame load (A/B: policies 1-4 and 7 without)
 #ifdef TASX_AB
-      if (st == 1 && (P.fpol == 0u || P.fpol == 5u))
+      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
 #else
       if (st == 1)
 #endif
@@ -271,13 +284,18 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // after the acquire), 1 nt, 2 plain, 3 sc1 nt, 4 sc0 nt (1-4 without the
       // acquire: 1, 2 and 4 serve stale lines, profiles/r04/r04g), 5 sc0 nt
       // after the acquire, 7 sc0 sc1 nt (round 4's first server), 9 no frame
-      // work at all (a latency breakdown; the fields stay stale)
+      // work at all (a latency breakdown; the fields stay stale), 10 adaptive:
+      // 7 after a gap longer than P.light_ticks since this workgroup's last
+      // batch, else 0
       switch (P.fpol) {
       case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
       case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
       case 4: case 5: ok = ok && srv_row<1 | 2>(rs, fo, tl, gl); break;
       case 7: ok = ok && srv_row<kSysNt>(rs, fo, tl, gl); break;
       case 9: break; // diagnostics only: no frame loads, no stores (wrong results)
+      case 10: // adaptive: system-scope loads on a lightly loaded ring (no acquire), else the product's
+        ok = ok && (s_light ? srv_row<kSysNt>(rs, fo, tl, gl) : srv_row(rs, fo, tl, gl));
+        break;
       default: ok = ok && srv_row(rs, fo, tl, gl); break;
       }
 #else

@@ -2216,6 +2216,7 @@ int tasx_server_start(int device)
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
+    prm.light_ticks = (uint64_t) khz * 8u / 1000u;
     prm.diag = 0;
     prm.k = SRV_K;
     prm.fpol = 0;
@@ -2227,6 +2228,8 @@ int tasx_server_start(int device)
       prm.fpol = (uint32_t) atoi(getenv("TASX_SRV_FPOL"));
     if (getenv("TASX_SRV_HOT_US"))
       prm.hot_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_HOT_US")) / 1000u;
+    if (getenv("TASX_SRV_LIGHT_US"))
+      prm.light_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_LIGHT_US")) / 1000u;
     if (getenv("TASX_SRV_COLD_US"))
       prm.cold_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_COLD_US")) / 1000u;
     S->khz = (uint32_t) khz;

@@ -122,6 +122,7 @@ typedef struct tasx_srv_params {
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
+  uint64_t light_ticks;  /* A/B builds (policy 10): a gap this long since a workgroup's last batch = light load */
   uint32_t diag;         /* A/B builds: timing sums (tasx_ab_server_diag) */
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
   uint32_t fpol;         /* A/B builds: the frame loads' cache policy (server_kernels.hip) */

@@ -22,5 +22,13 @@ for r in 1 2; do
   fb noacq32_r$r TASX_SRV_FPOL=4
   fb vram_nowork32_r$r TASX_SRV_VRAM=2 TASX_SRV_FPOL=9
   fb k1_nowork32_r$r TASX_SRV_K=1 TASX_SRV_FPOL=9
+  fb adapt32_r$r TASX_SRV_FPOL=10
 done
+for r in 1 2; do for p in 0 10; do
+  TASX_SRV_FPOL=$p timeout -k 10 200 tools/bin/feeder_bench_ab 3000 3 4 > $O/q3_fpol${p}_r$r.jsonl 2>&1 || { echo "q3 $p failed"; exit 1; }
+  grep -h '"mode": "server"' $O/q3_fpol${p}_r$r.jsonl | python3 -c "
+import sys,json
+for l in sys.stdin:
+    d=json.loads(l); print('q3 fpol$p r$r', d['threads'], d['latency_us'], round(d['frames_per_s']/1e6,2))"
+done; done
 echo done
