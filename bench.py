@@ -1189,6 +1189,10 @@ def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
                 res["fastpath_mt"] = fastpath_mt_leg()
             except xsum.TasxError as e:
                 res["fastpath_mt"] = {"error": str(e)}
+                try:  # never leave a server running under the legs that follow (HIP frees wait for it)
+                    xsum.server_stop(torch.cuda.current_device())
+                except xsum.TasxError:
+                    pass
         # the same frames as scattered mbufs: the CPU gathers only the summed
         # bytes (tasx_tcp4_cksum_batch_host_offs, staged)
         offs = np.arange(n, dtype=np.uint64) * np.uint64(STRIDE)
