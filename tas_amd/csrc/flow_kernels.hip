@@ -88,7 +88,10 @@ constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
 // 9 now), the same box (profiles/r04/INDEX.md r04d).  NTFS (A/B 10): the
 // flow-state key loads non-temporal too, so that the 2 MiB bucket table alone
 // competes for each XCD's 4 MiB L2: slower (13.33-13.37 us)
-template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false, bool NTFS = false>
+// KPOL >= 0 (A/B 12, 13): the frame keys by a raw buffer load with that
+// cache policy (aux bits: 1 sc0, 2 nt, 16 sc1) -- do uncached forms move fewer
+// bytes per 12-byte key than the non-temporal global load?
+template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false, bool NTFS = false, int KPOL = -1>
 __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
 {
   constexpr bool TAB = CRC == kCrcSlice4;
@@ -112,10 +115,15 @@ __global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
       // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
       // unaligned dwordx3 load (gfx950 global loads take any byte address)
       u32x3u k;
-      if constexpr (NTKEY)
+      if constexpr (KPOL >= 0) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) p.base, 0, -1, 0x00020000);
+        const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(rs, (uint32_t) (fr - p.base) + p.ip_off + 12u, 0, KPOL);
+        k = u32x3u{w.x, w.y, w.z};
+      } else if constexpr (NTKEY) {
         k = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
-      else
+      } else {
         k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+      }
       rip[f] = k.x;
       lip[f] = k.y;
       l4x[f] = k.z;
@@ -422,12 +430,12 @@ extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t 
 }
 #endif
 
-template <int F, bool NTKEY = false, bool NTFS = false>
+template <int F, bool NTKEY = false, bool NTFS = false, int KPOL = -1>
 static int launch_flow_f(const char *name, const tasx_flow_params *p, hipStream_t s)
 {
   const uint64_t blocks = ((uint64_t) p->n + 256u * F - 1) / (256u * F);
   tasx_note_kernel(name);
-  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY, NTFS>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
+  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY, NTFS, KPOL>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -458,6 +466,13 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
   case 9: return launch_flow_f<kFlowFramesPerLane, false>("flow_lookup_kernel<l2key>", p, s); // the round-3 product
   case 10: return launch_flow_f<kFlowFramesPerLane, true, true>("flow_lookup_kernel<ntfs>", p, s);
+  case 12: case 13: // keys by raw buffer loads: stride mode within 4 GiB, TAS layout
+    if (!p->off && p->l4_off == p->ip_off + 20u && (uint64_t) p->n * p->stride < (1ull << 32)) {
+      if (variant == 12)
+        return launch_flow_f<kFlowFramesPerLane, false, false, 1 | 16>("flow_lookup_kernel<key sc0 sc1>", p, s);
+      return launch_flow_f<kFlowFramesPerLane, false, false, 16 | 2>("flow_lookup_kernel<key sc1 nt>", p, s);
+    }
+    break;
   case 11: // TAS layout only (one 12-byte key load); other layouts take the product
     if (p->l4_off == p->ip_off + 20u)
       return launch_flow_partitioned(p, s);

@@ -102,7 +102,7 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 9, 10, 11])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 13])
 def test_gpu_flow_golden(flow_golden, variant):
     """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
     chunks, 2 / 4 frames per lane, L2-allocating keys (9: the round-3
@@ -124,11 +124,11 @@ def test_gpu_flow_golden(flow_golden, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 6, 7, 9, 10, 11])
+@pytest.mark.parametrize("variant", [0, 6, 7, 9, 10, 11, 12, 13])
 def test_gpu_flow_vs_oracle_large(oracle, variant):
     """64K flows in a TAS-sized table (2x entries), 256K frames: hits in random
     order, misses (unknown keys), hash-out off; the product and the 2 / 4
-    frames-per-lane forms (A/B 6, 7), 9-11, with a ragged batch end."""
+    frames-per-lane forms (A/B 6, 7), 9-13, with a ragged batch end."""
     import contextlib
     from tas_amd import xsum
     nflows, ent, n = 65536, 131072, 262144
