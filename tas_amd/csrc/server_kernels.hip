@@ -193,12 +193,14 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // into LDS), 0 = nothing yet, 2 = the header without all its entries (the
   // host still writing them, or a header-only poll: read the whole slot at
   // once), 3 = stop, 4 = the lease ran out
-  auto judge = [&](const SlotRead &v, uint64_t now) -> int {
+  auto judge = [&](const SlotRead &v, bool entries, uint64_t now) -> int {
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
     const uint32_t n = (uint32_t) (h0 & 0xffffu);
     const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
-    if (hdr && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (v.e >> 48) != tag) == 0ull) {
+    // a header-only read never takes the slot: unread entries (0) would match
+    // the tag of every position p with p + 1 = 0 mod 2^16
+    if (hdr && entries && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (v.e >> 48) != tag) == 0ull) {
       if ((uint32_t) lane < n) {
         s_off[lane] = (uint32_t) v.e;
         s_tl[lane] = (uint32_t) (v.e >> 32) & 0xffffu;
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // memory-path message, not a register read)
       uint64_t now = wall_clock64();
       for (uint32_t np = 1;; ++np) {
-        st = judge(read_slot(entries), now);
+        st = judge(read_slot(entries), entries, now);
         if (st == 1 || st >= 3)
           break;
         entries = true;

@@ -198,7 +198,8 @@ def test_server_refilled_mbufs_every_flush(oracle, mem):
 def test_server_ring_wrap_and_tag_wrap(oracle):
     """70,000 one-frame flushes with up to 8 in flight: the 8-slot ring wraps
     8,750 times and the 16-bit slot tags wrap (position 65,535 -> 0) with the
-    server reading every slot fresh; every frame right."""
+    server reading every slot fresh, once right after an idle spell that put
+    the ring on header-only polls; every frame right."""
     xsum.server_start(0)
     cx = _Ctxs([9])
     try:
@@ -210,6 +211,15 @@ def test_server_ring_wrap_and_tag_wrap(oracle):
         xsum.use_server(9)
         total, inflight = 70000, []
         for k in range(total):
+            if k in (65535, 65536 + 7):
+                # the ring idle past the header-only threshold (2 ms) just
+                # before the positions whose tag is 0 (p + 1 = 2^16): the
+                # header-only poll must not take a slot whose entries it did
+                # not read
+                for t in inflight:
+                    xsum.flush_wait(9, t)
+                inflight = []
+                time.sleep(0.005)
             xsum.tcp_checksums(9, pin.addr + (k % nf) * 2048)
             inflight.append(xsum.flush_submit(9))
             if len(inflight) >= 8:
