@@ -1,5 +1,7 @@
 set -u
 O=gpurun_out/r04m; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_server.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_server.log 2>&1 || { echo "server tests failed"; tail -20 $O/pytest_server.log; exit 1; }
+tail -n 1 $O/pytest_server.log
 fb() { # tag env...
   local tag=$1; shift
   env "$@" TASX_SRV_DIAG=1 timeout -k 10 200 tools/bin/feeder_bench_ab 3000 1 4 > $O/$tag.jsonl 2>&1
