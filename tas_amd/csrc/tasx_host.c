@@ -2142,6 +2142,13 @@ static int server_submit(struct tasx_ctx *c)
       const uint64_t fo = (uint64_t) (ip - TASX_TAS_IP_OFF - h16);
       slot[TASX_SRV_HDR / 8 + i] = fo | (uint64_t) tl << 32 | tag;
     }
+    /* the unused entries get this position's tag too: every entry word of a
+     * slot then carries either this position's tag or the one of the slot's
+     * previous position, so a word the server reads before the host wrote it
+     * can never pass for a current one (an entry left unwritten for 2^16
+     * positions, or never written, would carry a stale tag that matches) */
+    for (uint32_t i = cnt; i < TASX_SRV_FB; i++)
+      slot[TASX_SRV_HDR / 8 + i] = tag;
     __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
     __atomic_store_n(&slot[0], (uint64_t) cnt | (bytes > 0xffffffffull ? 0xffffffffull : bytes) << 16 | tag,
                      __ATOMIC_RELEASE);

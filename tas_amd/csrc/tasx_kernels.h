@@ -100,7 +100,8 @@ typedef struct tasx_flow_params {
  *     u64 h1 = region device address (48 bits) | tag << 48,
  *     then n <= TASX_SRV_FB entries u64 = frame offset in the region (32
  *     bits) | ip.total_length << 32 | tag << 48,
- *   tag = (p + 1) mod 2^16; the host writes the entries, then h1, then h0.
+ *   tag = (p + 1) mod 2^16; the host writes the entries (all TASX_SRV_FB of
+ *   them: the unused ones carry the tag alone), then h1, then h0.
  * Workgroup k of ring r's P.k takes its positions p = k mod P.k. */
 #define TASX_SRV_RING 8u   /* slots per ring */
 #define TASX_SRV_FB 64u    /* frames per slot */
