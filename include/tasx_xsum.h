@@ -415,8 +415,9 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * a frame start (ip - 14) not 16-byte aligned, or total_length outside
  * [38, 1522] -- are flushed by the context itself after its server tickets.
  * Frames must stay unmodified until their ticket completes; a frame whose
- * total_length changed meanwhile is left alone and the context's next
- * poll/wait returns -EIO.  The TAS path this replaces: tx_flush
+ * total_length changed meanwhile is left alone, and from then on the
+ * context's poll/wait return -EIO, until tasx_ctx_use_server(ctx, 0), which
+ * still detaches and returns -EIO once.  The TAS path this replaces: tx_flush
  * (tas/fast/fastemu.c:544-566) after tcp_checksums (fast_flows.c:1058-1069).
  *   tasx_server_start(device): launch the server kernel (2 * TASX_MAX_CTX
  *     workgroups of 1024 threads) and its keepalive thread; the kernel also

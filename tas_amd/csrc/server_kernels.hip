@@ -312,8 +312,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
-      if (s_bad)
-        st_sys32(dline + TASX_SRV_ERRW, 1u); // sticky: a frame changed after submission (or a malformed slot)
+      if (s_bad) { // sticky in the ring's line: a frame changed after submission (or a malformed slot)
+        st_sys32(dline + TASX_SRV_ERRW, 1u);
+        s_bad = 0u; // (the rows of the next batch set it only after the next barrier)
+      }
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
 #ifdef TASX_AB
       if (diag) {

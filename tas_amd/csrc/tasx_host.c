@@ -461,6 +461,7 @@ struct tasx_ctx {
   uint32_t sv_done_pos; /* positions the server has finished (as last seen) */
   uint32_t sv_ticket[TASX_SRV_RING]; /* ticket of the batch at each ring position */
   uint32_t n_server_flushes;
+  int sv_err; /* the server flagged a frame of this context (sticky until detach) */
   uint64_t sv_batches, sv_frames; /* since attach (this thread's own counters: no shared line per flush) */
 };
 
@@ -1289,12 +1290,16 @@ static int flush_reap(struct tasx_ctx *c, uint32_t upto)
  * ends the wait instead of spinning on. */
 static int feeder_error(const struct tasx_ctx *c);
 static int server_health(const struct tasx_ctx *c);
+static int server_err(const struct tasx_ctx *c);
+static int server_alive(const struct tasx_ctx *c);
 
 static int flush_wait(struct tasx_ctx *c, uint32_t ticket)
 {
   uint32_t k = 0;
   int rc;
   while (!flush_reap(c, ticket)) {
+    if (c->sv && c->sv_err)
+      return server_err(c);
     if ((++k & 4095u) == 0 && c->fd && feeder_error(c))
       return set_err(-EIO, "flush: the feeder thread failed");
     if ((k & 4095u) == 0 && c->sv && (rc = server_health(c)) != 0)
@@ -1313,7 +1318,7 @@ static int flush_wait(struct tasx_ctx *c, uint32_t ticket)
         return hip_err(e, "flush: hipStreamQuery");
     }
   }
-  return 0;
+  return c->sv && c->sv_err ? server_err(c) : 0;
 }
 
 static int zerocopy_ok(const struct tasx_ctx *c, uint32_t n)
@@ -1519,8 +1524,10 @@ int tasx_flush_poll(unsigned ctx_id, uint32_t ticket)
   if (!ticket_le(ticket, c->next_ticket))
     return set_err(-EINVAL, "flush ticket %u not submitted (last %u)", ticket, c->next_ticket);
   const int done = flush_reap(c, ticket);
+  if (c->sv && c->sv_err)
+    return server_err(c);
   if (!done && c->sv) {
-    const int rc = server_health(c);
+    const int rc = server_alive(c);
     if (rc)
       return rc;
   }
@@ -2061,11 +2068,15 @@ static void server_free(struct fserver *S)
 }
 
 /* 0 while the server kernel runs and has flagged no error */
-static int server_health(const struct tasx_ctx *c)
+static int server_err(const struct tasx_ctx *c)
 {
-  const unsigned id = (unsigned) (c - g_ctx);
-  if (__atomic_load_n(srv_dline(c->sv, id) + TASX_SRV_ERRW, __ATOMIC_ACQUIRE) != 0)
-    return set_err(-EIO, "flush server: a frame of ring %u changed after submission (or a malformed slot)", id);
+  return set_err(-EIO, "flush server: a frame of ctx %u changed after submission (its fields were left alone; "
+                 "sticky until tasx_ctx_use_server(ctx, 0))", (unsigned) (c - g_ctx));
+}
+
+/* 0 while the server kernel runs */
+static int server_alive(const struct tasx_ctx *c)
+{
   const hipError_t e = hipStreamQuery(c->sv->st);
   if (e == hipErrorNotReady)
     return 0;
@@ -2074,17 +2085,28 @@ static int server_health(const struct tasx_ctx *c)
   return hip_err(e, "flush server: hipStreamQuery");
 }
 
+/* 0 while the server kernel runs and has flagged no frame of this context */
+static int server_health(const struct tasx_ctx *c)
+{
+  return c->sv_err ? server_err(c) : server_alive(c);
+}
+
 /* the positions finished in order from sv_done_pos (the ring's workgroups
- * finish theirs out of order) */
+ * finish theirs out of order); the ring's error word (same line) moves into
+ * the context's sticky flag */
 static void server_reap(struct tasx_ctx *c)
 {
   const unsigned id = (unsigned) (c - g_ctx);
-  const uint32_t *done = srv_dline(c->sv, id);
+  uint32_t *done = srv_dline(c->sv, id);
   uint32_t d = c->sv_done_pos;
   while (d != c->sv_pos && __atomic_load_n(&done[d % TASX_SRV_RING], __ATOMIC_ACQUIRE) == d + 1u)
     d++;
   if (d == c->sv_done_pos)
     return;
+  if (__atomic_load_n(&done[TASX_SRV_ERRW], __ATOMIC_ACQUIRE) != 0) {
+    c->sv_err = 1;
+    __atomic_store_n(&done[TASX_SRV_ERRW], 0u, __ATOMIC_RELAXED);
+  }
   const uint32_t t = c->sv_ticket[(d - 1u) % TASX_SRV_RING];
   c->sv_done_pos = d;
   if (!ticket_le(t, c->done_ticket))
@@ -2378,6 +2400,9 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
     if (S) {
       c->sv_pos = c->sv_done_pos = S->ring_pos[id]; /* where the ring's workgroups wait */
+      c->sv_err = 0;
+      /* an error a previous context of this ring left (no batch of the ring is in flight) */
+      __atomic_store_n(srv_dline(S, id) + TASX_SRV_ERRW, 0u, __ATOMIC_RELEASE);
       c->sv_batches = c->sv_frames = 0;
       c->sv = S;
       __atomic_or_fetch(&S->attached, 1u << id, __ATOMIC_RELEASE);
@@ -2387,8 +2412,19 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
   }
   if (!c->sv)
     return 0;
-  if ((rc = flush_wait(c, c->next_ticket)) != 0)
+  /* the server's positions first: a frame it flagged does not stop the detach */
+  uint32_t k = 0;
+  while (c->sv_done_pos != c->sv_pos) {
+    server_reap(c);
+    if ((++k & 4095u) == 0 && (rc = server_alive(c)) != 0)
+      return rc;
+  }
+  const int had_err = c->sv_err;
+  c->sv_err = 0;
+  if ((rc = flush_wait(c, c->next_ticket)) != 0) {
+    c->sv_err = had_err;
     return rc;
+  }
   pthread_mutex_lock(&g_server_mu); /* the counts move to the server's totals atomically for tasx_server_stats */
   __atomic_fetch_add(&c->sv->batches, c->sv_batches, __ATOMIC_RELAXED);
   __atomic_fetch_add(&c->sv->frames, c->sv_frames, __ATOMIC_RELAXED);
@@ -2396,7 +2432,9 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
   __atomic_and_fetch(&c->sv->attached, ~(1u << id), __ATOMIC_RELEASE);
   pthread_mutex_unlock(&g_server_mu);
   c->sv = NULL;
-  return 0;
+  return had_err ? set_err(-EIO, "ctx %u detached from the flush server; a frame changed after submission since "
+                           "attach (its fields were left alone)", ctx_id)
+                 : 0;
 }
 
 int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes)

@@ -329,6 +329,57 @@ def test_server_frames_it_does_not_take(oracle):
             pass
 
 
+def test_server_changed_frame_is_reported(oracle):
+    """A frame whose total_length changes after tasx_flush_submit (TAS must
+    not touch a frame before its ticket completes) is left alone by the
+    server, and the context's poll and wait report -EIO from then on; the
+    detach still completes (reporting -EIO once), and re-attached the context
+    flushes correctly again."""
+    xsum.server_start(0)
+    cx = _Ctxs([13])
+    try:
+        nf = 8
+        pin, frames = _frames(nf, 121, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nf)
+        xsum.register_frames(13, pin.addr, pin.nbytes)
+        xsum.use_server(13)
+        seen, t = False, 0
+        for _ in range(50):
+            time.sleep(0.003)  # the ring idle: header-only polls, a few microseconds apart
+            xsum.tcp_checksums(13, pin.addr)
+            t = xsum.flush_submit(13)
+            pin.array[17] ^= 0x04  # total_length 52 -> 48 under the server
+            try:
+                xsum.flush_wait(13, t)
+            except xsum.TasxError as e:
+                assert e.code == -errno.EIO
+                seen = True
+            pin.array[17] ^= 0x04
+            if seen:
+                break
+        assert seen, "the frame was never changed before the server read it"
+        with pytest.raises(xsum.TasxError):
+            xsum.flush_poll(13, t)  # sticky until detached
+        with pytest.raises(xsum.TasxError) as ei:
+            xsum.use_server(13, False)  # detaches, and reports it once more
+        assert ei.value.code == -errno.EIO
+        xsum.use_server(13)
+        pin.array[:frames.size] = frames
+        for i in range(nf):
+            xsum.tcp_checksums(13, pin.addr + i * 2048)
+        xsum.tx_flush(13)
+        np.testing.assert_array_equal(pin.array[:frames.size], ref)
+        xsum.use_server(13, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
+
+
 def test_server_threads(oracle):
     """Eight fast-path threads, each with its own context bound
     (tasx_set_thread_ctx) and attached to the server, 60 tx_flush batches
