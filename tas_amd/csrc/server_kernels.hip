@@ -265,6 +265,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // a batch taken: this CU's L1 and the XCD's L2 drop their non-coherent
       // lines before any frame load (A/B: policies 1-4 and 7 without)
 #ifdef TASX_AB
+      if (st == 1 && P.fpol == 11u) // A/B 11: an agent-scope acquire instead (buffer_inv sc1)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (st == 1 && (P.fpol == 0u || P.fpol == 5u || (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
 #else
       if (st == 1)
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // after the acquire, 7 sc0 sc1 nt (round 4's first server), 9 no frame
       // work at all (a latency breakdown; the fields stay stale), 10 adaptive:
       // 7 after a gap longer than P.light_ticks since this workgroup's last
-      // batch, else 0
+      // batch, else 0; 11 nt after an agent-scope acquire
       switch (P.fpol) {
       case 2: ok = ok && srv_row<0>(rs, fo, tl, gl); break;
       case 3: ok = ok && srv_row<16 | 2>(rs, fo, tl, gl); break;
