@@ -435,6 +435,24 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     memory (e.g. torch.cuda.empty_cache) blocks until the stop
  *   tasx_server_stats: batches and frames submitted since start
  *   tasx_ctx_server_flushes: batches the context handed to the server */
+/* The fused TX segment build through the flush server (the copy of
+ * flow_tx_segment's payload from the app's TX buffer plus tcp_checksums,
+ * tas/fast/fast_flows.c:930-936, at tx_flush time with no HIP call): the
+ * fast-path core fills the headers as now and, instead of dma_read +
+ * tcp_checksums, hands each segment's descriptor (tasx_tx_seg; frame_off
+ * from the registered frame region's start, tx_base from the registered
+ * shared-memory region's start) to tasx_server_tx_segments, which returns a
+ * ticket (tasx_flush_poll / _wait, in order with the context's other
+ * tickets).  The server gathers the payload and writes it into the frame,
+ * both checksums included, over PCIe.  TAS layout (ip at +14, tcp at +34),
+ * frame starts 16-byte aligned, hdrs_len in [54, 240], room below 32 KiB,
+ * frames (and their rooms) inside the frame region: else -EINVAL and nothing
+ * is submitted.  Descriptors dma_read() would reject leave their frame as it
+ * is (tasx_tx_segment_batch_dev).
+ *   tasx_ctx_register_shm(ctx, shm, bytes): the app's shared-memory region
+ *     (pinned and mapped here unless it already is; below 4 GiB) */
+int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes);
+int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n, uint32_t *ticket);
 int tasx_server_start(int device);
 int tasx_server_stop(int device);
 int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames);

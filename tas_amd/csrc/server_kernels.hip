@@ -42,6 +42,7 @@
 #include "tasx_kernels.h"
 
 #include "xsum_device.h"
+#include "txseg_device.h"
 
 namespace {
 
@@ -147,7 +148,8 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
-  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad;
+  __shared__ uint64_t s_w[TASX_SRV_FB]; // a TX segment slot's entry words
+  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg;
 #ifdef TASX_AB
   __shared__ uint32_t s_light;
 #endif
@@ -196,16 +198,19 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   auto judge = [&](const SlotRead &v, bool entries, uint64_t now) -> int {
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
-    const uint32_t n = (uint32_t) (h0 & 0xffffu);
-    const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= TASX_SRV_FB;
+    const bool seg = (h0 & TASX_SRV_SEG) != 0u;
+    const uint32_t n = (uint32_t) (h0 & 0x7fffu), words = seg ? 2u + 4u * n : n;
+    const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= (seg ? TASX_SRV_SEGS : TASX_SRV_FB);
     // a header-only read never takes the slot: unread entries (0) would match
     // the tag of every position p with p + 1 = 0 mod 2^16
-    if (hdr && entries && __builtin_amdgcn_ballot_w64((uint32_t) lane < n && (v.e >> 48) != tag) == 0ull) {
-      if ((uint32_t) lane < n) {
+    if (hdr && entries && __builtin_amdgcn_ballot_w64((uint32_t) lane < words && (v.e >> 48) != tag) == 0ull) {
+      if ((uint32_t) lane < words) {
         s_off[lane] = (uint32_t) v.e;
         s_tl[lane] = (uint32_t) (v.e >> 32) & 0xffffu;
+        s_w[lane] = v.e;
       }
       if (lane == 0) {
+        s_seg = seg ? 1u : 0u;
         s_n = n;
         s_bytes = (uint32_t) (h0 >> 16);
         s_base = h1 & 0xffffffffffffull;
@@ -277,7 +282,29 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     if (s_cmd != 0u)
       break;
     const uint32_t row = threadIdx.x >> 4;
-    if (row < s_n) {
+    if (s_seg) {
+      // TX segment slot: row r builds segment r (payload gathered from the
+      // app's TX buffer into the frame, both checksums stored): the general
+      // row of the TX segment build (txseg_device.h), over PCIe both ways
+      if (row < s_n) {
+        const uint64_t w0 = s_w[2 + 4 * row], w1 = s_w[3 + 4 * row], w2 = s_w[4 + 4 * row], w3 = s_w[5 + 4 * row];
+        const uint32_t room16 = (uint32_t) (w2 >> 32) & 0xffffu;
+        const u32x4 d0 = u32x4{(uint32_t) w0, 0u, (uint32_t) w2, 0u};
+        const u32x4 d1 = u32x4{(uint32_t) w3, (uint32_t) w1, ((uint32_t) (w0 >> 32) & 0xffffu) | ((uint32_t) (w1 >> 32) << 16),
+                               (room16 & 0x7fffu) | ((room16 & 0x8000u) ? 0x80000000u : 0u)};
+        tasx_txseg_params tp;
+        tp.shm = (const uint8_t *) (uintptr_t) (s_w[0] & 0xffffffffffffull);
+        tp.shm_len = (uint32_t) s_w[1];
+        tp.frames = (uint8_t *) (uintptr_t) s_base;
+        tp.segs = nullptr;
+        tp.out = nullptr;
+        tp.n = s_n;
+        tp.ip_off = (uint32_t) (s_w[1] >> 32) & 0xffu;
+        tp.l4_off = (uint32_t) (s_w[1] >> 40) & 0xffu;
+        tp.dbg = 0u;
+        txseg_row_d<3, false>(tp, row, d0, d1, gl);
+      }
+    } else if (row < s_n) {
       const uint64_t base = s_base;
       __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (uintptr_t) base, 0, (int) s_bytes,
                                                                     (int) kRsrcWord3);
@@ -314,6 +341,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
+      if (s_seg) // the TX build's plain stores: every dirty line out of the L2 before the done word
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (s_bad) { // sticky in the ring's line: a frame changed after submission (or a malformed slot)
         st_sys32(dline + TASX_SRV_ERRW, 1u);
         s_bad = 0u; // (the rows of the next batch set it only after the next barrier)

@@ -444,6 +444,12 @@ struct tasx_ctx {
   uint8_t *zc_dev;
   size_t zc_bytes;
   int zc_registered; /* we called hipHostRegister on it */
+  /* the app's shared-memory region (tasx_ctx_register_shm): TX segment
+   * payload sources for tasx_server_tx_segments */
+  uint8_t *shm_host;
+  uint8_t *shm_dev;
+  size_t shm_bytes;
+  int shm_registered;
   uint32_t n_zerocopy_flushes, n_staged_flushes;
   /* shared feeder (tasx_ctx_use_feeder): zero-copy batches go to the GPU's
    * feeder thread through a single-producer / single-consumer queue */
@@ -532,6 +538,8 @@ static void ctx_release(struct tasx_ctx *c)
     hipFree(c->d_count);
   if (c->zc_registered)
     hipHostUnregister(c->zc_host);
+  if (c->shm_registered)
+    hipHostUnregister(c->shm_host);
   free(c->pend_ip);
   free(c->pend_l4);
   free(c->fq);
@@ -1219,6 +1227,42 @@ int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes)
   c->zc_host = (uint8_t *) base;
   c->zc_dev = (uint8_t *) dev;
   c->zc_bytes = bytes;
+  return 0;
+}
+
+int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  void *dev = NULL;
+  hipError_t e;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!shm || bytes == 0 || bytes >= (1ull << 32))
+    return set_err(-EINVAL, "register_shm: empty region or not below 4 GiB");
+  if (c->shm_host)
+    return set_err(-EINVAL, "ctx %u already has a shared-memory region", ctx_id);
+  HIPCHK(hipSetDevice(c->device));
+  e = hipHostGetDevicePointer(&dev, shm, 0);
+  if (e != hipSuccess) {
+    (void) hipGetLastError();
+    HIPCHK(hipHostRegister(shm, bytes, hipHostRegisterMapped));
+    c->shm_registered = 1;
+    e = hipHostGetDevicePointer(&dev, shm, 0);
+    if (e != hipSuccess) {
+      hipHostUnregister(shm);
+      c->shm_registered = 0;
+      return hip_err(e, "hipHostGetDevicePointer");
+    }
+  }
+  if ((uint64_t) (uintptr_t) dev + bytes >= (1ull << 48)) {
+    if (c->shm_registered)
+      hipHostUnregister(shm);
+    c->shm_registered = 0;
+    return set_err(-EINVAL, "register_shm: device address beyond 48 bits");
+  }
+  c->shm_host = (uint8_t *) shm;
+  c->shm_dev = (uint8_t *) dev;
+  c->shm_bytes = bytes;
   return 0;
 }
 
@@ -2187,6 +2231,87 @@ static int server_submit(struct tasx_ctx *c)
     }
     c->npend -= cnt;
   }
+  return 0;
+}
+
+/* TX segment batches through the server: validated up front (nothing is
+ * submitted unless every segment is safe to build in place), then packed
+ * TASX_SRV_SEGS to a slot (tasx_kernels.h) */
+int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n, uint32_t *ticket)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  int rc;
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (!c->sv)
+    return set_err(-EINVAL, "ctx %u is not attached to a flush server (tasx_ctx_use_server)", ctx_id);
+  if (!c->shm_host)
+    return set_err(-EINVAL, "ctx %u has no shared-memory region (tasx_ctx_register_shm)", ctx_id);
+  if (n > 0 && !segs)
+    return set_err(-EINVAL, "tx segments: NULL descriptors");
+  const uint32_t ip_off = TASX_TAS_IP_OFF, l4_off = TASX_TAS_L4_OFF;
+  for (uint32_t i = 0; i < n; i++) {
+    const tasx_tx_seg *g = &segs[i];
+    const uint32_t room = g->room & ~TASX_TXSEG_SCRATCH;
+    const uint64_t fend = (uint64_t) g->hdrs_len + g->payload;
+    if ((g->frame_off & 15u) != 0 || g->hdrs_len < l4_off + 20u || g->hdrs_len > 240u || room > 0x7fffu ||
+        g->tx_base >= (1ull << 32) || g->frame_off >= c->zc_bytes)
+      return set_err(-EINVAL, "tx segment %u: frame offset, header length or room outside what the server builds",
+                     i);
+    /* the row reads and writes whole 16-byte chunks of [frame, frame + max(end, room)) and sums up to
+     * ip_off + ip.total_length (TAS's own frames: hdrs_len - ip_off + payload, fast_flows.c:897) */
+    const uint8_t *ip = c->zc_host + g->frame_off + ip_off;
+    const uint64_t tl = ((uint32_t) ip[2] << 8) | ip[3];
+    uint64_t span = fend > ip_off + tl ? fend : ip_off + tl;
+    if (g->room & TASX_TXSEG_SCRATCH)
+      span = span > room ? span : room;
+    if (g->frame_off + ((span + 15u) & ~(uint64_t) 15) > c->zc_bytes)
+      return set_err(-EINVAL, "tx segment %u: frame (or its room) past the registered frame region", i);
+  }
+  /* a flush this context launched itself completes first (as server_submit) */
+  if (!ticket_le(c->local_last, c->done_ticket) && (rc = flush_wait(c, c->local_last)) != 0)
+    return rc;
+  struct fserver *S = c->sv;
+  const unsigned id = (unsigned) (c - g_ctx);
+  for (uint32_t i0 = 0; i0 < n; i0 += TASX_SRV_SEGS) {
+    const uint32_t cnt = n - i0 < TASX_SRV_SEGS ? n - i0 : TASX_SRV_SEGS;
+    uint32_t k = 0;
+    while (c->sv_pos - c->sv_done_pos >= TASX_SRV_RING) {
+      server_reap(c);
+      if ((++k & 4095u) == 0 && (rc = server_health(c)) != 0)
+        return rc;
+    }
+    const uint32_t pos = c->sv_pos;
+    const uint64_t tag = (uint64_t) ((pos + 1u) & 0xffffu) << 48;
+    uint64_t *slot = (uint64_t *) (S->h_ring + TASX_SRV_SLOTP(id, pos));
+    uint64_t *e = slot + TASX_SRV_HDR / 8;
+    e[0] = (uint64_t) (uintptr_t) c->shm_dev | tag;
+    e[1] = (uint64_t) (uint32_t) c->shm_bytes | (uint64_t) ip_off << 32 | (uint64_t) l4_off << 40 | tag;
+    for (uint32_t j = 0; j < cnt; j++) {
+      const tasx_tx_seg *g = &segs[i0 + j];
+      const uint32_t room16 = (g->room & 0x7fffu) | ((g->room & TASX_TXSEG_SCRATCH) ? 0x8000u : 0u);
+      e[2 + 4 * j] = (uint32_t) g->frame_off | (uint64_t) g->payload << 32 | tag;
+      e[3 + 4 * j] = g->pos | (uint64_t) g->hdrs_len << 32 | tag;
+      e[4 + 4 * j] = (uint32_t) g->tx_base | (uint64_t) room16 << 32 | tag;
+      e[5 + 4 * j] = g->tx_len | tag;
+    }
+    for (uint32_t w = 2 + 4 * cnt; w < TASX_SRV_FB; w++) /* every entry word tagged (server_submit) */
+      e[w] = tag;
+    const uintptr_t b16 = (uintptr_t) c->zc_dev;
+    __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
+    __atomic_store_n(&slot[0], (uint64_t) (cnt | TASX_SRV_SEG) |
+                     (uint64_t) (c->zc_bytes > 0xffffffffull ? 0xffffffffull : c->zc_bytes) << 16 | tag,
+                     __ATOMIC_RELEASE);
+    if (S->vram)
+      __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
+    c->sv_pos = pos + 1u;
+    c->n_server_flushes++;
+    __atomic_store_n(&c->sv_batches, c->sv_batches + 1u, __ATOMIC_RELAXED);
+    __atomic_store_n(&c->sv_frames, c->sv_frames + cnt, __ATOMIC_RELAXED);
+  }
+  if (ticket)
+    *ticket = c->next_ticket;
   return 0;
 }
 

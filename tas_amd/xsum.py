@@ -90,6 +90,8 @@ SIGNATURES = {
     "tasx_ctx_use_feeder": (_c_int, [_uns, _c_int]),
     "tasx_ctx_feeder_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
     "tasx_server_start": (_c_int, [_c_int]),
+    "tasx_ctx_register_shm": (_c_int, [_uns, _vp, _sz]),
+    "tasx_server_tx_segments": (_c_int, [_uns, _vp, _c_u32, ctypes.POINTER(ctypes.c_uint32)]),
     "tasx_server_stop": (_c_int, [_c_int]),
     "tasx_server_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
     "tasx_ctx_use_server": (_c_int, [_uns, _c_int]),
@@ -490,6 +492,24 @@ def server_stats(device: int = 0) -> tuple[int, int]:
     b, fr = ctypes.c_uint64(), ctypes.c_uint64()
     _check(lib().tasx_server_stats(device, ctypes.byref(b), ctypes.byref(fr)), "tasx_server_stats")
     return b.value, fr.value
+
+
+def register_shm(ctx_id: int, base_addr: int, nbytes: int) -> None:
+    """The app's shared-memory region, TX payload sources for
+    server_tx_segments (tasx_ctx_register_shm)."""
+    _check(lib().tasx_ctx_register_shm(ctx_id, base_addr, nbytes), "tasx_ctx_register_shm")
+
+
+def server_tx_segments(ctx_id: int, segs) -> int:
+    """Hand TX segments (pktgen.TX_SEG_DTYPE records: frame_off from the frame
+    region's start, tx_base from the shm region's start) to the flush server
+    (tasx_server_tx_segments); returns the ticket of the last one."""
+    import numpy as np
+    a = np.ascontiguousarray(segs)
+    assert a.dtype.itemsize == 32
+    t = ctypes.c_uint32()
+    _check(lib().tasx_server_tx_segments(ctx_id, a.ctypes.data, len(a), ctypes.byref(t)), "tasx_server_tx_segments")
+    return t.value
 
 
 def use_server(ctx_id: int, on: bool = True) -> None:

@@ -101,6 +101,8 @@ def test_abi_version_and_errors_without_gpu(L):
     assert L.tasx_server_stop(-1) == -errno.ENODEV
     assert L.tasx_ctx_use_server(3, 1) == -errno.EINVAL
     assert L.tasx_ctx_server_flushes(3, None) == -errno.EINVAL
+    assert L.tasx_ctx_register_shm(3, None, 0) == -errno.EINVAL
+    assert L.tasx_server_tx_segments(3, None, 0, None) == -errno.EINVAL
     if L.tasx_device_count() <= 0:  # no GPU in this container: start fails, nothing launched
         assert L.tasx_server_start(0) in (-errno.EIO, -errno.ENODEV)
 

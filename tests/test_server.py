@@ -468,3 +468,65 @@ def test_server_stop_is_bounded_and_restarts(oracle):
             xsum.server_stop(0)
         except xsum.TasxError:
             pass
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_server_tx_segments(oracle, odd):
+    """The fused TX segment build through the server (tasx_server_tx_segments,
+    SURVEY 8f rows 1 + 2 at TAS's batch size): payloads gathered from the
+    app's TX buffers in pinned host memory (wraps of the circular buffers,
+    odd buffer bases and lengths), written into the mbufs and both checksums
+    stored, 32 segments per flush (three ring slots each), against the oracle's
+    flow_tx_read + tcp_checksums; interleaved with checksum-only flushes of
+    the same context (ticket order); a descriptor the host refuses (frame not
+    16-byte aligned) submits nothing; dma_read-invalid ones (payload beyond
+    the buffer) leave their frame as it is, as the oracle does."""
+    n = 96
+    pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 37) % 1449, pktgen.TCP_MSS)
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=4096, nflows=12, odd=odd, seed=0x5E6 + odd,
+                                           room=pktgen.MBUF_ROOM)
+    segs = segs.copy()
+    segs["payload"][17] = 4097                     # > tx_len: dma_read would assert; left alone
+    exp_fr = fr.copy()
+    oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    xsum.server_start(0)
+    cx = _Ctxs([14])
+    try:
+        hs = xsum.PinnedBuffer(sl + 64)
+        hf = xsum.PinnedBuffer(fr.size + 4096)
+        cx.pins += [hs, hf]
+        hs.array[:sl] = shm[:sl]
+        hf.array[:] = 0
+        hf.array[:fr.size] = fr
+        # a checksum-only batch in the same frame region, after the segments' frames
+        tail = pktgen.tcp4_frames(2, payload=100, stride=2048, seed=99)
+        hf.array[fr.size:fr.size + tail.size] = tail[:4096]
+        tail_ref = tail.copy()
+        oracle.tcp4_batch(tail_ref, 2, stride=2048, inplace=True)
+        xsum.register_frames(14, hf.addr, hf.nbytes)
+        xsum.register_shm(14, hs.addr, sl)
+        xsum.use_server(14)
+        bad = segs[:1].copy()
+        bad["frame_off"] += 8
+        with pytest.raises(xsum.TasxError):
+            xsum.server_tx_segments(14, bad)
+        tickets = []
+        for b in range(0, n, 32):
+            tickets.append(xsum.server_tx_segments(14, segs[b:b + 32]))
+            if b == 32:
+                for i in range(2):
+                    xsum.tcp_checksums(14, hf.addr + fr.size + i * 2048)
+                tickets.append(xsum.flush_submit(14))
+        assert tickets == sorted(tickets) and len(set(tickets)) == len(tickets)
+        xsum.flush_wait(14, tickets[-1])
+        np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
+        np.testing.assert_array_equal(hf.array[fr.size:fr.size + 4096], tail_ref[:4096])
+        assert xsum.server_flushes(14) == 3 * 3 + 1
+        xsum.use_server(14, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        try:
+            xsum.server_stop(0)
+        except xsum.TasxError:
+            pass
