@@ -1089,8 +1089,11 @@ def fastpath_mt_leg(flushes: int = 3000) -> dict:
     half 1514-B data segments and half 66-B ACKs, with up to `in flight`
     batches out.  Per-context launches, the shared feeder and the persistent
     flush server at 1 thread x 1 in flight (latency), 8 x 3 and 8 x 7
-    (throughput).  The server's in-place fields of thread 0's last batches are
-    compared with the device-resident batch kernel on the same frames."""
+    (throughput); then the fused TX segment build through the server
+    (tasx_server_tx_segments: 32 segments of 1448 B per flush, payload gathered
+    from pinned TX buffers), the same shapes.  The server's in-place fields of
+    thread 0's last batches are compared with the device-resident batch kernel
+    on the same frames."""
     dev = torch.cuda.current_device()
     res = {"unit": "frames/s, us", "frames_per_flush": 32,
            "note": "latency_us from the submit call's return, latency_from_submit_us from its start (a "
@@ -1106,6 +1109,9 @@ def fastpath_mt_leg(flushes: int = 3000) -> dict:
             res[f"{mode}_{th}x{q}"] = r
             if kp is not None:
                 keep = kp
+    # the fused TX segment build (payload copy + checksums) handed to the server
+    for th, q in ((1, 1), (8, 3), (8, 7)):
+        res[f"txseg_server_{th}x{q}"] = benchloop.txseg_server_mt(dev, 8, th, q, flushes)
     n = len(keep) // STRIDE
     dres = xsum.tcp4_cksum_batch(torch.from_numpy(keep.copy()).cuda(), n, stride=STRIDE)
     torch.cuda.synchronize()

@@ -72,6 +72,9 @@ def lib() -> ctypes.CDLL:
                                        ctypes.POINTER(ctypes.c_double)]
         L.tasxb_fastpath_mt.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double), _vp, ctypes.c_size_t]
+        L.tasxb_txseg_server_mt.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_double)]
+        L.tasxb_txseg_server_mt.restype = ctypes.c_int
         for f in (L.tasxb_tcp4_loop, L.tasxb_raw_loop, L.tasxb_txseg_loop, L.tasxb_flow_loop, L.tasxb_rx_loop,
                   L.tasxb_flush_loop, L.tasxb_fastpath_mt):
             f.restype = ctypes.c_int
@@ -132,3 +135,17 @@ def fastpath_mt(device: int, ctx0: int, threads: int, inflight: int, flushes: in
         raise xsum.TasxError(rc, "tasxb_fastpath_mt")
     return {"frames_per_s": float(out[0]), "latency_us": round(float(out[1]), 2),
             "latency_from_submit_us": round(float(out[2]), 2), "core_us_per_flush": round(float(out[3]), 3)}
+
+
+def txseg_server_mt(device: int, ctx0: int, threads: int, inflight: int, flushes: int) -> dict:
+    """The fused TX segment build through the flush server from `threads`
+    fast-path threads, 32 segments (1448-B payloads) per flush
+    (tasxb_txseg_server_mt): segments/s, median latency and core time."""
+    import numpy as np
+    out = np.zeros(4, np.float64)
+    rc = lib().tasxb_txseg_server_mt(device, ctx0, threads, inflight, flushes,
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    if rc:
+        raise xsum.TasxError(rc, "tasxb_txseg_server_mt")
+    return {"segments_per_s": round(float(out[0])), "latency_us": round(float(out[1]), 2),
+            "core_us_per_flush": round(float(out[3]), 3)}

@@ -229,6 +229,7 @@ int tasxb_flush_loop(unsigned ctx, uint8_t *base, uint64_t stride, uint32_t n, i
 
 struct mt_thr {
   unsigned ctx, nslot, inflight;
+  const tasx_tx_seg *segs; /* TX segment mode: MT_BATCH descriptors per slot */
   int inited; /* tasx_ctx_init succeeded: destroyed at the end */
   uint8_t *pool;
   int flushes, n, err;
@@ -275,14 +276,23 @@ static void *mt_worker(void *arg)
       qh++, qn--;
     }
     const double t0 = tasxb_now_us();
-    for (unsigned i = 0; i < MT_BATCH && !T->err; i++)
-      if (tasx_tcp_checksums(TASX_CTX_SELF, NULL, slot + (size_t) i * MT_STRIDE, 0, 0, 0) != 0)
-        T->err = 3;
     uint32_t tk;
-    const double tsub = tasxb_now_us();
-    if (T->err || tasx_flush_submit(TASX_CTX_SELF, &tk) != 0) {
-      T->err = T->err ? T->err : 4;
-      break;
+    double tsub;
+    if (T->segs) { /* the whole batch's build (payload copy + checksums) to the server */
+      tsub = t0;
+      if (tasx_server_tx_segments(TASX_CTX_SELF, T->segs + (size_t) (b % T->nslot) * MT_BATCH, MT_BATCH, &tk) != 0) {
+        T->err = 8;
+        break;
+      }
+    } else {
+      for (unsigned i = 0; i < MT_BATCH && !T->err; i++)
+        if (tasx_tcp_checksums(TASX_CTX_SELF, NULL, slot + (size_t) i * MT_STRIDE, 0, 0, 0) != 0)
+          T->err = 3;
+      tsub = tasxb_now_us();
+      if (T->err || tasx_flush_submit(TASX_CTX_SELF, &tk) != 0) {
+        T->err = T->err ? T->err : 4;
+        break;
+      }
     }
     const double ts = tasxb_now_us();
     q[(qh + qn) % MT_MAXQ] = tk, qt[(qh + qn) % MT_MAXQ] = ts, qs[(qh + qn) % MT_MAXQ] = tsub, qn++;
@@ -427,6 +437,134 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
       tasx_ctx_destroy(T[k].ctx);
     if (T[k].pool)
       tasx_host_free(T[k].pool);
+    free(T[k].lat);
+    free(T[k].lat2);
+    free(T[k].core);
+  }
+  return rc;
+}
+
+/* The fused TX segment build through the flush server from several fast-path
+ * threads (bench.py's `txseg_server_mt`): thread k on context ctx0 + k, a
+ * pinned mbuf pool of slots of 32 frames (headers filled: 1514-B data
+ * segments) and a pinned shared-memory region of 32 flows' 16 KiB circular TX
+ * buffers; per flush tasx_server_tx_segments(32 descriptors) -- payload copy
+ * and both checksums on the GPU over PCIe -- then the polls and waits of the
+ * loop above.  out[] as tasxb_fastpath_mt (out[0] in segments/s, out[2] =
+ * out[1]: the submit call is the whole hand-over). */
+#define MT_FLOWS 32u
+#define MT_TXLEN 16384u
+
+int tasxb_txseg_server_mt(int device, unsigned ctx0, int threads, unsigned inflight, int flushes, double *out)
+{
+  if (threads < 1 || threads > MT_MAXT || inflight < 1 || inflight > MT_MAXQ - 1 || flushes < 1 ||
+      ctx0 + (unsigned) threads > TASX_MAX_CTX)
+    return -22;
+  struct mt_thr T[MT_MAXT];
+  uint8_t *shm[MT_MAXT];
+  tasx_tx_seg *segs[MT_MAXT];
+  pthread_t th[MT_MAXT];
+  int go = 0, rc = 0, started = 0;
+  const unsigned nslot = inflight + 1;
+  const size_t pool_bytes = (size_t) nslot * MT_BATCH * MT_STRIDE, shm_bytes = (size_t) MT_FLOWS * MT_TXLEN;
+  memset(T, 0, sizeof(T));
+  memset(shm, 0, sizeof(shm));
+  memset(segs, 0, sizeof(segs));
+  for (int k = 0; k < threads && !rc; k++) {
+    T[k].ctx = ctx0 + (unsigned) k, T[k].nslot = nslot, T[k].inflight = inflight, T[k].flushes = flushes;
+    T[k].pool = tasx_host_alloc(pool_bytes);
+    shm[k] = tasx_host_alloc(shm_bytes);
+    segs[k] = malloc(sizeof(tasx_tx_seg) * nslot * MT_BATCH);
+    T[k].lat = malloc(sizeof(double) * (size_t) flushes);
+    T[k].lat2 = malloc(sizeof(double) * (size_t) flushes);
+    T[k].core = malloc(sizeof(double) * (size_t) flushes);
+    if (!T[k].pool || !shm[k] || !segs[k] || !T[k].lat || !T[k].lat2 || !T[k].core) {
+      rc = -12;
+      break;
+    }
+    uint64_t r = 300 + (uint64_t) k;
+    memset(T[k].pool, 0, pool_bytes);
+    for (unsigned i = 0; i < nslot * MT_BATCH; i++) /* headers (the payload bytes are the build's) */
+      mt_frame(T[k].pool + (size_t) i * MT_STRIDE, 0, &r);
+    for (size_t i = 0; i < shm_bytes; i++) {
+      r = r * 6364136223846793005ull + 1442695040888963407ull;
+      shm[k][i] = (uint8_t) (r >> 56);
+    }
+    for (unsigned i = 0; i < nslot * MT_BATCH; i++) {
+      tasx_tx_seg *g = &segs[k][i];
+      g->frame_off = (uint64_t) i * MT_STRIDE;
+      g->tx_base = (uint64_t) (i % MT_FLOWS) * MT_TXLEN;
+      g->tx_len = MT_TXLEN;
+      g->pos = (i * 1448u + 77u * (i / MT_FLOWS)) % MT_TXLEN; /* wraps included */
+      g->payload = 1448;
+      g->hdrs_len = 66;
+      g->room = MT_STRIDE;
+    }
+    T[k].segs = segs[k];
+    if ((rc = tasx_ctx_init(T[k].ctx, device, 4u << 20)) != 0)
+      break;
+    T[k].inited = 1;
+    if ((rc = tasx_ctx_register_frames(T[k].ctx, T[k].pool, pool_bytes)) != 0 ||
+        (rc = tasx_ctx_register_shm(T[k].ctx, shm[k], shm_bytes)) != 0)
+      break;
+  }
+  if (!rc && (rc = tasx_server_start(device)) == 0)
+    started = 1;
+  for (int k = 0; k < threads && !rc; k++)
+    rc = tasx_ctx_use_server(T[k].ctx, 1);
+  double wall = 0.0;
+  if (!rc) {
+    int k;
+    for (k = 0; k < threads; k++) {
+      T[k].go = &go;
+      if (pthread_create(&th[k], NULL, mt_worker, &T[k]) != 0)
+        break;
+    }
+    const double t0 = tasxb_now_us();
+    __atomic_store_n(&go, k == threads ? 1 : 2, __ATOMIC_RELEASE);
+    for (int j = 0; j < k; j++)
+      pthread_join(th[j], NULL);
+    wall = tasxb_now_us() - t0;
+    if (k < threads)
+      rc = -11;
+  }
+  for (int k = 0; k < threads && !rc; k++)
+    if (T[k].err)
+      rc = -1000 - T[k].err;
+  if (!rc) {
+    size_t total = 0;
+    for (int k = 0; k < threads; k++)
+      total += (size_t) T[k].n;
+    double *all = malloc(sizeof(double) * total), *core = malloc(sizeof(double) * (size_t) threads * flushes);
+    if (all && core) {
+      size_t o = 0;
+      for (int k = 0; k < threads; k++) {
+        memcpy(all + o, T[k].lat, sizeof(double) * (size_t) T[k].n);
+        memcpy(core + (size_t) k * flushes, T[k].core, sizeof(double) * (size_t) flushes);
+        o += (size_t) T[k].n;
+      }
+      out[0] = (double) threads * flushes * MT_BATCH / (wall * 1e-6);
+      out[1] = out[2] = mt_median(all, total);
+      out[3] = mt_median(core, (size_t) threads * (size_t) flushes);
+    } else {
+      rc = -12;
+    }
+    free(all);
+    free(core);
+  }
+  for (int k = 0; k < threads; k++)
+    if (T[k].inited)
+      tasx_ctx_use_server(T[k].ctx, 0);
+  if (started)
+    tasx_server_stop(device);
+  for (int k = 0; k < threads; k++) {
+    if (T[k].inited)
+      tasx_ctx_destroy(T[k].ctx);
+    if (T[k].pool)
+      tasx_host_free(T[k].pool);
+    if (shm[k])
+      tasx_host_free(shm[k]);
+    free(segs[k]);
     free(T[k].lat);
     free(T[k].lat2);
     free(T[k].core);
