@@ -444,9 +444,12 @@ class TxSegWorkload:
         t = orc.bench_tx_segment(shm, self.shm_len, frames, self.segs_np, threads=threads, reps=1)
         reps = max(3, min(500, int(budget_s / max(t, 1e-6))))
         t = orc.bench_tx_segment(shm, self.shm_len, frames, self.segs_np, threads=threads, reps=reps)
+        # one core (what a TAS fast-path core pays per segment: the copy and the checksums)
+        t1 = orc.bench_tx_segment(shm, self.shm_len, frames, self.segs_np, threads=1, reps=3)
         return {"value": self.bytes_per_step / t / GIB, "unit": "GiB/s", "cores": threads, "kind": "port",
                 "sample": f"rotation 0's {self.n} segments, oracle flow_tx_read + tcp_checksums per segment, "
                           f"median of {reps} passes",
+                "single_core_us_per_segment": round(t1 / self.n * 1e6, 4),
                 "parity_vs_gpu": "bit-exact" if np.array_equal(frames, gpu_frames) else "MISMATCH"}
 
 
