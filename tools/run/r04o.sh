@@ -8,4 +8,12 @@ python3 -c "
 import json
 for l in open('$O/time.jsonl'):
     d=json.loads(l); print(d['tag'], d['rep'], d['us'], d['kernel'])"
+timeout -k 10 420 python bench.py > $O/bench.log 2>&1 || { echo "bench failed"; tail -30 $O/bench.log; exit 1; }
+python3 -c "
+import json
+for l in open('$O/bench.log'):
+    if l.startswith('{\"metric'):
+        d=json.loads(l); fm=d['e2e']['fastpath_mt']
+        print(d['value'], d['roofline']['frac'], d['tx_segment']['cpu_baseline'].get('single_core_us_per_segment'))
+        for k,v in fm.items(): print(k, v)"
 echo done
