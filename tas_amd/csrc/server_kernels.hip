@@ -34,7 +34,7 @@
 //
 // Exit: every wave of every workgroup leaves when the host sets the stop word,
 // or when the lease word has not changed for lease_ticks of the GPU's wall
-// clock (the host's keepalive thread bumps it every 50 ms while the server is
+// clock (the host's keepalive thread bumps it every 10 ms while the server is
 // started, so this only ends a server whose process is gone).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
