@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
     const bool seg = (h0 & TASX_SRV_SEG) != 0u;
-    const uint32_t n = (uint32_t) (h0 & 0x7fffu), words = seg ? 2u + 4u * n : n;
+    const uint32_t n = (uint32_t) (h0 & 0x7fffu), words = seg ? TASX_SRV_SEGW0 + 3u * n : n;
     const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= (seg ? TASX_SRV_SEGS : TASX_SRV_FB);
     // a header-only read never takes the slot: unread entries (0) would match
     // the tag of every position p with p + 1 = 0 mod 2^16
@@ -287,10 +287,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // app's TX buffer into the frame, both checksums stored): the general
       // row of the TX segment build (txseg_device.h), over PCIe both ways
       if (row < s_n) {
-        const uint64_t w0 = s_w[2 + 4 * row], w1 = s_w[3 + 4 * row], w2 = s_w[4 + 4 * row], w3 = s_w[5 + 4 * row];
-        const uint32_t room16 = (uint32_t) (w2 >> 32) & 0xffffu;
-        const u32x4 d0 = u32x4{(uint32_t) w0, 0u, (uint32_t) w2, 0u};
-        const u32x4 d1 = u32x4{(uint32_t) w3, (uint32_t) w1, ((uint32_t) (w0 >> 32) & 0xffffu) | ((uint32_t) (w1 >> 32) << 16),
+        const uint64_t wa = s_w[TASX_SRV_SEGW0 + 3 * row], wb = s_w[TASX_SRV_SEGW0 + 1 + 3 * row],
+                       wc = s_w[TASX_SRV_SEGW0 + 2 + 3 * row];
+        const uint32_t hl = (uint32_t) s_w[2] & 0xffffu, room16 = (uint32_t) (s_w[2] >> 16) & 0xffffu;
+        const uint32_t tx_len = ((uint32_t) (wb >> 32) & 0xffffu) | (((uint32_t) (wc >> 32) & 0xffffu) << 16);
+        const u32x4 d0 = u32x4{(uint32_t) wa, 0u, (uint32_t) wc, 0u};
+        const u32x4 d1 = u32x4{tx_len, (uint32_t) wb, ((uint32_t) (wa >> 32) & 0xffffu) | (hl << 16),
                                (room16 & 0x7fffu) | ((room16 & 0x8000u) ? 0x80000000u : 0u)};
         tasx_txseg_params tp;
         tp.shm = (const uint8_t *) (uintptr_t) (s_w[0] & 0xffffffffffffull);

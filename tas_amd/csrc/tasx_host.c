@@ -2236,7 +2236,8 @@ static int server_submit(struct tasx_ctx *c)
 
 /* TX segment batches through the server: validated up front (nothing is
  * submitted unless every segment is safe to build in place), then packed
- * TASX_SRV_SEGS to a slot (tasx_kernels.h) */
+ * up to TASX_SRV_SEGS to a slot, consecutive segments with one hdrs_len and
+ * room sharing it (tasx_kernels.h) */
 int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n, uint32_t *ticket)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
@@ -2273,8 +2274,12 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     return rc;
   struct fserver *S = c->sv;
   const unsigned id = (unsigned) (c - g_ctx);
-  for (uint32_t i0 = 0; i0 < n; i0 += TASX_SRV_SEGS) {
-    const uint32_t cnt = n - i0 < TASX_SRV_SEGS ? n - i0 : TASX_SRV_SEGS;
+  for (uint32_t i0 = 0; i0 < n;) {
+    /* a slot: up to TASX_SRV_SEGS consecutive segments with one hdrs_len and room */
+    uint32_t cnt = 1;
+    while (i0 + cnt < n && cnt < TASX_SRV_SEGS && segs[i0 + cnt].hdrs_len == segs[i0].hdrs_len &&
+           segs[i0 + cnt].room == segs[i0].room)
+      cnt++;
     uint32_t k = 0;
     while (c->sv_pos - c->sv_done_pos >= TASX_SRV_RING) {
       server_reap(c);
@@ -2285,17 +2290,19 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     const uint64_t tag = (uint64_t) ((pos + 1u) & 0xffffu) << 48;
     uint64_t *slot = (uint64_t *) (S->h_ring + TASX_SRV_SLOTP(id, pos));
     uint64_t *e = slot + TASX_SRV_HDR / 8;
+    const tasx_tx_seg *g0 = &segs[i0];
+    const uint32_t room16 = (g0->room & 0x7fffu) | ((g0->room & TASX_TXSEG_SCRATCH) ? 0x8000u : 0u);
     e[0] = (uint64_t) (uintptr_t) c->shm_dev | tag;
     e[1] = (uint64_t) (uint32_t) c->shm_bytes | (uint64_t) ip_off << 32 | (uint64_t) l4_off << 40 | tag;
+    e[2] = (uint64_t) g0->hdrs_len | (uint64_t) room16 << 16 | tag;
     for (uint32_t j = 0; j < cnt; j++) {
       const tasx_tx_seg *g = &segs[i0 + j];
-      const uint32_t room16 = (g->room & 0x7fffu) | ((g->room & TASX_TXSEG_SCRATCH) ? 0x8000u : 0u);
-      e[2 + 4 * j] = (uint32_t) g->frame_off | (uint64_t) g->payload << 32 | tag;
-      e[3 + 4 * j] = g->pos | (uint64_t) g->hdrs_len << 32 | tag;
-      e[4 + 4 * j] = (uint32_t) g->tx_base | (uint64_t) room16 << 32 | tag;
-      e[5 + 4 * j] = g->tx_len | tag;
+      uint64_t *w = e + TASX_SRV_SEGW0 + 3 * j;
+      w[0] = (uint32_t) g->frame_off | (uint64_t) g->payload << 32 | tag;
+      w[1] = g->pos | (uint64_t) (g->tx_len & 0xffffu) << 32 | tag;
+      w[2] = (uint32_t) g->tx_base | (uint64_t) (g->tx_len >> 16) << 32 | tag;
     }
-    for (uint32_t w = 2 + 4 * cnt; w < TASX_SRV_FB; w++) /* every entry word tagged (server_submit) */
+    for (uint32_t w = TASX_SRV_SEGW0 + 3 * cnt; w < TASX_SRV_FB; w++) /* every entry word tagged (server_submit) */
       e[w] = tag;
     const uintptr_t b16 = (uintptr_t) c->zc_dev;
     __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
@@ -2309,6 +2316,7 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     c->n_server_flushes++;
     __atomic_store_n(&c->sv_batches, c->sv_batches + 1u, __ATOMIC_RELAXED);
     __atomic_store_n(&c->sv_frames, c->sv_frames + cnt, __ATOMIC_RELAXED);
+    i0 += cnt;
   }
   if (ticket)
     *ticket = c->next_ticket;

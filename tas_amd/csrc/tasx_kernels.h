@@ -105,13 +105,15 @@ typedef struct tasx_flow_params {
  * Workgroup k of ring r's P.k takes its positions p = k mod P.k. */
 #define TASX_SRV_RING 8u   /* slots per ring */
 /* TX segment slots (tasx_server_tx_segments): h0's n field | TASX_SRV_SEG, at
- * most TASX_SRV_SEGS segments; entry 0 = shm device address (48 bits) | tag,
- * entry 1 = shm_len (32) | ip_off << 32 | l4_off << 40 | tag, then per segment
- * 4 entries: frame_off (32) | payload << 32, pos (32) | hdrs_len << 32,
- * tx_base (32) | room16 << 32 (room & 0x7fff, bit 15 = TASX_TXSEG_SCRATCH),
- * tx_len (32); each | tag << 48 */
+ * most TASX_SRV_SEGS segments sharing one hdrs_len and room; entry 0 = shm
+ * device address (48 bits), entry 1 = shm_len (32) | ip_off << 32 | l4_off <<
+ * 40, entry 2 = hdrs_len | room16 << 16 (room & 0x7fff, bit 15 =
+ * TASX_TXSEG_SCRATCH), then per segment 3 entries: frame_off (32) | payload
+ * << 32, pos (32) | (tx_len & 0xffff) << 32, tx_base (32) | (tx_len >> 16) <<
+ * 32; every entry | tag << 48 */
 #define TASX_SRV_SEG 0x8000u
-#define TASX_SRV_SEGS 15u
+#define TASX_SRV_SEGS 20u
+#define TASX_SRV_SEGW0 3u /* entry of segment 0's first word */
 #define TASX_SRV_FB 64u    /* frames per slot */
 #define TASX_SRV_KMAX 8u   /* workgroups per ring, a divisor of TASX_SRV_RING */
 #define TASX_SRV_SLOT 1024u

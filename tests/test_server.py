@@ -476,7 +476,7 @@ def test_server_tx_segments(oracle, odd):
     SURVEY 8f rows 1 + 2 at TAS's batch size): payloads gathered from the
     app's TX buffers in pinned host memory (wraps of the circular buffers,
     odd buffer bases and lengths), written into the mbufs and both checksums
-    stored, 32 segments per flush (three ring slots each), against the oracle's
+    stored, 32 segments per flush (two ring slots each), against the oracle's
     flow_tx_read + tcp_checksums; interleaved with checksum-only flushes of
     the same context (ticket order); a descriptor the host refuses (frame not
     16-byte aligned) submits nothing; dma_read-invalid ones (payload beyond
@@ -521,7 +521,7 @@ def test_server_tx_segments(oracle, odd):
         xsum.flush_wait(14, tickets[-1])
         np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
         np.testing.assert_array_equal(hf.array[fr.size:fr.size + 4096], tail_ref[:4096])
-        assert xsum.server_flushes(14) == 3 * 3 + 1
+        assert xsum.server_flushes(14) == 3 * 2 + 1     # 32 segments: two slots (20 + 12)
         xsum.use_server(14, False)
         xsum.server_stop(0)
     finally:
