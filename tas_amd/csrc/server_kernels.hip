@@ -23,14 +23,20 @@
 // acquire, tests/test_server.py::test_server_refilled_mbufs_every_flush
 // fails; with system-scope frame loads instead (round 4's first server) the
 // server tops out at 14-19 M frames/s from 8 cores, against 24-28 this way
-// (profiles/r04/r04g).  The two checksum fields are written by sc0 sc1
-// stores (write-through to host memory).  Each wave waits
-// for its stores (vmcnt(0)), the workgroup meets at a barrier, and only then
-// does one lane store the slot's done word, also sc0 sc1: the host sees the
-// word after the fields.  Descriptor words carry the 16-bit tag of their ring
-// position, so a slot read over PCIe while the host was still writing it is
-// recognised (a word with an older tag) and read again -- no separate
-// doorbell round trip.
+// (profiles/r04/r04g; 42-48 in the bench lines of round 4's last passes).
+// The two checksum fields are written by sc0 sc1 stores (write-through to host
+// memory).  Each wave waits for its stores (vmcnt(0)), the workgroup meets at
+// a barrier, and only then does one lane store the slot's done word, also sc0
+// sc1: the host sees the word after the fields.  Descriptor words carry the
+// 16-bit tag of their ring position (every entry word of a slot, used or not,
+// is rewritten per submit), so a slot read over PCIe while the host was still
+// writing it is recognised (a word with an older tag) and read again -- no
+// separate doorbell round trip.
+//
+// TX segment slots (TASX_SRV_SEG, tasx_server_tx_segments): the rows run the
+// general TX segment row (txseg_device.h) -- payload gathered from the app's
+// TX buffer into the frame, both checksums -- with plain stores, and one lane
+// issues a system-scope release (buffer_wbl2 sc0 sc1) before the done word.
 //
 // Exit: every wave of every workgroup leaves when the host sets the stop word,
 // or when the lease word has not changed for lease_ticks of the GPU's wall
