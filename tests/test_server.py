@@ -470,12 +470,13 @@ def test_server_stop_is_bounded_and_restarts(oracle):
             pass
 
 
-@pytest.mark.parametrize("odd", [False, True])
-def test_server_tx_segments(oracle, odd):
+@pytest.mark.parametrize("odd,shm_mem", [(False, "host_alloc"), (True, "host_alloc"), (True, "registered")])
+def test_server_tx_segments(oracle, odd, shm_mem):
     """The fused TX segment build through the server (tasx_server_tx_segments,
     SURVEY 8f rows 1 + 2 at TAS's batch size): payloads gathered from the
-    app's TX buffers in pinned host memory (wraps of the circular buffers,
-    odd buffer bases and lengths), written into the mbufs and both checksums
+    app's TX buffers in pinned host memory (tasx_host_alloc, or plain pages
+    pinned by tasx_ctx_register_shm; wraps of the circular buffers, odd buffer
+    bases and lengths), written into the mbufs and both checksums
     stored, 32 segments per flush (two ring slots each), against the oracle's
     flow_tx_read + tcp_checksums; interleaved with checksum-only flushes of
     the same context (ticket order); a descriptor the host refuses (frame not
@@ -492,10 +493,17 @@ def test_server_tx_segments(oracle, odd):
     xsum.server_start(0)
     cx = _Ctxs([14])
     try:
-        hs = xsum.PinnedBuffer(sl + 64)
         hf = xsum.PinnedBuffer(fr.size + 4096)
-        cx.pins += [hs, hf]
-        hs.array[:sl] = shm[:sl]
+        cx.pins.append(hf)
+        if shm_mem == "host_alloc":
+            hs = xsum.PinnedBuffer(sl + 64)
+            cx.pins.append(hs)
+            shm_arr, shm_addr = hs.array, hs.addr
+        else:  # plain pages, pinned by tasx_ctx_register_shm (hipHostRegister), as TAS's tas_shm would be
+            raw_shm = np.zeros(sl + 8192, np.uint8)
+            o = (-raw_shm.ctypes.data) % 4096
+            shm_arr, shm_addr = raw_shm[o:o + sl + 64], raw_shm.ctypes.data + o
+        shm_arr[:sl] = shm[:sl]
         hf.array[:] = 0
         hf.array[:fr.size] = fr
         # a checksum-only batch in the same frame region, after the segments' frames
@@ -504,7 +512,7 @@ def test_server_tx_segments(oracle, odd):
         tail_ref = tail.copy()
         oracle.tcp4_batch(tail_ref, 2, stride=2048, inplace=True)
         xsum.register_frames(14, hf.addr, hf.nbytes)
-        xsum.register_shm(14, hs.addr, sl)
+        xsum.register_shm(14, shm_addr, sl)
         xsum.use_server(14)
         bad = segs[:1].copy()
         bad["frame_off"] += 8
