@@ -349,7 +349,11 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
+#ifdef TASX_AB
+      if (s_seg && P.fpol != 12u) // A/B 12: no release (what the write-back costs; frames may lag the done word)
+#else
       if (s_seg) // the TX build's plain stores: every dirty line out of the L2 before the done word
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       if (s_bad) { // sticky in the ring's line: a frame changed after submission (or a malformed slot)
         st_sys32(dline + TASX_SRV_ERRW, 1u);
