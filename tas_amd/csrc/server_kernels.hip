@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 #ifdef TASX_AB
       if (st == 1 && P.fpol == 11u) // A/B 11: an agent-scope acquire instead (buffer_inv sc1)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
+      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || P.fpol == 12u || (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
 #else
       if (st == 1)
 #endif
