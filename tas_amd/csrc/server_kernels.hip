@@ -278,7 +278,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 #ifdef TASX_AB
       if (st == 1 && P.fpol == 11u) // A/B 11: an agent-scope acquire instead (buffer_inv sc1)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || P.fpol == 12u || (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
+      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || P.fpol == 12u || P.fpol == 13u ||
+                      (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
 #else
       if (st == 1)
 #endif
@@ -310,7 +311,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         tp.ip_off = (uint32_t) (s_w[1] >> 32) & 0xffu;
         tp.l4_off = (uint32_t) (s_w[1] >> 40) & 0xffu;
         tp.dbg = 0u;
-        txseg_row_d<3, false>(tp, row, d0, d1, gl);
+#ifdef TASX_AB
+        if (P.fpol == 13u) // A/B 13: write-through stores, no release
+          txseg_row_d<3, false, true>(tp, row, d0, d1, gl);
+        else
+#endif
+          txseg_row_d<3, false>(tp, row, d0, d1, gl);
       }
     } else if (row < s_n) {
       const uint64_t base = s_base;
@@ -350,7 +356,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     __syncthreads();
     if (threadIdx.x == 0) {
 #ifdef TASX_AB
-      if (s_seg && P.fpol != 12u) // A/B 12: no release (what the write-back costs; frames may lag the done word)
+      if (s_seg && P.fpol != 12u && P.fpol != 13u) // A/B 12: no release (what the write-back costs; frames may
+                                                   // lag the done word); 13: write-through stores instead
 #else
       if (s_seg) // the TX build's plain stores: every dirty line out of the L2 before the done word
 #endif

@@ -21,6 +21,44 @@ __device__ __forceinline__ u32x4 put_byte(u32x4 v, int b, uint32_t x)
 // store bytes [lo, hi) of v into the 16-byte aligned chunk at cp: whole
 // dwords as dword stores, the rest as byte stores (constant offsets from one
 // address)
+// write-through (sc0 sc1) vector stores: they reach host memory without an
+// L2 write-back (the flush server's TX segment slots, A/B 13)
+__device__ __forceinline__ void wt_store16(uint8_t *p, u32x4 v)
+{
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void wt_store4(uint8_t *p, uint32_t v)
+{
+  asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void wt_store1(uint8_t *p, uint32_t v)
+{
+  asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// store_range with write-through stores
+__device__ __forceinline__ void store_range_wt(uint8_t *cp, u32x4 v, int lo, int hi)
+{
+  if (lo >= hi)
+    return;
+  if (lo == 0 && hi == 16) {
+    wt_store16(cp, v);
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (lo <= 4 * j && 4 * j + 4 <= hi) {
+      wt_store4(cp + 4 * j, w[j]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * j + q >= lo && 4 * j + q < hi)
+          wt_store1(cp + 4 * j + q, w[j] >> (8 * q));
+    }
+  }
+}
+
 __device__ __forceinline__ void store_range(uint8_t *cp, u32x4 v, int lo, int hi, bool nt = true)
 {
   if (lo >= hi)
@@ -97,7 +135,7 @@ __device__ __noinline__ u32x4 gather16(const uint8_t *shm, uint32_t off, uint64_
 // The descriptor (tasx_tx_seg, two 16-byte words) is passed in: txseg_row
 // below loads it from p.segs; the flush server (server_kernels.hip) decodes it
 // from its ring slot.
-template <int U, bool NTS>
+template <int U, bool NTS, bool WT = false>
 __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t i, u32x4 d0, u32x4 d1, int gl)
 {
   const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
@@ -165,7 +203,9 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
       const bool in = k >= nhc && k < kpay && k != ks;
       if (in) {
         uint8_t *const cp = c0 + 16 * k;
-        if (NTS)
+        if (WT)
+          wt_store16(cp, a[u]);
+        else if (NTS)
           __builtin_nontemporal_store(a[u], (__attribute__((address_space(1))) u32x4 *) cp);
         else
           *(__attribute__((address_space(1))) u32x4 *) cp = a[u];
@@ -220,7 +260,10 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
     if (b < 16 && k < nhc)
       vh = v; // written back with the checksums at the end
     else
-      store_range(c0 + 16 * k, v, max(-o, 0), min(fend - o, 16), false);
+      if (WT)
+        store_range_wt(c0 + 16 * k, v, max(-o, 0), min(fend - o, 16));
+      else
+        store_range(c0 + 16 * k, v, max(-o, 0), min(fend - o, 16), false);
   }
   uint32_t part = acc;
   if (sum_end > fend) { // total_length reaches past the frame's written bytes
@@ -249,7 +292,10 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
     v = put_byte(v, fi + 1 - b0, res >> 8);
     v = put_byte(v, ck - b0, res >> 16);
     v = put_byte(v, ck + 1 - b0, res >> 24);
-    store_range(c0 + b0, v, max(fh - b0, 0), min(fh + fend - b0, 16), false);
+    if (WT)
+      store_range_wt(c0 + b0, v, max(fh - b0, 0), min(fh + fend - b0, 16));
+    else
+      store_range(c0 + b0, v, max(fh - b0, 0), min(fh + fend - b0, 16), false);
   }
 }
 
