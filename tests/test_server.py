@@ -538,3 +538,57 @@ def test_server_tx_segments(oracle, odd, shm_mem):
             xsum.server_stop(0)
         except xsum.TasxError:
             pass
+
+
+def test_server_beside_feeder_and_device_batches(oracle):
+    """The server shares its GPU: one context on the server, one on the shared
+    feeder, and 64K-frame device-resident batches on a torch stream, all
+    running together; every result right.  (The server's per-batch acquire
+    only drops the XCDs' non-coherent L2 lines; the feeder's and the batch
+    kernels' own launch boundaries keep them correct.)"""
+    n = 32
+    dev_n = 65536
+    dframes = torch.from_numpy(pktgen.tcp4_frames(dev_n, stride=2048, seed=4242)).cuda()
+    dref = xsum.tcp4_cksum_batch(dframes, dev_n, stride=2048).cpu().numpy()
+    xsum.server_start(0)
+    xsum.feeder_start(0)
+    cx = _Ctxs([3, 10])
+    try:
+        pins, refs = [], []
+        for k, c in enumerate((3, 10)):
+            pin, frames = _frames(8 * n, 610 + k, short=False)
+            cx.pins.append(pin)
+            pins.append(pin)
+            refs.append(_ref(oracle, frames, 8 * n))
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+        xsum.use_server(3)
+        xsum.use_feeder(10)
+        s = torch.cuda.Stream()
+        outs = []
+        tickets = {3: [], 10: []}
+        for b in range(8):
+            with torch.cuda.stream(s):
+                outs.append(xsum.tcp4_cksum_batch(dframes, dev_n, stride=2048, stream=s))
+            for k, c in enumerate((3, 10)):
+                for i in range(n):
+                    xsum.tcp_checksums(c, pins[k].addr + (b * n + i) * 2048)
+                tickets[c].append(xsum.flush_submit(c))
+        for c in (3, 10):
+            xsum.flush_wait(c, tickets[c][-1])
+        s.synchronize()
+        for k in range(2):
+            np.testing.assert_array_equal(pins[k].array[:refs[k].size], refs[k])
+        assert xsum.server_flushes(3) == 8
+        xsum.use_server(3, False)
+        xsum.use_feeder(10, False)
+        xsum.server_stop(0)   # before any copy back: HIP's synchronous copies may wait for every stream
+        xsum.feeder_stop(0)
+        for o in outs:
+            np.testing.assert_array_equal(o.cpu().numpy(), dref)
+    finally:
+        cx.close()
+        for stop in (xsum.server_stop, xsum.feeder_stop):
+            try:
+                stop(0)
+            except xsum.TasxError:
+                pass
