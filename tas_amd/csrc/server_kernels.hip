@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 #ifdef TASX_AB
       if (st == 1 && P.fpol == 11u) // A/B 11: an agent-scope acquire instead (buffer_inv sc1)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || P.fpol == 12u || P.fpol == 13u ||
+      if (st == 1 && (P.fpol == 0u || P.fpol == 5u || P.fpol == 12u || P.fpol == 13u || P.fpol == 14u ||
                       (P.fpol == 10u && t_act - t_prev <= P.light_ticks)))
 #else
       if (st == 1)
@@ -314,6 +314,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 #ifdef TASX_AB
         if (P.fpol == 13u) // A/B 13: write-through stores, no release
           txseg_row_d<3, false, true>(tp, row, d0, d1, gl);
+        else if (P.fpol == 14u) // A/B 14: non-temporal payload stores, then the release
+          txseg_row_d<3, true>(tp, row, d0, d1, gl);
         else
 #endif
           txseg_row_d<3, false>(tp, row, d0, d1, gl);
