@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 6
+#define TASX_ABI_VERSION 7
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -435,7 +435,7 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     memory (e.g. torch.cuda.empty_cache) blocks until the stop
  *   tasx_server_stats: batches and frames submitted since start
  *   tasx_ctx_server_flushes: batches the context handed to the server */
-/* The fused TX segment build through the flush server (the copy of
+/* (ABI 7) The fused TX segment build through the flush server (the copy of
  * flow_tx_segment's payload from the app's TX buffer plus tcp_checksums,
  * tas/fast/fast_flows.c:930-936, at tx_flush time with no HIP call): the
  * fast-path core fills the headers as now and, instead of dma_read +

@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 6
+    assert L.tasx_abi_version() == 7
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
