@@ -448,7 +448,9 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * frame starts 16-byte aligned, hdrs_len in [54, 240], room below 32 KiB,
  * frames (and their rooms) inside the frame region: else -EINVAL and nothing
  * is submitted.  Descriptors dma_read() would reject leave their frame as it
- * is (tasx_tx_segment_batch_dev).
+ * is (tasx_tx_segment_batch_dev).  Up to 20 segments go in one of the ring's
+ * 8 slots (a run of equal hdrs_len and room); with every slot out, the call
+ * waits inside for the oldest one to finish.
  *   tasx_ctx_register_shm(ctx, shm, bytes): the app's shared-memory region
  *     (pinned and mapped here unless it already is; below 4 GiB) */
 int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes);
