@@ -151,6 +151,17 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 // round trip.  The other 15 waves wait at the barrier meanwhile (no issue
 // slots).  Then row j sums frame j, and thread 0 posts done[p mod RING] =
 // p + 1 after every wave's stores completed.
+// Payload windows per lane in a TX segment row: 6 x 16 lanes x 16 B covers a
+// 1448-byte payload's chunks in one PCIe round trip (3 took two: 15.4-15.5
+// against 16.7-16.9 M segments/s at 8 x 3, 18.5-19.2 against 16.9-17.5 us at
+// 1 x 1, profiles/r04/r04w); 128 VGPRs, no scratch.  The A/B build keeps 3:
+// with its extra forms 6 would spill (48 bytes a lane) into every form
+#ifdef TASX_AB
+constexpr int kSrvTxU = 3;
+#else
+constexpr int kSrvTxU = 6;
+#endif
+
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
           txseg_row_d<3, true>(tp, row, d0, d1, gl);
         else
 #endif
-          txseg_row_d<3, false>(tp, row, d0, d1, gl);
+          txseg_row_d<kSrvTxU, false>(tp, row, d0, d1, gl);
       }
     } else if (row < s_n) {
       const uint64_t base = s_base;
