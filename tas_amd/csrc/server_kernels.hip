@@ -152,9 +152,9 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 // slots).  Then row j sums frame j, and thread 0 posts done[p mod RING] =
 // p + 1 after every wave's stores completed.
 // Payload windows per lane in a TX segment row: 6 x 16 lanes x 16 B covers a
-// 1448-byte payload's chunks in one PCIe round trip (3 took two: 15.4-15.5
-// against 16.7-16.9 M segments/s at 8 x 3, 18.5-19.2 against 16.9-17.5 us at
-// 1 x 1, profiles/r04/r04w); 128 VGPRs, no scratch.  The A/B build keeps 3:
+// 1448-byte payload's chunks in one PCIe round trip (3 took two: 15.5-15.8
+// against 16.5-16.6 M segments/s at 8 x 3, 18.6-19.6 against 16.8-17.8 us at
+// 1 x 1, profiles/r04/r04z); 128 VGPRs, no scratch.  The A/B build keeps 3:
 // with its extra forms 6 would spill (48 bytes a lane) into every form
 #ifdef TASX_AB
 constexpr int kSrvTxU = 3;
