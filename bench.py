@@ -697,16 +697,25 @@ def tcp4_pattern_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200)
                       "residency, words xor-folded instead of summed"}
 
 
-def read_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200) -> dict:
-    """A pure streaming read of the headline's algorithmic bytes per launch,
-    over the same buffer rotation, by both load paths (tasx_ab_stream_read,
-    the A/B build): register loads and LDS-DMA (global_load_lds_dwordx4 nt).
-    The faster is the read ceiling; the pattern ceiling above is the register
-    path, because LDS-DMA is the slower one (profiles/r04/INDEX.md r04a)."""
+# tasx_ab_stream_read paths: 0 register loads in grid order, 1 LDS-DMA, 2 + k
+# register loads with the blocks in XCD runs of 2^k (round 5, xcd_run: runs of
+# 64 read config 4's 12.6 GB fastest, profiles/r05/INDEX.md r05b)
+READ_PATHS = {"register": 0, "lds_dma": 1, "register_xcd64": 8, "register_xcd256": 10}
+
+
+def read_ceiling(wl, avg_us: float, launches: int = 200) -> dict:
+    """A pure streaming read of a leg's algorithmic bytes per launch, over the
+    same buffer rotation (wl.bufs), by each load path of tasx_ab_stream_read
+    (the A/B build): register loads in grid order and in XCD runs, LDS-DMA
+    (global_load_lds_dwordx4 nt).  The fastest is the read ceiling; the pattern
+    ceiling above is the register path, LDS-DMA being the slower one
+    (profiles/r04/INDEX.md r04a).  Launch counts shrink with the size (about
+    0.1 s of reads per path)."""
     ab = xsum._load(xsum.AB_LIB_PATH)
     s = torch.cuda.current_stream().cuda_stream
     R = len(wl.bufs)
-    nbytes = wl.bytes_per_step // 1024 * 1024
+    nbytes = min(wl.bytes_per_step, min(b.numel() for b in wl.bufs)) // 1024 * 1024
+    launches = max(10, min(launches, int(0.1 / (nbytes / 7e12))))
     sink = torch.zeros(1, dtype=torch.int32, device="cuda")
 
     def timed(path: int) -> float:
@@ -714,7 +723,7 @@ def read_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200) -> dict
             rc = ab.tasx_ab_stream_read(wl.bufs[k % R].data_ptr(), nbytes, path, sink.data_ptr(), s)
             if rc:
                 raise xsum.TasxError(rc, "tasx_ab_stream_read")
-        for k in range(20):
+        for k in range(min(20, launches)):
             rd(k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
@@ -724,12 +733,13 @@ def read_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200) -> dict
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3 / launches
-    reg, glds = timed(0), timed(1)
-    us = min(reg, glds)
-    return {"bound": "a pure streaming read of the same bytes", "bytes": nbytes, "register_us": round(reg, 3),
-            "lds_dma_us": round(glds, 3), "us": round(us, 3), "path": "register" if reg <= glds else "lds_dma",
+    per = {name: timed(path) for name, path in READ_PATHS.items()}
+    best = min(per, key=per.get)
+    us = per[best]
+    return {"bound": "a pure streaming read of the same bytes", "bytes": nbytes, "launches": launches,
+            **{f"{k}_us": round(v, 3) for k, v in per.items()}, "us": round(us, 3), "path": best,
             "frac": round(us / avg_us, 4), "achieved_gbs": round(nbytes / us / 1e3, 1),
-            "kernels": "stream_read_reg_kernel / stream_read_glds_kernel (libtasx_ab.so)"}
+            "kernels": "stream_read_reg_kernel (grid order / XCD runs) / stream_read_glds_kernel (libtasx_ab.so)"}
 
 
 def mix_bounds(mw: "FlushMixWorkload", launches: int = 200) -> dict:
@@ -1416,6 +1426,10 @@ def other_workload(args, ws, rank, info):
         desc = "16,384 TSO segments per GPU (ip.len 65535, L4 65,515 B), tcp_checksums() flag-off, hinted"
         scaling = "weak"
     r = leg(run, wl.bytes_per_step, args, ws, desc, kernel)
+    # the leg's own live read ceiling (configs 3-5 carry one too)
+    if rank == 0 and not info.get("rehearse"):
+        torch.cuda.synchronize()
+        r["roofline"]["read_ceiling"] = read_ceiling(wl, r["roofline"]["launch_avg_us"])
     # per-rank accounting: packets, algorithmic bytes, seconds for the K steps
     shards = {"packets": [int(v) for v in gather_over_ranks(float(wl.n), ws)],
               "bytes_per_step": [int(v) for v in gather_over_ranks(float(wl.bytes_per_step), ws)],

@@ -77,10 +77,16 @@ int tasx_ab_stream_copy(const void *src, void *dst, size_t bytes, void *stream);
 /* A pure streaming read of `bytes` (1 KiB multiple, 16-byte aligned) by one of
  * the two load paths (round 4): path 0 register loads (8 KiB per block, two
  * non-temporal 16-byte loads per lane), path 1 LDS-DMA (global_load_lds_dwordx4
- * nt into a 4-slot ring per wave).  bench.py times both beside the headline and
- * reports the faster as its read ceiling.  sink: a device word (never written
- * for real data). */
+ * nt into a 4-slot ring per wave); path 2 + k (round 5): the register path
+ * with the blocks XCD-ordered in runs of 2^k (xcd_run).  bench.py times them
+ * beside each leg and reports the fastest as its read ceiling.  sink: a device
+ * word (never written for real data). */
 int tasx_ab_stream_read(const void *src, size_t bytes, int path, uint32_t *sink, void *stream);
+
+/* XCD order of every grid launch_groups makes (round 5): xrun 0 = grid order,
+ * k > 0 = runs of 2^(k-1) blocks per XCD (xcd_run), -1 = the product's rule
+ * (runs of 256 from 16,384 blocks).  Default: TASX_XRUN, else -1. */
+int tasx_ab_set_xrun(int xrun);
 
 /* The flush server's timing sums for ring r (TASX_SRV_DIAG=1 in the
  * environment at tasx_server_start), in us: out[0] detection -> frames

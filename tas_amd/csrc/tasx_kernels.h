@@ -23,6 +23,7 @@ typedef struct tasx_raw_params {
   uint64_t stride;
   uint32_t len0;
   uint32_t n;
+  uint32_t xrun;         /* XCD-ordered grid (xcd_run), set by the launcher */
 } tasx_raw_params;
 
 typedef struct tasx_tcp4_params {
@@ -56,6 +57,7 @@ typedef struct tasx_tcp4_params {
   uint32_t fs_num;
   uint32_t fs_stride;
   uint32_t fs_key_off;
+  uint32_t xrun;          /* XCD-ordered grid (xcd_run), set by the launcher */
 } tasx_tcp4_params;
 
 typedef struct tasx_txseg_params {

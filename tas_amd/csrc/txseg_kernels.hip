@@ -1138,9 +1138,10 @@ __global__ __launch_bounds__(256) void stream_copy_kernel(const u32x4 *src, u32x
 //   lane (the fastest register shape measured: 15.40 us per 98.3 MB launch)
 //  LDS-DMA: global_load_lds_dwordx4 (nt) into a 4-slot ring of 1 KiB per
 //   wave, 2 blocks per CU, counted vmcnt, ds_read_b128 + v_sad_u16
-__global__ __launch_bounds__(256) void stream_read_reg_kernel(const u32x4 *src, size_t nchunks, uint32_t *sink)
+__global__ __launch_bounds__(256) void stream_read_reg_kernel(const u32x4 *src, size_t nchunks, uint32_t *sink,
+                                                             uint32_t xrun)
 {
-  const size_t c0 = (size_t) blockIdx.x * 512u + threadIdx.x;
+  const size_t c0 = (size_t) xcd_run(blockIdx.x, gridDim.x, xrun) * 512u + threadIdx.x;
   u32x4 a = {0u, 0u, 0u, 0u}, b = a;
   if (c0 < nchunks)
     a = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *) (src + c0));
@@ -1190,14 +1191,14 @@ __global__ __launch_bounds__(256) void stream_read_glds_kernel(const u32x4 *src,
 
 extern "C" int tasx_ab_stream_read(const void *src, size_t bytes, int path, uint32_t *sink, void *stream)
 {
-  if (!src || !sink || (bytes & 1023) || ((uintptr_t) src & 15) || (path != 0 && path != 1))
+  if (!src || !sink || (bytes & 1023) || ((uintptr_t) src & 15) || path < 0 || path > 13)
     return -22;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  if (path == 0)
+  if (path != 1) // 0: grid order; 2 + k: XCD runs of 2^k blocks (xcd_run)
     hipLaunchKernelGGL(stream_read_reg_kernel, dim3((uint32_t) ((bytes / 16 + 511) / 512)), dim3(256), 0,
-                       (hipStream_t) stream, (const u32x4 *) src, bytes / 16, sink);
+                       (hipStream_t) stream, (const u32x4 *) src, bytes / 16, sink, path == 0 ? 0u : (uint32_t) path - 1u);
   else
     hipLaunchKernelGGL(stream_read_glds_kernel, dim3((uint32_t) cus * 2u), dim3(256), 0, (hipStream_t) stream,
                        (const u32x4 *) src, (uint64_t) (bytes / 1024), sink);

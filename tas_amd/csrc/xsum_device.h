@@ -160,6 +160,24 @@ __device__ __forceinline__ uint64_t pkt_offset(const uint64_t *off, uint64_t str
   return off ? ldg(off, i) : (uint64_t) i * stride;
 }
 
+// The logical block of hardware block b in a grid of nb, XCD-ordered: the
+// dispatcher places blocks round-robin over the 8 XCDs (b -> XCD b % 8); in
+// every window of 8 S consecutive blocks (S = 2^(xrun - 1)) XCD x takes the S
+// consecutive logical blocks [x S, x S + S) of the window, in order, so each
+// XCD streams its own contiguous run while the 8 runs stay adjacent.  Blocks
+// past the last whole window, and every block when xrun = 0, keep grid order.
+// A bijection on [0, nb); xrun is uniform (a kernel argument).
+__device__ __forceinline__ uint32_t xcd_run(uint32_t b, uint32_t nb, uint32_t xrun)
+{
+  if (xrun == 0u)
+    return b;
+  const uint32_t sh = xrun - 1u, wmask = (8u << sh) - 1u;
+  if (b >= (nb & ~wmask))
+    return b;
+  const uint32_t o = b & wmask;
+  return (b & ~wmask) + ((o & 7u) << sh) + (o >> 3);
+}
+
 // ---------------------------------------------------------------------------
 // 16-lane packet groups (one DPP row each), one block per 16 packets.
 

@@ -206,12 +206,13 @@ template <int U, bool S32 = false, int G = 16>
 __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
 {
   const int gl = threadIdx.x & (G - 1);
-  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  const uint32_t blk = xcd_run(blockIdx.x, gridDim.x, p.xrun);
+  const uint32_t i = blk * (kBlock / G) + threadIdx.x / G;
   if (i >= p.n)
     return;
   const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
   const uint8_t *s = nullptr;
-  const uint8_t *const bb = p.base + (uint64_t) (blockIdx.x * (kBlock / G)) * p.stride;
+  const uint8_t *const bb = p.base + (uint64_t) (blk * (kBlock / G)) * p.stride;
   uint32_t o0 = 0, head, last;
   if constexpr (S32) {
     const uint32_t so = (threadIdx.x / G) * (uint32_t) p.stride;
@@ -374,7 +375,7 @@ template <int U>
 __global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
 {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
+  const uint32_t i0 = xcd_run(blockIdx.x, gridDim.x, p.xrun) * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
   if (i0 >= p.n) // wave-uniform
     return;
   const uint32_t i = i0 + (lane & 3u);
@@ -587,7 +588,7 @@ template <int U>
 __global__ __launch_bounds__(kBlock) void tcp4_wave_kernel(tasx_tcp4_params p)
 {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t i0 = blockIdx.x * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
+  const uint32_t i0 = xcd_run(blockIdx.x, gridDim.x, p.xrun) * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
   if (i0 >= p.n) // wave-uniform
     return;
   const uint32_t i = i0 + (lane & 3u);
@@ -1103,7 +1104,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX && FLOW != kFlowSplitX2) || !DONE,
                 "split grids post no completion word");
   const int gl = threadIdx.x & 15;
-  uint32_t vb = blockIdx.x; // this block's verify block
+  // this block's verify block (split grids: below); large batches XCD-ordered
+  uint32_t vb = FLOW == kFlowNone ? xcd_run(blockIdx.x, gridDim.x, p.xrun) : blockIdx.x;
   // kFlowRow: CRC32C from slice-by-4 tables the block builds in LDS first (before
   // any row leaves: every wave reaches the barriers; the bitwise CRC cost every
   // verify wave ~300 VALU)
@@ -1556,6 +1558,44 @@ static thread_local const char *t_last_kernel = "";
 // whether the calling thread's last tasx_launch_tcp4 posted p->done_word
 static thread_local int t_posted_done = 0;
 
+// XCD-ordered grids (xcd_run, round 5): from 16,384 blocks (a batch of 256K
+// frames or packets and up) each XCD works through runs of 256 consecutive
+// blocks (6 MB of 1500-byte packets), the 8 runs of a window adjacent.  In grid
+// order the 8 XCDs share every page of the ~30 MB the resident blocks span
+// (26.7K UTCL1 translation misses per 12.6 GB launch, the UTCL2 busy 1.1-1.6M
+// cycles); in runs each XCD's resident blocks lie in two or three 2 MB pages
+// (0-3.7K misses, UTCL2 busy 9K-230K).  8M x 1500 B RAW: 1.74-1.77 ms against
+// 1.87-2.00 (profiles/r05/INDEX.md r05a-r05c); 64K-frame batches (the headline)
+// are neutral to slower in any XCD order and stay in grid order.
+constexpr uint32_t kXrunMinBlocks = 16384u;
+constexpr uint32_t kXrun = 9u; // runs of 2^(9 - 1) = 256 blocks
+
+#ifdef TASX_AB
+// A/B: the xrun of every grid (0 = grid order; -1 = the product's rule), from
+// tasx_ab_set_xrun or TASX_XRUN
+static int g_xrun_ov = -2;
+extern "C" int tasx_ab_set_xrun(int xrun)
+{
+  if (xrun < -1 || xrun > 20)
+    return -22;
+  g_xrun_ov = xrun;
+  return 0;
+}
+#endif
+
+static uint32_t xrun_for(uint64_t blocks)
+{
+#ifdef TASX_AB
+  if (g_xrun_ov == -2) {
+    const char *e = getenv("TASX_XRUN");
+    g_xrun_ov = e ? atoi(e) : -1;
+  }
+  if (g_xrun_ov >= 0)
+    return (uint32_t) g_xrun_ov;
+#endif
+  return blocks >= kXrunMinBlocks ? kXrun : 0u;
+}
+
 template <int G = 16, int BS = kBlock, typename K, typename Prm>
 int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
@@ -1568,8 +1608,10 @@ int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_
     return 0;
   if (blocks > 0x7fffffffull)
     return -2;
+  Prm q = p;
+  q.xrun = xrun_for(blocks);
   t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds, s, p);
+  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds, s, q);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -96,6 +96,9 @@ SIGNATURES = {
     "tasx_server_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
     "tasx_ctx_use_server": (_c_int, [_uns, _c_int]),
     "tasx_ctx_server_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
+    "tasx_take_unfinished": (_c_int, [_uns, _vp, _c_u32]),
+    "tasx_take_unfinished_segs": (_c_int, [_uns, _vp, _c_u32]),
+    "tasx_server_abort": (_c_int, [_c_int]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_last_kernel": (ctypes.c_char_p, []),
     "tasx_host_alloc": (_vp, [_sz]),
@@ -120,6 +123,7 @@ AB_SIGNATURES = {
     "tasx_ab_tcp4_mix_pattern": (_c_int, [_vp, _c_u64, _c_u32, _vp, _c_u32, _c_int, _vp, _vp]),
     "tasx_ab_stream_copy": (_c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "tasx_ab_stream_read": (_c_int, [_vp, ctypes.c_size_t, _c_int, _vp, _vp]),
+    "tasx_ab_set_xrun": (_c_int, [_c_int]),
     "tasx_ab_ctx_set_tickets": (_c_int, [_uns, _c_u32]),
 }
 
@@ -515,6 +519,38 @@ def server_tx_segments(ctx_id: int, segs) -> int:
 def use_server(ctx_id: int, on: bool = True) -> None:
     """Attach the context to (or detach it from) its GPU's flush server."""
     _check(lib().tasx_ctx_use_server(ctx_id, 1 if on else 0), "tasx_ctx_use_server")
+
+
+def take_unfinished(ctx_id: int, chunk: int = 64) -> list[tuple[int, int]]:
+    """Error recovery (ABI 8): every frame the GPU did not finish, as (ip, l4)
+    host addresses, taken back from the context (tasx_take_unfinished; the
+    first call settles it).  The caller finishes them on the CPU."""
+    refs = (ctypes.c_void_p * (2 * chunk))()
+    got: list[tuple[int, int]] = []
+    while True:
+        k = _check(lib().tasx_take_unfinished(ctx_id, refs, chunk), "tasx_take_unfinished")
+        got += [(refs[2 * i] or 0, refs[2 * i + 1] or 0) for i in range(k)]
+        if k < chunk:
+            return got
+
+
+def take_unfinished_segs(ctx_id: int, chunk: int = 64):
+    """The TX segments (pktgen.TX_SEG_DTYPE records, as submitted) the flush
+    server did not build (tasx_take_unfinished_segs; after take_unfinished)."""
+    import numpy as np
+    from . import pktgen
+    out = []
+    buf = np.zeros(chunk, pktgen.TX_SEG_DTYPE)
+    while True:
+        k = _check(lib().tasx_take_unfinished_segs(ctx_id, buf.ctypes.data, chunk), "tasx_take_unfinished_segs")
+        out.append(buf[:k].copy())
+        if k < chunk:
+            return np.concatenate(out)
+
+
+def server_abort(device: int = 0) -> None:
+    """Stop the flush server's kernel with contexts still attached (ABI 8)."""
+    _check(lib().tasx_server_abort(device), "tasx_server_abort")
 
 
 def server_flushes(ctx_id: int) -> int:

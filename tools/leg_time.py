@@ -47,6 +47,12 @@ def make(leg: str, rotate: int = 16):
     if leg in ("shard8m", "shard1m"):  # config 4 at N = 1 (12.6 GB) / its per-GPU shard at N = 8 (1.57 GB)
         w = bench.shard8m_workload(1 if leg == "shard8m" else 8, 0)
         return w.loop(), w.bytes_per_step
+    if leg == "mixed":  # config 3: 1M RAW packets of {64,576,1500,9000} B
+        w = bench.mixed_workload(1, 0)
+        return w.loop(), w.bytes_per_step
+    if leg == "tso":  # config 5: 16,384 TSO segments
+        w = bench.tso_workload(0)
+        return w.loop(bench.HINT), w.bytes_per_step
     if leg == "flow":  # bench.py's flow_lookup leg: 256K lookups in TAS-sized tables
         w = bench.FlowLookupWorkload(4, pktgen.SEED + 3000)
         return w.loop(), w.N * 64
