@@ -83,6 +83,7 @@ def parse(argv=None):
                     help="N ranks may share the visible GPUs (gloo control plane): a rehearsal, not a scaling run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-server-cost", action="store_true", help="skip the resident flush server's price")
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--no-txseg", action="store_true")
     ap.add_argument("--no-flow", action="store_true")
@@ -1134,6 +1135,76 @@ def fastpath_mt_leg(flushes: int = 3000) -> dict:
     return res
 
 
+def server_cost_leg(rank: int, rot: int, flushes: int = 40000) -> dict:
+    """What the resident flush server costs the device-resident work on the
+    same GPU: the headline batch (2,000 launches) and the
+    TX segment build (800) timed with the server stopped, started but idle (its
+    32 workgroups of 1,024 threads resident, rings polled by their headers), and
+    started with 8 fast-path threads flushing through it meanwhile (32-frame
+    batches, 3 in flight each: tasxb_fastpath_mt in a second thread; the
+    flush rate of that run, which also spans the parts without device work, is
+    reported beside it).  Event-timed launches, each state's median of 3."""
+    import threading
+    dev = torch.cuda.current_device()
+    wl = Tcp4Workload(rot, pktgen.SEED + 7000 + rank, host=False)
+    tw = TxSegWorkload(rot, pktgen.SEED + 7100 + rank)
+    legs = {"headline": (wl.loop(HINT), wl.bytes_per_step, 2000), "tx_segment": (tw.loop(), tw.bytes_per_step, 800)}
+    for run, _, _ in legs.values():
+        prewarm(run)
+    torch.cuda.synchronize()
+
+    def timed(run, k):
+        # stream-level waits only: a device-wide synchronize would wait for the
+        # resident server kernel itself
+        cur = torch.cuda.current_stream()
+        run(0, 20)
+        cur.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        run(20, k)
+        e1.record(cur)
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / k
+
+    def measure():
+        return {name: float(np.median([timed(run, k) for _ in range(3)])) for name, (run, _, k) in legs.items()}
+    res = {"unit": "us per launch", "states": {}}
+    res["states"]["stopped"] = measure()
+    xsum.server_start(dev)
+    try:
+        res["states"]["idle"] = measure()
+    finally:
+        xsum.server_stop(dev)
+    flush = {}
+    th = threading.Thread(target=lambda: flush.update(benchloop.fastpath_mt(dev, 8, 8, 3, flushes, "server")))
+    th.start()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 10.0:  # the run has started its server and its threads are flushing
+        try:
+            if xsum.server_stats(dev)[0] > 2000:
+                break
+        except xsum.TasxError:
+            pass
+        time.sleep(0.001)
+    busy = measure()
+    try:
+        batches_after = xsum.server_stats(dev)[0]
+    except xsum.TasxError:
+        batches_after = None  # the flush run had already finished: the overlap was partial
+    th.join()
+    res["states"]["busy_8x3"] = busy
+    res["busy_flush_run"] = flush
+    res["busy_overlap_complete"] = batches_after is not None
+    for name, (_, nbytes, _) in legs.items():
+        st = {k: v[name] for k, v in res["states"].items()}
+        res[name] = {"us": {k: round(v, 3) for k, v in st.items()},
+                     "slowdown_idle": round(st["idle"] / st["stopped"], 4),
+                     "slowdown_busy": round(st["busy_8x3"] / st["stopped"], 4),
+                     "frac_busy": round(nbytes / st["busy_8x3"] / 1e3 / HBM_PEAK_GBS, 4)}
+    del res["states"]
+    return res
+
+
 def e2e_leg(ws: int, rank: int, reps: int = 5) -> dict:
     """Every rank at once, each from its own NUMA-local host thread (this
     process, pinned by numa_pin before these buffers were touched):
@@ -1679,6 +1750,9 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         torch.cuda.empty_cache()
 
     extra = {}
+    if not args.no_server_cost and rank == 0 and ws == 1:
+        extra["server_cost"] = server_cost_leg(rank, rot)
+        torch.cuda.empty_cache()
     if not args.no_e2e:
         extra["e2e"] = e2e_leg(ws, rank)
     if rank == 0 and ws == 1:
@@ -1753,6 +1827,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             line["flow_lookup"] = flow
         if rx_pass is not None:
             line["rx_pass"] = rx_pass
+        if "server_cost" in extra:
+            line["server_cost"] = extra["server_cost"]
         if "e2e" in extra:
             line["e2e"] = extra["e2e"]
         if "pmc" in extra:

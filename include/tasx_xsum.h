@@ -20,11 +20,13 @@
  *     on that stream; everything else returns after the work is complete.
  *   - Return 0 on success or a negative errno (-EINVAL bad argument, -ENOMEM,
  *     -ENODEV no usable GPU, -EIO a HIP runtime error; tasx_last_error()
- *     describes the last one).  There is NO CPU fallback: a frame whose
- *     checksum could not be computed on the GPU is reported, never silently
- *     computed elsewhere.  The reference's per-frame calls cannot fail
- *     (void); TAS's integration aborts on a non-zero
- *     return, as it does on its other invariant violations (fastemu.h:86-89).
+ *     describes the last one).  There is NO CPU fallback inside libtasx: a
+ *     frame whose checksum could not be computed on the GPU is reported, never
+ *     silently computed elsewhere.  The reference's per-frame calls cannot
+ *     fail (void), so the deferred forms hand such frames
+ *     back (tasx_take_unfinished, ABI 8) and TAS's integration finishes them
+ *     with its own rte_ipv4_cksum / rte_ipv4_udptcp_cksum and keeps running
+ *     (INTEGRATION.md section 3).
  *   - Checksum results are native (little-endian) uint16 values, exactly what
  *     tcp_checksums() stores into ip.chksum / tcp.chksum
  *     (include/packet_defs.h:96,165): their bytes are the network-order
@@ -44,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 7
+#define TASX_ABI_VERSION 8
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */
@@ -448,9 +450,10 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * frame starts 16-byte aligned, hdrs_len in [54, 240], room below 32 KiB,
  * frames (and their rooms) inside the frame region: else -EINVAL and nothing
  * is submitted.  Descriptors dma_read() would reject leave their frame as it
- * is (tasx_tx_segment_batch_dev).  Up to 20 segments go in one of the ring's
- * 8 slots (a run of equal hdrs_len and room); with every slot out, the call
- * waits inside for the oldest one to finish.
+ * is (tasx_tx_segment_batch_dev).  Up to 41 segments go in one of the ring's
+ * 8 slots (a run of equal hdrs_len and room: TAS's 32-segment flush takes one
+ * slot); with every slot out, the call waits inside for the oldest one to
+ * finish.
  *   tasx_ctx_register_shm(ctx, shm, bytes): the app's shared-memory region
  *     (pinned and mapped here unless it already is; below 4 GiB) */
 int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes);
@@ -460,6 +463,48 @@ int tasx_server_stop(int device);
 int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames);
 int tasx_ctx_use_server(unsigned ctx_id, int on);
 int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);
+
+/* ---------------------------------------------------------------------- */
+/* Error recovery (ABI 8).  SURVEY.md section 8b: TAS's per-frame calls cannot
+ * fail, so a batch whose GPU work fails must not drop frames.  libtasx still
+ * computes nothing on the CPU; instead it hands the unfinished frames back and
+ * the caller finishes them with TAS's own CPU path -- the #else branch of
+ * tcp_checksums (rte_ipv4_cksum / rte_ipv4_udptcp_cksum,
+ * tas/fast/fast_flows.c:1065-1067) for frames, flow_tx_read + tcp_checksums
+ * (fast_flows.c:930-936) for TX segments -- and keeps running
+ * (INTEGRATION.md section 3).
+ *   tasx_take_unfinished(ctx, frames, max): valid at any time, meant after any
+ *     call on the context returned non-zero.  The first call settles the
+ *     context: it waits for in-flight work whose path is still healthy, then
+ *     collects every recorded frame whose checksum fields the GPU did not
+ *     store -- batches of a server whose kernel has gone (stopped by
+ *     tasx_server_abort, its lease ran out, a fault), of a failed feeder, of a
+ *     failed or stalled stream, and frames recorded but not submitted -- marks
+ *     every ticket complete, and detaches the context from a dead server or
+ *     feeder.  Each call then writes up to max of them ({ip, l4} as recorded)
+ *     and returns how many, 0 once none are left; the context is usable again
+ *     (pending 0, every ticket polled complete).  A GPU that wrote a field
+ *     after all is harmless: the caller recomputes both fields from zero.
+ *   tasx_take_unfinished_segs(ctx, segs, max): the same for TX segments given
+ *     to tasx_server_tx_segments (descriptors as submitted; after an -EIO
+ *     from that call, its segments not yet handed to the server too).  Call
+ *     tasx_take_unfinished first (it settles the context).
+ *   tasx_server_abort(device): stops the server kernel even with contexts
+ *     attached (a watchdog, or TAS leaving the GPU path); their outstanding
+ *     batches become unfinished, their next poll/wait/submit returns -EIO, and
+ *     tasx_take_unfinished (or tasx_ctx_use_server(ctx, 0), which detaches
+ *     from a gone kernel with -EIO) hands them back; tasx_server_stop then
+ *     releases it once every context has detached.
+ * A frame the server left alone because its total_length changed after
+ * submission (the sticky -EIO above) is not returned: the caller broke the
+ * deferred contract, and the frame's bytes are no longer what was submitted. */
+typedef struct tasx_frame_ref {
+  void *ip; /* the IPv4 header, as recorded */
+  void *l4; /* the TCP header */
+} tasx_frame_ref;
+int tasx_take_unfinished(unsigned ctx_id, tasx_frame_ref *frames, uint32_t max);
+int tasx_take_unfinished_segs(unsigned ctx_id, tasx_tx_seg *segs, uint32_t max);
+int tasx_server_abort(int device);
 
 /* ---------------------------------------------------------------------- */
 /* Kernel selection, for tests and A/B runs.  Per calling thread (TAS runs one

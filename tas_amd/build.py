@@ -102,7 +102,8 @@ C_TEST_BIN = ROOT / "tests" / "c" / "bin" / "boundary_test"
 def build_c_tests(force: bool = False) -> Path | None:
     if not (REF_INCLUDE / "packet_defs.h").exists():
         return C_TEST_BIN if C_TEST_BIN.exists() else None
-    deps = [C_TEST_SRC, C_TEST_SRC.with_name("tas_glue.h"), ROOT / "include" / "tasx_xsum.h", LIB]
+    deps = [C_TEST_SRC, C_TEST_SRC.with_name("tas_glue.h"), C_TEST_SRC.with_name("rte_standin.h"),
+            ROOT / "include" / "tasx_xsum.h", LIB]
     if force or not C_TEST_BIN.exists() or C_TEST_BIN.stat().st_mtime < max(d.stat().st_mtime for d in deps):
         C_TEST_BIN.parent.mkdir(parents=True, exist_ok=True)
         _run(["gcc", "-std=gnu99", "-O2", "-Wall", "-I", str(REF_INCLUDE), "-I", str(ROOT / "include"),

@@ -165,7 +165,7 @@ constexpr int kSrvTxU = 6;
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
-  __shared__ uint64_t s_w[TASX_SRV_FB]; // a TX segment slot's entry words
+  __shared__ uint64_t s_w[TASX_SRV_WORDS]; // a TX segment slot's entry words
   __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg;
 #ifdef TASX_AB
   __shared__ uint32_t s_light;
@@ -226,9 +226,27 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         s_tl[lane] = (uint32_t) (v.e >> 32) & 0xffffu;
         s_w[lane] = v.e;
       }
+      // a TX slot's entries past the first 64: the host wrote them before
+      // the header this read saw, so one more round trip has them all
+      // (tagged all the same; a mismatch is read again)
+      bool torn = false;
+      if (words > TASX_SRV_FB) {
+        const uint64_t *e2 = (const uint64_t *) (ring + TASX_SRV_SLOTP(r, p) + TASX_SRV_HDR) + TASX_SRV_FB;
+        const bool mine = (uint32_t) lane < words - TASX_SRV_FB;
+        uint64_t w2 = 0ull;
+        torn = true;
+        for (int t = 0; t < 64 && torn; ++t) { // bounded: a host that broke the protocol ends up flagged
+          w2 = mine ? ld_sys64(e2 + lane) : 0ull;
+          torn = __builtin_amdgcn_ballot_w64(mine && (w2 >> 48) != tag) != 0ull;
+        }
+        if (mine)
+          s_w[TASX_SRV_FB + lane] = w2;
+      }
       if (lane == 0) {
         s_seg = seg ? 1u : 0u;
-        s_n = n;
+        s_n = torn ? 0u : n; // a slot still torn is not built, and flags the ring
+        if (torn)
+          s_bad = 1u;
         s_bytes = (uint32_t) (h0 >> 16);
         s_base = h1 & 0xffffffffffffull;
       }
@@ -322,14 +340,20 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         tp.ip_off = (uint32_t) (s_w[1] >> 32) & 0xffu;
         tp.l4_off = (uint32_t) (s_w[1] >> 40) & 0xffu;
         tp.dbg = 0u;
+        // reads stay inside the region the host validated the frame against
+        // (s_bytes from the frame region's start, the frame 16-byte aligned in it)
+        const uint32_t rb = s_bytes > (uint32_t) wa ? s_bytes - (uint32_t) wa : 0u;
+        bool good;
 #ifdef TASX_AB
         if (P.fpol == 13u) // A/B 13: write-through stores, no release
-          txseg_row_d<3, false, true>(tp, row, d0, d1, gl);
+          good = txseg_row_d<3, false, true>(tp, row, d0, d1, gl, rb);
         else if (P.fpol == 14u) // A/B 14: non-temporal payload stores, then the release
-          txseg_row_d<3, true>(tp, row, d0, d1, gl);
+          good = txseg_row_d<3, true>(tp, row, d0, d1, gl, rb);
         else
 #endif
-          txseg_row_d<kSrvTxU, false>(tp, row, d0, d1, gl);
+          good = txseg_row_d<kSrvTxU, false>(tp, row, d0, d1, gl, rb);
+        if (gl == 15 && !good) // total_length changed since submission: frame left alone, ring flagged
+          atomicOr(&s_bad, 1u);
       }
     } else if (row < s_n) {
       const uint64_t base = s_base;

@@ -469,6 +469,12 @@ struct tasx_ctx {
   uint32_t n_server_flushes;
   int sv_err; /* the server flagged a frame of this context (sticky until detach) */
   uint64_t sv_batches, sv_frames; /* since attach (this thread's own counters: no shared line per flush) */
+  /* frames and TX segments a failed flush left unfinished, handed back by
+   * tasx_take_unfinished / _segs (ctx_settle fills them) */
+  tasx_frame_ref *unf;
+  uint32_t unf_n, unf_cap, unf_pos;
+  tasx_tx_seg *unf_seg;
+  uint32_t unf_seg_n, unf_seg_cap, unf_seg_pos;
 };
 
 #define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
@@ -507,6 +513,82 @@ static int ticket_le(uint32_t a, uint32_t b)
   return (int32_t) (a - b) <= 0;
 }
 
+/* Host ranges this library pinned (hipHostRegister) for contexts' frame and
+ * shared-memory regions, reference-counted: every core registers the same
+ * tas_shm, and the pin must outlive every context that
+ * maps it, not only the first registrant's. */
+#define MAX_PINS (2u * TASX_MAX_CTX)
+static struct pin {
+  uint8_t *base;
+  size_t bytes;
+  uint32_t refs;
+} g_pins[MAX_PINS];
+static pthread_mutex_t g_pins_mu = PTHREAD_MUTEX_INITIALIZER;
+
+/* The device address of [base, base + bytes): a range inside one this library
+ * pinned takes a reference on that pin (*owned = 1); memory pinned elsewhere
+ * (tasx_host_alloc, hipHostMalloc) is used as it is (*owned = 0); anything
+ * else is pinned here (*owned = 1). */
+static int pin_acquire(uint8_t *base, size_t bytes, void **dev, int *owned)
+{
+  hipError_t e;
+  int rc = 0;
+  *owned = 0;
+  pthread_mutex_lock(&g_pins_mu);
+  for (uint32_t k = 0; k < MAX_PINS; k++) {
+    struct pin *q = &g_pins[k];
+    if (q->refs && base >= q->base && base + bytes <= q->base + q->bytes) {
+      if ((e = hipHostGetDevicePointer(dev, base, 0)) != hipSuccess) {
+        rc = hip_err(e, "hipHostGetDevicePointer");
+      } else {
+        q->refs++;
+        *owned = 1;
+      }
+      pthread_mutex_unlock(&g_pins_mu);
+      return rc;
+    }
+  }
+  if (hipHostGetDevicePointer(dev, base, 0) == hipSuccess) {
+    pthread_mutex_unlock(&g_pins_mu);
+    return 0;
+  }
+  (void) hipGetLastError();
+  uint32_t k = 0;
+  while (k < MAX_PINS && g_pins[k].refs)
+    k++;
+  if (k == MAX_PINS)
+    rc = set_err(-ENOMEM, "more than %u pinned regions", MAX_PINS);
+  else if ((e = hipHostRegister(base, bytes, hipHostRegisterMapped)) != hipSuccess)
+    rc = hip_err(e, "hipHostRegister");
+  else if ((e = hipHostGetDevicePointer(dev, base, 0)) != hipSuccess) {
+    hipHostUnregister(base);
+    rc = hip_err(e, "hipHostGetDevicePointer");
+  } else {
+    g_pins[k] = (struct pin){base, bytes, 1u};
+    *owned = 1;
+  }
+  pthread_mutex_unlock(&g_pins_mu);
+  return rc;
+}
+
+/* drop the reference pin_acquire took for a range starting at base */
+static void pin_release(uint8_t *base)
+{
+  pthread_mutex_lock(&g_pins_mu);
+  for (uint32_t k = 0; k < MAX_PINS; k++) {
+    struct pin *q = &g_pins[k];
+    if (q->refs && base >= q->base && base < q->base + q->bytes) {
+      if (--q->refs == 0) {
+        hipHostUnregister(q->base);
+        q->base = NULL;
+        q->bytes = 0;
+      }
+      break;
+    }
+  }
+  pthread_mutex_unlock(&g_pins_mu);
+}
+
 static void ctx_release(struct tasx_ctx *c)
 {
   int s;
@@ -537,12 +619,14 @@ static void ctx_release(struct tasx_ctx *c)
   if (c->d_count)
     hipFree(c->d_count);
   if (c->zc_registered)
-    hipHostUnregister(c->zc_host);
+    pin_release(c->zc_host);
   if (c->shm_registered)
-    hipHostUnregister(c->shm_host);
+    pin_release(c->shm_host);
   free(c->pend_ip);
   free(c->pend_l4);
   free(c->fq);
+  free(c->unf);
+  free(c->unf_seg);
   memset(c, 0, sizeof(*c));
 }
 
@@ -1203,7 +1287,6 @@ int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
   void *dev = NULL;
-  hipError_t e;
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   if (!base || bytes == 0)
@@ -1211,19 +1294,10 @@ int tasx_ctx_register_frames(unsigned ctx_id, void *base, size_t bytes)
   if (c->zc_host)
     return set_err(-EINVAL, "ctx %u already has a frame region", ctx_id);
   HIPCHK(hipSetDevice(c->device));
-  /* already pinned (tasx_host_alloc / hipHostMalloc)?  else pin it */
-  e = hipHostGetDevicePointer(&dev, base, 0);
-  if (e != hipSuccess) {
-    (void) hipGetLastError();
-    HIPCHK(hipHostRegister(base, bytes, hipHostRegisterMapped));
-    c->zc_registered = 1;
-    e = hipHostGetDevicePointer(&dev, base, 0);
-    if (e != hipSuccess) {
-      hipHostUnregister(base);
-      c->zc_registered = 0;
-      return hip_err(e, "hipHostGetDevicePointer");
-    }
-  }
+  /* already pinned (tasx_host_alloc / hipHostMalloc, or by another context)?  else pin it */
+  int rc = pin_acquire((uint8_t *) base, bytes, &dev, &c->zc_registered);
+  if (rc)
+    return rc;
   c->zc_host = (uint8_t *) base;
   c->zc_dev = (uint8_t *) dev;
   c->zc_bytes = bytes;
@@ -1234,7 +1308,6 @@ int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
   void *dev = NULL;
-  hipError_t e;
   if (!c)
     return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
   if (!shm || bytes == 0 || bytes >= (1ull << 32))
@@ -1242,21 +1315,13 @@ int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes)
   if (c->shm_host)
     return set_err(-EINVAL, "ctx %u already has a shared-memory region", ctx_id);
   HIPCHK(hipSetDevice(c->device));
-  e = hipHostGetDevicePointer(&dev, shm, 0);
-  if (e != hipSuccess) {
-    (void) hipGetLastError();
-    HIPCHK(hipHostRegister(shm, bytes, hipHostRegisterMapped));
-    c->shm_registered = 1;
-    e = hipHostGetDevicePointer(&dev, shm, 0);
-    if (e != hipSuccess) {
-      hipHostUnregister(shm);
-      c->shm_registered = 0;
-      return hip_err(e, "hipHostGetDevicePointer");
-    }
-  }
+  /* every core registers the same tas_shm: one pin, counted (pin_acquire) */
+  int rc = pin_acquire((uint8_t *) shm, bytes, &dev, &c->shm_registered);
+  if (rc)
+    return rc;
   if ((uint64_t) (uintptr_t) dev + bytes >= (1ull << 48)) {
     if (c->shm_registered)
-      hipHostUnregister(shm);
+      pin_release((uint8_t *) shm);
     c->shm_registered = 0;
     return set_err(-EINVAL, "register_shm: device address beyond 48 bits");
   }
@@ -1495,12 +1560,13 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   f->n = cnt;
   f->zerocopy = zc;
   f->ticket = t;
-  c->local_last = t;
   fused_done(&p, c->d_done + DONE_STRIDE * (uint32_t) s, c->d_count + DONE_STRIDE * (uint32_t) s, t);
+  /* a failed launch leaves the frames pending (ctx_settle hands them back) */
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
   if (!tasx_last_launch_posted_done() && post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "completion-word launch");
+  c->local_last = t;
   c->next_ticket = t;
   if (cnt < c->npend) {
     memmove(c->pend_ip, c->pend_ip + cnt, (size_t) (c->npend - cnt) * sizeof(*c->pend_ip));
@@ -1679,12 +1745,16 @@ static int feeder_submit(struct tasx_ctx *c)
     if (!ticket_le(c->local_last, c->done_ticket) && (rc = flush_wait(c, c->local_last)) != 0)
       return rc;
     const uint32_t cnt = c->npend < FB_MAX ? c->npend : FB_MAX;
+    /* the slot is reused once the feeder has taken its previous batch AND
+     * completed it: until then its frame pointers are what ctx_settle hands
+     * back should the feeder fail */
     uint32_t k = 0;
-    while (c->fq_head - __atomic_load_n(&c->fq_tail, __ATOMIC_ACQUIRE) >= FQ) {
+    struct fbatch *b = &c->fq[c->fq_head % FQ];
+    while (c->fq_head - __atomic_load_n(&c->fq_tail, __ATOMIC_ACQUIRE) >= FQ ||
+           !ticket_le(b->ticket, __atomic_load_n(&c->fd_done, __ATOMIC_ACQUIRE))) {
       if ((++k & 4095u) == 0 && feeder_error(c))
         return set_err(-EIO, "flush: the feeder thread failed");
     }
-    struct fbatch *b = &c->fq[c->fq_head % FQ];
     b->ticket = ++c->next_ticket;
     b->n = cnt;
     memcpy(b->ip, c->pend_ip, (size_t) cnt * sizeof(*b->ip));
@@ -1949,6 +2019,8 @@ int tasx_ctx_use_feeder(unsigned ctx_id, int on)
     pthread_mutex_lock(&g_feeder_mu);
     struct feeder *F = c->device < MAX_DEVICES ? g_feeder[c->device] : NULL;
     if (F) {
+      for (uint32_t q = 0; q < FQ; q++) /* free slots: their "previous batch" is complete */
+        fq[q].ticket = c->next_ticket;
       c->fq = fq;
       c->fq_head = c->fq_tail = 0;
       c->fd_done = c->next_ticket;
@@ -2024,6 +2096,7 @@ struct fserver {
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
+  int aborted;                     /* tasx_server_abort stopped the kernel (and the keepalive thread) */
 };
 
 struct grave {
@@ -2033,6 +2106,9 @@ struct grave {
 
 static struct fserver *g_server[MAX_DEVICES];
 static pthread_mutex_t g_server_mu = PTHREAD_MUTEX_INITIALIZER;
+static int server_settle(struct tasx_ctx *c);
+static void ctx_settle(struct tasx_ctx *c);
+static int unf_seg(struct tasx_ctx *c, const tasx_tx_seg *g);
 
 /* HIP's frees wait for every stream of the device, the server's kernel too:
  * refused (-EBUSY) while any server runs, instead of waiting for its stop */
@@ -2234,6 +2310,21 @@ static int server_submit(struct tasx_ctx *c)
   return 0;
 }
 
+/* segments per TX slot: TASX_SRV_SEGS (A/B: TASX_SRV_SEGMAX, e.g. round 4's 20) */
+static uint32_t srv_segs_max(void)
+{
+#ifdef TASX_AB
+  static uint32_t m = 0;
+  if (m == 0) {
+    const char *e = getenv("TASX_SRV_SEGMAX");
+    m = e && atoi(e) > 0 && (uint32_t) atoi(e) <= TASX_SRV_SEGS ? (uint32_t) atoi(e) : TASX_SRV_SEGS;
+  }
+  return m;
+#else
+  return TASX_SRV_SEGS;
+#endif
+}
+
 /* TX segment batches through the server: validated up front (nothing is
  * submitted unless every segment is safe to build in place), then packed
  * up to TASX_SRV_SEGS to a slot, consecutive segments with one hdrs_len and
@@ -2255,8 +2346,10 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     const tasx_tx_seg *g = &segs[i];
     const uint32_t room = g->room & ~TASX_TXSEG_SCRATCH;
     const uint64_t fend = (uint64_t) g->hdrs_len + g->payload;
-    if ((g->frame_off & 15u) != 0 || g->hdrs_len < l4_off + 20u || g->hdrs_len > 240u || room > 0x7fffu ||
-        g->tx_base >= (1ull << 32) || g->frame_off + g->hdrs_len > c->zc_bytes)
+    /* frame_off first: the sums below cannot wrap once it lies inside the region */
+    if (g->frame_off >= c->zc_bytes || (g->frame_off & 15u) != 0 || g->hdrs_len < l4_off + 20u ||
+        g->hdrs_len > 240u || room > 0x7fffu || g->tx_base >= (1ull << 32) ||
+        g->hdrs_len > c->zc_bytes - g->frame_off)
       return set_err(-EINVAL, "tx segment %u: frame offset, header length or room outside what the server builds",
                      i);
     /* the row reads and writes whole 16-byte chunks of [frame, frame + max(end, room)) and sums up to
@@ -2266,7 +2359,7 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     uint64_t span = fend > ip_off + tl ? fend : ip_off + tl;
     if (g->room & TASX_TXSEG_SCRATCH)
       span = span > room ? span : room;
-    if (g->frame_off + ((span + 15u) & ~(uint64_t) 15) > c->zc_bytes)
+    if (((span + 15u) & ~(uint64_t) 15) > c->zc_bytes - g->frame_off)
       return set_err(-EINVAL, "tx segment %u: frame (or its room) past the registered frame region", i);
   }
   /* a flush this context launched itself completes first (as server_submit) */
@@ -2277,14 +2370,19 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
   for (uint32_t i0 = 0; i0 < n;) {
     /* a slot: up to TASX_SRV_SEGS consecutive segments with one hdrs_len and room */
     uint32_t cnt = 1;
-    while (i0 + cnt < n && cnt < TASX_SRV_SEGS && segs[i0 + cnt].hdrs_len == segs[i0].hdrs_len &&
+    while (i0 + cnt < n && cnt < srv_segs_max() && segs[i0 + cnt].hdrs_len == segs[i0].hdrs_len &&
            segs[i0 + cnt].room == segs[i0].room)
       cnt++;
     uint32_t k = 0;
     while (c->sv_pos - c->sv_done_pos >= TASX_SRV_RING) {
       server_reap(c);
-      if ((++k & 4095u) == 0 && (rc = server_health(c)) != 0)
+      if ((++k & 4095u) == 0 && (rc = server_health(c)) != 0) {
+        /* the segments not handed over go to the unfinished store with the
+         * server's (tasx_take_unfinished_segs) */
+        for (uint32_t i = i0; i < n; i++)
+          (void) unf_seg(c, &segs[i]);
         return rc;
+      }
     }
     const uint32_t pos = c->sv_pos;
     const uint64_t tag = (uint64_t) ((pos + 1u) & 0xffffu) << 48;
@@ -2302,7 +2400,9 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
       w[1] = g->pos | (uint64_t) (g->tx_len & 0xffffu) << 32 | tag;
       w[2] = (uint32_t) g->tx_base | (uint64_t) (g->tx_len >> 16) << 32 | tag;
     }
-    for (uint32_t w = TASX_SRV_SEGW0 + 3 * cnt; w < TASX_SRV_FB; w++) /* every entry word tagged (server_submit) */
+    /* every entry word the first poll reads tagged (server_submit); the words
+     * past TASX_SRV_FB are read only after the header, which comes after them */
+    for (uint32_t w = TASX_SRV_SEGW0 + 3 * cnt; w < TASX_SRV_FB; w++)
       e[w] = tag;
     const uintptr_t b16 = (uintptr_t) c->zc_dev;
     __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
@@ -2441,8 +2541,10 @@ int tasx_server_stop(int device)
     return set_err(-EBUSY, "flush server for device %d still serves contexts", device);
   }
   __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
-  __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
-  pthread_join(S->keep, NULL);
+  if (!S->aborted) {
+    __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
+    pthread_join(S->keep, NULL);
+  }
   /* bounded wait for every workgroup to leave */
   hipError_t e = hipErrorNotReady;
   const struct timespec ts = {0, 100 * 1000};
@@ -2531,6 +2633,11 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
       return rc;
     pthread_mutex_lock(&g_server_mu);
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
+    if (S && (S->aborted || hipStreamQuery(S->st) != hipErrorNotReady)) {
+      pthread_mutex_unlock(&g_server_mu);
+      return set_err(-EIO, "the flush server for device %d is not running (aborted, or its lease ran out): "
+                     "tasx_server_stop it", c->device);
+    }
     if (S) {
       c->sv_pos = c->sv_done_pos = S->ring_pos[id]; /* where the ring's workgroups wait */
       c->sv_err = 0;
@@ -2545,12 +2652,14 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
   }
   if (!c->sv)
     return 0;
-  /* the server's positions first: a frame it flagged does not stop the detach */
-  uint32_t k = 0;
-  while (c->sv_done_pos != c->sv_pos) {
-    server_reap(c);
-    if ((++k & 4095u) == 0 && (rc = server_alive(c)) != 0)
-      return rc;
+  /* the server's positions first: a frame it flagged does not stop the detach;
+   * a kernel that has gone leaves its positions unfinished: they move to the
+   * context's unfinished store (tasx_take_unfinished) and the detach completes */
+  if (server_settle(c) != 0) {
+    ctx_settle(c); /* the rest of the context too: every ticket complete, pending frames handed back */
+    return set_err(-EIO, "ctx %u detached from a flush server whose kernel has gone; %u frame(s) and %u TX "
+                   "segment(s) unfinished (tasx_take_unfinished)", ctx_id, c->unf_n - c->unf_pos,
+                   c->unf_seg_n - c->unf_seg_pos);
   }
   const int had_err = c->sv_err;
   c->sv_err = 0;
@@ -2578,6 +2687,249 @@ int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes)
   if (server_flushes)
     *server_flushes = c->n_server_flushes;
   return 0;
+}
+
+int tasx_server_abort(int device)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "server: device %d out of range", device);
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = g_server[device];
+  if (!S) {
+    pthread_mutex_unlock(&g_server_mu);
+    return set_err(-EINVAL, "no flush server running for device %d", device);
+  }
+  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+  if (!S->aborted) {
+    __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
+    pthread_join(S->keep, NULL);
+    S->aborted = 1;
+  }
+  hipError_t e = hipErrorNotReady;
+  const struct timespec ts = {0, 100 * 1000};
+  for (uint32_t t = 0; t < SRV_STOP_WAIT_MS * 10u && (e = hipStreamQuery(S->st)) == hipErrorNotReady; t++)
+    nanosleep(&ts, NULL);
+  pthread_mutex_unlock(&g_server_mu);
+  if (e == hipErrorNotReady)
+    return set_err(-EIO, "flush server for device %d did not stop within %u ms", device, SRV_STOP_WAIT_MS);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------- */
+/* Error recovery (ABI 8): tasx_take_unfinished.  ctx_settle brings every
+ * path of the context to rest -- waiting while the path is healthy -- and
+ * moves the frames (and TX segments) no GPU work finished into the
+ * context's unfinished store; the caller takes them from there and finishes
+ * them with TAS's own CPU path.  Nothing here computes a checksum. */
+
+static int unf_frame(struct tasx_ctx *c, uint8_t *ip, uint8_t *l4)
+{
+  if (c->unf_n == c->unf_cap) {
+    const uint32_t cap = c->unf_cap ? 2u * c->unf_cap : 256u;
+    tasx_frame_ref *n = realloc(c->unf, (size_t) cap * sizeof(*n));
+    if (!n)
+      return -ENOMEM;
+    c->unf = n;
+    c->unf_cap = cap;
+  }
+  c->unf[c->unf_n++] = (tasx_frame_ref){ip, l4};
+  return 0;
+}
+
+static int unf_seg(struct tasx_ctx *c, const tasx_tx_seg *g)
+{
+  if (c->unf_seg_n == c->unf_seg_cap) {
+    const uint32_t cap = c->unf_seg_cap ? 2u * c->unf_seg_cap : 64u;
+    tasx_tx_seg *n = realloc(c->unf_seg, (size_t) cap * sizeof(*n));
+    if (!n)
+      return -ENOMEM;
+    c->unf_seg = n;
+    c->unf_seg_cap = cap;
+  }
+  c->unf_seg[c->unf_seg_n++] = *g;
+  return 0;
+}
+
+/* ring position q's batch back from its slot (the host wrote it; the server
+ * only reads slots): frames as host pointers, or the TX segments' descriptors */
+static int server_slot_unfinished(struct tasx_ctx *c, uint32_t q)
+{
+  const unsigned id = (unsigned) (c - g_ctx);
+  const uint64_t *slot = (const uint64_t *) (c->sv->h_ring + TASX_SRV_SLOTP(id, q));
+  const uint64_t *e = slot + TASX_SRV_HDR / 8;
+  const uint32_t n = (uint32_t) slot[0] & 0xffffu;
+  int rc = 0;
+  if (n & TASX_SRV_SEG) {
+    const uint32_t hl = (uint32_t) e[2] & 0xffffu, room16 = (uint32_t) (e[2] >> 16) & 0xffffu;
+    for (uint32_t j = 0; j < (n & ~TASX_SRV_SEG) && !rc; j++) {
+      const uint64_t *w = e + TASX_SRV_SEGW0 + 3 * j;
+      tasx_tx_seg g;
+      memset(&g, 0, sizeof(g));
+      g.frame_off = (uint32_t) w[0];
+      g.payload = (uint16_t) (w[0] >> 32);
+      g.pos = (uint32_t) w[1];
+      g.tx_len = ((uint32_t) (w[1] >> 32) & 0xffffu) | (((uint32_t) (w[2] >> 32) & 0xffffu) << 16);
+      g.tx_base = (uint32_t) w[2];
+      g.hdrs_len = (uint16_t) hl;
+      g.room = (room16 & 0x7fffu) | ((room16 & 0x8000u) ? TASX_TXSEG_SCRATCH : 0u);
+      rc = unf_seg(c, &g);
+    }
+  } else {
+    const uint8_t *h16 = c->zc_host - ((uintptr_t) c->zc_dev & 15u); /* host view of the slot's base */
+    for (uint32_t i = 0; i < n && !rc; i++) {
+      uint8_t *ip = (uint8_t *) h16 + (uint32_t) e[i] + TASX_TAS_IP_OFF;
+      rc = unf_frame(c, ip, ip + 20);
+    }
+  }
+  return rc;
+}
+
+/* The server part: wait while its kernel runs for the context's positions;
+ * if the kernel has gone, the positions it did not finish become unfinished
+ * and the context detaches.  Returns 1 when it detached from a gone kernel. */
+static int server_settle(struct tasx_ctx *c)
+{
+  const unsigned id = (unsigned) (c - g_ctx);
+  struct fserver *S = c->sv;
+  int gone = 0;
+  for (uint32_t k = 1; c->sv_done_pos != c->sv_pos; k++) {
+    server_reap(c);
+    if ((k & 4095u) == 0 && hipStreamQuery(S->st) != hipErrorNotReady) {
+      server_reap(c);
+      gone = c->sv_done_pos != c->sv_pos;
+      break;
+    }
+  }
+  if (!gone && (S->aborted || hipStreamQuery(S->st) != hipErrorNotReady))
+    gone = 1; /* idle, but nothing will serve this ring again */
+  if (gone) {
+    const uint32_t *done = srv_dline(S, id);
+    for (uint32_t q = c->sv_done_pos; q != c->sv_pos; q++)
+      if (__atomic_load_n(&done[q % TASX_SRV_RING], __ATOMIC_ACQUIRE) != q + 1u)
+        (void) server_slot_unfinished(c, q); /* finished out of order: done */
+    c->sv_done_pos = c->sv_pos;
+  }
+  if (!gone)
+    return 0;
+  pthread_mutex_lock(&g_server_mu);
+  __atomic_fetch_add(&S->batches, c->sv_batches, __ATOMIC_RELAXED);
+  __atomic_fetch_add(&S->frames, c->sv_frames, __ATOMIC_RELAXED);
+  S->ring_pos[id] = c->sv_pos;
+  __atomic_and_fetch(&S->attached, ~(1u << id), __ATOMIC_RELEASE);
+  pthread_mutex_unlock(&g_server_mu);
+  c->sv = NULL;
+  return 1;
+}
+
+/* a stream's queued work drained (or failed), at most 5 s */
+static void stream_drain(hipStream_t st)
+{
+  const struct timespec ts = {0, 100 * 1000};
+  for (uint32_t t = 0; t < SRV_STOP_WAIT_MS * 10u && hipStreamQuery(st) == hipErrorNotReady; t++)
+    nanosleep(&ts, NULL);
+  (void) hipGetLastError();
+}
+
+static void ctx_settle(struct tasx_ctx *c)
+{
+  /* 1. the flush server's positions (a changed frame the server flagged was
+   * left alone and is not handed back: the sticky error ends here) */
+  if (c->sv)
+    (void) server_settle(c);
+  c->sv_err = 0;
+  /* 2. the feeder's batches: complete, or unfinished if it failed; its slots
+   * keep a batch's frames until the batch completes (feeder_submit) */
+  if (c->fd) {
+    const uint32_t last = c->fq_head ? c->fq[(c->fq_head - 1u) % FQ].ticket : c->fd_done;
+    while (!ticket_le(last, __atomic_load_n(&c->fd_done, __ATOMIC_ACQUIRE)) && !feeder_error(c))
+      sched_yield();
+    if (feeder_error(c)) {
+      struct feeder *F = c->fd;
+      stream_drain(F->st); /* a sweep still running writes nothing after this */
+      const uint32_t fdone = __atomic_load_n(&c->fd_done, __ATOMIC_ACQUIRE);
+      for (uint32_t q = c->fq_head >= FQ ? c->fq_head - FQ : 0u; q != c->fq_head; q++) {
+        const struct fbatch *b = &c->fq[q % FQ];
+        if (!ticket_le(b->ticket, fdone))
+          for (uint32_t i = 0; i < b->n; i++)
+            (void) unf_frame(c, b->ip[i], b->ip[i] + 20);
+      }
+      pthread_mutex_lock(&g_feeder_mu);
+      __atomic_and_fetch(&F->attached, ~(1u << (unsigned) (c - g_ctx)), __ATOMIC_RELEASE);
+      pthread_mutex_unlock(&g_feeder_mu);
+      c->fd = NULL;
+      free(c->fq);
+      c->fq = NULL;
+    }
+  }
+  /* 3. the context's own flushes: wait while its stream works on them */
+  if (!ticket_le(c->local_last, c->done_ticket)) {
+    stream_drain(c->st[0]);
+    for (int s = 0; s < NSLOT; s++) {
+      struct flush_slot *f = &c->fl[s];
+      const uint32_t t = f->ticket;
+      if (f->n == 0 || ticket_le(t, c->done_ticket) || !ticket_le(t, c->local_last))
+        continue;
+      if (__atomic_load_n(c->h_done + DONE_STRIDE * (uint32_t) s, __ATOMIC_ACQUIRE) == t) {
+        if (!f->zerocopy) { /* finished, not yet reaped: its results into its frames */
+          const uint16_t *r = c->h_out[s];
+          for (uint32_t i = 0; i < f->n; i++) {
+            memcpy(f->ip[i] + 10, &r[2 * i], 2);
+            memcpy(f->l4[i] + 16, &r[2 * i + 1], 2);
+          }
+        }
+      } else {
+        for (uint32_t i = 0; i < f->n; i++)
+          (void) unf_frame(c, f->ip[i], f->l4[i]);
+      }
+    }
+  }
+  /* 4. frames recorded but never handed to the GPU (a failed submit; a
+   * launch that failed before its completion word may still be running) */
+  if (c->npend) {
+    stream_drain(c->st[0]);
+    for (uint32_t i = 0; i < c->npend; i++)
+      (void) unf_frame(c, c->pend_ip[i], c->pend_l4[i]);
+    c->npend = 0;
+  }
+  /* every ticket handed out is complete now */
+  c->done_ticket = c->local_last = c->next_ticket;
+  if (c->fd)
+    __atomic_store_n(&c->fd_done, c->next_ticket, __ATOMIC_RELEASE);
+  for (int s = 0; s < NSLOT; s++)
+    c->fl[s].n = 0;
+}
+
+int tasx_take_unfinished(unsigned ctx_id, tasx_frame_ref *frames, uint32_t max)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (max > 0 && !frames)
+    return set_err(-EINVAL, "take_unfinished: NULL frames");
+  if (c->unf_pos == c->unf_n) { /* nothing left from an earlier settle: settle now */
+    c->unf_n = c->unf_pos = 0;
+    hipSetDevice(c->device);
+    ctx_settle(c);
+  }
+  uint32_t k = 0;
+  while (k < max && c->unf_pos < c->unf_n)
+    frames[k++] = c->unf[c->unf_pos++];
+  return (int) k;
+}
+
+int tasx_take_unfinished_segs(unsigned ctx_id, tasx_tx_seg *segs, uint32_t max)
+{
+  struct tasx_ctx *c = get_ctx(ctx_id);
+  if (!c)
+    return set_err(-EINVAL, "ctx %u not initialised", ctx_id);
+  if (max > 0 && !segs)
+    return set_err(-EINVAL, "take_unfinished_segs: NULL segs");
+  uint32_t k = 0;
+  while (k < max && c->unf_seg_pos < c->unf_seg_n)
+    segs[k++] = c->unf_seg[c->unf_seg_pos++];
+  if (c->unf_seg_pos == c->unf_seg_n)
+    c->unf_seg_n = c->unf_seg_pos = 0;
+  return (int) k;
 }
 
 /* ---------------------------------------------------------------------- */

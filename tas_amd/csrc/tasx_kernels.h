@@ -112,9 +112,13 @@ typedef struct tasx_flow_params {
  * 40, entry 2 = hdrs_len | room16 << 16 (room & 0x7fff, bit 15 =
  * TASX_TXSEG_SCRATCH), then per segment 3 entries: frame_off (32) | payload
  * << 32, pos (32) | (tx_len & 0xffff) << 32, tx_base (32) | (tx_len >> 16) <<
- * 32; every entry | tag << 48 */
+ * 32; every entry | tag << 48.  Round 5: a TX slot uses the whole 1 KiB
+ * (TASX_SRV_WORDS entries, 41 segments: TAS's 32-segment flush in one slot);
+ * the server reads the entries past TASX_SRV_FB in a second round trip, once
+ * the first has shown a taken header (the host wrote them before it). */
 #define TASX_SRV_SEG 0x8000u
-#define TASX_SRV_SEGS 20u
+#define TASX_SRV_WORDS 126u /* entry words in a 1 KiB slot */
+#define TASX_SRV_SEGS 41u   /* (TASX_SRV_WORDS - TASX_SRV_SEGW0) / 3 */
 #define TASX_SRV_SEGW0 3u /* entry of segment 0's first word */
 #define TASX_SRV_FB 64u    /* frames per slot */
 #define TASX_SRV_KMAX 8u   /* workgroups per ring, a divisor of TASX_SRV_RING */

@@ -134,9 +134,15 @@ __device__ __noinline__ u32x4 gather16(const uint8_t *shm, uint32_t off, uint64_
 // segment i on the 16 lanes of one DPP row (lane gl); any frame layout
 // The descriptor (tasx_tx_seg, two 16-byte words) is passed in: txseg_row
 // below loads it from p.segs; the flush server (server_kernels.hip) decodes it
-// from its ring slot.
+// from its ring slot.  rbound: the bytes from the frame start the row may read
+// (whole chunks); a frame whose ip.total_length reaches past its written bytes
+// and past rbound is left untouched and the row returns false (the server's
+// frames were validated against their region when submitted: a total_length
+// changed since then must not make the row read beyond the region).  Every
+// other row returns true, those dma_read() rejects (frame untouched) included.
 template <int U, bool NTS, bool WT = false>
-__device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t i, u32x4 d0, u32x4 d1, int gl)
+__device__ __forceinline__ bool txseg_row_d(const tasx_txseg_params &p, uint32_t i, u32x4 d0, u32x4 d1, int gl,
+                                            uint32_t rbound = 0xffffffffu)
 {
   const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
   const uint64_t tx_base = d0.z | ((uint64_t) d0.w << 32);
@@ -146,7 +152,7 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
   if (!ok) {
     if (gl == 15 && p.out)
       stg(p.out, i, 0u);
-    return;
+    return true;
   }
   uint8_t *const f = p.frames + frame_off;
   uint8_t *const ip = f + p.ip_off;
@@ -171,6 +177,8 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
   // ---- up-front loads: IPv4 header words, total_length, this lane's header
   // chunk, its boundary chunk's window, the straddle chunk's piece-2 window
   const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
+  // (the row's lanes agree: one uniform load)
+  const bool tl_ok = p.ip_off + tl <= (uint32_t) fend || ((p.ip_off + tl + 15u) & ~15u) <= rbound;
   const int wl = min(gl, 9);
   const uint32_t w_ = ld8(ip + 2 * wl) | (ld8(ip + 2 * wl + 1) << 8);
   const uint32_t w = gl < 10 ? w_ : 0u;
@@ -201,7 +209,7 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
     for (int u = 0; u < U; ++u) {
       const int k = base + gl + 16 * u;
       const bool in = k >= nhc && k < kpay && k != ks;
-      if (in) {
+      if (in && tl_ok) {
         uint8_t *const cp = c0 + 16 * k;
         if (WT)
           wt_store16(cp, a[u]);
@@ -213,6 +221,11 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
       const uint32_t t = sad4(a[u], acc);
       acc = in ? t : acc;
     }
+  }
+  if (!tl_ok) {
+    if (gl == 15 && p.out)
+      stg(p.out, i, 0u);
+    return false;
   }
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   const int sum_lo = (int) p.l4_off, sum_end = sum_lo + (int) len, sum_hi = min(sum_end, fend);
@@ -297,12 +310,13 @@ __device__ __forceinline__ void txseg_row_d(const tasx_txseg_params &p, uint32_t
     else
       store_range(c0 + b0, v, max(fh - b0, 0), min(fh + fend - b0, 16), false);
   }
+  return true;
 }
 
 template <int U, bool NTS>
 __device__ __forceinline__ void txseg_row(const tasx_txseg_params &p, uint32_t i, int gl)
 {
-  txseg_row_d<U, NTS>(p, i, ld16((const u32x4 *) p.segs, 2 * i), ld16((const u32x4 *) p.segs, 2 * i + 1), gl);
+  (void) txseg_row_d<U, NTS>(p, i, ld16((const u32x4 *) p.segs, 2 * i), ld16((const u32x4 *) p.segs, 2 * i + 1), gl);
 }
 
 

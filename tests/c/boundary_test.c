@@ -14,6 +14,11 @@
  * TXBUF_SIZE batch, staged, zero-copy (mbufs in a registered pool) and through
  * the shared feeder, with
  * the thread-bound context (TASX_CTX_SELF) as the only context plumbing.
+ * Then the error contract (ABI 8): a flush server whose
+ * kernel is aborted with the batch queued fails the flush; the glue takes the
+ * unfinished frames back, finishes them with TAS's CPU path (the test's DPDK
+ * stand-in, tests/c/rte_standin.h) and goes on, and the next flush runs on the
+ * GPU again -- every frame bit-exact against the fixture.
  *
  *   usage: boundary_test tests/golden/ref_frames.bin
  */
@@ -38,6 +43,8 @@ static inline uint16_t tx_xsum_enable(struct network_buf_handle *nbh, struct ip_
   abort(); /* the offload branch is not under test */
 }
 
+/* TAS links DPDK for its CPU checksums; the test links this stand-in */
+#include "rte_standin.h"
 #include "tas_glue.h"
 
 /* the unit test's dummy mbuf: buf_addr points data_off bytes past the header */
@@ -180,10 +187,49 @@ int main(int argc, char **argv)
     return 1;
   }
 
+  /* a failed flush: the flush server's kernel aborted while the context is
+   * attached, then a batch recorded and flushed.  tx_flush_checksums sees the
+   * error and finishes every frame on the CPU; TAS keeps running. */
+  if (tasx_server_start(0) != 0 || tasx_ctx_use_server(TASX_CTX_SELF, 1) != 0) {
+    fprintf(stderr, "server: %s\n", tasx_last_error());
+    return 1;
+  }
+  CHECK(tasx_server_abort(0) == 0, "server abort: %s", tasx_last_error());
+  unsigned recovered = 0;
+  {
+    for (uint32_t i = 0; i < n; i++) { /* record as run_batch does */
+      struct fake_mbuf *m = pm[i];
+      memcpy(m->buf_addr, frames + (size_t) i * room, room);
+      m->data_len = (uint16_t) r[i].len;
+      struct pkt_tcp *p = (struct pkt_tcp *) m->buf_addr;
+      if (r[i].kind == 2)
+        fast_flows_kernelxsums((struct network_buf_handle *) m, p);
+      else
+        tcp_checksums((struct network_buf_handle *) m, p, p->ip.src, p->ip.dest, f_beui16(p->ip.len) - sizeof(p->ip));
+    }
+    CHECK(tasx_flush(TASX_CTX_SELF) != 0, "a flush through an aborted server succeeded");
+    recovered = tasx_finish_unfinished();
+    CHECK(recovered == n, "%u frames handed back, expected %u", recovered, n);
+    CHECK(tasx_pending(TASX_CTX_SELF) == 0, "frames left pending after the recovery");
+    for (uint32_t i = 0; i < n; i++) {
+      const struct pkt_tcp *p = (const struct pkt_tcp *) pm[i]->buf_addr;
+      CHECK(p->ip.chksum == r[i].ip && p->tcp.chksum == r[i].tcp, "recovered frame %u: %04x/%04x, expected %04x/%04x",
+            i, p->ip.chksum, p->tcp.chksum, r[i].ip, r[i].tcp);
+    }
+  }
+  /* the context detached from the gone kernel; the next flush is the GPU's again */
+  CHECK(tasx_server_stop(0) == 0, "server stop after the recovery: %s", tasx_last_error());
+  tasx_ctx_stats(TASX_CTX_SELF, &zc0, &st0);
+  run_batch("after-recovery", pm, frames, r, 0, n, room);
+  tasx_ctx_stats(TASX_CTX_SELF, &zc1, &st1);
+  CHECK(zc1 == zc0 + 1, "the flush after the recovery did not run on the GPU");
+
   tasx_ctx_destroy(TASX_CTX_SELF);
   tasx_set_thread_ctx(TASX_CTX_SELF);
   CHECK(tasx_thread_ctx() < 0, "thread context still bound");
   printf("boundary_test: %u frames (unit-test KAT + %u-frame tx_flush batch), staged, zero-copy and feeder: %s\n", n,
          n - 1, fails ? "FAILED" : "OK");
+  printf("boundary_test: aborted flush server, %u frames finished by the glue's CPU path, then the GPU again: %s\n",
+         recovered, fails ? "FAILED" : "OK");
   return fails ? 1 : 0;
 }

@@ -9,6 +9,10 @@
  * (tas/fast/fastemu.h:97-102, the offload branch, untouched) and the opaque
  * struct network_buf_handle (tas/fast/network.h:37).
  *
+ * It also provides the CPU checksum functions TAS's own build links from DPDK
+ * (rte_ipv4_cksum, rte_ipv4_udptcp_cksum; here tests/c/rte_standin.h): the
+ * glue's error recovery finishes the frames libtasx hands back with them.
+ *
  * Context plumbing: tcp_checksums() and fast_flows_kernelxsums() carry no
  * dataplane_context (fast_flows.c:1058,1071), but each fast-path thread runs
  * exactly one context (dataplane_loop, tas/fast/fastemu.c:142), so the thread
@@ -36,8 +40,10 @@ static inline void tcp_checksums(struct network_buf_handle *nbh,
   } else {
     p->tcp.chksum = 0;
     if (tasx_tcp_checksums(TASX_CTX_SELF, nbh, p, ip_s.x, ip_d.x, l3_paylen) != 0) {
-      fprintf(stderr, "tcp_checksums: %s\n", tasx_last_error());
-      abort(); /* as tx_send on a full TX buffer, fastemu.h:86-89 */
+      /* not recorded (the context's pending capacity): this frame takes
+       * TAS's own CPU path, the reference's #else branch */
+      p->ip.chksum = rte_ipv4_cksum((void *) &p->ip);
+      p->tcp.chksum = rte_ipv4_udptcp_cksum((void *) &p->ip, (void *) &p->tcp);
     }
   }
 }
@@ -51,14 +57,37 @@ static inline void fast_flows_kernelxsums(struct network_buf_handle *nbh,
       f_beui16(p->ip.len) - sizeof(p->ip));
 }
 
+/* Error recovery (ABI 8): after any failed libtasx call the frames the GPU
+ * did not finish come back from tasx_take_unfinished and take TAS's own CPU
+ * path (fast_flows.c:1065-1067); returns how many did */
+static inline unsigned tasx_finish_unfinished(void)
+{
+  tasx_frame_ref fr[64];
+  unsigned done = 0;
+  int k;
+  while ((k = tasx_take_unfinished(TASX_CTX_SELF, fr, 64)) > 0) {
+    for (int i = 0; i < k; i++) {
+      struct ip_hdr *ip = (struct ip_hdr *) fr[i].ip;
+      struct tcp_hdr *tcp = (struct tcp_hdr *) fr[i].l4;
+      ip->chksum = 0;
+      tcp->chksum = 0;
+      ip->chksum = rte_ipv4_cksum((void *) ip);
+      tcp->chksum = rte_ipv4_udptcp_cksum((void *) ip, (void *) tcp);
+    }
+    done += (unsigned) k;
+  }
+  return done;
+}
+
 /* the checksum part of tx_flush (tas/fast/fastemu.c:544-566), before
- * network_send(): every recorded frame gets both fields */
+ * network_send(): every recorded frame gets both fields -- from the GPU, or,
+ * when its flush fails, from the CPU path above; TAS keeps running */
 static inline void tx_flush_checksums(void)
 {
   if (!config.fp_xsumoffload && tasx_pending(TASX_CTX_SELF) > 0 &&
       tasx_flush(TASX_CTX_SELF) != 0) {
-    fprintf(stderr, "tx_flush: tasx_flush: %s\n", tasx_last_error());
-    abort();
+    fprintf(stderr, "tx_flush: tasx_flush: %s; finishing on the CPU\n", tasx_last_error());
+    tasx_finish_unfinished();
   }
 }
 

@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 7
+    assert L.tasx_abi_version() == 8
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -103,6 +103,11 @@ def test_abi_version_and_errors_without_gpu(L):
     assert L.tasx_ctx_server_flushes(3, None) == -errno.EINVAL
     assert L.tasx_ctx_register_shm(3, None, 0) == -errno.EINVAL
     assert L.tasx_server_tx_segments(3, None, 0, None) == -errno.EINVAL
+    # ABI 8 error recovery: argument errors before any HIP call
+    assert L.tasx_take_unfinished(3, None, 0) == -errno.EINVAL
+    assert L.tasx_take_unfinished_segs(3, None, 0) == -errno.EINVAL
+    assert L.tasx_server_abort(0) == -errno.EINVAL
+    assert L.tasx_server_abort(-1) == -errno.ENODEV
     if L.tasx_device_count() <= 0:  # no GPU in this container: start fails, nothing launched
         assert L.tasx_server_start(0) in (-errno.EIO, -errno.ENODEV)
 

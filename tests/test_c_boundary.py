@@ -77,8 +77,12 @@ def test_boundary_binary_links_only_libtasx():
 def test_c_boundary_glue_on_gpu():
     """INTEGRATION.md's glue, compiled against the reference's types, over fake
     mbufs: the unit-test frame and a 32-frame tx_flush batch, staged,
-    zero-copy and through the shared feeder, bit-exact against the fixture."""
+    zero-copy and through the shared feeder, bit-exact against the fixture;
+    then a flush through an aborted flush server, recovered by the glue."""
     assert BIN.exists(), f"{BIN} not built (python -c 'import __graft_entry__ as g; g.build()' with /root/reference)"
     r = subprocess.run([str(BIN), str(FIXTURE)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "staged, zero-copy and feeder: OK" in r.stdout
+    # ABI 8 error contract: an aborted server fails the flush, the glue finishes
+    # all 33 frames on TAS's CPU path (bit-exact), the next flush is the GPU's
+    assert "aborted flush server, 33 frames finished by the glue's CPU path, then the GPU again: OK" in r.stdout

@@ -31,6 +31,19 @@ def _lib():
         pass
 
 
+@pytest.fixture(autouse=True)
+def _stop_server_after_each_test():
+    """A test that fails between its server_start and its server_stop must not
+    fail every later test with "already running": after each test (its own
+    finally blocks have destroyed its contexts, which detaches them) stop the
+    server if one is still running."""
+    yield
+    try:
+        xsum.server_stop(0)
+    except xsum.TasxError:
+        pass  # not running (the test stopped it)
+
+
 def _frames(nframes: int, seed: int, short: bool = True):
     """tx_flush-shaped frames (data segments of 0..1448 B, pure ACKs) at a
     2048 B mbuf stride in a pinned region, checksum fields stale."""
@@ -529,7 +542,7 @@ def test_server_tx_segments(oracle, odd, shm_mem):
         xsum.flush_wait(14, tickets[-1])
         np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
         np.testing.assert_array_equal(hf.array[fr.size:fr.size + 4096], tail_ref[:4096])
-        assert xsum.server_flushes(14) == 3 * 2 + 1     # 32 segments: two slots (20 + 12)
+        assert xsum.server_flushes(14) == 3 * 1 + 1     # 32 segments: one slot (up to 41)
         xsum.use_server(14, False)
         xsum.server_stop(0)
     finally:
@@ -592,3 +605,192 @@ def test_server_beside_feeder_and_device_batches(oracle):
                 stop(0)
             except xsum.TasxError:
                 pass
+
+
+def _finish_on_cpu(oracle, pin, refs):
+    """The glue's recovery step: the frames handed
+    back by tasx_take_unfinished take TAS's CPU path (here the oracle's
+    tcp_checksums, in place)."""
+    offs = np.array([ip - 14 - pin.addr for ip, l4 in refs], np.uint64)
+    assert all(l4 == ip + 20 for ip, l4 in refs)
+    if len(offs):
+        oracle.tcp4_batch(pin.array, len(offs), offsets=offs, inplace=True)
+    return offs
+
+
+def test_server_abort_hands_back_unfinished(oracle):
+    """ABI 8 error contract: batches queued to a server whose
+    kernel is aborted come back through tasx_take_unfinished; finished on the
+    CPU, every frame equals the oracle's.  Batches the server completed before
+    the abort are not handed back; the context works again afterwards (zero-copy
+    flush of its own), the server stops once it is detached, and restarts."""
+    n, nb = 32, 6
+    xsum.server_start(0)
+    cx = _Ctxs([5])
+    try:
+        pin, frames = _frames(nb * n, 900, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nb * n)
+        xsum.register_frames(5, pin.addr, pin.nbytes)
+        xsum.use_server(5)
+        for i in range(n):                               # one batch the server finishes
+            xsum.tcp_checksums(5, pin.addr + i * 2048)
+        xsum.tx_flush(5)
+        xsum.server_abort(0)
+        for b in range(1, nb):                           # queued to the gone kernel
+            for i in range(n):
+                xsum.tcp_checksums(5, pin.addr + (b * n + i) * 2048)
+            xsum.flush_submit(5)
+        with pytest.raises(xsum.TasxError):
+            xsum.flush_wait(5, nb)
+        back = xsum.take_unfinished(5)
+        offs = _finish_on_cpu(oracle, pin, back)
+        assert sorted(offs.tolist()) == [k * 2048 for k in range(n, nb * n)]
+        np.testing.assert_array_equal(pin.array[:ref.size], ref)
+        assert xsum.pending(5) == 0 and xsum.take_unfinished(5) == []
+        assert xsum.flush_poll(5, nb) is True            # every ticket settled
+        with pytest.raises(xsum.TasxError):
+            xsum.use_server(5)                           # the aborted server takes no context
+        xsum.server_stop(0)                              # detached by the settle
+        pin.array[:frames.size] = frames                 # the context's own (zero-copy) flush
+        for i in range(n):
+            xsum.tcp_checksums(5, pin.addr + i * 2048)
+        xsum.tx_flush(5)
+        np.testing.assert_array_equal(pin.array[:n * 2048], ref[:n * 2048])
+        xsum.server_start(0)                             # and a new server serves it again
+        xsum.use_server(5)
+        for i in range(n):
+            xsum.tcp_checksums(5, pin.addr + (n + i) * 2048)
+        pin.array[n * 2048:2 * n * 2048] = frames[n * 2048:2 * n * 2048]
+        xsum.tx_flush(5)
+        np.testing.assert_array_equal(pin.array[:2 * n * 2048], ref[:2 * n * 2048])
+        xsum.use_server(5, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_detach_from_gone_kernel(oracle):
+    """a context attached to a server whose kernel has gone, with
+    batches outstanding, detaches (-EIO once, its frames in the unfinished
+    store), so the server stops and a new one starts; destroying such a context
+    needs no detach of its own."""
+    n = 32
+    xsum.server_start(0)
+    cx = _Ctxs([6, 7])
+    try:
+        pins = []
+        for k, c in enumerate((6, 7)):
+            pin, frames = _frames(3 * n, 950 + k, short=False)
+            cx.pins.append(pin)
+            pins.append((pin, _ref(oracle, frames, 3 * n)))
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_server(c)
+        xsum.server_abort(0)
+        for k, c in enumerate((6, 7)):
+            for b in range(3):
+                for i in range(n):
+                    xsum.tcp_checksums(c, pins[k][0].addr + (b * n + i) * 2048)
+                xsum.flush_submit(c)
+        with pytest.raises(xsum.TasxError):
+            xsum.use_server(6, False)                    # -EIO: detached from the gone kernel
+        xsum.use_server(6, False)                        # already detached
+        back = xsum.take_unfinished(6)
+        assert len(back) == 3 * n
+        _finish_on_cpu(oracle, pins[0][0], back)
+        np.testing.assert_array_equal(pins[0][0].array[:pins[0][1].size], pins[0][1])
+        xsum.ctx_destroy(7)                              # still attached: destroy detaches it
+        cx.ids.remove(7)
+        xsum.server_stop(0)
+        xsum.server_start(0)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_tx_segments_abort_and_bad_offsets(oracle):
+    """TX segments queued to an aborted server come back through
+    tasx_take_unfinished_segs as submitted; built on the CPU (the oracle's
+    flow_tx_read + tcp_checksums) every frame equals the oracle's.  A
+    descriptor whose frame_off would wrap the bounds check is refused."""
+    n = 40
+    shm, fr, segs, sl = pktgen.tx_segments(n, tx_len=4096, nflows=8, seed=0x7A7, room=pktgen.MBUF_ROOM)
+    exp_fr = fr.copy()
+    oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    xsum.server_start(0)
+    cx = _Ctxs([9])
+    try:
+        hf = xsum.PinnedBuffer(fr.size + 4096)
+        hs = xsum.PinnedBuffer(sl + 64)
+        cx.pins += [hf, hs]
+        hs.array[:sl] = shm[:sl]
+        hf.array[:] = 0
+        hf.array[:fr.size] = fr
+        xsum.register_frames(9, hf.addr, hf.nbytes)
+        xsum.register_shm(9, hs.addr, sl)
+        xsum.use_server(9)
+        for off in (0xFFFFFFFFFFFFFFF0, hf.nbytes, hf.nbytes - 16):
+            bad = segs[:1].copy()
+            bad["frame_off"] = off
+            with pytest.raises(xsum.TasxError):
+                xsum.server_tx_segments(9, bad)
+        xsum.server_abort(0)
+        t = xsum.server_tx_segments(9, segs)             # 40 segments: two slots of 20
+        with pytest.raises(xsum.TasxError):
+            xsum.flush_wait(9, t)
+        assert xsum.take_unfinished(9) == []
+        back = xsum.take_unfinished_segs(9)
+        assert len(back) == n
+        np.testing.assert_array_equal(np.sort(back, order="frame_off"), np.sort(segs, order="frame_off"))
+        frames_now = hf.array[:fr.size].copy()
+        oracle.tx_segment_batch(shm, sl, frames_now, back)
+        np.testing.assert_array_equal(frames_now, exp_fr)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_shm_registered_by_two_contexts(oracle):
+    """every core registers the same tas_shm; the pin is counted,
+    so destroying the first context to register it leaves it mapped for the
+    others -- TX segments through the second context still build right."""
+    n = 32
+    shm, fr, segs, sl = pktgen.tx_segments(n, tx_len=4096, nflows=4, seed=0x5A5, room=pktgen.MBUF_ROOM)
+    exp_fr = fr.copy()
+    oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    raw_shm = np.zeros(sl + 8192, np.uint8)              # plain pages: pinned by the library
+    o = (-raw_shm.ctypes.data) % 4096
+    shm_arr, shm_addr = raw_shm[o:o + sl + 64], raw_shm.ctypes.data + o
+    shm_arr[:sl] = shm[:sl]
+    cx = _Ctxs([11, 12])
+    try:
+        hf = xsum.PinnedBuffer(fr.size + 4096)
+        cx.pins.append(hf)
+        hf.array[:] = 0
+        hf.array[:fr.size] = fr
+        for c in (11, 12):
+            xsum.register_shm(c, shm_addr, sl)
+        xsum.register_frames(12, hf.addr, hf.nbytes)
+        xsum.ctx_destroy(11)                             # the first registrant goes
+        cx.ids.remove(11)
+        xsum.server_start(0)
+        xsum.use_server(12)
+        xsum.flush_wait(12, xsum.server_tx_segments(12, segs))
+        np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
+        xsum.use_server(12, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_left_running_by_a_failed_test_a():
+    """(With _b.) A test that fails with its server started: the per-test
+    fixture stops it, so the next test's server_start succeeds."""
+    xsum.server_start(0)
+    xsum.ctx_init(13, 0, 1 << 20)
+    xsum.ctx_destroy(13)                                 # no server_stop: as a failed test leaves it
+
+
+def test_server_left_running_by_a_failed_test_b():
+    xsum.server_start(0)
+    xsum.server_stop(0)
