@@ -1135,7 +1135,7 @@ def fastpath_mt_leg(flushes: int = 3000) -> dict:
     return res
 
 
-def server_cost_leg(rank: int, rot: int, flushes: int = 40000) -> dict:
+def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
     """What the resident flush server costs the device-resident work on the
     same GPU: the headline batch (2,000 launches) and the
     TX segment build (800) timed with the server stopped, started but idle (its
@@ -1143,7 +1143,10 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 40000) -> dict:
     started with 8 fast-path threads flushing through it meanwhile (32-frame
     batches, 3 in flight each: tasxb_fastpath_mt in a second thread; the
     flush rate of that run, which also spans the parts without device work, is
-    reported beside it).  Event-timed launches, each state's median of 3."""
+    reported beside it; it is sized to outlast the timed launches, and
+    busy_overlap_complete says whether it did).  Event-timed launches, each
+    state's median of 3; "stopped" is measured before and after the other
+    states and the lower taken (the first pass can still meet clocks ramping)."""
     import threading
     dev = torch.cuda.current_device()
     wl = Tcp4Workload(rot, pktgen.SEED + 7000 + rank, host=False)
@@ -1192,6 +1195,8 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 40000) -> dict:
     except xsum.TasxError:
         batches_after = None  # the flush run had already finished: the overlap was partial
     th.join()
+    after = measure()
+    res["states"]["stopped"] = {k: min(v, after[k]) for k, v in res["states"]["stopped"].items()}
     res["states"]["busy_8x3"] = busy
     res["busy_flush_run"] = flush
     res["busy_overlap_complete"] = batches_after is not None

@@ -1,6 +1,8 @@
 /*
  * tasx_ab.h -- extra entry points of the A/B build of libtasx
- * (tas_amd/_lib/libtasx_ab.so, compiled with -DTASX_AB; used by tools/ and the
+ * (tas_amd/_lib/libtasx_ab.so: the product's own objects plus
+ * tas_amd/csrc/ab/, which hooks its variants and knobs into the product
+ * launchers through tasx_ext; used by tools/, bench.py's live ceilings and the
  * variant tests, never by the product path).  Everything in tasx_xsum.h is
  * exported as well, and tasx_set_kernel_variant() also accepts:
  *   1  the first-generation group-per-packet kernels (raw_cksum_kernel,
@@ -28,9 +30,17 @@
  *      the verify blocks; slower wherever ACKs are present
  *   28  tcp4_tas14_kernel<hints_sorted>: per-frame hints, a block's rows take
  *      its frames long ones first, so waves of short frames load one chunk
- * and the environment knobs TASX_TAS14_*_LDS, TASX_WAVE_TCP4_LDS (KiB of
- * reserved LDS) and TASX_TXSEG_DEBUG (TX segment diagnostics kernels; 29 =
- * tx_segment_wave_kernel, one segment per wave from aligned loads) apply.
+ *   27, 29..43  RX-pass and row forms (tasx_rx_batch_dev split grids, lookup
+ *      placements, timing ablations; profiles/r03, profiles/r04)
+ *   45..48  RAW rows of 32 / 64 lanes and without the residency cap
+ * The environment knobs, read once at load: TASX_TAS14_*_LDS and
+ * TASX_WAVE_TCP4_LDS (KiB of reserved LDS for the A/B variants' launches),
+ * TASX_TXSEG_DEBUG (TX segment diagnostics kernels; 29 =
+ * tx_segment_wave_kernel, one segment per wave from aligned loads), TASX_XRUN
+ * (XCD order of every grid), TASX_FEEDER_SWEEPS, and for the flush server
+ * TASX_SRV_K (workgroups per ring), TASX_SRV_HOT_US / TASX_SRV_COLD_US (poll
+ * backoff), TASX_SRV_SEGMAX (TX segments per slot), TASX_SRV_DIAG (its
+ * timing form: tasx_ab_server_diag).
  */
 #ifndef TASX_AB_H_
 #define TASX_AB_H_

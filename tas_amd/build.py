@@ -17,14 +17,18 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "tas_amd" / "csrc"
 OUT_DIR = ROOT / "tas_amd" / "_lib"
 LIB = OUT_DIR / "libtasx.so"
-# the A/B build (-DTASX_AB): the product kernels plus the kernels and knobs kept
-# for comparisons (include/tasx_ab.h); used by tools/ and the variant tests only
+# the A/B build: the product's own objects plus tas_amd/csrc/ab/ (the kernels
+# and knobs kept for comparisons, include/tasx_ab.h), which hook in through
+# tasx_ext (tasx_kernels.h); used by tools/, bench.py's ceilings and the
+# variant tests only
 LIB_AB = OUT_DIR / "libtasx_ab.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
 HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip", "flow_kernels.hip", "server_kernels.hip"]
 C_SRCS = ["tasx_host.c"]
+AB_HIP_SRCS = ["ab/ab_xsum.hip", "ab/ab_txseg.hip", "ab/ab_flow.hip", "ab/ab_server.hip"]
+AB_C_SRCS = ["ab/ab_host.c"]
 
 
 def _run(cmd: list[str]) -> None:
@@ -36,27 +40,33 @@ def _stale(lib: Path) -> bool:
     if not lib.exists():
         return True
     t = lib.stat().st_mtime
-    deps = list(CSRC.glob("*")) + list((ROOT / "include").glob("*.h")) + [Path(__file__)]
+    deps = (list(CSRC.glob("*")) + list((CSRC / "ab").glob("*")) + list((ROOT / "include").glob("*.h")) +
+            [Path(__file__)])
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _build_one(lib: Path, defines: list[str], tag: str, extra_hip_flags: list[str] | None) -> Path:
+def _objects(hip_srcs: list[str], c_srcs: list[str], extra_hip_flags: list[str] | None) -> list[Path]:
     OUT_DIR.mkdir(parents=True, exist_ok=True)
     objs = []
     hipcc = str(ROCM / "bin" / "hipcc")
-    for s in HIP_SRCS:
-        o = OUT_DIR / (Path(s).stem + tag + ".o")
+    for s in hip_srcs:
+        o = OUT_DIR / (Path(s).stem + ".o")
         _run([hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-              "-Wall", "-Werror", "-Wno-unused-function", *defines,
+              "-Wall", "-Werror", "-Wno-unused-function",
               "-I", str(ROOT / "include"), *(extra_hip_flags or []),
               "-c", str(CSRC / s), "-o", str(o)])
         objs.append(o)
-    for s in C_SRCS:
-        o = OUT_DIR / (Path(s).stem + tag + ".o")
-        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror", *defines,
+    for s in c_srcs:
+        o = OUT_DIR / (Path(s).stem + ".o")
+        _run(["gcc", "-std=gnu99", "-O2", "-fPIC", "-Wall", "-Werror",
               "-D__HIP_PLATFORM_AMD__", "-I", str(ROCM / "include"),
               "-I", str(ROOT / "include"), "-c", str(CSRC / s), "-o", str(o)])
         objs.append(o)
+    return objs
+
+
+def _link(lib: Path, objs: list[Path]) -> Path:
+    hipcc = str(ROCM / "bin" / "hipcc")
     tmp = lib.with_suffix(".so.tmp")
     # -Bsymbolic: each library's internal calls bind to its own definitions, so
     # the product and the A/B build can be loaded into one process side by side
@@ -76,10 +86,17 @@ BENCH_SRC = ROOT / "tas_amd" / "benchsrc" / "bench_loop.c"
 def build(force: bool = False, extra_hip_flags: list[str] | None = None, ab: bool = True) -> Path:
     """Build libtasx.so (and, with ab=True, libtasx_ab.so; and the bench loop
     library) when stale; returns the product library's path."""
+    prod_objs = None
     if force or _stale(LIB):
-        _build_one(LIB, [], "", extra_hip_flags)
+        prod_objs = _objects(HIP_SRCS, C_SRCS, extra_hip_flags)
+        _link(LIB, prod_objs)
     if ab and (force or _stale(LIB_AB)):
-        _build_one(LIB_AB, ["-DTASX_AB"], "_ab", extra_hip_flags)
+        if prod_objs is None:
+            prod_objs = [OUT_DIR / (Path(s).stem + ".o") for s in HIP_SRCS + C_SRCS]
+            if not all(o.exists() for o in prod_objs):
+                prod_objs = _objects(HIP_SRCS, C_SRCS, extra_hip_flags)
+        # the A/B library: the product's own objects, plus its variants and knobs
+        _link(LIB_AB, prod_objs + _objects(AB_HIP_SRCS, AB_C_SRCS, extra_hip_flags))
     for out, dep, name in ((LIB_BENCH, LIB, "tasx"), (LIB_BENCH_AB, LIB_AB, "tasx_ab")):
         if not dep.exists():
             continue

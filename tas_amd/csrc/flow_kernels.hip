@@ -13,475 +13,22 @@
 // chains are in flight per CU.  CRC32C is computed bit by bit on the VALU by default (a
 // slice-by-4 variant from LDS tables built at compile time measured the same:
 // the CRC is not on the critical path).
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-
-#include "tasx_kernels.h"
-#include "xsum_device.h"
-
-namespace {
-
-// CRC32C slice-by-4 tables: CrcTables / make_crc_tables / kCrc (xsum_device.h)
-
-// byte-position tables for the whole 12-byte key: CRC32C from state 0 is
-// linear, so flow_hash = XOR over key byte positions p of b[p][key[p]], with
-// b[p][x] = CRC of byte x followed by 11 - p zero bytes: 12 independent LDS
-// reads instead of a 96-step dependent chain
-struct CrcKeyTables {
-  uint32_t t[12][256];
-};
-
-constexpr CrcKeyTables make_crc_key_tables()
-{
-  CrcKeyTables T{};
-  const CrcTables S = make_crc_tables();
-  for (uint32_t i = 0; i < 256; ++i)
-    T.t[11][i] = S.t[0][i];
-  for (int p = 10; p >= 0; --p)
-    for (uint32_t i = 0; i < 256; ++i)
-      T.t[p][i] = (T.t[p + 1][i] >> 8) ^ S.t[0][T.t[p + 1][i] & 0xffu];
-  return T;
-}
-
-__constant__ CrcKeyTables kCrcKey = make_crc_key_tables();
-
-// SSE4.2 crc32 on one 32-bit little-endian word (crc32c_sse42_u32(w, crc)):
-// slice-by-4 from the LDS copy of the tables, or bit by bit on the VALU
-template <bool TAB>
-__device__ __forceinline__ uint32_t crc32c_word(const uint32_t (*t)[256], uint32_t crc, uint32_t w)
-{
-  if constexpr (TAB)
-    return crc32c_u32_tab(t, crc, w);
-  return crc32c_u32(crc, w);
-}
-
-__device__ __forceinline__ uint32_t ld32b(const uint8_t *p)
-{
-  return ld8(p) | (ld8(p + 1) << 8) | (ld8(p + 2) << 16) | (ld8(p + 3) << 24);
-}
-
-// the 16 bytes starting at address x, from the one or two aligned chunks that
-// hold its first n (<= 16) bytes (a second chunk is loaded only if needed)
-__device__ __forceinline__ u32x4 load_window(const uint8_t *x, int n)
-{
-  const uintptr_t a = (uintptr_t) x;
-  const u32x4 *c0 = (const u32x4 *) (a & ~(uintptr_t) 15);
-  const u32x4 *c1 = (const u32x4 *) ((a + (uintptr_t) n - 1) & ~(uintptr_t) 15);
-  return funnel16(ld16(c0, 0), ld16(c1, 0), (int) (a & 15));
-}
-
-
-// CRC: 0 bitwise on the VALU, 1 slice-by-4 from LDS, 2 byte-position tables
-// from LDS (3: no CRC, a diagnostic build only -- wrong flow ids); CHUNK: key
-// fields from 16-byte chunk loads (else byte loads)
-enum { kCrcBitwise = 0, kCrcSlice4 = 1, kCrcKeyTab = 2, kCrcNone = 3 };
-constexpr int kFlowFramesPerLane = 2; // the product's frames per lane
-
-// F frames per lane (frames blockIdx.x * 256 F + f * 256 + lane): every
-// level's loads of all F frames are issued together, so each lane keeps F
-// dependent chains in flight -- at 8 waves per SIMD one frame per lane leaves
-// 256K frames two generations of waves deep, each paying the whole chain.
-// NTKEY (round 4, the product): the frame-key loads non-temporal, so the
-// 33.5 MB of streamed frame lines per 256K-frame launch do not evict the
-// table lines from the XCDs' L2s between launches: 256K
-// lookups 11.67-11.73 us against 12.17-12.29 with L2-allocating key loads (A/B
-// 9 now), the same box (profiles/r04/INDEX.md r04d).  NTFS (A/B 10): the
-// flow-state key loads non-temporal too, so that the 2 MiB bucket table alone
-// competes for each XCD's 4 MiB L2: slower (13.33-13.37 us)
-// KPOL >= 0 (A/B 12, 13): the frame keys by a raw buffer load with that
-// cache policy (aux bits: 1 sc0, 2 nt, 16 sc1) -- do uncached forms move fewer
-// bytes per 12-byte key than the non-temporal global load?
-template <int CRC, bool CHUNK, int F = 1, bool NTKEY = false, bool NTFS = false, int KPOL = -1>
-__global__ __launch_bounds__(256) void flow_lookup_kernel(tasx_flow_params p)
-{
-  constexpr bool TAB = CRC == kCrcSlice4;
-  __shared__ uint32_t lt[TAB ? 4 : 1][256];
-  __shared__ uint32_t kt[CRC == kCrcKeyTab ? 12 : 1][256];
-  uint32_t i0[F], i[F], rip[F], lip[F], l4x[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    i0[f] = blockIdx.x * (256u * F) + 256u * (uint32_t) f + threadIdx.x;
-    i[f] = min(i0[f], p.n - 1u); // lanes past the batch repeat the last frame (no store)
-    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    // key = (local = destination, remote = source), network byte order:
-    // ip.src/ip.dst are bytes [12, 20) of the IPv4 header, the ports bytes
-    // [0, 4) of the TCP header
-    if constexpr (CHUNK) {
-      const u32x4 ipw = load_window(fr + p.ip_off + 12, 8), l4w = load_window(fr + p.l4_off, 4);
-      rip[f] = ipw.x;
-      lip[f] = ipw.y;
-      l4x[f] = l4w.x;
-    } else if (p.l4_off == p.ip_off + 20u) {
-      // TAS's layout: ip.src, ip.dst and the ports are 12 contiguous bytes, one
-      // unaligned dwordx3 load (gfx950 global loads take any byte address)
-      u32x3u k;
-      if constexpr (KPOL >= 0) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) p.base, 0, -1, 0x00020000);
-        const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(rs, (uint32_t) (fr - p.base) + p.ip_off + 12u, 0, KPOL);
-        k = u32x3u{w.x, w.y, w.z};
-      } else if constexpr (NTKEY) {
-        k = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
-      } else {
-        k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
-      }
-      rip[f] = k.x;
-      lip[f] = k.y;
-      l4x[f] = k.z;
-    } else {
-      rip[f] = ld32b(fr + p.ip_off + 12);
-      lip[f] = ld32b(fr + p.ip_off + 16);
-      l4x[f] = ld32b(fr + p.l4_off);
-    }
-  }
-  // tables into LDS while the key loads are in flight
-  if constexpr (TAB) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      lt[k][threadIdx.x] = kCrc.t[k][threadIdx.x];
-  }
-  if constexpr (CRC == kCrcKeyTab) {
-#pragma unroll
-    for (int k = 0; k < 12; ++k)
-      kt[k][threadIdx.x] = kCrcKey.t[k][threadIdx.x];
-  }
-  if constexpr (TAB || CRC == kCrcKeyTab)
-    __syncthreads();
-  // flow_hash: crc32c_sse42_u32(ports, crc32c_sse42_u64(lip | rip << 32, 0))
-  uint32_t ports[F], h[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    ports[f] = (l4x[f] >> 16) | (l4x[f] << 16); // tcp.dest | tcp.src << 16
-    if constexpr (CRC == kCrcKeyTab) {
-      h[f] = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        h[f] ^= kt[b][(lip[f] >> (8 * b)) & 0xffu] ^ kt[4 + b][(rip[f] >> (8 * b)) & 0xffu] ^
-                kt[8 + b][(ports[f] >> (8 * b)) & 0xffu];
-    } else if constexpr (CRC == kCrcNone) {
-      h[f] = lip[f] ^ rip[f] ^ ports[f];
-    } else {
-      h[f] = crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, crc32c_word<TAB>(lt, 0u, lip[f]), rip[f]), ports[f]);
-    }
-  }
-  // buckets: entries (h + j) % ht_entries, j < NBSZ, all frames' loaded together
-  uint64_t e[F][TASX_FLOWHT_NBSZ];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
-  // candidates' keys, loaded together (non-candidates read flow 0)
-  bool cand[F][TASX_FLOWHT_NBSZ];
-  uint32_t fid[F][TASX_FLOWHT_NBSZ];
-  u32x3 key[F][TASX_FLOWHT_NBSZ];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-      const uint32_t ffid = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
-      fid[f][j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-      cand[f][j] = (ffid & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
-      const uint8_t *fsk = p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off;
-      if constexpr (NTFS)
-        key[f][j] = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3 *) fsk);
-      else
-        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) fsk;
-    }
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    uint32_t res = TASX_FLOW_NONE;
-#pragma unroll
-    for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j) // first match wins
-      if (cand[f][j] && key[f][j].x == lip[f] && key[f][j].y == rip[f] && key[f][j].z == ports[f])
-        res = fid[f][j];
-    if (i0[f] < p.n) {
-      stg(p.fid_out, i[f], res);
-      if (p.hash_out)
-        stg(p.hash_out, i[f], h[f]);
-    }
-  }
-}
-
-#ifdef TASX_AB
-// The lookup's access pattern with no hashing or key logic (the ceiling its
-// dependent chain allows, tools/flow_ceiling.hip): the 12-byte key of each
-// frame (HBM), then its 4-entry bucket (flowht), then the candidate flow's key
-// line plus three reads of flow 0 (flowst), each level dependent on the last.
-__device__ __forceinline__ uint32_t mix32(uint32_t x)
-{
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  return x;
-}
-
-__global__ __launch_bounds__(256) void flow_pattern_kernel(tasx_flow_params p)
-{
-  constexpr int F = kFlowFramesPerLane; // the product's frames per lane
-  uint32_t i0[F], i[F], h[F], r[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    i0[f] = blockIdx.x * (256u * F) + 256u * (uint32_t) f + threadIdx.x;
-    i[f] = min(i0[f], p.n - 1u);
-    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    // the product's key load (non-temporal since round 4)
-    const u32x3u k = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
-    h[f] = mix32(k.x ^ k.y ^ k.z);
-  }
-  uint64_t e[F][TASX_FLOWHT_NBSZ];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-    r[f] = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-      r[f] += (uint32_t) e[f][j] ^ (uint32_t) (e[f][j] >> 32);
-  }
-  u32x3 key[F][TASX_FLOWHT_NBSZ];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-      const uint32_t fid = j == 0 ? mix32(h[f] ^ r[f]) % p.fs_num : 0u;
-      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst + (uint64_t) fid * p.fs_stride +
-                                                                      p.fs_key_off);
-    }
-#pragma unroll
-  for (int f = 0; f < F; ++f) {
-#pragma unroll
-    for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-      r[f] ^= key[f][j].x ^ key[f][j].y ^ key[f][j].z;
-    if (i0[f] < p.n)
-      stg(p.fid_out, i[f], r[f]);
-  }
-}
-#endif
-
-#ifdef TASX_AB
-// A/B 11: the hash-range-partitioned lookup, two
-// launches.  flow_route_kernel: per frame the key (non-temporal) and its hash
-// (hash_out in frame order), then a 16-byte record {key, frame index} into
-// the region of (bucket slice x = (h mod entries) / (entries / 8), route
-// block) -- LDS counters, no global atomics.  flow_probe_kernel: workgroup b
-// serves slice b mod 8, so (with the observed round-robin placement) every
-// slice's bucket lines are read on one XCD and that XCD's L2 serves its
-// 1/8 of flowht (256 KiB in TAS's table) to all its lookups; then the
-// flow-state check as the product does it (flowst unpartitioned) and fid_out
-// by frame index.
-constexpr uint32_t kRouteFrames = 512;  // frames per route block = records per region
-constexpr uint32_t kProbeRegions = 8;   // regions per probe block
-
-__global__ __launch_bounds__(256) void flow_route_kernel(tasx_flow_params p, u32x4 *rec, uint32_t *cnt)
-{
-  __shared__ uint32_t s_cnt[8];
-  if (threadIdx.x < 8)
-    s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t slice = (p.ht_entries + 7u) / 8u;
-  u32x3u k[2];
-  uint32_t i0[2], i[2];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    i0[f] = blockIdx.x * kRouteFrames + 256u * (uint32_t) f + threadIdx.x;
-    i[f] = min(i0[f], p.n - 1u);
-    const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    k[f] = __builtin_nontemporal_load((__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12));
-  }
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const uint32_t ports = (k[f].z >> 16) | (k[f].z << 16);
-    const uint32_t h = tas_flow_hash(k[f].y, k[f].x, ports);
-    if (i0[f] < p.n) {
-      if (p.hash_out)
-        stg(p.hash_out, i[f], h);
-      const uint32_t x = min((h % p.ht_entries) / slice, 7u);
-      const uint32_t pos = atomicAdd(&s_cnt[x], 1u);
-      rec[(uint64_t) (x * gridDim.x + blockIdx.x) * kRouteFrames + pos] = u32x4{k[f].x, k[f].y, k[f].z, i[f]};
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 8)
-    cnt[threadIdx.x * gridDim.x + blockIdx.x] = s_cnt[threadIdx.x];
-}
-
-__global__ __launch_bounds__(256) void flow_probe_kernel(tasx_flow_params p, const u32x4 *rec, const uint32_t *cnt,
-                                                         uint32_t nrb, uint32_t M)
-{
-  __shared__ uint32_t s_pre[kProbeRegions + 1];
-  const uint32_t g = blockIdx.x % 8u, m = blockIdx.x / 8u;
-  if (threadIdx.x == 0) {
-    uint32_t a = 0;
-    for (uint32_t j = 0; j < kProbeRegions; ++j) {
-      s_pre[j] = a;
-      const uint32_t r = m + j * M;
-      a += r < nrb ? cnt[g * nrb + r] : 0u;
-    }
-    s_pre[kProbeRegions] = a;
-  }
-  __syncthreads();
-  const uint32_t total = s_pre[kProbeRegions];
-  for (uint32_t base = 0; base < total; base += 512u) {
-    uint32_t t[2], idx[2], lip[2], rip[2], ports[2], h[2];
-    bool live[2];
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      t[f] = base + 256u * (uint32_t) f + threadIdx.x;
-      live[f] = t[f] < total;
-      const uint32_t tt = live[f] ? t[f] : 0u;
-      uint32_t j = 0;
-#pragma unroll
-      for (uint32_t q = 1; q < kProbeRegions; ++q)
-        j += tt >= s_pre[q] ? 1u : 0u;
-      const u32x4 v = live[f] ? rec[(uint64_t) (g * nrb + m + j * M) * kRouteFrames + (tt - s_pre[j])]
-                              : u32x4{0u, 0u, 0u, 0u};
-      rip[f] = v.x;
-      lip[f] = v.y;
-      ports[f] = (v.z >> 16) | (v.z << 16);
-      idx[f] = v.w;
-      h[f] = tas_flow_hash(lip[f], rip[f], ports[f]);
-    }
-    uint64_t e[2][TASX_FLOWHT_NBSZ];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j)
-        e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
-    bool cand[2][TASX_FLOWHT_NBSZ];
-    uint32_t fid[2][TASX_FLOWHT_NBSZ];
-    u32x3 key[2][TASX_FLOWHT_NBSZ];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (uint32_t j = 0; j < TASX_FLOWHT_NBSZ; ++j) {
-        const uint32_t ffid = (uint32_t) e[f][j], eh = (uint32_t) (e[f][j] >> 32);
-        fid[f][j] = ffid & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-        cand[f][j] = (ffid & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
-        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
-            (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off);
-      }
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      uint32_t res = TASX_FLOW_NONE;
-#pragma unroll
-      for (int j = (int) TASX_FLOWHT_NBSZ - 1; j >= 0; --j)
-        if (cand[f][j] && key[f][j].x == lip[f] && key[f][j].y == rip[f] && key[f][j].z == ports[f])
-          res = fid[f][j];
-      if (live[f])
-        stg(p.fid_out, idx[f], res);
-    }
-  }
-}
-#endif
-
-} // namespace
-
-#ifdef TASX_AB
-// A/B 11's scratch: records and region counts, grown on demand, never freed
-static u32x4 *g_part_rec;
-static uint32_t *g_part_cnt;
-static size_t g_part_blocks;
-
-static int launch_flow_partitioned(const tasx_flow_params *p, hipStream_t s)
-{
-  const uint32_t nrb = (p->n + kRouteFrames - 1) / kRouteFrames;
-  if (nrb > g_part_blocks) {
-    if (hipMalloc((void **) &g_part_rec, (size_t) 8 * nrb * kRouteFrames * sizeof(u32x4)) != hipSuccess ||
-        hipMalloc((void **) &g_part_cnt, (size_t) 8 * nrb * sizeof(uint32_t)) != hipSuccess)
-      return -1;
-    g_part_blocks = nrb;
-  }
-  const uint32_t M = (nrb + kProbeRegions - 1) / kProbeRegions;
-  tasx_note_kernel("flow_route_kernel + flow_probe_kernel");
-  hipLaunchKernelGGL(flow_route_kernel, dim3(nrb), dim3(256), 0, s, *p, g_part_rec, g_part_cnt);
-  hipLaunchKernelGGL(flow_probe_kernel, dim3(8u * M), dim3(256), 0, s, *p, (const u32x4 *) g_part_rec,
-                     (const uint32_t *) g_part_cnt, nrb, M);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-#endif
-
-#ifdef TASX_AB
-// A/B build only (include/tasx_ab.h): the flow lookup's bare access pattern
-extern "C" int tasx_ab_flow_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t ip_off,
-    const void *flowht, uint32_t ht_entries, const void *flowst, uint32_t fs_num, uint32_t fs_stride,
-    uint32_t fs_key_off, uint32_t *out, void *stream)
-{
-  tasx_flow_params p = {};
-  p.base = (const uint8_t *) base;
-  p.stride = stride;
-  p.n = n;
-  p.ip_off = ip_off;
-  p.flowht = (const uint32_t *) flowht;
-  p.ht_entries = ht_entries;
-  p.flowst = (const uint8_t *) flowst;
-  p.fs_num = fs_num;
-  p.fs_stride = fs_stride;
-  p.fs_key_off = fs_key_off;
-  p.fid_out = out;
-  if (n == 0)
-    return 0;
-  tasx_note_kernel("flow_pattern_kernel");
-  hipLaunchKernelGGL(flow_pattern_kernel, dim3((n + 256u * kFlowFramesPerLane - 1) / (256u * kFlowFramesPerLane)),
-                     dim3(256), 0, (hipStream_t) stream, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-#endif
-
-template <int F, bool NTKEY = false, bool NTFS = false, int KPOL = -1>
-static int launch_flow_f(const char *name, const tasx_flow_params *p, hipStream_t s)
-{
-  const uint64_t blocks = ((uint64_t) p->n + 256u * F - 1) / (256u * F);
-  tasx_note_kernel(name);
-  hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, false, F, NTKEY, NTFS, KPOL>), dim3((uint32_t) blocks), dim3(256), 0, s, *p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
+#include "flow_device.h"
 
 extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream)
 {
   if (p->n == 0)
     return 0;
   hipStream_t s = (hipStream_t) stream;
-  // A/B (TASX_AB builds, tasx_set_kernel_variant; tools/flow_probe.py,
-  // profiles/r01_flow_variants.jsonl): bitwise CRC + byte loads (the product
-  // kernel) 12.6-12.7 us, LDS slice-by-4 12.4-13.0 us, LDS byte-position tables
-  // (5) 12.6 us, 16-byte chunk key loads +1.7 us: the lookup is bound by its
-  // dependent load chain (frame header -> bucket -> flow state), not by the
-  // CRC arithmetic
-#ifdef TASX_AB
-  const dim3 g((uint32_t) (((uint64_t) p->n + 255) / 256)), b(256); // one frame per lane
-  switch (variant) {
-  case 2: tasx_note_kernel("flow_lookup_kernel<bitwise,chunk>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcBitwise, true>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 3: tasx_note_kernel("flow_lookup_kernel<slice4>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-  case 4: tasx_note_kernel("flow_lookup_kernel<slice4,chunk>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcSlice4, true>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-#ifdef TASX_FLOW_NOCRC_DIAG
-  case 5: tasx_note_kernel("flow_lookup_kernel<nocrc>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcNone, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-#else
-  case 5: tasx_note_kernel("flow_lookup_kernel<keytab>"); hipLaunchKernelGGL((flow_lookup_kernel<kCrcKeyTab, false>), g, b, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1;
-#endif
-  case 6: return launch_flow_f<1>("flow_lookup_kernel<f1>", p, s); // 1 / 4 frames per lane
-  case 7: return launch_flow_f<4>("flow_lookup_kernel<f4>", p, s);
-  case 8: return launch_flow_f<3>("flow_lookup_kernel<f3>", p, s);
-  case 9: return launch_flow_f<kFlowFramesPerLane, false>("flow_lookup_kernel<l2key>", p, s); // the round-3 product
-  case 10: return launch_flow_f<kFlowFramesPerLane, true, true>("flow_lookup_kernel<ntfs>", p, s);
-  case 12: case 13: // keys by raw buffer loads: stride mode within 4 GiB, TAS layout
-    if (!p->off && p->l4_off == p->ip_off + 20u && (uint64_t) p->n * p->stride < (1ull << 32)) {
-      if (variant == 12)
-        return launch_flow_f<kFlowFramesPerLane, false, false, 1 | 16>("flow_lookup_kernel<key sc0 sc1>", p, s);
-      return launch_flow_f<kFlowFramesPerLane, false, false, 16 | 2>("flow_lookup_kernel<key sc1 nt>", p, s);
-    }
-    break;
-  case 11: // TAS layout only (one 12-byte key load); other layouts take the product
-    if (p->l4_off == p->ip_off + 20u)
-      return launch_flow_partitioned(p, s);
-    break;
-  default: break;
+  // A/B variants (libtasx_ab.so, ab/ab_flow.hip: CRC forms, frames per
+  // lane, key cache policies, the partitioned lookup): the lookup is bound by
+  // its dependent load chain (frame header -> bucket -> flow state), not by
+  // the CRC arithmetic (profiles/r01_flow_variants.jsonl, profiles/r04)
+  if (variant != 0 && tasx_ext && tasx_ext->flow) {
+    const int r = tasx_ext->flow(p, variant, stream);
+    if (r != TASX_EXT_PASS)
+      return r;
   }
-#else
-  (void) variant;
-#endif
   // two frames per lane: 256K lookups 11.85 us against 12.53 with one and
   // 12.98 with four (register pressure; profiles/r02/r02ca); the frame keys
   // non-temporal (round 4, above)

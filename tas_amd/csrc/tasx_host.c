@@ -71,27 +71,16 @@ int tasx_device_count(void)
  * 0 = automatic */
 static __thread int g_variant = 0;
 
-#ifdef TASX_AB
-static uint64_t *g_diag = NULL;
-
-int tasx_set_diag_buffer(void *dev_buf)
-{
-  g_diag = (uint64_t *) dev_buf;
-  return 0;
-}
-#define TASX_MAX_VARIANT 48
-#else
-#define TASX_MAX_VARIANT 7
-#endif
+/* the A/B build's hooks (tasx_kernels.h); NULL in libtasx.so */
+const tasx_ext_hooks *tasx_ext = NULL;
 
 int tasx_set_kernel_variant(int variant)
 {
-  if (variant < 0 || variant > TASX_MAX_VARIANT)
+  const int maxv = tasx_ext ? tasx_ext->max_variant : 7;
+  if (variant < 0 || variant > maxv)
     return set_err(-EINVAL, "kernel variant %d out of range", variant);
-#ifndef TASX_AB
-  if (variant == 1 || variant == 4 || variant == 5)
+  if (!tasx_ext && (variant == 1 || variant == 4 || variant == 5))
     return set_err(-EINVAL, "kernel variant %d is an A/B build variant (libtasx_ab.so)", variant);
-#endif
   g_variant = variant;
   return 0;
 }
@@ -176,9 +165,7 @@ int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
   p.flen = flen;
   p.flen0 = flen0;
   p.room = room;
-#ifdef TASX_AB
-  p.diag = g_diag;
-#endif
+  p.diag = tasx_ext ? tasx_ext->diag : NULL;
   r = tasx_launch_tcp4(&p, g_variant, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
@@ -298,12 +285,7 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   p.n = n;
   p.ip_off = ip_off;
   p.l4_off = l4_off;
-#ifdef TASX_AB
-  {
-    const char *e = getenv("TASX_TXSEG_DEBUG");
-    p.dbg = e ? (uint32_t) atoi(e) : 0u;
-  }
-#endif
+  p.dbg = 0u;  /* the A/B build's txseg hook sets its diagnostics form */
   if (tasx_launch_txseg(&p, stream) != 0)
     return hip_err(hipGetLastError(), "tx segment kernel launch");
   return 0;
@@ -1343,11 +1325,11 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
   return 0;
 }
 
-#ifdef TASX_AB
-/* A/B test hook: restart the context's tickets at `start` (nothing in flight),
- * so a test can run flushes across the 2^32 wrap.  Every completion word holds
- * `start`, which no upcoming ticket equals (as 0 does after tasx_ctx_init). */
-int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start)
+/* Test support (the A/B build exports it as tasx_ab_ctx_set_tickets):
+ * restart the context's tickets at `start` (nothing in flight), so a test can
+ * run flushes across the 2^32 wrap.  Every completion word holds `start`,
+ * which no upcoming ticket equals (as 0 does after tasx_ctx_init). */
+int tasx_ctx_set_tickets_internal(unsigned ctx_id, uint32_t start)
 {
   struct tasx_ctx *c = get_ctx(ctx_id);
   if (!c)
@@ -1359,7 +1341,6 @@ int tasx_ab_ctx_set_tickets(unsigned ctx_id, uint32_t start)
   c->next_ticket = c->done_ticket = c->local_last = c->fd_done = start;
   return 0;
 }
-#endif
 
 /* Complete every flush up to `upto` whose completion word has arrived, oldest
  * first (the staged path copies its results into the frames); returns 1 when
@@ -1461,36 +1442,11 @@ static size_t staged_rec(uint32_t tl)
   return ((size_t) TASX_TAS_IP_OFF + 20 + staged_l4(tl) + 15) & ~(size_t) 15;
 }
 
-/* A/B: flush kernels that post their own completion word (TASX_FUSED_DONE=1;
- * xsum_kernels.hip block_done) */
-static void fused_done(tasx_tcp4_params *p, uint32_t *word, uint32_t *count, uint32_t seq)
-{
-#ifdef TASX_AB
-  static int on = -1;
-  if (on < 0)
-    on = getenv("TASX_FUSED_DONE") != NULL;
-  if (on) {
-    p->done_word = word;
-    p->done_count = count;
-    p->done_seq = seq;
-  }
-#else
-  (void) p, (void) word, (void) count, (void) seq;
-#endif
-}
-
-/* Post a completion word after the stream's earlier work (A/B: the
- * command-processor write hipStreamWriteValue32 instead of the one-lane
- * kernel, TASX_POST_WRITEVALUE=1) */
+/* Post a completion word after the stream's earlier work (the one-lane
+ * kernel; the command processor's hipStreamWriteValue32 measured no faster,
+ * profiles/r02/INDEX.md) */
 static int post_done(uint32_t *word, uint32_t seq, hipStream_t st)
 {
-#ifdef TASX_AB
-  static int cp_write = -1;
-  if (cp_write < 0)
-    cp_write = getenv("TASX_POST_WRITEVALUE") != NULL;
-  if (cp_write)
-    return hipStreamWriteValue32(st, word, seq, 0) == hipSuccess ? 0 : -1;
-#endif
   return tasx_launch_post_done(word, seq, st);
 }
 
@@ -1517,10 +1473,6 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   p.n = cnt;
   p.off = f->d_off;
   p.flen = f->d_flen;
-#ifdef TASX_AB
-  if (getenv("TASX_FLUSH_HEADER_RECORDS")) /* A/B: round-1 records at the IPv4 header */
-    lead = 0;
-#endif
   if (zc) {
     /* frame starts (ip - 14) where the region holds them: the TAS-layout
      * kernels (tcp4_tas14_kernel<hints,offs>); else records at the header */
@@ -1560,11 +1512,10 @@ static int flush_launch(struct tasx_ctx *c, uint32_t t, uint32_t cnt, int zc)
   f->n = cnt;
   f->zerocopy = zc;
   f->ticket = t;
-  fused_done(&p, c->d_done + DONE_STRIDE * (uint32_t) s, c->d_count + DONE_STRIDE * (uint32_t) s, t);
   /* a failed launch leaves the frames pending (ctx_settle hands them back) */
   if (tasx_launch_tcp4(&p, g_variant, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
-  if (!tasx_last_launch_posted_done() && post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
+  if (post_done(c->d_done + DONE_STRIDE * (uint32_t) s, t, c->st[0]) != 0)
     return hip_err(hipGetLastError(), "completion-word launch");
   c->local_last = t;
   c->next_ticket = t;
@@ -1811,10 +1762,9 @@ static int feeder_launch(struct feeder *F, struct fsweep *w, uint32_t seq)
   p.ip_off = TASX_TAS_IP_OFF;
   p.l4_off = TASX_TAS_L4_OFF;
   p.flags = TASX_F_INPLACE;
-  fused_done(&p, F->d_done + DONE_STRIDE * (seq % F->nsweep), F->d_count + DONE_STRIDE * (seq % F->nsweep), seq);
   if (tasx_launch_tcp4(&p, 0, F->st) != 0)
     return -1;
-  return tasx_last_launch_posted_done() ? 0 : post_done(F->d_done + DONE_STRIDE * (seq % F->nsweep), seq, F->st);
+  return post_done(F->d_done + DONE_STRIDE * (seq % F->nsweep), seq, F->st);
 }
 
 static void *feeder_main(void *arg)
@@ -1915,13 +1865,8 @@ int tasx_feeder_start(int device)
   F->device = device;
   F->running = 1;
   F->nsweep = NSWEEP;
-#ifdef TASX_AB
-  {
-    const char *e = getenv("TASX_FEEDER_SWEEPS"); /* A/B: 4 sweeps in flight */
-    if (e && atoi(e) == 4)
-      F->nsweep = 4u;
-  }
-#endif
+  if (tasx_ext && tasx_ext->feeder_sweeps == 4u) /* the A/B build: 4 sweeps in flight */
+    F->nsweep = 4u;
   if ((e = hipSetDevice(device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&F->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP_MAX, hipHostMallocCoherent)) != hipSuccess ||
@@ -2085,14 +2030,12 @@ struct fserver {
   int device;
   hipStream_t st;
   uint8_t *h_mem, *d_mem; /* coherent pinned block (tasx_kernels.h TASX_SRV_*) */
-  uint8_t *h_ring, *d_ring; /* the host-written lines (control word, slots): h_mem / d_mem,
-                               A/B TASX_SRV_VRAM=1: uncached device memory written over the BAR */
-  void *vram;
+  uint8_t *h_ring, *d_ring; /* the host-written lines (control word, slots): h_mem / d_mem */
   uint32_t attached;      /* bit r: ring r serves a context */
   int keep_run;
   pthread_t keep;
   uint64_t batches, frames; /* submitted by contexts since detached (statistics) */
-  uint32_t khz;             /* wall clock rate (A/B diagnostics) */
+  uint32_t khz;             /* wall clock rate (the A/B build's timing sums) */
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
@@ -2180,8 +2123,6 @@ static void server_free(struct fserver *S)
 {
   if (S->h_mem)
     hipHostFree(S->h_mem);
-  if (S->vram)
-    hipFree(S->vram);
   if (S->st)
     hipStreamDestroy(S->st);
   free(S);
@@ -2294,8 +2235,6 @@ static int server_submit(struct tasx_ctx *c)
     __atomic_store_n(&slot[1], (uint64_t) b16 | tag, __ATOMIC_RELEASE);
     __atomic_store_n(&slot[0], (uint64_t) cnt | (bytes > 0xffffffffull ? 0xffffffffull : bytes) << 16 | tag,
                      __ATOMIC_RELEASE);
-    if (S->vram) /* A/B device-memory slots: push the stores out of the write-combining buffers */
-      __atomic_thread_fence(__ATOMIC_SEQ_CST);
     c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
     c->sv_pos = pos + 1u;
     c->n_server_flushes++;
@@ -2310,19 +2249,11 @@ static int server_submit(struct tasx_ctx *c)
   return 0;
 }
 
-/* segments per TX slot: TASX_SRV_SEGS (A/B: TASX_SRV_SEGMAX, e.g. round 4's 20) */
+/* segments per TX slot: TASX_SRV_SEGS (the A/B build: TASX_SRV_SEGMAX, e.g. round 4's 20) */
 static uint32_t srv_segs_max(void)
 {
-#ifdef TASX_AB
-  static uint32_t m = 0;
-  if (m == 0) {
-    const char *e = getenv("TASX_SRV_SEGMAX");
-    m = e && atoi(e) > 0 && (uint32_t) atoi(e) <= TASX_SRV_SEGS ? (uint32_t) atoi(e) : TASX_SRV_SEGS;
-  }
-  return m;
-#else
-  return TASX_SRV_SEGS;
-#endif
+  return tasx_ext && tasx_ext->srv_segmax && tasx_ext->srv_segmax <= TASX_SRV_SEGS ? tasx_ext->srv_segmax
+                                                                                     : TASX_SRV_SEGS;
 }
 
 /* TX segment batches through the server: validated up front (nothing is
@@ -2409,8 +2340,6 @@ int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n
     __atomic_store_n(&slot[0], (uint64_t) (cnt | TASX_SRV_SEG) |
                      (uint64_t) (c->zc_bytes > 0xffffffffull ? 0xffffffffull : c->zc_bytes) << 16 | tag,
                      __ATOMIC_RELEASE);
-    if (S->vram)
-      __atomic_thread_fence(__ATOMIC_SEQ_CST);
     c->sv_ticket[pos % TASX_SRV_RING] = ++c->next_ticket;
     c->sv_pos = pos + 1u;
     c->n_server_flushes++;
@@ -2458,44 +2387,23 @@ int tasx_server_start(int device)
     memset(S->h_mem, 0, TASX_SRV_BYTES);
     S->h_ring = S->h_mem;
     S->d_ring = S->d_mem;
-#ifdef TASX_AB
-    if (getenv("TASX_SRV_VRAM")) { /* A/B: the slots in device memory, the host's stores posted over the BAR */
-      hipPointerAttribute_t at;
-      if ((e = hipExtMallocWithFlags(&S->vram, TASX_SRV_BYTES, hipDeviceMallocUncached)) != hipSuccess ||
-          (e = hipMemset(S->vram, 0, TASX_SRV_BYTES)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess ||
-          (e = hipPointerGetAttributes(&at, S->vram)) != hipSuccess)
-        rc = hip_err(e, "server: device-memory slots");
-      else if (!at.hostPointer && atoi(getenv("TASX_SRV_VRAM")) != 2)
-        rc = set_err(-ENOTSUP, "server: device-memory slots have no host mapping (TASX_SRV_VRAM=2 stores to the device address)");
-      else {
-        S->h_ring = at.hostPointer ? at.hostPointer : S->vram;
-        S->d_ring = S->vram;
-      }
-    }
-#endif
     prm.mem = S->d_mem;
     prm.ring = S->d_ring;
     prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
-    prm.light_ticks = (uint64_t) khz * 8u / 1000u;
     prm.diag = 0;
     prm.k = SRV_K;
-    prm.fpol = 0;
-#ifdef TASX_AB
-    prm.diag = getenv("TASX_SRV_DIAG") != NULL;
-    if (getenv("TASX_SRV_K")) /* A/B: workgroups per ring, 1/2/4/8 */
-      prm.k = (uint32_t) atoi(getenv("TASX_SRV_K"));
-    if (getenv("TASX_SRV_FPOL")) /* A/B: the frame loads' cache policy */
-      prm.fpol = (uint32_t) atoi(getenv("TASX_SRV_FPOL"));
-    if (getenv("TASX_SRV_HOT_US"))
-      prm.hot_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_HOT_US")) / 1000u;
-    if (getenv("TASX_SRV_LIGHT_US"))
-      prm.light_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_LIGHT_US")) / 1000u;
-    if (getenv("TASX_SRV_COLD_US"))
-      prm.cold_ticks = (uint64_t) khz * (uint64_t) atoi(getenv("TASX_SRV_COLD_US")) / 1000u;
+    if (tasx_ext) { /* the A/B build's knobs: timing sums, workgroups per ring, poll backoff */
+      prm.diag = tasx_ext->srv_diag;
+      if (tasx_ext->srv_k)
+        prm.k = tasx_ext->srv_k;
+      if (tasx_ext->srv_hot_us >= 0)
+        prm.hot_ticks = (uint64_t) khz * (uint64_t) tasx_ext->srv_hot_us / 1000u;
+      if (tasx_ext->srv_cold_us >= 0)
+        prm.cold_ticks = (uint64_t) khz * (uint64_t) tasx_ext->srv_cold_us / 1000u;
+    }
     S->khz = (uint32_t) khz;
-#endif
     S->k = prm.k;
     if (prm.k == 0u || TASX_SRV_RING % prm.k != 0u || prm.k > TASX_SRV_KMAX)
       rc = set_err(-EINVAL, "server: %u workgroups per ring (a divisor of %u)", prm.k, TASX_SRV_RING);
@@ -2586,12 +2494,12 @@ int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
   return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
 }
 
-#ifdef TASX_AB
-/* A/B: ring r's timing sums over its workgroups (TASX_SRV_DIAG=1 at
+/* Test support (the A/B build exports it as tasx_ab_server_diag): ring r's
+ * timing sums over its workgroups (the timing form, TASX_SRV_DIAG=1 at
  * tasx_server_start), in us: out[0] detection -> frames loaded, [1] frames
  * loaded -> stores acknowledged, [2] a workgroup's completion -> its next
  * detection, summed over out[3] batches; out[4] empty polls */
-int tasx_ab_server_diag(int device, unsigned r, double *out)
+int tasx_server_diag_internal(int device, unsigned r, double *out)
 {
   if (device < 0 || device >= MAX_DEVICES || r >= TASX_MAX_CTX || !out)
     return set_err(-EINVAL, "server diag: bad argument");
@@ -2611,7 +2519,6 @@ int tasx_ab_server_diag(int device, unsigned r, double *out)
   pthread_mutex_unlock(&g_server_mu);
   return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
 }
-#endif
 
 int tasx_ctx_use_server(unsigned ctx_id, int on)
 {
@@ -2939,13 +2846,6 @@ void *tasx_host_alloc(size_t bytes)
 {
   void *p = NULL;
   unsigned flags = 0;
-#ifdef TASX_AB
-  { /* A/B: hipHostMalloc flags (TASX_HOST_ALLOC_FLAGS, e.g. 0x80000000 = non-coherent) */
-    const char *fe = getenv("TASX_HOST_ALLOC_FLAGS");
-    if (fe)
-      flags = (unsigned) strtoul(fe, NULL, 0);
-  }
-#endif
   hipError_t e = hipHostMalloc(&p, bytes, flags);
   if (e != hipSuccess) {
     hip_err(e, "hipHostMalloc");

@@ -40,11 +40,11 @@ typedef struct tasx_tcp4_params {
   uint32_t flen0;        /* uniform hint; 0 = none */
   uint32_t room;         /* bytes from each frame's start that may be read (the
                           * mbuf data room); 0 = unknown */
-  uint64_t *diag;        /* diagnostic timestamp buffer (TASX_AB diag variant) */
-  /* completion posted by the kernel itself (flushes): the last block to finish
-   * resets *done_count and stores done_seq into *done_word (system scope).
-   * done_word == NULL: none; tasx_last_launch_posted_done() tells whether the
-   * launched kernel did it (else the caller posts the word itself). */
+  uint64_t *diag;        /* diagnostic timestamp buffer (the A/B build's wave-timeline variant) */
+  /* completion posted by the kernel itself (tcp4_tas14_kernel<..., DONE>: the
+   * last block to finish resets *done_count and stores done_seq into
+   * *done_word, system scope); the product posts completion words with
+   * tasx_launch_post_done and leaves these NULL (round 2: no faster) */
   uint32_t *done_word;
   uint32_t *done_count;  /* device memory, 0 between launches */
   uint32_t done_seq;
@@ -69,7 +69,7 @@ typedef struct tasx_txseg_params {
   uint32_t n;
   uint32_t ip_off;
   uint32_t l4_off;
-  uint32_t dbg;            /* TASX_AB builds: TASX_TXSEG_DEBUG diagnostics (0 = product) */
+  uint32_t dbg;            /* the A/B build's TASX_TXSEG_DEBUG diagnostics forms (0 = product) */
 } tasx_txseg_params;
 
 typedef struct tasx_flow_params {
@@ -134,15 +134,12 @@ typedef struct tasx_flow_params {
 
 typedef struct tasx_srv_params {
   uint8_t *mem;          /* device view of the server's pinned block (the GPU-written lines) */
-  uint8_t *ring;         /* device view of the host-written lines (control word, slots): mem,
-                            or A/B builds' device-memory copy */
+  uint8_t *ring;         /* device view of the host-written lines (control word, slots): mem */
   uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
-  uint64_t light_ticks;  /* A/B builds (policy 10): a gap this long since a workgroup's last batch = light load */
-  uint32_t diag;         /* A/B builds: timing sums (tasx_ab_server_diag) */
+  uint32_t diag;         /* the A/B build's timing form: per-batch timing sums (tasx_ab_server_diag) */
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
-  uint32_t fpol;         /* A/B builds: the frame loads' cache policy (server_kernels.hip) */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
@@ -159,8 +156,6 @@ TASX_INTERNAL int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant
 /* one-lane kernel storing seq into *word (pinned host memory, device view)
  * with system-scope release, after everything before it on the stream */
 TASX_INTERNAL int tasx_launch_post_done(uint32_t *word, uint32_t seq, void *stream);
-/* 1 if the calling thread's last tasx_launch_tcp4 posted p->done_word itself */
-TASX_INTERNAL int tasx_last_launch_posted_done(void);
 /* offload branch of tcp_checksums: pseudo-header sums into tcp.chksum */
 TASX_INTERNAL int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream);
 /* fused TX segment build (txseg_kernels.hip) */
@@ -169,6 +164,36 @@ TASX_INTERNAL int tasx_launch_txseg(const tasx_txseg_params *p, void *stream);
 TASX_INTERNAL int tasx_launch_server(const tasx_srv_params *p, void *stream);
 /* record the name of the kernel the calling thread launches (tasx_last_kernel) */
 TASX_INTERNAL void tasx_note_kernel(const char *name);
+
+/* The extension point the A/B build uses.  libtasx_ab.so is the product's objects
+ * plus tas_amd/csrc/ab/ (kernels and knobs kept for comparisons, include/
+ * tasx_ab.h): a constructor there points tasx_ext at its hooks.  In libtasx.so
+ * it stays NULL and no hook is ever called.  A launch hook returns
+ * TASX_EXT_PASS for a variant it does not own: the product path runs. */
+#define TASX_EXT_PASS 1
+typedef struct tasx_ext_hooks {
+  int max_variant; /* the highest tasx_set_kernel_variant value */
+  int (*raw)(const tasx_raw_params *p, int variant, void *stream);
+  int (*tcp4)(const tasx_tcp4_params *p, int variant, void *stream);
+  int (*verify)(const tasx_tcp4_params *p, int variant, void *stream);
+  int (*rx)(const tasx_tcp4_params *p, int variant, void *stream);
+  int (*flow)(const tasx_flow_params *p, int variant, void *stream);
+  int (*txseg)(const tasx_txseg_params *p, void *stream);
+  int (*server)(const tasx_srv_params *p, void *stream); /* the server with timing sums (p->diag) */
+  int (*xrun)(uint64_t blocks); /* >= 0: the XCD order of a grid of `blocks` blocks */
+  /* host knobs (from the environment, read once by the A/B build) */
+  uint64_t *diag;         /* p.diag of TCP4 launches (the wave-timeline variant) */
+  uint32_t feeder_sweeps; /* sweeps in flight (TASX_FEEDER_SWEEPS: 2 or 4), 0 = the product's */
+  uint32_t srv_k;         /* workgroups per ring (TASX_SRV_K), 0 = the product's */
+  uint32_t srv_segmax;    /* TX segments per server slot (TASX_SRV_SEGMAX), 0 = the product's */
+  uint32_t srv_diag;      /* the server's timing sums (TASX_SRV_DIAG) */
+  int32_t srv_hot_us, srv_cold_us; /* poll backoff times (TASX_SRV_HOT_US / _COLD_US), < 0 = the product's */
+} tasx_ext_hooks;
+TASX_INTERNAL extern const tasx_ext_hooks *tasx_ext;
+/* test support for the A/B build's exports (tasx_ab_ctx_set_tickets,
+ * tasx_ab_server_diag): library-internal, never exported */
+TASX_INTERNAL int tasx_ctx_set_tickets_internal(unsigned ctx_id, uint32_t start);
+TASX_INTERNAL int tasx_server_diag_internal(int device, unsigned r, double *out);
 
 #ifdef __cplusplus
 }

@@ -34,1606 +34,18 @@
 //       a uniform frame-length hint; per-row total_length modes otherwise),
 //   7 = raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
 //       chunk sequence).
-// Built only with -DTASX_AB (libtasx_ab.so, tools/ and the A/B tests): 1 = the
-// first-generation group-per-packet kernels, 4 = tcp4_tas_kernel with
-// wave-timeline stamps, 5 = tcp4_tas_kernel with 32-lane groups, 8 =
-// tcp4_wave_kernel, RAW variant 2 = raw_group_kernel, and the environment knobs
-// that steer residency (TASX_*_LDS) and the TX segment diagnostics.
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <stdlib.h>
-#include <errno.h>
-#include <string.h>
-
-#include "tasx_kernels.h"
-
-#include "xsum_device.h"
-
-namespace {
-
-#ifdef TASX_AB
-// ---------------------------------------------------------------------------
-// First-generation kernels (variant 1, the A/B baseline): one G-lane group per
-// packet, xor-shuffle reductions, byte loads for the TCP4 header.
-// RAW: out[i] = rte_raw_cksum(base + off_i, len_i)   
-
-template <int G, int U>
-__global__ __launch_bounds__(kBlock) void raw_cksum_kernel(tasx_raw_params p)
-{
-  const int gl = threadIdx.x & (G - 1);
-  const uint32_t gpb = kBlock / G;
-  const uint32_t ngroups = gridDim.x * gpb;
-  for (uint32_t i = blockIdx.x * gpb + threadIdx.x / G; i < p.n; i += ngroups) {
-    const uint8_t *s = p.base + pkt_offset(p.off, p.stride, i);
-    const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
-    uint32_t part = lane_partial<G, U>(s, len, gl);
-    uint32_t tot = group_sum<G>(part);
-    if (gl == 0) {
-      uint32_t f = fold32_to_16(tot);
-      if (((uintptr_t) s) & 1)
-        f = bswap16(f);
-      stg(p.out, i, (uint16_t) f);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// TCP4: per frame, tcp_checksums() flag-off branch:
-//   ip.chksum  = rte_ipv4_cksum(ip)            (ip.chksum taken as 0)
-//   tcp.chksum = rte_ipv4_udptcp_cksum(ip, l4) (tcp.chksum taken as 0)
-// out[2i] = ip.chksum, out[2i+1] = tcp.chksum (native u16, as TAS stores them)
-
-template <int G, int U>
-__global__ __launch_bounds__(kBlock) void tcp4_cksum_kernel(tasx_tcp4_params p)
-{
-  static_assert(G >= 16, "header needs 11 lanes");
-  const int gl = threadIdx.x & (G - 1);
-  const int gbase = (threadIdx.x & 63) & ~(G - 1); // first lane of the group in the wave
-  const uint32_t gpb = kBlock / G;
-  const uint32_t ngroups = gridDim.x * gpb;
-
-  for (uint32_t i = blockIdx.x * gpb + threadIdx.x / G; i < p.n; i += ngroups) {
-    uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-    uint8_t *ip = f + p.ip_off;
-    uint8_t *l4 = f + p.l4_off;
-
-    // header words, relative to the header start: lanes 0..9 hold ip word gl
-    uint32_t w = 0;
-    if (gl < 10)
-      w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
-    // total_length = bswap(word 1)
-    const uint32_t w1 = (uint32_t) __shfl(w, gbase + 1, 64);
-    const uint32_t tl = bswap16(w1);
-    const uint32_t l4len = tl >= 20 ? tl - 20 : 0;
-
-    // checksum field bytes of the L4 header, inside the summed range only
-    uint32_t fix = 0;
-    if (gl == 10 && l4len > 16) {
-      uint32_t fw = ld8(l4 + 16);
-      if (l4len > 17)
-        fw |= ld8(l4 + 17) << 8;
-      fix = (~fw) & 0xffffu; // -fw mod 0xffff, L4-start frame
-    }
-
-    // header channels: ip sum (words 0..9 but 5) and pseudo header
-    // (src/dst words 6..9, proto<<8 from word 4)
-    uint32_t c_ip = (gl < 10 && gl != 5) ? w : 0;
-    uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0);
-
-    uint32_t part = lane_partial<G, U>(l4, l4len, gl);
-
-    c_ip = group_sum<G>(c_ip);
-    c_ph = group_sum<G>(c_ph);
-    part = group_sum<G>(part);
-    fix = group_sum<G>(fix);
-
-    if (gl == 0) {
-      const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
-      uint32_t tcpc = 0;
-      if (tl >= 20) {
-        uint32_t r4 = fold32_to_16(part);
-        if (((uintptr_t) l4) & 1)
-          r4 = bswap16(r4);
-        const uint32_t lw = bswap16(l4len); // htons(l4len) as a LE word
-        uint32_t s = r4 + fix + c_ph + lw;
-        tcpc = inv_result(residue(fold32_to_16(s)));
-      }
-      if (p.out)
-        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-      if (p.flags & TASX_F_INPLACE) {
-        st8(ip + 10, ipc);
-        st8(ip + 11, ipc >> 8);
-        st8(l4 + 16, tcpc);
-        st8(l4 + 17, tcpc >> 8);
-      }
-    }
-  }
-}
-
-// RAW, any layout: out[i] = rte_raw_cksum(base + off_i, len_i)
-template <int U>
-__global__ __launch_bounds__(kBlock) void raw_group_kernel(tasx_raw_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t ngroups = gridDim.x * (kBlock / 16);
-  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  // descriptor prefetch (every lane of the group reads the same word)
-  uint64_t off = 0;
-  uint32_t len = p.len0;
-  if (i < p.n) {
-    off = pkt_offset(p.off, p.stride, i);
-    if (p.len)
-      len = ldg(p.len, i);
-  }
-  for (; i < p.n; i += ngroups) {
-    const uint8_t *s = p.base + off;
-    const Chunks<U> r = chunk_range<U>(s, len);
-    const uint32_t inext = i + ngroups;
-    uint32_t part = group_lane_sum<U>(r, gl);
-    if (inext < p.n) {
-      off = pkt_offset(p.off, p.stride, inext);
-      if (p.len)
-        len = ldg(p.len, inext);
-    }
-    part = row_sum16(part);
-    if (gl == 15) {
-      uint32_t f = fold32_to_16(part);
-      if (r.head & 1)
-        f = bswap16(f);
-      stg(p.out, i, (uint16_t) f);
-    }
-  }
-}
-#endif // TASX_AB
-
-// RAW, any layout, word sums by v_sad_u16 into exact 32-bit accumulators
-// (variant 6).  Rounds of U chunk loads per lane, clamped to the packet's last
-// chunk and issued back to back; chunk-index selects keep the clamped
-// re-reads out.  Bytes before the packet in chunk 0 come off on lane 0; bytes
-// past it in the last chunk on lane 15, whose last load of the final round is
-// always that chunk (its partial may wrap: the group total, < 2^32 for
-// TASX_RAW_MAX_LEN, is exact mod 2^32).
-// S32: stride mode from a 16-byte aligned base (host-checked): 32-bit byte
-// offsets from the block's first packet (a uniform 64-bit base: 16 strides
-// from a 16-byte aligned base stay 16-byte aligned), so each load is
-// global_load_dwordx4 v, v_off, s[base] (one VGPR per address) at any batch size.
-// G (A/B, round 4): lanes per packet -- 16 (the product: one DPP row), 32 or
-// 64 with U = 3 / 2 loads per lane for a 1500-byte packet: fewer loads in
-// flight per lane and more packets' worth of short-lived waves, the shape of
-// the fastest trivial streaming read at config 4's sizes (profiles/r04/INDEX.md
-// r04b); lane G - 1 holds the last chunk and the group total (group_total<G>).
-template <int U, bool S32 = false, int G = 16>
-__global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
-{
-  const int gl = threadIdx.x & (G - 1);
-  const uint32_t blk = xcd_run(blockIdx.x, gridDim.x, p.xrun);
-  const uint32_t i = blk * (kBlock / G) + threadIdx.x / G;
-  if (i >= p.n)
-    return;
-  const uint32_t len = p.len ? ldg(p.len, i) : p.len0;
-  const uint8_t *s = nullptr;
-  const uint8_t *const bb = p.base + (uint64_t) (blk * (kBlock / G)) * p.stride;
-  uint32_t o0 = 0, head, last;
-  if constexpr (S32) {
-    const uint32_t so = (threadIdx.x / G) * (uint32_t) p.stride;
-    o0 = so & ~15u;
-    head = so & 15u;
-    last = (head + len - 1u) >> 4; // valid when len > 0
-  } else {
-    s = p.base + pkt_offset(p.off, p.stride, i);
-    head = (uint32_t) ((uintptr_t) s & 15u);
-    last = (head + len - 1u) >> 4;
-  }
-  const u32x4 *c0p = (const u32x4 *) ((uintptr_t) s & ~(uintptr_t) 15);
-  uint32_t acc = 0;
-  if (len) {
-    u32x4 t;
-    for (uint32_t cb = 0; cb <= last; cb += (uint32_t) G * U) {
-      u32x4 v[U];
-      if constexpr (S32) {
-        const uint32_t lb = o0 + 16u * (cb + (uint32_t) gl), lastoff = o0 + 16u * last;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          v[u] = ld16nt_off(bb, min(lb + 16u * G * u, lastoff));
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          v[u] = ld16nt(c0p, min(cb + (uint32_t) gl + (uint32_t) G * u, last));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t a = sad4(v[u], acc);
-        acc = cb + (uint32_t) gl + (uint32_t) G * u <= last ? a : acc;
-      }
-      if (cb == 0)
-        acc -= gl == 0 ? sad_below(v[0], head) : 0u;
-      t = v[U - 1];
-    }
-    acc -= gl == G - 1 ? sad_from(t, head + len - 16u * last) : 0u;
-  }
-  acc = group_total<G>(acc);
-  if (gl == G - 1) {
-    uint32_t f = fold32_to_16(acc);
-    if (head & 1)
-      f = bswap16(f);
-    stg(p.out, i, (uint16_t) f);
-  }
-}
-
-// RAW with per-packet lengths (variant 7; the automatic choice when lengths
-// are given).  The 16-lane-group kernels keep a wave for as many rounds as its
-// longest packet needs while the other groups' lanes idle: on the
-// {64,576,1500,9000} B mix two waves in three hold a 9000 B packet and keep
-// ~30% of their lanes loading.  Here a wave's 4 packets form ONE chunk
-// sequence (packet k owns flattened chunks [P_k, P_k+1)) and all 64 lanes load
-// consecutive flattened chunks, U per lane per round: ceil(total / 64U) rounds.
-// Whole chunks go into cumulative accumulators A_j = sum over the chunks of
-// packets >= j, so packet k's sum is A_k - A_{k+1}, exact mod 2^32 (every
-// packet sum is < 2^32 for len <= TASX_RAW_MAX_LEN).  The bytes outside
-// packet k in its first / last chunk come off on lane k / 4 + k, whose loads
-// of those two chunks are issued before round 0 (their addresses come from
-// the descriptors: no dependent load phase).
-template <int U, bool S32>
-__device__ __forceinline__ void wave_chunk_sums(uint64_t lo, const uint64_t (&B)[4], const uint32_t (&P)[4],
-                                                uint32_t T, uint32_t lane, uint32_t (&A)[4])
-{
-  // B[k] = chunk-aligned start of packet k - 16 P_k (mod 2^64): flattened
-  // chunk f of packet k is at B[k] + 16 f.  S32: every chunk lies within
-  // 4 GiB above lo, so the address is lo + 32-bit offset (one VGPR).
-  uint32_t d[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    d[k] = (uint32_t) (B[k] - lo);
-  const uint8_t *sb = (const uint8_t *) (uintptr_t) lo;
-  for (uint32_t f0 = 0; f0 < T; f0 += 64u * U) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t fc = min(f0 + 64u * u + lane, T - 1u);
-      if constexpr (S32) {
-        const uint32_t dk = fc >= P[3] ? d[3] : fc >= P[2] ? d[2] : fc >= P[1] ? d[1] : d[0];
-        v[u] = ld16nt_off(sb, dk + 16u * fc);
-      } else {
-        const uint64_t bk = fc >= P[3] ? B[3] : fc >= P[2] ? B[2] : fc >= P[1] ? B[1] : B[0];
-        v[u] = __builtin_nontemporal_load((gcu4 *) (uintptr_t) (bk + 16ull * fc));
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t f = f0 + 64u * u + lane;
-      const uint32_t s = f < T ? sad4(v[u], 0u) : 0u;
-      A[0] += s;
-      A[1] += f >= P[1] ? s : 0u;
-      A[2] += f >= P[2] ? s : 0u;
-      A[3] += f >= P[3] ? s : 0u;
-    }
-  }
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l)
-{
-  const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) x, l);
-  const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) (x >> 32), l);
-  return ((uint64_t) hi << 32) | lo;
-}
-
-// The flattened sum of a wave's 4 packets (raw_wave_kernel, tcp4_wave_kernel):
-// lanes k and 4 + k hold packet k's start address a and length len (len 0 =
-// nothing to sum); returns on lane k < 4 the exact 32-bit sum of packet k's
-// little-endian 16-bit words counted in the address frame (from even addresses).
-template <int U>
-__device__ __forceinline__ uint32_t wave4_sums(uint32_t lane, uint64_t a, uint32_t len)
-{
-  const uint32_t k = lane & 3u;
-  const uint32_t head = (uint32_t) a & 15u;
-  const uint32_t nch = len ? (head + len + 15u) >> 4 : 0u;
-  const uint64_t c0 = a & ~15ull;
-  // packet k's first (lane k) and last (lane 4 + k) chunk, in flight with round 0
-  u32x4 bv = {0u, 0u, 0u, 0u};
-  if (lane < 8u && nch)
-    bv = ld16nt((const u32x4 *) (uintptr_t) c0, lane < 4u ? 0u : nch - 1u);
-
-  uint64_t B[4];
-  uint32_t P[4];
-  uint32_t T = 0;
-  uint64_t lo = ~0ull, hi = 0;
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const uint32_t nk = (uint32_t) __builtin_amdgcn_readlane((int) nch, kk);
-    const uint64_t ck = readlane64(c0, kk);
-    P[kk] = T;
-    B[kk] = ck - 16ull * T;
-    if (nk) {
-      lo = min(lo, ck);
-      hi = max(hi, ck + 16ull * nk);
-    }
-    T += nk;
-  }
-  uint32_t A[4] = {0u, 0u, 0u, 0u};
-  if (T) {
-    if (hi - lo <= 0xffffffffull)
-      wave_chunk_sums<U, true>(lo, B, P, T, lane, A);
-    else
-      wave_chunk_sums<U, false>(lo, B, P, T, lane, A);
-  }
-  // boundary bytes of packet k off A_0..A_k (packet k's sum is A_k - A_{k+1})
-  uint32_t corr = 0;
-  if (lane < 8u && nch)
-    corr = lane < 4u ? sad_below(bv, head) : sad_from(bv, head + len - 16u * (nch - 1u));
-  A[0] -= corr;
-  A[1] -= k >= 1u ? corr : 0u;
-  A[2] -= k >= 2u ? corr : 0u;
-  A[3] -= k == 3u ? corr : 0u;
-  uint32_t t[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    t[j] = (uint32_t) __builtin_amdgcn_readlane((int) group_total<64>(A[j]), 63);
-  return k == 0u ? t[0] - t[1] : k == 1u ? t[1] - t[2] : k == 2u ? t[2] - t[3] : t[3];
-}
-
-template <int U>
-__global__ __launch_bounds__(kBlock) void raw_wave_kernel(tasx_raw_params p)
-{
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t i0 = xcd_run(blockIdx.x, gridDim.x, p.xrun) * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
-  if (i0 >= p.n) // wave-uniform
-    return;
-  const uint32_t i = i0 + (lane & 3u);
-  // lanes k and 4 + k hold packet k's descriptor
-  uint64_t a = 0;
-  uint32_t len = 0;
-  if (lane < 8u && i < p.n) {
-    a = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i);
-    len = p.len ? ldg(p.len, i) : p.len0;
-  }
-  const uint32_t s = wave4_sums<U>(lane, a, len);
-  if (lane < 4u && i < p.n) {
-    uint32_t f = fold32_to_16(s);
-    if (a & 1u)
-      f = bswap16(f);
-    stg(p.out, i, (uint16_t) f);
-  }
-}
-
-// The bytes a frame owns from its start: the batch's room, else its stride
-// slot (stride mode); ~0 when nothing bounds it.
-__device__ __forceinline__ uint32_t slot_bound(const tasx_tcp4_params &p)
-{
-  if (p.room)
-    return p.room;
-  if (!p.off && p.stride)
-    return p.stride < 0xffffffffull ? (uint32_t) p.stride : 0xffffffffu;
-  return 0xffffffffu;
-}
-
-// Receive-side read bound of a frame, in bytes from its start: the received
-// frame length (the hint: the mbuf data_len) capped at the frame's room or
-// stride slot (a hint beyond them is not trusted for reads), else the room /
-// slot; ~0 when nothing bounds it (offsets without hints or room: the buffer
-// must then hold ip_off + total_length bytes, as DPDK assumes).
-__device__ __forceinline__ uint32_t rx_bound(const tasx_tcp4_params &p, uint32_t hint)
-{
-  const uint32_t b = slot_bound(p);
-  return hint ? min(hint, b) : b;
-}
-
-// TCP4, any frame layout: header words and the checksum-field bytes by byte
-// loads, then the segment chunks.  With a frame-length hint (the mbuf
-// data_len tx_send() sets before tx_flush) the chunk loads are issued together
-// with the header loads; the hint drives only the prefetch: results always
-// follow ip.total_length (chunks past it are dropped, chunks the hint missed
-// are loaded after the header arrives).
-//
-// VERIFY = true is the receive-side check (TAS itself
-// never verifies, fast_flows.c:242-251): the checksum fields are summed as they
-// are, and out[i] gets a flag byte: bit 0 = the header folds to 0xffff, bit 1
-// = rte_ipv4_udptcp_cksum_verify passes (DPDK >= 21.11: fold1(raw(L4) +
-// phdr) == 0xffff; total_length < 20 fails), bit 2 = IHL != 5 (TAS drops
-// such frames, fast_flows.c:247; bits 0/1 then describe a 20-byte header).
-// Received frames are untrusted: reads stay below the frame's rx_bound() (the
-// received length, else the room, else the stride slot), and a datagram whose
-// total_length reaches past it fails the L4 check (bit 1 clear) without being
-// read; the 20-byte IPv4 header is always read.
-// One frame (i) per 16-lane DPP row, lane gl (the body of tcp4_frame_kernel).
-template <int U, bool VERIFY = false>
-__device__ __forceinline__ void tcp4_frame_row(const tasx_tcp4_params &p, uint32_t i, int gl)
-{
-  uint8_t *f = p.base + pkt_offset(p.off, p.stride, i);
-  uint8_t *ip = f + p.ip_off;
-  uint8_t *l4 = f + p.l4_off;
-  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
-  // speculative chunk loads first, then the header bytes
-  const uint32_t slen = hint > p.l4_off ? min(hint - p.l4_off, 65535u) : 0u;
-  const Chunks<U> sr = chunk_range<U>(l4, slen);
-  u32x4 v[U];
-  if (sr.nch) {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt(sr.c0p, min((uint32_t) gl + 16u * u, sr.nch - 1));
-  }
-  const uint32_t tl = (ld8(ip + 2) << 8) | ld8(ip + 3);
-  uint32_t w = 0;
-  if (gl < 10)
-    w = ld8(ip + 2 * gl) | (ld8(ip + 2 * gl + 1) << 8);
-  const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  bool trunc = false; // RX: the datagram reaches past the frame's bound
-  uint32_t rlen = len;
-  if constexpr (VERIFY) {
-    const uint32_t b = rx_bound(p, hint);
-    const uint32_t have = b > p.l4_off ? b - p.l4_off : 0u;
-    trunc = len > have;
-    rlen = trunc ? have : len;
-  }
-  const Chunks<U> r = chunk_range<U>(l4, rlen);
-  // first 16*U chunks: reuse the speculative loads when they cover them
-  uint64_t acc = 0;
-  if (r.nch) {
-    const uint32_t need = min(r.nch, 16u * U);
-    if (sr.nch < need) { // hint too short (or absent): load now
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = ld16nt(r.c0p, min((uint32_t) gl + 16u * u, r.nch - 1));
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool keep = (uint32_t) gl + 16u * u < r.nch;
-      acc += keep ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
-    }
-    if (gl == 0 && r.head)
-      acc -= chunk_prefix_sum(v[0], r.head);
-    const uint32_t last = r.nch - 1;
-    if (last < 16u * U && (last & 15u) == (uint32_t) gl && r.tail < 16) {
-      const uint32_t ut = last >> 4;
-      u32x4 t = v[0];
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        if (ut == (uint32_t) u)
-          t = v[u];
-      acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, r.tail);
-    }
-  }
-  if (!VERIFY && len > 16) {
-    // tcp.chksum (segment bytes 16, 17) is taken as zero: subtract its bytes
-    // exactly on the lane that holds their chunk (chunk index <= 2, so u = 0)
-    const int p16 = r.head + 16, p17 = p16 + 1;
-    if (gl == (p16 >> 4))
-      acc -= (uint64_t) chunk_byte(v[0], p16 & 15) << (8 * (p16 & 3));
-    if (len > 17 && gl == (p17 >> 4))
-      acc -= (uint64_t) chunk_byte(v[0], p17 & 15) << (8 * (p17 & 3));
-  }
-  uint32_t part = fold64_to_18(acc);
-  if (r.nch > 16u * U) { // long segments: the rest in the plain loop
-    Chunks<U> rest = r;
-    rest.c0p = r.c0p + 16u * U;
-    rest.nch = r.nch - 16u * U;
-    rest.head = 0;
-    part += group_lane_sum<U>(rest, gl);
-  }
-  uint32_t c_ip = (gl < 10 && (VERIFY || gl != 5)) ? w : 0u;
-  uint32_t c_ph = (gl >= 6 && gl < 10) ? w : (gl == 4 ? (w & 0xff00u) : 0u);
-  const uint32_t w0 = (uint32_t) __shfl((int) w, (threadIdx.x & 63) & ~15, 64); // version/IHL byte
-  part = row_sum16(part);
-  c_ip = row_sum16(c_ip);
-  c_ph = row_sum16(c_ph);
-  if (VERIFY && gl == 15) {
-    // exact rte_raw_cksum values: every sum above is exact and non-negative
-    const uint32_t ri = fold32_to_16(c_ip);
-    uint32_t flags = (ri == 0xffffu) ? 1u : 0u;
-    if (tl >= 20 && !trunc) {
-      uint32_t r4 = fold32_to_16(part);
-      if (r.head & 1)
-        r4 = bswap16(r4);
-      const uint32_t ph = fold32_to_16(c_ph + bswap16(len)); // rte_ipv4_phdr_cksum
-      uint32_t c = r4 + ph;
-      c = (c >> 16) + (c & 0xffffu);
-      flags |= (c == 0xffffu) ? 2u : 0u;
-    }
-    if ((w0 & 0x0fu) != 5u)
-      flags |= 4u;
-    stg((uint8_t *) p.out, i, (uint8_t) flags);
-  }
-  if (!VERIFY && gl == 15) {
-    const uint32_t ipc = inv_result(residue(fold32_to_16(c_ip)));
-    uint32_t tcpc = 0;
-    if (tl >= 20) {
-      uint32_t r4 = fold32_to_16(part);
-      if (r.head & 1)
-        r4 = bswap16(r4);
-      tcpc = inv_result(residue(fold32_to_16(r4 + c_ph + bswap16(len))));
-    }
-    if (p.out)
-      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-    if (p.flags & TASX_F_INPLACE) {
-      st8(ip + 10, ipc);
-      st8(ip + 11, ipc >> 8);
-      st8(l4 + 16, tcpc);
-      st8(l4 + 17, tcpc >> 8);
-    }
-  }
-}
-
-template <int U, bool VERIFY = false>
-__global__ __launch_bounds__(kBlock) void tcp4_frame_kernel(tasx_tcp4_params p)
-{
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return; // whole 16-lane group (one DPP row) leaves together
-  tcp4_frame_row<U, VERIFY>(p, i, threadIdx.x & 15);
-}
-
-#ifdef TASX_AB
-// TCP4 batches of mixed frame lengths with per-frame hints (a tx_flush batch:
-// flow_tx_segment data frames among flow_tx_ack / inject_tcp_ts frames,
-// fast_flows.c:877-1030).  One row per frame leaves the rows of short frames
-// idle while the wave's longest frame is read; here a wave's 4 frames are one
-// flattened chunk sequence, as in raw_wave_kernel: each datagram [ip, ip +
-// hint - ip_off) is summed whole (exact 32-bit word sum; the IPv4 header is at
-// an even address), then lane k takes frame k's header words off it:
-//   L4 sum  = datagram sum - the 10 IPv4 header words - tcp.chksum as stored
-//   IP sum  = the IPv4 header words - ip.chksum as stored
-// (exact subtractions of words the datagram sum holds; tcp.chksum lies inside
-// it because the hint covers ip + 40).  The header words are loaded up front,
-// in flight with round 0.  A frame whose ip.total_length is not the hinted
-// datagram length, whose hint does not cover ip + 40, or whose header sits at
-// an odd address is redone by one 16-lane row (tcp4_frame_row): the results
-// always follow ip.total_length, the hint only decides the reads.
-// Measured (tools/ackmix_probe.py, profiles/r01_ackmix.jsonl): slower than
-// tcp4_tas_kernel's row per frame at every ACK fraction (0 / 25 / 50 / 75 %:
-// 18.0 / 15.9 / 14.9 / 14.0 us against 17.2 / 15.0 / 13.8 / 12.7 us for 64K
-// frames).  These batches are bound by per-wave dependent latency (hint ->
-// data -> store) over ~2.7 generations of resident waves, not by bytes, and
-// the flattened pass adds VALU and registers (70 VGPRs against 55 for
-// raw_wave_kernel) without removing a dependent step.  Kept as variant 8 (A/B).
-template <int U>
-__global__ __launch_bounds__(kBlock) void tcp4_wave_kernel(tasx_tcp4_params p)
-{
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t i0 = xcd_run(blockIdx.x, gridDim.x, p.xrun) * (kBlock / 16) + (threadIdx.x >> 6) * 4u;
-  if (i0 >= p.n) // wave-uniform
-    return;
-  const uint32_t i = i0 + (lane & 3u);
-  uint64_t a = 0;
-  uint32_t len = 0;
-  if (lane < 8u && i < p.n) {
-    const uint32_t h = p.flen ? ldg(p.flen, i) : p.flen0;
-    const uint64_t ipa = (uint64_t) (uintptr_t) p.base + pkt_offset(p.off, p.stride, i) + p.ip_off;
-    if (h >= p.ip_off + 40u && !(ipa & 1u)) {
-      a = ipa;
-      len = min(h - p.ip_off, 65535u);
-    }
-  }
-  uint32_t w[10], wt = 0;
-#pragma unroll
-  for (int j = 0; j < 10; ++j)
-    w[j] = 0;
-  if (lane < 4u && len) {
-    const uint16_t *ip16 = (const uint16_t *) (uintptr_t) a;
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      w[j] = ldg(ip16, (uint32_t) j);
-    wt = ldg(ip16, 18u); // tcp.chksum: ip + 20 + 16 (l4_off == ip_off + 20)
-  }
-  const uint32_t s = wave4_sums<U>(lane, a, len);
-  bool redo = false;
-  if (lane < 4u && i < p.n) {
-    const uint32_t tl = bswap16(w[1]);
-    redo = len == 0u || tl != len;
-    if (!redo) {
-      uint32_t ipall = 0;
-#pragma unroll
-      for (int j = 0; j < 10; ++j)
-        ipall += w[j];
-      const uint32_t ph = w[6] + w[7] + w[8] + w[9] + (w[4] & 0xff00u); // src, dst, {0, proto}
-      const uint32_t ipc = inv_result(residue(fold32_to_16(ipall - w[5])));
-      const uint32_t r = fold32_to_16(s - ipall - wt) + fold32_to_16(ph) + bswap16(tl - 20u);
-      const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
-      if (p.out)
-        stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-      if (p.flags & TASX_F_INPLACE) {
-        uint8_t *ip = (uint8_t *) (uintptr_t) a;
-        st8(ip + 10, ipc);
-        st8(ip + 11, ipc >> 8);
-        st8(ip + 36, tcpc);
-        st8(ip + 37, tcpc >> 8);
-      }
-    }
-  }
-  const uint64_t rb = __builtin_amdgcn_ballot_w64(redo);
-  if (rb) { // row r (lanes 16r..16r+15) redoes frame i0 + r
-    const uint32_t r = lane >> 4;
-    if ((rb >> r) & 1ull)
-      tcp4_frame_row<3>(p, i0 + r, (int) (lane & 15u)); // (3 per round: keeps the rare redo below the flattened pass's registers)
-  }
-}
-
-#endif // TASX_AB
-
-// mask of the bytes of a dword (first byte at ip-relative offset `base`) that
-// fall in [lo, hi)
-__device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
-{
-  const int bl = min(max(lo - base, 0), 4);
-  const int bh = min(max(hi - base, 0), 4);
-  if (bh <= bl)
-    return 0u;
-  return (uint32_t) (((1ull << (8 * bh)) - 1ull) & ~((1ull << (8 * bl)) - 1ull));
-}
-
-template <int BS>
-__device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
-{
-  // 100 MHz global clock; one record of 4 stamps per wave
-  const uint64_t t = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63) == 0) {
-    const uint64_t w = ((uint64_t) blockIdx.x * (BS / 64) + threadIdx.x / 64);
-    p.diag[w * 4 + slot] = t;
-  }
-}
-
-// TCP4, TAS frame layout (tcp = ip + 20), stride mode: one chunk range
-// [ip, ip + 20 + L4 length) carries the IPv4 header, the pseudo-header fields
-// and the segment, so no byte loads are issued at all.  The (up to 4) lanes
-// holding chunks with header bytes split them into three channels:
-//   IP = header bytes [0,10) + [12,20)            (ip.chksum taken as 0)
-//   PH = proto (offset 9) + src/dst [12,20)       (pseudo-header fields)
-//   L4 = [20, 20+len) minus the tcp.chksum bytes [36,38)
-// with byte masks from three 64-bit constants (bit x+16 = ip-relative byte x
-// is in the channel) expanded by one multiply.  total_length comes from the
-// chunk holding offsets 2..3 by a lane shuffle.  32-bit byte offsets from the
-// 16-byte aligned batch base make every load global_load_dwordx4 v, v_off,
-// s[base] (one VGPR per address).  With a frame-length hint all chunk loads
-// are issued at once; without one, after total_length is known.
-constexpr uint64_t kPatIP = (((1ull << 10) - 1) << 16) | (((1ull << 8) - 1) << 28);  // [0,10)+[12,20)
-constexpr uint64_t kPatPH = (1ull << 25) | (((1ull << 8) - 1) << 28);                // {9}+[12,20)
-constexpr uint64_t kPatNL4 = ((1ull << 36) - 1) | (3ull << 52);                     // [-16,20)+{36,37}
-// receive-side check: the checksum fields are summed as received
-constexpr uint64_t kPatIPV = ((1ull << 20) - 1) << 16;                               // [0,20)
-constexpr uint64_t kPatNL4V = (1ull << 36) - 1;                                      // [-16,20)
-
-__device__ __forceinline__ uint32_t expand4(uint32_t bits)
-{
-  return ((bits * 0x204081u) & 0x01010101u) * 0xffu; // 4 bits -> 4 byte masks
-}
-
-__device__ __forceinline__ uint32_t pat_bits(uint64_t pat, int s)
-{
-  return s < 64 ? (uint32_t) (pat >> s) & 0xfu : 0u;
-}
-
-
-// one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave.
-// VERIFY: the receive-side flags of tcp4_frame_kernel<U, true> instead.
-template <int U, int DIAG = 0, int G = 16, bool VERIFY = false>
-__device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, int gl, int gbase)
-{
-  constexpr uint64_t pat_ip = VERIFY ? kPatIPV : kPatIP, pat_nl4 = VERIFY ? kPatNL4V : kPatNL4;
-  const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
-  const uint32_t fo = (uint32_t) pkt_offset(p.off, p.stride, i);
-  const uint32_t ipo = fo + p.ip_off;
-  const uint32_t a0 = ipo & ~15u;
-  const int hb = (int) (ipo & 15u);
-  const uint32_t hint = p.flen ? ldg(p.flen, i) : p.flen0;
-  const uint32_t hend = hint > p.ip_off + 20u ? min(hint - p.ip_off, 65535u) : 20u;
-  const uint32_t nld = (uint32_t) (hb + hend + 15) >> 4;
-  // round 1: U loads back to back, no branches (lanes past the hinted range
-  // re-read its last chunk: same line, no extra HBM traffic)
-  u32x4 v[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + (uint32_t) G * u, nld - 1));
-  const int ca = (hb + 2) >> 4, cb = (hb + 3) >> 4;
-  const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
-  const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
-  const uint32_t tl = (ba << 8) | bb;
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 1);
-  const uint32_t len = tl >= 20 ? tl - 20 : 0;
-  int E = 20 + (int) len;
-  bool trunc = false; // RX: the datagram reaches past the frame's bound (rx_bound)
-  if constexpr (VERIFY) {
-    const uint32_t b = rx_bound(p, hint);
-    const uint32_t have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-    trunc = (uint32_t) E > have;
-    E = trunc ? (int) have : E;
-  }
-  const uint32_t nch = (uint32_t) (hb + E + 15) >> 4;
-  const uint32_t need = min(nch, (uint32_t) G * U);
-  if (__builtin_amdgcn_ballot_w64(nld < need) != 0ull) {
-    const uint32_t top = max(need, nld);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(base, a0 + 16u * min((uint32_t) gl + (uint32_t) G * u, top - 1));
-  }
-  const uint32_t last = nch - 1;
-  const int tail = (int) ((ipo + (uint32_t) E) - ((ipo + (uint32_t) E - 1) & ~15u));
-  uint64_t acc = 0, acc_ip = 0, acc_ph = 0;
-  if (gl < 4) {
-    const uint32_t w[4] = {v[0].x, v[0].y, v[0].z, v[0].w};
-    const bool l4ok = (uint32_t) gl <= last;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int sft = 16 * gl + 4 * j - hb + 16;
-      acc_ip += w[j] & expand4(pat_bits(pat_ip, sft));
-      acc_ph += w[j] & expand4(pat_bits(kPatPH, sft));
-      uint32_t ml4 = ~expand4(pat_bits(pat_nl4, sft));
-      if ((uint32_t) gl == last) // a short segment ends in this chunk: bytes < tail only
-        ml4 &= in_range(4 * j, 0, tail);
-      acc += l4ok ? (w[j] & ml4) : 0u;
-    }
-  } else if ((uint32_t) gl < nch) {
-    acc += (uint64_t) v[0].x + v[0].y + v[0].z + v[0].w;
-  }
-#pragma unroll
-  for (int u = 1; u < U; ++u) {
-    const uint32_t c = (uint32_t) gl + (uint32_t) G * u;
-    acc += c < nch ? (uint64_t) v[u].x + v[u].y + v[u].z + v[u].w : 0ull;
-  }
-  if (last >= 4u && last < (uint32_t) G * U && (last % G) == (uint32_t) gl && tail < 16) {
-    const uint32_t ut = last / G;
-    u32x4 t = v[0];
-#pragma unroll
-    for (int u = 1; u < U; ++u)
-      if (ut == (uint32_t) u)
-        t = v[u];
-    acc -= (uint64_t) t.x + t.y + t.z + t.w - chunk_prefix_sum(t, tail);
-  }
-  uint32_t part = fold64_to_18(acc);
-  if (nch > (uint32_t) G * U) {
-    Chunks<U> rest;
-    rest.c0p = (const u32x4 *) (base + a0) + (uint32_t) G * U;
-    rest.nch = nch - (uint32_t) G * U;
-    rest.head = 0;
-    rest.tail = tail;
-    part += group_lane_sum<U, G>(rest, gl);
-  }
-  uint32_t c_ip = fold64_to_18(acc_ip);
-  uint32_t c_ph = fold64_to_18(acc_ph);
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 2);
-  part = group_total<G>(part);
-  c_ip = group_total<G>(c_ip);
-  c_ph = group_total<G>(c_ph);
-  if constexpr (VERIFY) {
-    const uint32_t vihl = (uint32_t) __shfl((int) chunk_byte(v[0], hb & 15), gbase + (hb >> 4), 64);
-    if (gl == G - 1) {
-      // every sum above is exact, so the folds are rte_raw_cksum's values
-      uint32_t ri = fold32_to_16(c_ip);
-      if (hb & 1)
-        ri = bswap16(ri);
-      uint32_t flags = ri == 0xffffu ? TASX_RX_IP_OK : 0u;
-      if (tl >= 20 && !trunc) {
-        uint32_t r4 = fold32_to_16(part), rp = fold32_to_16(c_ph);
-        if (hb & 1) {
-          r4 = bswap16(r4);
-          rp = bswap16(rp);
-        }
-        uint32_t c = r4 + fold32_to_16(rp + bswap16(len)); // + rte_ipv4_phdr_cksum
-        c = (c >> 16) + (c & 0xffffu);
-        flags |= c == 0xffffu ? TASX_RX_L4_OK : 0u;
-      }
-      flags |= (vihl & 0xfu) != 5u ? TASX_RX_IHL_NOT5 : 0u;
-      stg((uint8_t *) p.out, i, (uint8_t) flags);
-    }
-  } else if (gl == G - 1) {
-    uint32_t ri = fold32_to_16(c_ip), rp = fold32_to_16(c_ph), r4 = fold32_to_16(part);
-    if (hb & 1) {
-      ri = bswap16(ri);
-      rp = bswap16(rp);
-      r4 = bswap16(r4);
-    }
-    const uint32_t ipc = inv_result(residue(ri));
-    uint32_t tcpc = 0;
-    if (tl >= 20)
-      tcpc = inv_result(residue(fold32_to_16(r4 + rp + bswap16(len))));
-    if (p.out)
-      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-    if (p.flags & TASX_F_INPLACE) {
-      uint8_t *ip = p.base + ipo;
-      st8(ip + 10, ipc);
-      st8(ip + 11, ipc >> 8);
-      st8(ip + 36, tcpc);
-      st8(ip + 37, tcpc >> 8);
-    }
-  }
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 3);
-}
-
-template <int U, int DIAG = 0, int G = 16>
-__global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
-{
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 0);
-  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-  if (i >= p.n)
-    return;
-  tcp4_tas_frame<U, DIAG, G>(p, i, threadIdx.x & (G - 1), (threadIdx.x & 63) & ~(G - 1));
-}
-
-// TCP4 headline kernel: TAS frames in 16-byte aligned mbuf rooms (IPv4 header
-// at 14 mod 16, TCP at +20), one frame per 16-lane DPP row, U = 6 chunks per
-// lane (96 chunks: datagrams up to 1522 B in one round).  The per-lane work is
-// the fold itself: one v_sad_u16 per dword (both LE 16-bit words of the dword
-// added into a 32-bit accumulator: the address-aligned word sum, exact), U
-// loads, U selects, and a fixed header split.  Chunk map (chunk c = frame
-// bytes [16c, 16c+16), dN = its dword N):
-//   chunk 0 = eth[0,14) + ip[0,2)   IP: d3.hi
-//   chunk 1 = ip[2,18)              IP: d0, d1, d2.hi, d3 (ip.chksum = d2.lo left out)
-//                                   PH: d1 byte 3 (proto), d2.hi, d3 (src, dst)
-//   chunk 2 = ip[18,20) + tcp[0,14) IP, PH: d0.lo;  L4: d0.hi, d1..d3
-//   chunk 3 = tcp[14,30)            L4: d0.lo, d1..d3 (tcp.chksum = d0.hi left out)
-//   chunks 4.. = the segment        L4 (bytes past ip + total_length subtracted
-//                                   on the lane holding the last chunk)
-// Lane 1 (chunk 1) forms IP and PH with chunk 0's d3 and chunk 2's d0 moved in
-// by DPP.  How a row learns its datagram's extent (MODE):
-//   kHint    one uniform frame-length hint (flen0, the mbuf data_len of a
-//            uniform-MTU batch) fixes the geometry for every row; a row whose
-//            ip.total_length differs is redone by the general body.  One
-//            dependent memory latency per frame.
-//   kTlFirst the row reads chunk 1 (ip.total_length; all 16 lanes, one line)
-//            first, then exactly its datagram: two dependent latencies, no
-//            byte read past ip.total_length (DPDK's own trust in the header).
-//   kHintArr per-frame hints (the mbuf data_len of each frame): the row's own
-//            hint fixes its geometry and lane 15 checks it against
-//            ip.total_length after the loads (a mismatch, or a hint outside
-//            [ip_off + 38, ip_off + 1522] or beyond the room, is redone by
-//            the general body).  One dependent latency after the hint load,
-//            which 4 rows share a line of.
-//   kHead5   chunks 0..4 (a whole pure ACK, ip.len 52) are loaded with the
-//            total_length, the rest after it: ACK rows take one latency, data
-//            rows two.  Needs a room of 80 B (the chunk-4 read).
-//   kRoom    all 96 chunks of the frame's room at once, masked per row by its
-//            total_length after the loads: one latency for every frame, at the
-//            price of reading whole rooms.  Needs a room of 1536 B.
-// Rows with total_length outside [38 (51 for kHead5), 1522], or beyond the RX
-// read bound, take the general body (tcp4_tas_frame; tcp4_frame_row with OFFS).
-// OFFS (not kHint): frames at base + off[i] instead of i * stride; a row whose
-// frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned loads
-// only the aligned chunk holding the IPv4 header start and is redone by the
-// general row body.
-enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */,
-                       kHintArr = 5 /* per-frame hints as the geometry */,
-                       kHintArrP = 6 /* the same, lanes past the last chunk load nothing (A/B) */,
-                       kHintArrS = 7 /* kHintArr, a block's rows sorted long frames first (A/B, variant 28):
-                                        bit-exact, slower at every ACK fraction (64K frames, 0 / 50 / 100 %
-                                        ACKs: 16.7-17.0 / 10.9-11.1 / 7.9-8.0 us against 16.5 / 10.2 / 7.1-7.2;
-                                        profiles/r02/r02cg) -- the block's 16 hints and two ballots per
-                                        row cost more than the loads pure-ACK waves skip */ };
-
-// The row body after the loads: v[] holds the row's chunks (lane gl: chunks
-// gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
-// the general body for a row the fast path cannot take.
-template <int U, int MODE, bool VERIFY, bool OFFS, bool FALLBACK = true, bool ROWFB = false>
-__device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t i, int gl, const uint8_t *fb,
-                                             uint32_t a0, uint32_t hend, bool in_range, const u32x4 (&v)[U])
-{
-  const uint32_t last = (14u + hend - 1u) >> 4;
-  const uint32_t tail = 14u + hend - 16u * last; // bytes of the last chunk inside, 1..16
-
-  // chunks 0..3: the L4 part of chunk gl (none for 0, 1), whole chunks elsewhere
-  const u32x4 h = v[0];
-  const uint32_t m0 = gl == 2 ? 0xffff0000u : (gl == 3 && !VERIFY ? 0x0000ffffu : 0xffffffffu);
-  uint32_t acc = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
-  acc = (gl < 2 || (uint32_t) gl > last) ? 0u : acc;
-  // IP and PH channels on lane 1
-  const uint32_t c0d3 = row_shr<1>(h.w), c2d0 = row_shl<1>(h.x);
-  const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u))); // src, dst
-  const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
-  uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
-  if constexpr (VERIFY) // the received ip.chksum is part of the check
-    ipsum = sadw(h.z & 0xffffu, ipsum);
-  const uint32_t tlw = h.x & 0xffffu; // ip[2,4): total_length, network order
-#pragma unroll
-  for (int u = 1; u < U; ++u) {
-    const uint32_t s = sad4(v[u], acc);
-    acc = ((uint32_t) gl + 16u * u <= last) ? s : acc;
-  }
-  // bytes [tail, 16) of the last chunk lie past the datagram: the lane holding
-  // that chunk takes them off (its own partial may wrap; the group total is
-  // exact mod 2^32).  Clamped loads leave it in lane 15's last slot; kRoom
-  // picks slot last / 16 on lane last % 16.
-  {
-    uint32_t gm[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t k = tail > 4u * j ? min(tail - 4u * j, 4u) : 0u;
-      gm[j] = (uint32_t) (~0ull << (8u * k));
-    }
-    u32x4 t = v[U - 1];
-    uint32_t tlane = 15u;
-    if constexpr (MODE == kRoom || MODE == kHintArrP) {
-      const uint32_t ut = last >> 4;
-      t = v[0];
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        t = ut == (uint32_t) u ? v[u] : t;
-      tlane = last & 15u;
-    }
-    const uint32_t g = sad4(u32x4{t.x & gm[0], t.y & gm[1], t.z & gm[2], t.w & gm[3]}, 0u);
-    acc -= (uint32_t) gl == tlane ? g : 0u;
-  }
-  acc = row_sum16(acc);
-  const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  constexpr bool kArr = MODE == kHintArr || MODE == kHintArrP || MODE == kHintArrS;
-  const bool bad = MODE == kHint ? tl15 != hend : kArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
-  if constexpr (VERIFY) {
-    const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
-    if (gl == 15 && !bad) {
-      // exact rte_raw_cksum values (every sum above is exact)
-      uint32_t flags = fold32_to_16(ip15) == 0xffffu ? TASX_RX_IP_OK : 0u;
-      uint32_t c = fold32_to_16(acc) + fold32_to_16(ph15 + bswap16(hend - 20u)); // + rte_ipv4_phdr_cksum
-      c = (c >> 16) + (c & 0xffffu);
-      flags |= c == 0xffffu ? TASX_RX_L4_OK : 0u;
-      flags |= (vihl & 0xfu) != 5u ? TASX_RX_IHL_NOT5 : 0u;
-      stg((uint8_t *) p.out, i, (uint8_t) flags);
-    }
-  } else if (gl == 15 && !bad) {
-    const uint32_t ipc = inv_result(residue(fold32_to_16(ip15)));
-    const uint32_t r = fold32_to_16(acc) + fold32_to_16(ph15) + bswap16(hend - 20u);
-    const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
-    if (p.out)
-      stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-    if (p.flags & TASX_F_INPLACE) {
-      uint8_t *ip = (uint8_t *) fb + a0 + 14u;
-      st8(ip + 10, ipc);
-      st8(ip + 11, ipc >> 8);
-      st8(ip + 36, tcpc);
-      st8(ip + 37, tcpc >> 8);
-    }
-  }
-  if (FALLBACK && __builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
-    const int gbase = (threadIdx.x & 63) & ~15;
-    const bool rbad = (MODE == kHint || kArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
-    if (rbad) {
-      if constexpr (OFFS || ROWFB) // ROWFB (A/B): the any-layout row body in stride mode too
-        tcp4_frame_row<3, VERIFY>(p, i, gl);
-      else
-        tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
-    }
-  }
-}
-
-// A/B (TASX_FUSED_DONE=1 with libtasx_ab.so): the kernel's own completion word
-// (DONE, the flush forms).  Measured against the product's second one-lane
-// launch: the submitting core pays less (5.5 -> 3.4 us per 32-frame flush) and
-// a synchronous flush is ~2 us shorter, but every block's agent-scope release
-// writes back L2 (gfx950: agent scope spans the XCDs' separate L2s), and the
-// feeder's sweeps and concurrent flushes get slower (8 threads: 26 against 31
-// M frames/s; profiles/r02/r02am).  Every block makes its stores visible at
-// agent scope and counts itself in (acquire-release on a device-memory
-// counter); the last one resets the counter and release-stores the sequence
-// number into the pinned word the host polls, at system scope.  Vector atomics
-// on device memory only.
-__device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
-{
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(p.done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1u) {
-      __hip_atomic_store(p.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.done_word, p.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-// FLOW (RX, with VERIFY): the frames' flow lookup (fast_flows_packet_fss,
-// tas/fast/fast_flows.c:1084-1163) in the same launch.
-//  kFlowSplit / kFlowSplit1 (the round-2 product, A/B 36 / 27): the grid's first blocks run
-//   flow_lookup_lanes, F frames per lane (F BS consecutive frames per block),
-//   the rest are the verify blocks.  The lookup's dependent chain (key ->
-//   bucket -> flow key) is the long one, so its blocks start first and
-//   overlap the verify rows instead of forming the grid's tail.  64K received
-//   frames: 1.24-1.40x the two kernels in turn.
-//  kFlowRow (A/B variant 26): lanes 0..3 of each verify row load the 12-byte
-//   key before the chunk loads, hash it, probe bucket entry h + lane and load
-//   that candidate's key while the chunks land.  Each wave of 4 rows pays a
-//   whole bitwise CRC for 4 frames, and the bucket (issued after the chunks,
-//   vector loads return in order) waits for all of them: slower wherever
-//   ACKs are present.  Measured and not taken either: lookup blocks
-//   interleaved one per BS frames (their chains end the grid), and the key
-//   hashed beside the row's first load with the bucket issued before the
-//   chunks (the per-row CRC stays).
-//  kFlowSplit / kFlowSplit1: two / one frames per lookup lane -- two for
-//   uniform-length (data) bursts, one for the row forms (data/ACK mixes),
-//   the other choice as A/B variant 27.
-//  kFlowInter (round 3): groups of 128 verify blocks followed by 8 lookup
-//   blocks (136 = 17 x 8 blocks, so every block keeps blockIdx % 8: its XCD
-//   under round-robin placement).  Lookup block x of a group takes the 256
-//   frames of the group's verify blocks on its own XCD (x, x + 8, ...), one per
-//   lane, after them; those rows load their first 256 bytes L2-allocating, so
-//   the lookup reads each frame's 12-byte key from that XCD's L2 instead of
-//   fetching the line again.
-//  kFlowSplitX (round 3, the product for the row forms; kFlowSplitX2 for a
-//   uniform received length): the split grid with the lookup blocks first, one
-//   frame per lane, each lookup block taking the frames of the 16 verify blocks
-//   that land on its own XCD (blocks are placed round-robin over the 8 XCDs
-//   by blockIdx; the lookup block count is a multiple of 8, so verify block vb
-//   keeps vb % 8).  The lookup's plain key load leaves the frame's first line in
-//   that XCD's L2, where the verify row's chunk-0 load then finds it.
-//   kFlowSplitX2: the same with two frames per lookup lane (32 verify blocks
-//   per lookup block).
-// LOPT bit of tcp4_tas14_kernel<kHintArr> (A/B): prefetch the hint line one
-// generation ahead; a generation = 256 CUs x 8 blocks of 16 rows (gfx950 at 8
-// waves per SIMD)
-constexpr int kHintPrefetch = 16;
-// LOPT bit (A/B): a stride-mode row the fast path cannot take is redone by the
-// any-layout row body (tcp4_frame_row, as the OFFS forms) instead of
-// tcp4_tas_frame, whose registers spill at 8 waves per SIMD
-constexpr int kRowFallback = 32;
-// LOPT bit (A/B, timing only): a split grid's verify blocks exit at once
-constexpr int kLookupOnly = 64;
-// LOPT bit (A/B, timing only): a split grid's lookup blocks exit at once
-constexpr int kVerifyOnly = 128;
-// LOPT bit (A/B): a split grid's lookup waves run at the highest issue priority
-constexpr int kLookupPrio = 256;
-// LOPT bit (A/B, kHintArr): rows of the second generation of resident blocks
-// take the other half of the hint lines the first generation read (block b
-// and block b + kGenBlocks, same XCD), so their hint loads hit L2 -- no extra
-// instruction, unlike kHintPrefetch.  A generation = 256 CUs x 8 blocks.
-constexpr int kLinePair = 512;
-constexpr uint32_t kGenBlocks = 256u * 8u;
-// frame of row `row` (of 16) in verify block vb of nblk, kLinePair order:
-// blocks 2kG + r and (2k + 1)G + r share hint line kG + r (32 frames); blocks
-// past the last whole pair of generations keep the identity order
-__device__ __forceinline__ uint32_t line_pair_frame(uint32_t vb, uint32_t row, uint32_t nblk)
-{
-  constexpr uint32_t G = kGenBlocks;
-  const uint32_t P = nblk / (2u * G);
-  if (vb >= 2u * G * P)
-    return vb * 16u + row;
-  const uint32_t g = vb / G, r = vb % G;
-  return 32u * ((g / 2u) * G + r) + 16u * (g & 1u) + row;
-}
-constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
-// lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
-template <uint32_t F>
-__host__ __device__ constexpr uint32_t splitx_lookup_blocks(uint32_t nv) { return ((nv + 16u * F - 1u) / (16u * F) + 7u) & ~7u; }
-constexpr uint32_t kInterV = 128u, kInterL = 8u; // verify / lookup blocks per group
-// frames per lane of a split grid's lookup blocks
-template <int FLOW>
-constexpr uint32_t split_frames() { return FLOW == kFlowSplit1 ? 1u : 2u; }
-template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
-          int FLOW = kFlowNone, int LOPT = 0>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
-{
-  static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
-  static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
-  static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
-  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX && FLOW != kFlowSplitX2) || !DONE,
-                "split grids post no completion word");
-  const int gl = threadIdx.x & 15;
-  // this block's verify block (split grids: below); large batches XCD-ordered
-  uint32_t vb = FLOW == kFlowNone ? xcd_run(blockIdx.x, gridDim.x, p.xrun) : blockIdx.x;
-  // kFlowRow: CRC32C from slice-by-4 tables the block builds in LDS first (before
-  // any row leaves: every wave reaches the barriers; the bitwise CRC cost every
-  // verify wave ~300 VALU)
-  __shared__ uint32_t lt[FLOW == kFlowRow ? 4 : 1][256];
-  if constexpr (FLOW == kFlowRow) {
-    static_assert(BS == 256, "one table entry per thread");
-    uint32_t c = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
-    lt[0][threadIdx.x] = c;
-    __syncthreads();
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      c = (c >> 8) ^ lt[0][c & 0xffu];
-      lt[k][threadIdx.x] = c;
-    }
-    __syncthreads();
-  }
-  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1) {
-    // the lookup blocks first: their dependent chains are the long ones, so
-    // they start at once and overlap the verify blocks instead of forming the
-    // grid's tail (interleaved one per BS frames they did: DESIGN.md 5.2)
-    constexpr uint32_t kF = split_frames<FLOW>(); // frames per lookup lane (flow_kernels.hip: kFlowFramesPerLane)
-    const uint32_t nl = (uint32_t) (((uint64_t) p.n + BS * kF - 1u) / (BS * kF)); // 64-bit: n near 2^32
-    if (blockIdx.x < nl) {
-      flow_lookup_lanes<kF, BS, LOPT>(p, blockIdx.x);
-      return;
-    }
-    vb = blockIdx.x - nl;
-  }
-  if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2) {
-    static_assert(BS == 256, "16 verify rows per block, one lookup lane per row of 16 blocks");
-    constexpr uint32_t kF = FLOW == kFlowSplitX2 ? 2u : 1u;
-    const uint32_t nl = splitx_lookup_blocks<kF>((uint32_t) (((uint64_t) p.n + BS / 16 - 1u) / (BS / 16)));
-    if (blockIdx.x < nl) {
-      if constexpr ((LOPT & kVerifyOnly) != 0)
-        return; // A/B timing: the verify blocks alone
-      if constexpr ((LOPT & kLookupPrio) != 0)
-        __builtin_amdgcn_s_setprio(3); // A/B: the lookup waves' instructions issue first
-      // lane t, frame f: row t % 16 of verify block 8 (16 F (b / 8) + 16 f + t / 16) + b % 8 (past the batch: no store)
-      const uint32_t b = blockIdx.x;
-      uint32_t i0[kF];
-#pragma unroll
-      for (uint32_t f = 0; f < kF; ++f) {
-        const uint32_t vbk = 8u * (16u * kF * (b / 8u) + 16u * f + threadIdx.x / 16u) + (b & 7u);
-        i0[f] = vbk * (BS / 16) + (threadIdx.x & 15u);
-        if constexpr ((LOPT & kLinePair) != 0) // the verify rows' frame order (past the batch: still >= n)
-          i0[f] = line_pair_frame(vbk, threadIdx.x & 15u, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
-      }
-      flow_lookup_lanes_at<kF, BS, LOPT>(p, i0);
-      return;
-    }
-    if constexpr ((LOPT & kLookupOnly) != 0)
-      return; // A/B timing: the lookup blocks alone
-    vb = blockIdx.x - nl;
-  }
-  if constexpr (FLOW == kFlowInter) {
-    static_assert(BS == 256, "16 verify rows per block, one lookup lane per frame of 16 blocks");
-    const uint32_t g = blockIdx.x / (kInterV + kInterL), r = blockIdx.x % (kInterV + kInterL);
-    if (r >= kInterV) {
-      // lane t: row t % 16 of the group's verify block x + 8 (t / 16)
-      const uint32_t x = r - kInterV;
-      const uint32_t i0[1] = {(g * kInterV + x + kInterL * (threadIdx.x / 16u)) * (BS / 16) + (threadIdx.x & 15u)};
-      flow_lookup_lanes_at<1, BS, LOPT>(p, i0);
-      return;
-    }
-    vb = g * kInterV + r;
-  }
-  uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
-  if constexpr ((LOPT & kLinePair) != 0 && MODE == kHintArr && BS == 256)
-    i = line_pair_frame(vb, threadIdx.x / 16, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
-  uint32_t hs = 0; // kHintArrS: the row's hint
-  if constexpr (MODE == kHintArrS) {
-    // The block's rows take its frames long ones first (stable), so that the
-    // frames that fit in one chunk per lane (pure ACKs) share waves, and those
-    // waves issue one load instead of U.  Every row reads the block's BS / 16
-    // hints, one per lane, and computes the same permutation: no LDS, no barrier.
-    static_assert(BS / 16 <= 16, "one lane per frame of the block");
-    const uint32_t f0 = vb * (BS / 16), fi = f0 + (uint32_t) gl;
-    const bool mine = gl < BS / 16 && fi < p.n;
-    const uint32_t hh = mine ? ldg(p.flen, fi) : 0u;
-    const bool lng = mine && hh > p.ip_off + 242u; // more than one chunk per lane of a row
-    const uint32_t sh = (threadIdx.x & 63u) & ~15u;
-    const uint32_t lm = (uint32_t) (__builtin_amdgcn_ballot_w64(lng) >> sh) & 0xffffu;
-    const uint32_t below = __builtin_popcount(lm & ((1u << gl) - 1u));
-    const uint32_t dest = lng ? below : (uint32_t) __builtin_popcount(lm) + (uint32_t) gl - below;
-    const uint32_t row = threadIdx.x / 16u;
-    const uint32_t fm = (uint32_t) (__builtin_amdgcn_ballot_w64(dest == row && gl < BS / 16) >> sh) & 0xffffu;
-    const int f = fm ? __builtin_ctz(fm) : 0;
-    hs = (uint32_t) __shfl((int) hh, (int) sh + f, 64);
-    i = f0 + (uint32_t) f;
-  }
-  if (i >= p.n)
-    return;
-  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
-  const uint8_t *ipp;         // the IPv4 header (FLOW)
-  uint32_t a0;
-  bool row_ok = true;
-  if constexpr (OFFS) {
-    const uint64_t fo = (uint64_t) (uintptr_t) p.base + ldg(p.off, i) + (p.ip_off & ~15u);
-    row_ok = (fo & 15u) == 0u;
-    fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
-    a0 = 0;
-    ipp = (const uint8_t *) (uintptr_t) (fo + 14u);
-  } else {
-    a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
-    ipp = fb + a0 + 14u;
-  }
-  constexpr int kNb = (int) TASX_FLOWHT_NBSZ;
-  u32x3 fkey = {0u, 0u, 0u};
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) // ip.src, ip.dst, tcp.src | tcp.dst << 16 (little-endian dwords)
-      fkey = *(__attribute__((address_space(1))) const u32x3u *) (ipp + 12);
-  }
-  // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
-  uint32_t have = 65535u;
-  if constexpr (VERIFY && MODE != kHint) {
-    const uint32_t b = rx_bound(p, MODE == kHintArrS ? hs : p.flen ? ldg(p.flen, i) : p.flen0);
-    have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-  }
-  // FLOW (kFlowRow): the key arrived with the hint, so the hash and the bucket
-  // probe go out BEFORE the chunk loads (vector loads complete in order: a
-  // bucket issued after the chunks could be used only once they all landed)
-  uint32_t fh = 0;
-  uint64_t fe = 0;
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) {
-      fh = crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, fkey.y), fkey.x), (fkey.z >> 16) | (fkey.z << 16));
-      const uint32_t ht = p.ht_entries;
-      const uint32_t hb = (ht & (ht - 1u)) == 0u ? (fh & (ht - 1u)) : fh % ht; // the bucket's first entry
-      const uint32_t ej = hb + (uint32_t) gl;
-      // one subtraction wraps ej < ht + kNb; tables smaller than a bucket take the modulo
-      fe = ldg((const uint64_t *) p.flowht, ht >= (uint32_t) kNb ? (ej >= ht ? ej - ht : ej) : ej % ht);
-    }
-  }
-  // the datagram [ip, ip + hend): uniform from the hint, or per row from the
-  // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
-  const uint32_t lo = a0 + 16u * (uint32_t) gl;
-  uint32_t hend;
-  bool in_range = true;
-  u32x4 v[U];
-  if constexpr (MODE == kHint) {
-    hend = p.flen0 - p.ip_off;
-    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kTlFirst) {
-    const uint32_t tl0 = bswap16(ld16nt_off(fb, a0 + (row_ok ? 16u : 0u)).x & 0xffffu);
-    // from 38 (tcp.chksum inside the datagram, so the last chunk's bytes past
-    // the end never include the masked field; pure ACKs, ip.len 52, qualify)
-    // to 1522 (96 chunks)
-    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    // out of range: the header only, then the general body (a misaligned row: chunk 0 only)
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-    const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kHintArr || MODE == kHintArrP) {
-    // the row's own hint (mbuf data_len) fixes its geometry; lane 15 checks
-    // it against total_length afterwards, as kHint does for a uniform hint
-    const uint32_t h = ldg(p.flen, i);
-    const uint32_t hl = h > p.ip_off ? h - p.ip_off : 0u;
-    in_range = row_ok && hl >= 38u && hl <= 1522u && h <= slot_bound(p); // reads stay inside the room / slot
-    hend = in_range ? hl : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (MODE == kHintArrP) {
-        v[u] = u32x4{0u, 0u, 0u, 0u};
-        if ((uint32_t) gl + 16u * u <= last) // the tail comes from v[last / 16] on lane last % 16
-          v[u] = ld16nt_off(fb, lo + 256u * u);
-      } else if (FLOW == kFlowInter && u == 0) { // the key's line stays in L2 for the lookup block
-        v[u] = ld16_off(fb, min(lo, lastoff));
-      } else {
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-      }
-    }
-  } else if constexpr (MODE == kHintArrS) {
-    const uint32_t hl = hs > p.ip_off ? hs - p.ip_off : 0u;
-    in_range = row_ok && hl >= 38u && hl <= 1522u && hs <= slot_bound(p);
-    hend = in_range ? hl : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
-    v[0] = ld16nt_off(fb, min(lo, lastoff));
-    if (__builtin_amdgcn_ballot_w64(last >= 16u) != 0ull) { // a wave-uniform branch
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    } else { // every row of the wave ends in its first 256 bytes; lane 15's v[U-1] = the last chunk
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = v[0];
-    }
-  } else if constexpr (MODE == kHead5) {
-    v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
-    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
-    // from 51: the last chunk is chunk 4 or later, so lane 15 holds it
-    in_range = row_ok && tl0 >= 51u && tl0 <= 1522u && tl0 <= have;
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4;
-    if (last > 4u) { // the datagram goes on past chunk 4
-      const uint32_t lastoff = a0 + 16u * last;
-      if (gl > 4)
-        v[0] = ld16nt_off(fb, min(lo, lastoff));
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    } else {
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = v[0]; // excluded below; lane 15's v[U-1] = chunk 4, the last one
-    }
-  } else { // kRoom
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, row_ok ? lo + 256u * u : a0);
-    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
-    in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-  }
-  // LOPT & kHintPrefetch (A/B, kHintArr): after its chunk loads, one lane per
-  // hint line (32 rows) loads the line of the row one generation of resident
-  // rows later, so that row's first load (its hint) is an L2 hit (block b and
-  // block b + kPrefetchRows / 16 run on the same XCD)
-  uint32_t pf = 0;
-  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS) {
-    const uint32_t j = i + kPrefetchRows;
-    if (gl == 0 && (i & 31u) == 0u && j < p.n)
-      pf = ldg(p.flen, j);
-  }
-  // FLOW: the flow-state key load goes out while the chunks are in flight (the
-  // bucket, issued before them, has returned first)
-  uint32_t ffid = 0;
-  u32x3 ck = {0u, 0u, 0u};
-  bool fcand = false;
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) {
-      const uint32_t ef = (uint32_t) fe, eh = (uint32_t) (fe >> 32);
-      ffid = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-      fcand = (ef & TASX_FLOWHTE_VALID) && eh == fh && ffid < p.fs_num;
-      ck = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
-                                                              (uint64_t) (fcand ? ffid : 0u) * p.fs_stride +
-                                                              p.fs_key_off);
-    }
-  }
-  tas14_finish<U, MODE, VERIFY, OFFS, true, (LOPT & kRowFallback) != 0>(p, i, gl, fb, a0, hend, in_range, v);
-  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS)
-    asm volatile("" ::"v"(pf)); // the prefetch is not dead code
-  if constexpr (FLOW == kFlowRow) {
-    const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16);
-    const bool match = gl < kNb && fcand && ck.x == fkey.y && ck.y == fkey.x && ck.z == ports;
-    const uint32_t rm = (uint32_t) (__builtin_amdgcn_ballot_w64(match) >> ((threadIdx.x & 63u) & ~15u)) & 0xfu;
-    const int first = rm ? __builtin_ctz(rm) : 0; // the first matching entry wins
-    if (gl == first)
-      stg(p.fid_out, i, rm ? ffid : TASX_FLOW_NONE);
-    if (gl == 0 && p.hash_out)
-      stg(p.hash_out, i, fh);
-  }
-  if constexpr (DONE)
-    block_done(p);
-}
-
-#ifdef TASX_AB
-// A whole short datagram (ip.len 38..66: a pure ACK, flow_tx_ack
-// fast_flows.c:957-1030, is 52) in ONE lane: c[] = chunks 0..4 of the frame
-// (IPv4 at a0 + 14, tcp4_tas14_kernel's chunk map), both results stored.
-__device__ __forceinline__ void tas14_short_lane(const tasx_tcp4_params &p, uint32_t i, const uint8_t *fb, uint32_t a0,
-                                                 uint32_t tl, const u32x4 (&c)[5])
-{
-  const uint32_t addrs = sadw(c[1].z & 0xffff0000u, sadw(c[1].w, sadw(c[2].x & 0xffffu, 0u))); // src, dst
-  const uint32_t ph = sadw(c[1].y & 0xff000000u, addrs);                                      // + proto
-  const uint32_t ipsum = sadw(c[0].w & 0xffff0000u, sadw(c[1].x, sadw(c[1].y, addrs)));      // ip.chksum left out
-  // L4 = frame bytes [34, 14 + tl): chunk 2 from byte 2, chunk 3 without
-  // tcp.chksum (its bytes 2..3), chunk 4 up to the datagram's end
-  const int end = 14 + (int) tl; // 52..80
-  u32x4 c3 = mask_chunk(c[3], 0, min(end - 48, 16));
-  c3.x &= 0x0000ffffu;
-  uint32_t l4 = sad4(mask_chunk(c[2], 2, 16), 0u);
-  l4 = sad4(c3, l4);
-  l4 = sad4(mask_chunk(c[4], 0, max(end - 64, 0)), l4);
-  const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
-  const uint32_t r = fold32_to_16(l4) + fold32_to_16(ph) + bswap16(tl - 20u);
-  const uint32_t tcpc = inv_result(residue(fold32_to_16(r)));
-  if (p.out)
-    stg((uint32_t *) p.out, i, ipc | (tcpc << 16));
-  if (p.flags & TASX_F_INPLACE) {
-    uint8_t *ip = (uint8_t *) fb + a0 + 14u;
-    st8(ip + 10, ipc);
-    st8(ip + 11, ipc >> 8);
-    st8(ip + 36, tcpc);
-    st8(ip + 37, tcpc >> 8);
-  }
-}
-
-// tcp4_mix_kernel: TX batches that mix data segments and pure ACKs (what
-// tx_flush sends: flow_tx_segment's ~1.5 KB frames and flow_tx_ack's 66 B
-// frames, fastemu.c:544-566), TAS frames in stride mode, a room of >= 80 B.
-// One wave takes 16 frames.  Phase 1: lane l < 16 loads chunks 0..4 of frame
-// 16w + l (a whole ACK) and classifies the frame by its own total_length:
-// short (38..66: finished by that lane alone, one memory latency), data
-// (67..1522) or other (the general body, tcp4_tas_frame).  Phase 2: the data
-// frames, compacted by a forward lane permute, go 4 per pass to the wave's
-// 16-lane rows, and every pass's loads are in flight before the first is
-// summed (tcp4_tas14_kernel's row body).  kTlFirst spends a 16-lane row and
-// a second dependent latency on every ACK, and needs two generations of
-// resident waves for 64K frames; here an ACK costs one lane and the 64K-frame
-// batch fits one generation (4 waves per SIMD x 16 frames).
-// A/B only (variant 19; TASX_MIX_F8=1: 8 frames per wave): bit-exact, but
-// slower than kTlFirst wherever data frames are present (64K frames in 2048 B
-// rooms, 0 / 50 / 100 % ACKs: 19.5-20.2 / 12.6-12.9 / 6.5-6.6 us with 16
-// frames per wave, 18.7 / 12.2-12.3 / 6.1 us with 8, against 16.9-17.3 /
-// 10.7-10.9 / 6.9 us; profiles/r02/r02m, r02n): a wave issues its data only
-// after the slowest of its frames' phase-1 loads, a kTlFirst row as soon as
-// its own total_length lands.
-template <int U, int F = 16>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(F == 16 ? 4 : 6))) void tcp4_mix_kernel(tasx_tcp4_params p)
-{
-  static_assert(U == 6, "96 chunks cover the 1522-byte datagram bound");
-  static_assert(F == 8 || F == 16, "frames per wave: 2 or 4 passes of 4 rows");
-  constexpr int NP = F / 4;
-  const int lane = (int) (threadIdx.x & 63u), gl = lane & 15, row = lane >> 4;
-  const uint32_t w0 = (blockIdx.x * (kBlock / 64) + threadIdx.x / 64) * (uint32_t) F; // the wave's first frame
-  if (w0 >= p.n)
-    return; // the whole wave leaves together
-  const uint8_t *fb = p.base; // loads at fb + 32-bit offsets (tas14_stride_ok)
-  const uint32_t ipa = p.ip_off & ~15u, nf = min(p.n - w0, (uint32_t) F);
-  const uint32_t st = (uint32_t) p.stride;
-
-  // phase 1: frame w0 + lane on lanes 0..15
-  const bool mine = lane < 16 && (uint32_t) lane < nf;
-  const uint32_t a0 = (w0 + (uint32_t) gl) * st + ipa;
-  u32x4 c[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k)
-    c[k] = u32x4{0u, 0u, 0u, 0u};
-  if (mine) {
-#pragma unroll
-    for (int k = 0; k < 5; ++k)
-      c[k] = ld16nt_off(fb, a0 + 16u * (uint32_t) k);
-  }
-  const uint32_t tl = bswap16(c[1].x & 0xffffu);
-  const bool shortf = mine && tl >= 38u && tl <= 66u;
-  const bool data = mine && tl > 66u && tl <= 1522u;
-  const bool other = mine && !shortf && !data;
-  const uint64_t dm = __builtin_amdgcn_ballot_w64(data), om = __builtin_amdgcn_ballot_w64(other);
-  // compaction: data frame of rank r -> lane r, other frame of rank r -> lane
-  // 32 + r (everything else lands in lanes 16..31 / 48..63, never read)
-  const uint32_t below = (1u << (lane & 31)) - 1u; // lanes < 16 only matter
-  const uint32_t rd = (uint32_t) __builtin_popcount((uint32_t) dm & below);
-  const uint32_t ro = (uint32_t) __builtin_popcount((uint32_t) om & below);
-  const int dst = data ? (int) rd : other ? 32 + (int) ro : lane < 16 ? 48 + lane : 16 + (lane & 15);
-  const uint32_t pk = (uint32_t) __builtin_amdgcn_ds_permute(dst * 4, (int) ((uint32_t) gl | (tl << 8)));
-  if (shortf)
-    tas14_short_lane(p, w0 + (uint32_t) gl, fb, a0, tl, c);
-
-  // phase 2: data frames 4 per pass, all passes' loads issued first.  The
-  // loads are unconditional (an idle row reads the wave's first frame's
-  // chunk 1, a line phase 1 just fetched) so that the waits before each pass
-  // count exactly the loads ahead of it: under a branch the compiler must wait
-  // for all of them before the first pass.
-  const uint32_t nd = (uint32_t) __builtin_popcountll(dm);
-  u32x4 v[NP][U];
-  uint32_t q[NP];
-#pragma unroll
-  for (int ps = 0; ps < NP; ++ps) {
-    q[ps] = (uint32_t) __shfl((int) pk, 4 * ps + row, 64);
-    const bool act = 4u * ps + (uint32_t) row < nd;
-    const uint32_t hend = act ? q[ps] >> 8 : 20u;
-    const uint32_t r0 = (w0 + (act ? (q[ps] & 15u) : 0u)) * st + ipa;
-    const uint32_t lastoff = r0 + 16u * ((14u + hend - 1u) >> 4), lo = r0 + 16u * (uint32_t) gl;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[ps][u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  }
-#pragma unroll
-  for (int ps = 0; ps < NP; ++ps) {
-    if (nd > 4u * ps && 4u * ps + (uint32_t) row < nd) {
-      const uint32_t r0 = (w0 + (q[ps] & 15u)) * st + ipa;
-      tas14_finish<U, kTlFirst, false, false, false>(p, w0 + (q[ps] & 15u), gl, fb, r0, q[ps] >> 8, true, v[ps]);
-    }
-  }
-
-  // other frames (total_length outside 38..1522): the general body, 4 per pass
-  const uint32_t no = (uint32_t) __builtin_popcountll(om);
-  for (uint32_t o = 0; o < no; o += 4u) {
-    const uint32_t qo = (uint32_t) __shfl((int) pk, 32 + (int) o + row, 64);
-    if (o + (uint32_t) row < no)
-      tcp4_tas_frame<U, 0, 16, false>(p, w0 + (qo & 15u), gl, lane & ~15);
-  }
-}
-#endif
-
-// tcp4_tas14_kernel's total_length-first rows as a persistent loop: row r
-// takes frames r, r + R, r + 2R, ... (R rows in the grid) and loads the next
-// frame's total_length while the current frame's data is in flight, so in the
-// steady state a frame costs one dependent memory latency instead of two
-// (stride mode; TX and RX as tcp4_tas14_kernel<kTlFirst>).
-template <int U, bool VERIFY = false, int WPE = 8>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_rows_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t R = gridDim.x * (kBlock / 16);
-  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return;
-  const uint8_t *fb = p.base;
-  const uint32_t ipa = p.ip_off & ~15u;
-  uint32_t tln = bswap16(ldg((const uint32_t *) (fb + i * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
-  for (; i < p.n; i += R) { // row-uniform
-    const uint32_t a0 = i * (uint32_t) p.stride + ipa;
-    uint32_t have = 65535u;
-    if constexpr (VERIFY) {
-      const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
-      have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-    }
-    const uint32_t tl0 = tln;
-    const bool in_range = tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    const uint32_t hend = in_range ? tl0 : 20u;
-    const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    const uint32_t inext = i + R;
-    if (inext < p.n) // the next frame's total_length, in flight with this frame's data
-      tln = bswap16(ldg((const uint32_t *) (fb + inext * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
-    tas14_finish<U, kTlFirst, VERIFY, false>(p, i, gl, fb, a0, hend, in_range, v);
-  }
-}
-
-// Dynamic LDS reserved (never used) by the v_sad_u16 kernels to cap residency
-// at 5 blocks = 20 waves per CU: with ~100 VALU per wave they would otherwise
-// run 8 waves per SIMD, and the extra bytes in flight only lengthen the queue
-// (interleaved sweeps: 64K TAS frames -0.4%, 64K x 1500 B RAW -1%, 8M x 1500 B
-// RAW -1.5%; profiles/r01_sweeps_s2.jsonl).
-constexpr uint32_t kOccLds = 30u * 1024u;
-
-// raw_wave_kernel: chunks per lane per round and the LDS reservation
-#ifndef TASX_WAVE_U
-#define TASX_WAVE_U 6
-#endif
-#ifndef TASX_WAVE_LDS
-#define TASX_WAVE_LDS kOccLds
-#endif
-
-// the launched kernel's name, per calling thread (tasx_last_kernel)
-static thread_local const char *t_last_kernel = "";
-// whether the calling thread's last tasx_launch_tcp4 posted p->done_word
-static thread_local int t_posted_done = 0;
-
-// XCD-ordered grids (xcd_run, round 5): from 16,384 blocks (a batch of 256K
-// frames or packets and up) each XCD works through runs of 256 consecutive
-// blocks (6 MB of 1500-byte packets), the 8 runs of a window adjacent.  In grid
-// order the 8 XCDs share every page of the ~30 MB the resident blocks span
-// (26.7K UTCL1 translation misses per 12.6 GB launch, the UTCL2 busy 1.1-1.6M
-// cycles); in runs each XCD's resident blocks lie in two or three 2 MB pages
-// (0-3.7K misses, UTCL2 busy 9K-230K).  8M x 1500 B RAW: 1.74-1.77 ms against
-// 1.87-2.00 (profiles/r05/INDEX.md r05a-r05c); 64K-frame batches (the headline)
-// are neutral to slower in any XCD order and stay in grid order.
-constexpr uint32_t kXrunMinBlocks = 16384u;
-constexpr uint32_t kXrun = 9u; // runs of 2^(9 - 1) = 256 blocks
-
-#ifdef TASX_AB
-// A/B: the xrun of every grid (0 = grid order; -1 = the product's rule), from
-// tasx_ab_set_xrun or TASX_XRUN
-static int g_xrun_ov = -2;
-extern "C" int tasx_ab_set_xrun(int xrun)
-{
-  if (xrun < -1 || xrun > 20)
-    return -22;
-  g_xrun_ov = xrun;
-  return 0;
-}
-#endif
-
-static uint32_t xrun_for(uint64_t blocks)
-{
-#ifdef TASX_AB
-  if (g_xrun_ov == -2) {
-    const char *e = getenv("TASX_XRUN");
-    g_xrun_ov = e ? atoi(e) : -1;
-  }
-  if (g_xrun_ov >= 0)
-    return (uint32_t) g_xrun_ov;
-#endif
-  return blocks >= kXrunMinBlocks ? kXrun : 0u;
-}
-
-template <int G = 16, int BS = kBlock, typename K, typename Prm>
-int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
-{
-  // one G-lane group per packet, BS / G groups per block: the grid covers
-  // the batch once (measured faster than persistent grids at these batch
-  // sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
-  constexpr uint64_t fpb = BS / G;
-  const uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
-  if (blocks == 0)
-    return 0;
-  if (blocks > 0x7fffffffull)
-    return -2;
-  Prm q = p;
-  q.xrun = xrun_for(blocks);
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(BS), lds, s, q);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-#ifdef TASX_AB
-template <typename K, typename P>
-int launch(const char *name, K kern, const P &p, uint32_t groups_per_block, int max_blocks, hipStream_t s)
-{
-  uint64_t blocks = ((uint64_t) p.n + groups_per_block - 1) / groups_per_block;
-  if (blocks > (uint64_t) max_blocks)
-    blocks = (uint64_t) max_blocks;
-  if (blocks == 0)
-    return 0;
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-#endif
-
-} // namespace
+// The device code lives in xsum_rows.h.  The A/B build (libtasx_ab.so =
+// these objects plus ab/, include/tasx_ab.h) adds its variants through the
+// tasx_ext hooks (tasx_kernels.h): the first-generation group-per-packet
+// kernels, wave-timeline stamps, 32-lane groups, tcp4_wave_kernel, forced row
+// modes, block sizes, the RX pass's split and ablation forms.
+#include "xsum_rows.h"
 
 // ---------------------------------------------------------------------------
 // launchers (C ABI, internal to libtasx)
+
+// the launched kernel's name, per calling thread (tasx_last_kernel)
+static thread_local const char *t_last_kernel = "";
 
 extern "C" const char *tasx_last_kernel(void)
 {
@@ -1643,80 +55,6 @@ extern "C" const char *tasx_last_kernel(void)
 extern "C" void tasx_note_kernel(const char *name)
 {
   t_last_kernel = name;
-}
-
-extern "C" int tasx_last_launch_posted_done(void)
-{
-  return t_posted_done;
-}
-
-#ifdef TASX_AB
-// residency knobs (KiB of reserved LDS / waves per SIMD) for A/B runs
-static uint32_t env_lds(const char *name, uint32_t dflt)
-{
-  const char *e = getenv(name);
-  return e ? (uint32_t) atoi(e) * 1024u : dflt;
-}
-#define TASX_LDS(name, dflt) env_lds(name, dflt)
-#else
-#define TASX_LDS(name, dflt) (dflt)
-#endif
-
-// tcp4_tas_kernel preconditions: TAS layout, 16-byte aligned base, stride mode,
-// every frame within 4 GiB of the base (32-bit offsets)
-static bool tas_kernel_ok(const tasx_tcp4_params &p)
-{
-  return p.l4_off == p.ip_off + 20 && ((uintptr_t) p.base & 15u) == 0 && p.off == nullptr &&
-         (uint64_t) p.n * p.stride + 65536u + p.ip_off < (1ull << 32);
-}
-
-// tcp4_tas14_kernel in stride mode: in addition the IPv4 header at 14 mod 16
-// in every frame (a 16-byte multiple stride)
-static bool tas14_stride_ok(const tasx_tcp4_params &p)
-{
-  return tas_kernel_ok(p) && (p.ip_off & 15u) == 14u && (p.stride & 15u) == 0;
-}
-
-// ... with one uniform hint whose datagram spans 5..96 chunks and covers tcp.chksum
-static bool tas14_ok(const tasx_tcp4_params &p)
-{
-  if (!tas14_stride_ok(p) || p.flen || !p.flen0)
-    return false;
-  if (p.flen0 < p.ip_off + 64u || p.flen0 - p.ip_off > 65535u)
-    return false;
-  return ((14u + (p.flen0 - p.ip_off) + 15u) >> 4) <= 16u * 6u;
-}
-
-// ... without a uniform hint (per-frame hints only steer reads: a row's
-// results follow its own total_length), stride mode or frames by an offsets array (IPv4 at 14
-// mod 16 from the frame start; frames not 16-byte aligned are checked per row)
-static bool tas14_nohint_ok(const tasx_tcp4_params &p)
-{
-  return tas14_stride_ok(p) && !p.flen0;
-}
-static bool tas14_offs_ok(const tasx_tcp4_params &p)
-{
-  return p.off != nullptr && p.l4_off == p.ip_off + 20 && (p.ip_off & 15u) == 14u && !p.flen0;
-}
-
-// Row mode without a uniform hint.  A room covering a full-MTU frame lets rows
-// of a batch that carries no per-frame lengths load the whole MTU at once
-// (bulk TX batches: 64K MTU frames 15.9 us against 16.9 us total_length
-// first).  Batches with per-frame hints are data/ACK mixes, where whole-room
-// reads cost every ACK row 1.5 KB (16.0 us at any ACK share) and total_length
-// first wins (25 / 50 / 75 % ACKs: 13.6 / 10.6 / 8.5 us); the head-5 mode
-// (an ACK's 80 bytes with the total_length) lost to it everywhere but all-ACK
-// batches (6.3 against 6.8 us) and is an A/B variant (10).  With per-frame
-// hints each row takes its own hint as its geometry (kHintArr: no dependent
-// total_length read; 0 / 25 / 50 / 75 % ACKs 16.5 / 13.2 / 10.4-10.5 / 8.3 us
-// against 17.0 / 13.6-13.7 / 10.6-10.8 / 8.6 us, all-ACK 7.2 against 6.9).
-// tools/ackmix_probe.py, profiles/r02/r02d_ackmix_modes.jsonl, r02o.
-static int tas14_mode(const tasx_tcp4_params &p)
-{
-  const uint32_t from_a0 = p.room > (p.ip_off & ~15u) ? p.room - (p.ip_off & ~15u) : 0u;
-  if (p.flen)
-    return kHintArr;
-  return from_a0 >= 1536u ? kRoom : kTlFirst;
 }
 
 // completion word: stream-ordered after the work before it, one lane stores
@@ -1771,157 +109,6 @@ __global__ __launch_bounds__(kBlock) void tcp4_offload_kernel(tasx_tcp4_params p
 }
 } // namespace
 
-#ifdef TASX_AB
-// The headline kernel's access pattern with no checksum logic: the same rows,
-// the same 6 clamped chunk loads per lane at 32-bit offsets from the SGPR
-// base, the same 4-byte result store per frame and LDS reservation; the
-// loaded words are only xor-folded.  bench.py times it beside the headline
-// (its pattern_ceiling).
-namespace {
-__global__ __launch_bounds__(kBlock) void tcp4_pattern_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return;
-  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u), hend = p.flen0 - p.ip_off;
-  const uint32_t lastoff = a0 + 16u * ((14u + hend - 1u) >> 4), lo = a0 + 16u * (uint32_t) gl;
-  u32x4 v[6];
-#pragma unroll
-  for (int u = 0; u < 6; ++u)
-    v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
-  uint32_t x = 0;
-#pragma unroll
-  for (int u = 0; u < 6; ++u)
-    x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  x = row_sum16(x);
-  if (gl == 15)
-    stg((uint32_t *) p.out, i, x);
-}
-
-// The data/ACK mix's access pattern (tcp4_tas14_kernel<hints>, the flush_mix
-// leg) with no checksum logic, for its latency roofline (bench.py
-// mix_bounds): each row reads its hint, then (CHAIN = 0) the same clamped
-// chunk loads as the product, xor-folded, or (CHAIN = 1) only the chunk
-// holding the frame's end on lane 15 -- the row's dependent chain (hint ->
-// frame -> result store) with almost no bytes behind it; 8 waves per SIMD as
-// the product.
-template <int CHAIN>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void tcp4_mix_pattern_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if constexpr (CHAIN == 2) {
-    // two frames per row, i and i + n / 2 (rounded up): both hints, then both
-    // frames' chunk loads, one generation of resident rows for 64K frames
-    const uint32_t half = (p.n + 1u) / 2u;
-    if (i >= half)
-      return;
-    const uint32_t i2 = min(i + half, p.n - 1u);
-    const uint32_t h1 = ldg(p.flen, i), h2 = ldg(p.flen, i2);
-    uint32_t x1 = 0, x2 = 0;
-    u32x4 v1[6], v2[6];
-    {
-      const uint32_t a1 = i * (uint32_t) p.stride + (p.ip_off & ~15u), a2 = i2 * (uint32_t) p.stride + (p.ip_off & ~15u);
-      const uint32_t hl1 = h1 > p.ip_off + 20u ? min(h1 - p.ip_off, 1522u) : 20u;
-      const uint32_t hl2 = h2 > p.ip_off + 20u ? min(h2 - p.ip_off, 1522u) : 20u;
-      const uint32_t l1 = a1 + 16u * ((14u + hl1 - 1u) >> 4), l2 = a2 + 16u * ((14u + hl2 - 1u) >> 4);
-#pragma unroll
-      for (int u = 0; u < 6; ++u)
-        v1[u] = ld16nt_off(p.base, min(a1 + 16u * (uint32_t) gl + 256u * u, l1));
-#pragma unroll
-      for (int u = 0; u < 6; ++u)
-        v2[u] = ld16nt_off(p.base, min(a2 + 16u * (uint32_t) gl + 256u * u, l2));
-    }
-#pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      x1 ^= v1[u].x ^ v1[u].y ^ v1[u].z ^ v1[u].w;
-      x2 ^= v2[u].x ^ v2[u].y ^ v2[u].z ^ v2[u].w;
-    }
-    x1 = row_sum16(x1);
-    x2 = row_sum16(x2);
-    if (gl == 15) {
-      stg((uint32_t *) p.out, i, x1);
-      if (i + half < p.n)
-        stg((uint32_t *) p.out, i2, x2);
-    }
-    return;
-  }
-  if (i >= p.n)
-    return;
-  const uint32_t a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
-  const uint32_t h = ldg(p.flen, i);
-  const uint32_t hl = h > p.ip_off + 20u ? min(h - p.ip_off, 1522u) : 20u;
-  const uint32_t lastoff = a0 + 16u * ((14u + hl - 1u) >> 4), lo = a0 + 16u * (uint32_t) gl;
-  uint32_t x = 0;
-  if constexpr (CHAIN) {
-    if (gl == 15) {
-      const u32x4 t = ld16nt_off(p.base, lastoff);
-      x = t.x ^ t.y ^ t.z ^ t.w;
-    }
-  } else {
-    u32x4 v[6];
-#pragma unroll
-    for (int u = 0; u < 6; ++u)
-      v[u] = ld16nt_off(p.base, min(lo + 256u * u, lastoff));
-#pragma unroll
-    for (int u = 0; u < 6; ++u)
-      x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-  }
-  x = row_sum16(x);
-  if (gl == 15)
-    stg((uint32_t *) p.out, i, x);
-}
-} // namespace
-
-extern "C" int tasx_ab_tcp4_mix_pattern(const void *base, uint64_t stride, uint32_t n, const uint32_t *flen,
-                                        uint32_t ip_off, int chain, uint32_t *out, void *stream)
-{
-  tasx_tcp4_params p;
-  memset(&p, 0, sizeof(p));
-  p.base = (uint8_t *) base;
-  p.stride = stride;
-  p.n = n;
-  p.flen = flen;
-  p.ip_off = ip_off;
-  p.l4_off = ip_off + 20u;
-  p.out = (uint16_t *) out;
-  // the product's own geometry checks: 16-byte aligned rooms of at least 1536 bytes, 32-bit offsets
-  if (!out || !flen || !base || (ip_off & 15u) != 14u || (stride & 15u) || stride < 1536u ||
-      (uint64_t) n * stride > 0xffffffffull || ((uintptr_t) base & 15u))
-    return -EINVAL;
-  if (chain == 2) { // two frames per row: half the rows
-    tasx_tcp4_params q = p;
-    q.n = (n + 1u) / 2u;
-    const uint64_t blocks = ((uint64_t) q.n + kBlock / 16 - 1) / (kBlock / 16);
-    if (blocks == 0)
-      return 0;
-    t_last_kernel = "tcp4_mix_pattern_kernel<pair>";
-    hipLaunchKernelGGL(tcp4_mix_pattern_kernel<2>, dim3((uint32_t) blocks), dim3(kBlock), 0, (hipStream_t) stream, p);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
-  return chain ? launch_groups("tcp4_mix_pattern_kernel<chain>", tcp4_mix_pattern_kernel<1>, p, (hipStream_t) stream, 0u)
-               : launch_groups("tcp4_mix_pattern_kernel", tcp4_mix_pattern_kernel<0>, p, (hipStream_t) stream, 0u);
-}
-
-extern "C" int tasx_ab_tcp4_pattern(const void *base, uint64_t stride, uint32_t n, uint32_t flen0, uint32_t ip_off,
-                                    uint32_t *out, void *stream)
-{
-  tasx_tcp4_params p;
-  memset(&p, 0, sizeof(p));
-  p.base = (uint8_t *) base;
-  p.stride = stride;
-  p.n = n;
-  p.flen0 = flen0;
-  p.ip_off = ip_off;
-  p.l4_off = ip_off + 20u;
-  p.out = (uint16_t *) out;
-  if (!out || !tas14_ok(p))
-    return -EINVAL;
-  return launch_groups("tcp4_pattern_kernel", tcp4_pattern_kernel, p, (hipStream_t) stream, kOccLds);
-}
-#endif
-
 extern "C" int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream)
 {
   const uint64_t blocks = ((uint64_t) p->n + kBlock - 1) / kBlock;
@@ -1937,244 +124,67 @@ extern "C" int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream)
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
+  if (variant != 0 && tasx_ext && tasx_ext->raw) { // the A/B build's variants
+    const int r = tasx_ext->raw(p, variant, stream);
+    if (r != TASX_EXT_PASS)
+      return r;
+  }
   switch (variant) {
-#ifdef TASX_AB
-  case 1:
-    return launch("raw_cksum_kernel", raw_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
-  case 2:
-    return launch_groups("raw_group_kernel", raw_group_kernel<6>, *p, s);
-#else
   case 2: // the general form
     return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
-#endif
   case 7:
     return launch_groups("raw_wave_kernel", raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
-#ifdef TASX_AB
-  // round 4 (stride mode from a 16-byte aligned base, else automatic): 45 / 46
-  // = 32 / 64 lanes per packet with 3 / 2 loads per lane, no residency cap; 47 =
-  // the product's 16-lane rows without the cap; 48 = 32 lanes with the cap
-  case 45: case 46: case 47: case 48:
-    if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
-        (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32)) {
-      switch (variant) {
-      case 45: return launch_groups<32>("raw_sad_kernel<s32,g32>", raw_sad_kernel<3, true, 32>, *p, s, 0u);
-      case 46: return launch_groups<64>("raw_sad_kernel<s32,g64>", raw_sad_kernel<2, true, 64>, *p, s, 0u);
-      case 47: return launch_groups("raw_sad_kernel<s32,nocap>", raw_sad_kernel<6, true>, *p, s, 0u);
-      default: return launch_groups<32>("raw_sad_kernel<s32,g32,cap>", raw_sad_kernel<3, true, 32>, *p, s, kOccLds);
-      }
-    }
-    return tasx_launch_raw(p, 0, stream);
-#endif
-  case 0:
   case 3:
-  case 6:
-    if (variant == 0 && p->len)
+  case 6: // the 16-lane rows whatever the lengths
+    break;
+  default: // 0 automatic (TCP4-only variants run it too): per-packet lengths -> 7
+    if (p->len)
       return launch_groups("raw_wave_kernel", raw_wave_kernel<TASX_WAVE_U>, *p, s, TASX_WAVE_LDS);
-    if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
-        (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32))
-      return launch_groups("raw_sad_kernel<s32>", raw_sad_kernel<6, true>, *p, s, kOccLds);
-    return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
-  default: // TCP4-only variants run the automatic RAW kernel
-    return tasx_launch_raw(p, 0, stream);
+    break;
   }
+  if (p->off == nullptr && ((uintptr_t) p->base & 15u) == 0 &&
+      (uint64_t) (kBlock / 16) * p->stride + TASX_RAW_MAX_LEN + 16u < (1ull << 32))
+    return launch_groups("raw_sad_kernel<s32>", raw_sad_kernel<6, true>, *p, s, kOccLds);
+  return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
 }
 
 template <bool OFFS>
-static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t s)
+static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s)
 {
-  const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u);
-  switch (mode) {
-  case kHintArr:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,verify,offs>" : "tcp4_tas14_kernel<hints,verify>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, OFFS>, p, s, lds);
-  default:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,verify,offs>" : "tcp4_tas14_kernel<tl_first,verify>",
-                         tcp4_tas14_kernel<6, kTlFirst, true, 8, OFFS>, p, s, lds);
-  }
-}
-
-// the split grid of tcp4_tas14_kernel<..., kFlowSplit*>: one lookup block per
-// F * BS frames, then the verify blocks
-template <uint32_t F = 2, int BS = kBlock, typename K>
-static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  const uint64_t nv = ((uint64_t) p.n + BS / 16 - 1) / (BS / 16), nl = ((uint64_t) p.n + F * BS - 1) / (F * BS);
-  if (nv == 0)
-    return 0;
-  if (nv + nl > 0x7fffffffull)
-    return -2;
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) (nv + nl)), dim3(BS), lds, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// the grid of tcp4_tas14_kernel<..., kFlowInter>: per group of kInterV verify
-// blocks, kInterL lookup blocks after them
-template <typename K>
-static int launch_inter(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
-  const uint64_t groups = (nv + kInterV - 1) / kInterV, blocks = groups * (kInterV + kInterL);
-  if (nv == 0)
-    return 0;
-  if (blocks > 0x7fffffffull)
-    return -2;
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// the grid of tcp4_tas14_kernel<..., kFlowSplitX*>: the XCD-matched lookup blocks, then the verify blocks
-template <uint32_t F = 1, typename K>
-static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
-  if (nv == 0)
-    return 0;
-  const uint64_t blocks = nv + splitx_lookup_blocks<F>((uint32_t) nv);
-  if (blocks > 0x7fffffffull)
-    return -2;
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-template <bool OFFS, int MODE, int FLOW>
-static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  // kernel names by FLOW: kFlowRow, kFlowSplit, kFlowSplit1, kFlowSplitX (the product), kFlowSplitX2
-  static const char *const names[2][2][5] = {
-      {{"tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,flow>",
-        "tcp4_tas14_kernel<tl_first,verify,flow_xcd2>"},
-       {"tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,offs,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>",
-        "tcp4_tas14_kernel<tl_first,verify,offs,flow_xcd2>"}},
-      {{"tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,flow_split1>", "tcp4_tas14_kernel<hints,verify,flow>",
-        "tcp4_tas14_kernel<hints,verify,flow_xcd2>"},
-       {"tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,offs,flow_split1>", "tcp4_tas14_kernel<hints,verify,offs,flow>",
-        "tcp4_tas14_kernel<hints,verify,offs,flow_xcd2>"}}};
-  static_assert(FLOW == kFlowRow || FLOW == kFlowSplit || FLOW == kFlowSplit1 || FLOW == kFlowSplitX ||
-                    FLOW == kFlowSplitX2, "a row form of the RX pass");
-  const int fi = FLOW == kFlowRow ? 0 : FLOW == kFlowSplit ? 1 : FLOW == kFlowSplit1 ? 2 : FLOW == kFlowSplitX ? 3 : 4;
-  const char *name = names[MODE == kHintArr][OFFS][fi];
-  auto kern = tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kBlock, false, FLOW>;
-  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1)
-    return launch_split<split_frames<FLOW>()>(name, kern, p, s, lds);
-  if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2)
-    return launch_splitx<FLOW == kFlowSplitX2 ? 2u : 1u>(name, kern, p, s, lds);
-  return launch_groups(name, kern, p, s, lds);
-}
-
-template <bool OFFS>
-static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s, int variant)
-{
-  const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u);
-#ifdef TASX_AB
-  if (variant == 26) // A/B: the lookup inside the rows
-    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowRow>(p, s, lds)
-                            : launch_rx_rows<OFFS, kTlFirst, kFlowRow>(p, s, lds);
-  if (variant == 27) // A/B: two frames per lookup lane, lookup blocks over consecutive frames
-    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit>(p, s, lds)
-                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplit>(p, s, lds);
-  if (variant == 35) // A/B: XCD-matched lookup blocks with two frames per lane
-    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX2>(p, s, lds)
-                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX2>(p, s, lds);
-  if (variant == 36) // A/B: the round-2 product (one frame per lane, lookup blocks over consecutive frames)
-    return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplit1>(p, s, lds)
-                            : launch_rx_rows<OFFS, kTlFirst, kFlowSplit1>(p, s, lds);
-  if (variant == 43 && mode == kHintArr && !OFFS) // A/B: the product with non-temporal flow-state key loads
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,fsnt>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, 1024>, p, s, lds);
-  if (variant == 42 && mode == kHintArr && !OFFS) // A/B: the product with line-paired generations
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,linepair>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLinePair>, p, s, lds);
-  if (variant == 41 && mode == kHintArr && !OFFS) // A/B: the product with the lookup waves at issue priority 3
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prio>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLookupPrio>, p, s, lds);
-  if (variant == 40 && mode == kHintArr && !OFFS) // A/B timing: the product's verify blocks alone (results wrong)
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,verify_only>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kVerifyOnly>, p, s, lds);
-  if (variant == 39 && mode == kHintArr && !OFFS) // A/B timing: the product's lookup blocks alone (results wrong)
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,lookup_only>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kLookupOnly>, p, s, lds);
-  if (variant == 38 && mode == kHintArr && !OFFS) // A/B: the product with the row-body fallback
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,rowfb>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kRowFallback>, p, s, lds);
-  if (variant == 37 && mode == kHintArr && !OFFS) // A/B: the product with the next generation's hint lines prefetched
-    return launch_splitx("tcp4_tas14_kernel<hints,verify,flow,prefetch>",
-                         tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplitX, kHintPrefetch>, p, s, lds);
-  if (variant == 28 && mode == kHintArr && !OFFS) // A/B: lookup blocks after their verify blocks, same XCD
-    return launch_inter("tcp4_tas14_kernel<hints,verify,flow_inter>",
-                        tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowInter>, p, s, lds);
-  // timing-only ablations of the round-2 product's lookup blocks (results
-  // wrong): 29 no frame key load, 30 no CRC, 31 no flow-state key load, 33 no
-  // bucket loads, 34 the frame key only
-  if (variant == 33 && mode == kHintArr && !OFFS)
-    return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,nobucket>",
-                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 8>, p, s, lds);
-  if (variant == 34 && mode == kHintArr && !OFFS)
-    return launch_split<1>("tcp4_tas14_kernel<hints,verify,flow,keyonly>",
-                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 12>, p, s, lds);
-  if (variant >= 29 && variant <= 31 && mode == kHintArr && !OFFS) {
-    static const char *const nm[3] = {"tcp4_tas14_kernel<hints,verify,flow,nokey>", "tcp4_tas14_kernel<hints,verify,flow,nocrc>",
-                                      "tcp4_tas14_kernel<hints,verify,flow,nofskey>"};
-    const char *name = nm[variant - 29];
-    if (variant == 29)
-      return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 1>, p, s, lds);
-    if (variant == 30)
-      return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 2>, p, s, lds);
-    return launch_split<1>(name, tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowSplit1, 4>, p, s, lds);
-  }
-#else
-  (void) variant;
-#endif
   // RX bursts without a uniform length are data/ACK mixes: one frame per
   // lookup lane, each lookup block over the frames of the 16 verify blocks on
   // its own XCD, so that the verify rows find the frames' first lines in L2
   // (64K frames, 0 / 50 / 100 % ACKs: 17.4 / 12.1 / 7.7-7.9 us against 18.3-18.6
   // / 12.8-12.9 / 8.8-9.0 for lookup blocks over consecutive frames, and 16.9 /
   // 13.0 / 7.1-7.3 with two frames per lane; profiles/r03/INDEX.md r03b)
-  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX>(p, s, lds)
-                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX>(p, s, lds);
+  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX>(p, s, 0u)
+                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX>(p, s, 0u);
 }
 
 // RX verification + flow lookup: the row kernels' selection (as
 // tasx_launch_tcp4_verify) with the lookup blocks first in the same grid
-// (kFlowSplit); batches no row kernel takes run the general verify kernel and
-// then flow_lookup_kernel
+// (kFlowSplitX*); batches no row kernel takes run the general verify kernel
+// and then flow_lookup_kernel
 extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
+  if (variant != 0 && tasx_ext && tasx_ext->rx) { // the A/B build's split and ablation forms
+    const int r = tasx_ext->rx(p, variant, stream);
+    if (r != TASX_EXT_PASS)
+      return r;
+  }
   const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
   if (auto6 && tas14_ok(*p)) {
-    const uint32_t lds = TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds);
-#ifdef TASX_AB
-    if (variant == 26)
-      return launch_groups("tcp4_tas14_kernel<hint,verify,flow_row>",
-                           tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowRow>, *p, s, lds);
-    if (variant == 27)
-      return launch_split<1>("tcp4_tas14_kernel<hint,verify,flow_f1>",
-                             tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit1>, *p, s, lds);
-    if (variant == 32)
-      return launch_splitx<1>("tcp4_tas14_kernel<hint,verify,flow_xcd>",
-                              tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX>, *p, s, lds);
-    if (variant == 36) // the round-2 product: lookup blocks over consecutive frames
-      return launch_split<2>("tcp4_tas14_kernel<hint,verify,flow_split2>",
-                             tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplit>, *p, s, lds);
-#endif
     // a uniform received length is a data burst: two frames per lookup lane,
     // each lookup block over the frames of the 32 verify blocks on its own XCD
     // (64K frames: 16.8 against 17.1 us with one frame per lane and 17.6-17.9
     // with lookup blocks over consecutive frames; profiles/r03/INDEX.md r03b)
     return launch_splitx<2>("tcp4_tas14_kernel<hint,verify,flow>",
-                            tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, lds);
+                            tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, kOccLds);
   }
   if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
     const int mode = p->flen ? kHintArr : kTlFirst;
-    return p->off ? launch_tas14_rx<true>(*p, mode, s, variant) : launch_tas14_rx<false>(*p, mode, s, variant);
+    return p->off ? launch_tas14_rx<true>(*p, mode, s) : launch_tas14_rx<false>(*p, mode, s);
   }
   int r = tasx_launch_tcp4_verify(p, variant, stream);
   if (r != 0)
@@ -2202,10 +212,14 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
+  if (variant != 0 && tasx_ext && tasx_ext->verify) { // the A/B build's row forms
+    const int r = tasx_ext->verify(p, variant, stream);
+    if (r != TASX_EXT_PASS)
+      return r;
+  }
   const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
   if (auto6 && tas14_ok(*p))
-    return launch_groups("tcp4_tas14_kernel<hint,verify>", tcp4_tas14_kernel<6, kHint, true>, *p, s,
-                         TASX_LDS("TASX_TAS14_VERIFY_HINT_LDS", kOccLds));
+    return launch_groups("tcp4_tas14_kernel<hint,verify>", tcp4_tas14_kernel<6, kHint, true>, *p, s, kOccLds);
   // RX batches mix data and ACKs too: as the TX form, 8 waves per SIMD and no
   // LDS cap (64K frames, per-frame hints, 0 / 25 / 50 / 75 % ACKs: 17.0 / 14.2
   // / 11.9 / 10.2 -> 17.1 / 13.8 / 10.9 / 8.7 us; profiles/r01_ackmix_verify_ab.txt),
@@ -2216,196 +230,31 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
   // bursts are mixes, where whole-room rows lose (64K frames, room 2048, 0 /
   // 50 % ACKs: 16.3 / 16.3 us against 16.9 / 10.8-11.1; profiles/r02/r02ad).
   if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
-    int mode = p->flen ? kHintArr : kTlFirst;
-#ifdef TASX_AB
-    if (variant == 9) // A/B: total_length first whatever the call carries
-      mode = kTlFirst;
-    if (variant == 42 && mode == kHintArr && !p->off) // line-paired generations
-      return launch_groups("tcp4_tas14_kernel<hints,verify,linepair>",
-                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kLinePair>, *p, s,
-                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
-    if (variant == 38 && mode == kHintArr && !p->off) // the row-body fallback
-      return launch_groups("tcp4_tas14_kernel<hints,verify,rowfb>",
-                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
-                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
-    if (variant == 37 && mode == kHintArr && !p->off) // next generation's hint lines prefetched
-      return launch_groups("tcp4_tas14_kernel<hints,verify,prefetch>",
-                           tcp4_tas14_kernel<6, kHintArr, true, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
-                           TASX_LDS("TASX_TAS14_VERIFY_LDS", 0u));
-#endif
+    const int mode = p->flen ? kHintArr : kTlFirst;
     return p->off ? launch_tas14_verify<true>(*p, mode, s) : launch_tas14_verify<false>(*p, mode, s);
   }
   return launch_groups("tcp4_frame_kernel<verify>", tcp4_frame_kernel<6, true>, *p, s);
 }
 
-// tcp4_tas14_kernel without a uniform hint, in the mode the room allows (or
-// the one an A/B variant forces).  Built for 8 waves per SIMD (64 VGPRs; the
-// spills are confined to the general-body fallback after the fast path's
-// stores): data/ACK mixes are latency-bound and gain from the residency (64K
-// frames at 50 / 75 / 100 % ACKs: 11.2 / 9.3-9.9 / 7.38 -> 10.8 / 8.6 / 6.97
-// us; uniform MTU 17.05 -> 17.0; profiles/r01_ackmix_wpe_ab.txt).
-template <bool OFFS>
-static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
-{
-  const uint32_t lds = TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u);
-  switch (OFFS && mode == kMix ? kTlFirst : mode) { // the mix kernel is a stride-mode form
-  case kHintArr:
-#ifdef TASX_AB
-    if (OFFS && p.done_word && p.done_count) { // a flush whose kernel posts its own completion
-      const int r = launch_groups("tcp4_tas14_kernel<hints,offs,done>",
-                                  tcp4_tas14_kernel<6, kHintArr, false, 8, true, kBlock, true>, p, s, lds);
-      t_posted_done = r == 0 && p.n > 0;
-      return r;
-    }
-#endif
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints,offs>" : "tcp4_tas14_kernel<hints>",
-                         tcp4_tas14_kernel<6, kHintArr, false, 8, OFFS>, p, s, lds);
-#ifdef TASX_AB
-  case kHintArrP:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints_pred,offs>" : "tcp4_tas14_kernel<hints_pred>",
-                         tcp4_tas14_kernel<6, kHintArrP, false, 8, OFFS>, p, s, lds);
-  case kHintArrS:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<hints_sorted,offs>" : "tcp4_tas14_kernel<hints_sorted>",
-                         tcp4_tas14_kernel<6, kHintArrS, false, 8, OFFS>, p, s, lds);
-  case kMix:
-    if (getenv("TASX_MIX_F8"))
-      return launch_groups<8>("tcp4_mix_kernel<f8>", tcp4_mix_kernel<6, 8>, p, s);
-    return launch_groups<4>("tcp4_mix_kernel", tcp4_mix_kernel<6>, p, s);
-#endif
-  case kRoom:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<room,offs>" : "tcp4_tas14_kernel<room>",
-                         tcp4_tas14_kernel<6, kRoom, false, 8, OFFS>, p, s, lds);
-  case kHead5:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<head5,offs>" : "tcp4_tas14_kernel<head5>",
-                         tcp4_tas14_kernel<6, kHead5, false, 8, OFFS>, p, s, lds);
-  default:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,offs>" : "tcp4_tas14_kernel<tl_first>",
-                         tcp4_tas14_kernel<6, kTlFirst, false, 8, OFFS>, p, s, lds);
-  }
-}
-
-// persistent grids: blocks resident at once on the current device (8 waves of
-// 64 VGPRs per SIMD = 8 blocks of 256 threads per CU)
-static uint32_t resident_blocks()
-{
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-    cus = 256;
-  return (uint32_t) cus * 8u;
-}
-
-template <typename K>
-static int launch_rows(const char *name, K kern, const tasx_tcp4_params &p, uint32_t frames_per_row, hipStream_t s)
-{
-  const uint64_t need = ((uint64_t) p.n + 16u * frames_per_row - 1) / (16u * frames_per_row);
-  uint64_t blocks = frames_per_row ? need : resident_blocks();
-  if (!frames_per_row && blocks > ((uint64_t) p.n + 15u) / 16u)
-    blocks = ((uint64_t) p.n + 15u) / 16u;
-  if (blocks == 0)
-    return 0;
-  t_last_kernel = name;
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), 0, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  t_posted_done = 0;
-  int mode = tas14_mode(*p);
-  if (variant == 7) // RAW-only variant
-    variant = 0;
-#ifdef TASX_AB
-  // 9 / 10 / 11: force the total_length-first / head-5 / whole-room row mode
-  // where its room requirement holds (else as 0)
-  if ((variant >= 9 && variant <= 11) || (variant >= 19 && variant <= 21) || variant == 28) {
-    const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
-    const int m = variant == 9 ? kTlFirst : variant == 10 ? kHead5 : variant == 11 ? kRoom : variant == 19 ? kMix
-                : variant == 20 ? kHintArr : variant == 28 ? kHintArrS : kHintArrP;
-    if ((m == kTlFirst) || ((m == kHintArr || m == kHintArrP || m == kHintArrS) && p->flen) || ((m == kHead5 || m == kMix) && from_a0 >= 80u) || (m == kRoom && from_a0 >= 1536u))
-      mode = m;
-    variant = 0;
+  if (variant != 0 && tasx_ext && tasx_ext->tcp4) { // the A/B build's variants
+    const int r = tasx_ext->tcp4(p, variant, stream);
+    if (r != TASX_EXT_PASS)
+      return r;
   }
-  // 12 / 13 / 14: the persistent total_length-first rows (resident grid / 2 /
-  // 4 frames per row) where tcp4_tas14_kernel's stride form applies
-  // 15 / 16 / 17 / 18: tcp4_tas14_kernel<tl_first> (stride mode) in blocks of
-  // 64 / 128 / 512 / 1024 threads instead of 256
-  // 22 / 23 / 24 / 25: tcp4_tas14_kernel<hints> (stride mode, per-frame hints)
-  // in blocks of 64 / 128 / 512 / 1024 threads
-  // 43 / 44: the whole-room / total_length-first rows with the headline's
-  // residency (no waves-per-EU floor, the 30 KiB LDS cap) instead of 8 waves per SIMD
-  if ((variant == 43 || variant == 44) && !p->flen && !tas14_ok(*p) && tas14_nohint_ok(*p)) {
-    const uint32_t from_a0 = p->room > (p->ip_off & ~15u) ? p->room - (p->ip_off & ~15u) : 0u;
-    if (variant == 43 && from_a0 >= 1536u)
-      return launch_groups("tcp4_tas14_kernel<room,occ>", tcp4_tas14_kernel<6, kRoom, false, 1>, *p, s, kOccLds);
-    if (variant == 44)
-      return launch_groups("tcp4_tas14_kernel<tl_first,occ>", tcp4_tas14_kernel<6, kTlFirst, false, 1>, *p, s, kOccLds);
-  }
-  if (variant == 42 && p->flen && !tas14_ok(*p) && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) // hints, line-paired generations
-    return p->off ? launch_groups("tcp4_tas14_kernel<hints,offs,linepair>",
-                                  tcp4_tas14_kernel<6, kHintArr, false, 8, true, kBlock, false, kFlowNone, kLinePair>, *p, s,
-                                  TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u))
-                  : launch_groups("tcp4_tas14_kernel<hints,linepair>",
-                                  tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kLinePair>, *p, s,
-                                  TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
-  if (variant == 38 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, the row-body fallback
-    return launch_groups("tcp4_tas14_kernel<hints,rowfb>",
-                         tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kRowFallback>, *p, s,
-                         TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
-  if (variant == 37 && p->flen && !p->off && !tas14_ok(*p) && tas14_nohint_ok(*p)) // hints, next generation's hint lines prefetched
-    return launch_groups("tcp4_tas14_kernel<hints,prefetch>",
-                         tcp4_tas14_kernel<6, kHintArr, false, 8, false, kBlock, false, kFlowNone, kHintPrefetch>, *p, s,
-                         TASX_LDS("TASX_TAS14_NOHINT_LDS", 0u));
-  if (variant >= 22 && variant <= 25 && p->flen && tas14_nohint_ok(*p)) {
-    switch (variant) {
-    case 22: return launch_groups<16, 64>("tcp4_tas14_kernel<hints,bs64>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 64>, *p, s);
-    case 23: return launch_groups<16, 128>("tcp4_tas14_kernel<hints,bs128>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 128>, *p, s);
-    case 24: return launch_groups<16, 512>("tcp4_tas14_kernel<hints,bs512>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 512>, *p, s);
-    default: return launch_groups<16, 1024>("tcp4_tas14_kernel<hints,bs1024>", tcp4_tas14_kernel<6, kHintArr, false, 8, false, 1024>, *p, s);
-    }
-  }
-  if (variant >= 15 && variant <= 18 && !tas14_ok(*p) && tas14_nohint_ok(*p)) {
-    switch (variant) {
-    case 15: return launch_groups<16, 64>("tcp4_tas14_kernel<tl_first,bs64>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 64>, *p, s);
-    case 16: return launch_groups<16, 128>("tcp4_tas14_kernel<tl_first,bs128>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 128>, *p, s);
-    case 17: return launch_groups<16, 512>("tcp4_tas14_kernel<tl_first,bs512>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 512>, *p, s);
-    default: return launch_groups<16, 1024>("tcp4_tas14_kernel<tl_first,bs1024>", tcp4_tas14_kernel<6, kTlFirst, false, 8, false, 1024>, *p, s);
-    }
-  }
-  if (variant >= 12 && variant <= 14 && !tas14_ok(*p) && tas14_nohint_ok(*p))
-    return launch_rows("tcp4_tas14_rows_kernel", tcp4_tas14_rows_kernel<6>, *p,
-                       variant == 12 ? 0u : variant == 13 ? 2u : 4u, s);
-  if (variant == 8 && p->l4_off == p->ip_off + 20u) {
-    static const uint32_t lds = env_lds("TASX_WAVE_TCP4_LDS", 0u);
-    return launch_groups("tcp4_wave_kernel", tcp4_wave_kernel<TASX_WAVE_U>, *p, s, lds);
-  }
-  switch (variant) {
-  case 1:
-    return launch("tcp4_cksum_kernel", tcp4_cksum_kernel<16, 8>, *p, kBlock / 16, 256 * 64, s);
-  case 4:
-    return p->diag && tas_kernel_ok(*p) ? launch_groups("tcp4_tas_kernel<diag>", tcp4_tas_kernel<6, 1>, *p, s)
-                                         : -2;
-  case 5: // 32-lane groups (A/B: slower than 16, profiles/r01_variant_sweeps.jsonl)
-    if (tas_kernel_ok(*p))
-      return launch_groups<32>("tcp4_tas_kernel<g32>", tcp4_tas_kernel<3, 0, 32>, *p, s);
-    break;
-  default:
-    break;
-  }
-  if (variant == 1 || variant >= 4)
-    variant = 0;
-#endif
-  if (variant == 0 || variant == 6) {
+  if (variant != 2 && variant != 3)
+    variant = 0; // 6 = the automatic choice; RAW-only and A/B-only numbers run it too
+  if (variant == 0) {
     // TAS frames in 16-byte rooms: a uniform hint, per-frame hints or none ->
     // tcp4_tas14_kernel; frames by offsets -> its OFFS form
     if (tas14_ok(*p))
-      return launch_groups("tcp4_tas14_kernel<hint>", tcp4_tas14_kernel<6, kHint>, *p, s,
-                           TASX_LDS("TASX_TAS14_HINT_LDS", kOccLds));
+      return launch_groups("tcp4_tas14_kernel<hint>", tcp4_tas14_kernel<6, kHint>, *p, s, kOccLds);
     if (tas14_nohint_ok(*p))
-      return launch_tas14_rows<false>(*p, mode, s);
+      return launch_tas14_rows<false>(*p, tas14_mode(*p), s);
     if (tas14_offs_ok(*p))
-      return launch_tas14_rows<true>(*p, mode, s);
+      return launch_tas14_rows<true>(*p, tas14_mode(*p), s);
     // other TAS-layout batches with a hint -> 3, the rest -> 2
     variant = tas_kernel_ok(*p) && (p->flen || p->flen0) ? 3 : 2;
   }

@@ -12,7 +12,7 @@ rm -f "$out"/*.h
 git -C "$root" show "$rev:tas_amd/csrc/$src.hip" > "$out/$src.hip"
 objs=()
 for o in "$root"/tas_amd/_lib/*.o; do
-  case "$o" in *_ab.o) continue;; esac
+  case "$(basename "$o")" in ab_*.o) continue;; esac
   b=$(basename "$o" .o)
   if [ "$b" = "$src" ]; then objs+=("$out/$src.o"); else objs+=("$o"); fi
 done

@@ -26,16 +26,16 @@ step bench 400 python bench.py
 fi
 [ "${PART:-ab}" = "a" ] && { echo done; exit 0; }
 # the driver's step count: ms_per_step against the event-timed launch
-step bench_k20 300 python bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline
+step bench_k20 300 python bench.py --steps 20 --warmup 5 --no-pmc --no-cpu-baseline --no-server-cost
 for w in mixed shard8m tso; do
   step bench_$w 300 python bench.py --workload $w --steps 20 --warmup 3
 done
 # the N>1 code path: bench.py spawns 2 ranks itself; --rehearse lets them
 # share this one GPU (gloo control plane; not a scaling measurement)
-step bench_n2 300 python bench.py --gpus 2 --rehearse --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts --no-flushmix --no-e2e
+step bench_n2 300 python bench.py --gpus 2 --rehearse --steps 20 --warmup 3 --no-txseg --no-flow --no-contexts --no-flushmix --no-e2e --no-server-cost
 # the RCCL collectives bench.py makes for N > 1, on one rank (RCCL refuses two
 # ranks on one GPU; the 8-GPU curve is the driver's run)
 step rccl_selftest 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29561 tools/rccl_selftest.py
 export TMPDIR=/tmp
-step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --steps 100 --warmup 10
+step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu-baseline --no-e2e --no-pmc --no-contexts --no-server-cost --steps 100 --warmup 10
 echo done
