@@ -1126,6 +1126,9 @@ def fastpath_mt_leg(flushes: int = 3000) -> dict:
     # the fused TX segment build (payload copy + checksums) handed to the server
     for th, q in ((1, 1), (8, 3), (8, 7)):
         res[f"txseg_server_{th}x{q}"] = benchloop.txseg_server_mt(dev, 8, th, q, flushes)
+    res["txseg_note"] = ("a 32-segment flush is ONE TX segment slot (41 segments a slot since round 5; round 4's "
+                         "20-segment slots took two), so 7 in flight fit a ring's 8 slots and 8x7's "
+                         "core_us_per_flush holds no wait for a free slot; segments_per_s over all threads")
     n = len(keep) // STRIDE
     dres = xsum.tcp4_cksum_batch(torch.from_numpy(keep.copy()).cuda(), n, stride=STRIDE)
     torch.cuda.synchronize()

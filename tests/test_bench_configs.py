@@ -125,6 +125,21 @@ def test_bench_config4_shard(oracle, rank):
     np.testing.assert_array_equal(host(wl.outs[0]).view(np.uint16), exp)
 
 
+def test_bench_config4_whole_on_one_gpu(oracle):
+    """Config 4 at N = 1: all 8,388,608 x 1500 B (12.6 GB) on one GPU, as
+    bench.py --workload shard8m --gpus 1 times it: 524,288 blocks, so the grid
+    runs in XCD runs of 256 blocks (xcd_run, round 5); every packet compared
+    with the oracle."""
+    wl = bench.shard8m_workload(1, 0)
+    assert wl.n == bench.SHARD8M_N == 1 << 23
+    wl.loop()(0, 1)
+    assert xsum.last_kernel() == "raw_sad_kernel<s32>"
+    got = host(wl.outs[0]).view(np.uint16)
+    buf = host(wl.bufs[0])
+    exp = oracle.raw_batch(buf, wl.n, stride=wl.len0, len0=wl.len0)
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_bench_config5_tso(oracle):
     """Config 5: 16,384 TSO segments (ip.len 65535, L4 65,515 B) in 65,552 B
     rooms, the frame length 65,549 as the uniform hint; out of place, then in
