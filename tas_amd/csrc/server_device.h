@@ -124,13 +124,21 @@ constexpr int kSrvTxU = 6;
 // (A/B 1-14: no acquire, system-scope loads, write-through TX stores, no
 // release, ...; profiles/r04/INDEX.md r04g-r04v) lost to this form and are
 // gone from the source.
-template <bool DIAG>
+// ACQ: the per-batch acquire -- 0 system scope (the product), and in the A/B
+// build's price diagnostics only (TASX_SRV_ACQ, profiles/r05 r05l) 1 agent
+// scope (this CU's L1 alone) and 2 none, to tell what the server costs the
+// device-resident work beside it.
+template <bool DIAG, int ACQ = 0>
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
   __shared__ uint64_t s_w[TASX_SRV_WORDS]; // a TX segment slot's entry words
   __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg;
   __shared__ uint64_t s_base;
+  // DIAG sums, kept in LDS (registers are the TX rows' budget: in registers
+  // they spilled): detection -> loaded, loaded -> acked, gap, batches, empty
+  // polls, the last batch's end
+  __shared__ uint64_t s_d[6];
   const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
   uint8_t *const mem = P.mem;
@@ -138,11 +146,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
   if (threadIdx.x == 0)
     s_bad = 0u;
+  if (DIAG && threadIdx.x < 6)
+    s_d[threadIdx.x] = threadIdx.x == 5 ? wall_clock64() : 0ull;
   __syncthreads();
   uint32_t p = blockIdx.x % K; // the server starts on a zeroed block: every ring at position 0
   uint64_t t_act = wall_clock64(), t_lease = t_act;
   uint32_t lease = 0u;
-  uint64_t d_load = 0, d_ack = 0, d_gap = 0, d_n = 0, d_empty = 0, t_end = t_act; // DIAG
   uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
@@ -204,7 +213,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       return 1;
     }
     if constexpr (DIAG)
-      d_empty++;
+      if (lane == 0)
+        s_d[4]++;
     if ((uint32_t) c != 0u)
       return 3;
     if ((uint32_t) (c >> 32) != lease) {
@@ -246,7 +256,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // a batch taken: this CU's L1 and the XCD's L2 drop their non-coherent
       // lines before any frame load (A/B: policies 1-4 and 7 without)
       if (st == 1)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      {
+        if constexpr (ACQ == 0)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        else if constexpr (ACQ == 1)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
     }
     __syncthreads();
     if (s_cmd != 0u)
@@ -304,16 +319,13 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
       if constexpr (DIAG) {
         const uint64_t t_acked = wall_clock64();
-        d_load += t_loaded - t_act;
-        d_ack += t_acked - t_loaded;
-        d_gap += t_act - t_end;
-        d_n++;
-        t_end = t_acked;
-        st_sys64(dd, d_load);
-        st_sys64(dd + 1, d_ack);
-        st_sys64(dd + 2, d_gap);
-        st_sys64(dd + 3, d_n);
-        st_sys64(dd + 4, d_empty);
+        s_d[0] += t_loaded - t_act;
+        s_d[1] += t_acked - t_loaded;
+        s_d[2] += t_act - s_d[5];
+        s_d[3]++;
+        s_d[5] = t_acked;
+        for (int k = 0; k < 5; ++k)
+          st_sys64(dd + k, s_d[k]);
       }
     }
     p += K;

@@ -179,7 +179,7 @@ typedef struct tasx_ext_hooks {
   int (*rx)(const tasx_tcp4_params *p, int variant, void *stream);
   int (*flow)(const tasx_flow_params *p, int variant, void *stream);
   int (*txseg)(const tasx_txseg_params *p, void *stream);
-  int (*server)(const tasx_srv_params *p, void *stream); /* the server with timing sums (p->diag) */
+  int (*server)(const tasx_srv_params *p, void *stream); /* the server's other forms (timing sums, price diagnostics) */
   int (*xrun)(uint64_t blocks); /* >= 0: the XCD order of a grid of `blocks` blocks */
   /* host knobs (from the environment, read once by the A/B build) */
   uint64_t *diag;         /* p.diag of TCP4 launches (the wave-timeline variant) */
