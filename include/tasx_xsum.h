@@ -483,7 +483,8 @@ int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);
  *     every ticket complete, and detaches the context from a dead server or
  *     feeder.  Each call then writes up to max of them ({ip, l4} as recorded)
  *     and returns how many, 0 once none are left; the context is usable again
- *     (pending 0, every ticket polled complete).  A GPU that wrote a field
+ *     (pending 0, every ticket polled complete).  -ENOMEM (once, after the
+ *     rest) if the library could not allocate room to keep some of them.  A GPU that wrote a field
  *     after all is harmless: the caller recomputes both fields from zero.
  *   tasx_take_unfinished_segs(ctx, segs, max): the same for TX segments given
  *     to tasx_server_tx_segments (descriptors as submitted; after an -EIO

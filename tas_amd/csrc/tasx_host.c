@@ -457,6 +457,7 @@ struct tasx_ctx {
   uint32_t unf_n, unf_cap, unf_pos;
   tasx_tx_seg *unf_seg;
   uint32_t unf_seg_n, unf_seg_cap, unf_seg_pos;
+  uint32_t unf_lost; /* frames / segments the store could not hold (no memory): reported, never silent */
 };
 
 #define DONE_STRIDE 16u /* uint32 words between completion words (64 B) */
@@ -2634,8 +2635,10 @@ static int unf_frame(struct tasx_ctx *c, uint8_t *ip, uint8_t *l4)
   if (c->unf_n == c->unf_cap) {
     const uint32_t cap = c->unf_cap ? 2u * c->unf_cap : 256u;
     tasx_frame_ref *n = realloc(c->unf, (size_t) cap * sizeof(*n));
-    if (!n)
+    if (!n) {
+      c->unf_lost++;
       return -ENOMEM;
+    }
     c->unf = n;
     c->unf_cap = cap;
   }
@@ -2648,8 +2651,10 @@ static int unf_seg(struct tasx_ctx *c, const tasx_tx_seg *g)
   if (c->unf_seg_n == c->unf_seg_cap) {
     const uint32_t cap = c->unf_seg_cap ? 2u * c->unf_seg_cap : 64u;
     tasx_tx_seg *n = realloc(c->unf_seg, (size_t) cap * sizeof(*n));
-    if (!n)
+    if (!n) {
+      c->unf_lost++;
       return -ENOMEM;
+    }
     c->unf_seg = n;
     c->unf_seg_cap = cap;
   }
@@ -2821,6 +2826,12 @@ int tasx_take_unfinished(unsigned ctx_id, tasx_frame_ref *frames, uint32_t max)
   uint32_t k = 0;
   while (k < max && c->unf_pos < c->unf_n)
     frames[k++] = c->unf[c->unf_pos++];
+  if (k == 0 && c->unf_lost) { /* everything held was handed out; say what was not */
+    const uint32_t lost = c->unf_lost;
+    c->unf_lost = 0;
+    return set_err(-ENOMEM, "ctx %u: %u unfinished frames / segments could not be kept (out of memory)", ctx_id,
+                   lost);
+  }
   return (int) k;
 }
 
