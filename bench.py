@@ -1181,28 +1181,53 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
         res["states"]["idle"] = measure()
     finally:
         xsum.server_stop(dev)
-    flush = {}
-    th = threading.Thread(target=lambda: flush.update(benchloop.fastpath_mt(dev, 8, 8, 3, flushes, "server")))
-    th.start()
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 10.0:  # the run has started its server and its threads are flushing
-        try:
-            if xsum.server_stats(dev)[0] > 2000:
-                break
-        except xsum.TasxError:
-            pass
-        time.sleep(0.001)
-    busy = measure()
-    try:
-        batches_after = xsum.server_stats(dev)[0]
-    except xsum.TasxError:
-        batches_after = None  # the flush run had already finished: the overlap was partial
-    th.join()
+
+    def busy_pass(nflush):
+        """the timed launches while a flush run of nflush flushes per thread
+        goes through the server; (times, flush run, overlapped, seconds the
+        run took to start flushing, seconds the timed launches took)"""
+        flush, err = {}, []
+
+        def body():
+            try:
+                flush.update(benchloop.fastpath_mt(dev, 8, 8, 3, nflush, "server"))
+            except Exception as e:  # reported, and the pass counts as not overlapped
+                err.append(repr(e))
+        th = threading.Thread(target=body)
+        th.start()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 10.0 and th.is_alive():  # started its server, its threads flushing
+            try:
+                if xsum.server_stats(dev)[0] > 2000:
+                    break
+            except xsum.TasxError:
+                pass
+            time.sleep(0.001)
+        def batches():
+            try:
+                return xsum.server_stats(dev)[0]
+            except xsum.TasxError:
+                return None
+        b1, t1 = batches(), time.perf_counter()
+        times = measure()
+        b2, t2 = batches(), time.perf_counter()
+        overlapped = th.is_alive() and b2 is not None  # the run outlasted the timed launches
+        th.join()
+        if err:
+            flush["error"] = err[0]
+        # the flush run's own rate while the timed launches ran
+        flush["frames_per_s_meanwhile"] = round((b2 - b1) * 32 / (t2 - t1)) if b1 is not None and b2 else None
+        return times, flush, overlapped and not err, round(t1 - t0, 3), round(t2 - t1, 3)
+    busy, flush, overlapped, t_start, t_meas = busy_pass(flushes)
+    if not overlapped:  # once more, with a run four times as long
+        busy, flush, overlapped, t_start, t_meas = busy_pass(4 * flushes)
+    batches_after = overlapped
     after = measure()
     res["states"]["stopped"] = {k: min(v, after[k]) for k, v in res["states"]["stopped"].items()}
     res["states"]["busy_8x3"] = busy
     res["busy_flush_run"] = flush
-    res["busy_overlap_complete"] = batches_after is not None
+    res["busy_overlap_complete"] = bool(batches_after)
+    res["busy_seconds"] = {"run_start": t_start, "timed_launches": t_meas}
     for name, (_, nbytes, _) in legs.items():
         st = {k: v[name] for k, v in res["states"].items()}
         res[name] = {"us": {k: round(v, 3) for k, v in st.items()},

@@ -794,3 +794,35 @@ def test_server_left_running_by_a_failed_test_a():
 def test_server_left_running_by_a_failed_test_b():
     xsum.server_start(0)
     xsum.server_stop(0)
+
+
+def test_take_unfinished_without_a_failure(oracle):
+    """ABI 8 on a healthy context, no server: tasx_take_unfinished waits for
+    the flushes in flight (they finish on the GPU: nothing comes back for
+    them) and hands back the frames recorded but never submitted -- the glue
+    finishes those on the CPU; the context flushes on the GPU afterwards."""
+    n = 32
+    cx = _Ctxs([12])
+    try:
+        pin, frames = _frames(4 * n, 977, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, 4 * n)
+        xsum.register_frames(12, pin.addr, pin.nbytes)
+        for b in range(2):                               # two zero-copy flushes in flight
+            for i in range(n):
+                xsum.tcp_checksums(12, pin.addr + (b * n + i) * 2048)
+            xsum.flush_submit(12)
+        for i in range(n):                               # recorded, never submitted
+            xsum.tcp_checksums(12, pin.addr + (2 * n + i) * 2048)
+        back = xsum.take_unfinished(12)
+        offs = _finish_on_cpu(oracle, pin, back)
+        assert sorted(offs.tolist()) == [k * 2048 for k in range(2 * n, 3 * n)]
+        np.testing.assert_array_equal(pin.array[:3 * n * 2048], ref[:3 * n * 2048])
+        assert xsum.pending(12) == 0 and xsum.take_unfinished(12) == []
+        assert xsum.flush_poll(12, 2) is True
+        for i in range(n):                               # and the GPU path again
+            xsum.tcp_checksums(12, pin.addr + (3 * n + i) * 2048)
+        xsum.tx_flush(12)
+        np.testing.assert_array_equal(pin.array[:4 * n * 2048], ref[:4 * n * 2048])
+    finally:
+        cx.close()
