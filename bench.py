@@ -1154,22 +1154,35 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
     dev = torch.cuda.current_device()
     wl = Tcp4Workload(rot, pktgen.SEED + 7000 + rank, host=False)
     tw = TxSegWorkload(rot, pktgen.SEED + 7100 + rank)
-    legs = {"headline": (wl.loop(HINT), wl.bytes_per_step, 2000), "tx_segment": (tw.loop(), tw.bytes_per_step, 800)}
+    # the timed launches on a stream of their own, waited for by stream and
+    # event only: the null stream's synchronize waited for the flush run's
+    # whole server lifetime in the full bench process (profiles/r05 r05q)
+    ts = torch.cuda.Stream()
+    legs = {"headline": (wl.loop(HINT, streams=[ts]), wl.bytes_per_step, 2000),
+            "tx_segment": (tw.loop(streams=[ts]), tw.bytes_per_step, 800)}
     for run, _, _ in legs.values():
         prewarm(run)
     torch.cuda.synchronize()
 
+    walls = []  # host seconds per timed() phase: warm launches, their wait, timed launches, their wait
+
     def timed(run, k):
         # stream-level waits only: a device-wide synchronize would wait for the
         # resident server kernel itself
-        cur = torch.cuda.current_stream()
+        cur = ts
+        w0 = time.perf_counter()
         run(0, 20)
+        w1 = time.perf_counter()
         cur.synchronize()
+        w2 = time.perf_counter()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(cur)
         run(20, k)
+        w3 = time.perf_counter()
         e1.record(cur)
         e1.synchronize()
+        w4 = time.perf_counter()
+        walls.append([round(w1 - w0, 4), round(w2 - w1, 4), round(w3 - w2, 4), round(w4 - w3, 4)])
         return e0.elapsed_time(e1) * 1e3 / k
 
     def measure():
@@ -1209,7 +1222,9 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
             except xsum.TasxError:
                 return None
         b1, t1 = batches(), time.perf_counter()
+        walls.clear()
         times = measure()
+        flush["host_walls_s"] = list(walls)
         b2, t2 = batches(), time.perf_counter()
         overlapped = th.is_alive() and b2 is not None  # the run outlasted the timed launches
         th.join()

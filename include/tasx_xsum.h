@@ -403,7 +403,9 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
 
 /* Flush server (ABI 6): a persistent kernel per GPU takes the flushes of
  * every attached context from pinned host memory, so a fast-path core's
- * tasx_flush_submit() makes NO HIP call and the GPU pays no launch per batch.
+ * tasx_flush_submit(), _poll() and _wait() make NO HIP call (the server's
+ * keepalive thread watches the kernel, every 10 ms) and the GPU pays no launch
+ * per batch.
  * Each context has a ring of TASX_SRV_RING (8) descriptor slots, up to 64
  * frames each: submit writes the frames' offsets in the context's registered
  * region and their ip.total_length into the next slot, the header last, and

@@ -2041,6 +2041,12 @@ struct fserver {
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
   int aborted;                     /* tasx_server_abort stopped the kernel (and the keepalive thread) */
+  /* the kernel's state as the keepalive thread last saw it (hipStreamQuery
+   * every 10 ms once launched): 0 running, 1 exited, < 0 -hipError_t.  The
+   * fast-path cores read this word: their polls make no HIP call (a
+   * hipStreamQuery per poll from 8 cores serialised in the runtime's locks and
+   * stalled the process's other HIP work, profiles/r05 r05o) */
+  int launched, kstate;
 };
 
 struct grave {
@@ -2100,8 +2106,14 @@ static void *server_keepalive(void *arg)
   uint32_t *lease = (uint32_t *) (S->h_ring + TASX_SRV_CTL) + 1;
   uint32_t k = 1;
   const struct timespec ts = {0, 10 * 1000 * 1000};
+  hipSetDevice(S->device);
   while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(lease, k++, __ATOMIC_RELEASE);
+    if (__atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0) {
+      const hipError_t e = hipStreamQuery(S->st);
+      if (e != hipErrorNotReady)
+        __atomic_store_n(&S->kstate, e == hipSuccess ? 1 : -(int) e, __ATOMIC_RELEASE);
+    }
     nanosleep(&ts, NULL);
   }
   return NULL;
@@ -2139,12 +2151,20 @@ static int server_err(const struct tasx_ctx *c)
 /* 0 while the server kernel runs */
 static int server_alive(const struct tasx_ctx *c)
 {
-  const hipError_t e = hipStreamQuery(c->sv->st);
-  if (e == hipErrorNotReady)
-    return 0;
-  if (e == hipSuccess)
+  struct fserver *S = c->sv;
+  int st = __atomic_load_n(&S->kstate, __ATOMIC_ACQUIRE);
+  if (st == 0) {
+    if (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE))
+      return 0; /* the keepalive thread watches the kernel */
+    /* it has stopped (an abort or a stop under way): ask the runtime */
+    const hipError_t e = hipStreamQuery(S->st);
+    if (e == hipErrorNotReady)
+      return 0;
+    st = e == hipSuccess ? 1 : -(int) e;
+  }
+  if (st == 1)
     return set_err(-EIO, "flush server: the kernel has exited (stopped, or its lease ran out)");
-  return hip_err(e, "flush server: hipStreamQuery");
+  return hip_err((hipError_t) -st, "flush server: hipStreamQuery");
 }
 
 /* 0 while the server kernel runs and has flagged no frame of this context */
@@ -2419,6 +2439,8 @@ int tasx_server_start(int device)
       rc = hip_err(hipGetLastError(), "server kernel launch");
       __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
       pthread_join(S->keep, NULL);
+    } else {
+      __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
     }
   }
   if (rc) {
