@@ -91,6 +91,7 @@ def parse(argv=None):
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
+    ap.add_argument("--server-cost-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx", "flushmix", "tso", "shard8m"], help=argparse.SUPPRESS)
     ap.add_argument("--control-selftest", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank plumbing
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
@@ -1154,12 +1155,7 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
     dev = torch.cuda.current_device()
     wl = Tcp4Workload(rot, pktgen.SEED + 7000 + rank, host=False)
     tw = TxSegWorkload(rot, pktgen.SEED + 7100 + rank)
-    # the timed launches on a stream of their own, waited for by stream and
-    # event only: the null stream's synchronize waited for the flush run's
-    # whole server lifetime in the full bench process (profiles/r05 r05q)
-    ts = torch.cuda.Stream()
-    legs = {"headline": (wl.loop(HINT, streams=[ts]), wl.bytes_per_step, 2000),
-            "tx_segment": (tw.loop(streams=[ts]), tw.bytes_per_step, 800)}
+    legs = {"headline": (wl.loop(HINT), wl.bytes_per_step, 2000), "tx_segment": (tw.loop(), tw.bytes_per_step, 800)}
     for run, _, _ in legs.values():
         prewarm(run)
     torch.cuda.synchronize()
@@ -1169,7 +1165,7 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
     def timed(run, k):
         # stream-level waits only: a device-wide synchronize would wait for the
         # resident server kernel itself
-        cur = ts
+        cur = torch.cuda.current_stream()
         w0 = time.perf_counter()
         run(0, 20)
         w1 = time.perf_counter()
@@ -1250,6 +1246,28 @@ def server_cost_leg(rank: int, rot: int, flushes: int = 300000) -> dict:
                      "slowdown_busy": round(st["busy_8x3"] / st["stopped"], 4),
                      "frac_busy": round(nbytes / st["busy_8x3"] / 1e3 / HBM_PEAK_GBS, 4)}
     del res["states"]
+    return res
+
+
+def server_cost_child_leg(rot: int) -> dict:
+    """server_cost_leg in a fresh child process (bench.py --server-cost-child):
+    run inside the full bench process after the two-context and flush-mix
+    legs, the busy pass's first synchronize blocked until the flush run had
+    ended (profiles/r05 r05q), so that process measured nothing busy; a fresh
+    process measures the leg as tools/price_leg.py does."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-u", str(ROOT / "bench.py"), "--server-cost-child", "--rotate", str(rot)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "server_cost child: no answer within 400 s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"server_cost child rc={r.returncode}: {r.stderr[-400:]}"}
+    res = json.loads(lines[-1])
+    res["process"] = "a child process of its own (bench.py --server-cost-child)"
     return res
 
 
@@ -1630,6 +1648,11 @@ def control_selftest(ws: int, rank: int, info: dict) -> None:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.server_cost_child:
+        torch.cuda.set_device(0)
+        xsum.lib()
+        print(json.dumps(server_cost_leg(0, args.rotate)), flush=True)
+        return 0
     if args.pmc_child:
         pmc_child(args.pmc_child, args.steps)
         return 0
@@ -1799,7 +1822,7 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
 
     extra = {}
     if not args.no_server_cost and rank == 0 and ws == 1:
-        extra["server_cost"] = server_cost_leg(rank, rot)
+        extra["server_cost"] = server_cost_child_leg(rot)
         torch.cuda.empty_cache()
     if not args.no_e2e:
         extra["e2e"] = e2e_leg(ws, rank)
