@@ -46,7 +46,8 @@
 extern "C" {
 #endif
 
-#define TASX_ABI_VERSION 8
+#define TASX_XSUM_ABI 8
+#define TASX_ABI_VERSION TASX_XSUM_ABI /* tasx_abi_version() */
 
 /* flags for the TCP4 batch entry points */
 #define TASX_F_INPLACE 0x1u /* also store ip.chksum / tcp.chksum into the frames */

@@ -51,7 +51,7 @@ static int hip_err(hipError_t e, const char *what)
       return hip_err(e_, #call);                       \
   } while (0)
 
-int tasx_abi_version(void) { return TASX_ABI_VERSION; }
+int tasx_abi_version(void) { return TASX_XSUM_ABI; }
 const char *tasx_last_error(void) { return g_err; }
 
 int tasx_device_count(void)
