@@ -8,6 +8,10 @@ TAG=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
+# a heartbeat: a bench step prints only at its end, which can be minutes
+(while sleep 50; do echo "hb $(date +%T)"; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
   echo "== $name: $*"
