@@ -826,3 +826,117 @@ def test_take_unfinished_without_a_failure(oracle):
         np.testing.assert_array_equal(pin.array[:4 * n * 2048], ref[:4 * n * 2048])
     finally:
         cx.close()
+
+
+def test_server_random_flushes(oracle):
+    """A seeded random walk over the server's contract: 1,500 flushes of 1 to
+    130 frames (batches over 64 frames take several slots), up to 1-8 in
+    flight (the depth changing as it goes), mbufs refilled with new frames as
+    soon as their flush completed (the lines an earlier batch read must never
+    be served again), a few frames the server does not take (their batches go
+    through the context itself), submit or synchronous flush at random; every
+    frame of every flush checked against the oracle when its ticket completes."""
+    rng = np.random.default_rng(0x5EED)
+    nt, nmb = 1024, 600
+    tmpl, _ = _frames(nt, 4242, short=True)              # templates: data segments, ACKs, a few short
+    tmpl_arr = tmpl.array[:nt * 2048].copy()
+    tmpl.free()
+    ref = tmpl_arr.copy()
+    oracle.tcp4_batch(ref, nt, stride=2048, inplace=True)
+    tv, rv = tmpl_arr.reshape(nt, 2048), ref.reshape(nt, 2048)
+    xsum.server_start(0)
+    cx = _Ctxs([13])
+    try:
+        pin = xsum.PinnedBuffer(nmb * 2048)
+        cx.pins.append(pin)
+        mb = pin.array[:nmb * 2048].reshape(nmb, 2048)
+        xsum.register_frames(13, pin.addr, pin.nbytes)
+        xsum.use_server(13)
+        free = list(range(nmb))
+        out = []                                         # (ticket, [(mbuf, template)])
+        depth, checked = 4, 0
+
+        def complete_oldest():
+            nonlocal checked
+            t, items = out.pop(0)
+            xsum.flush_wait(13, t)
+            for m, k in items:
+                np.testing.assert_array_equal(mb[m], rv[k], err_msg=f"ticket {t} mbuf {m} template {k}")
+                free.append(m)
+            checked += len(items)
+
+        for f in range(1500):
+            if f % 100 == 0:
+                depth = int(rng.integers(1, 9))
+            n = int(rng.integers(1, 33)) if rng.random() < 0.9 else int(rng.integers(33, 131))
+            while len(out) >= depth or len(free) < n:
+                complete_oldest()
+            pick = [free.pop(int(rng.integers(0, len(free)))) for _ in range(n)]
+            items = []
+            for m in pick:
+                k = int(rng.integers(0, nt))
+                mb[m] = tv[k]
+                xsum.tcp_checksums(13, pin.addr + m * 2048)
+                items.append((m, k))
+            if rng.random() < 0.1:                       # a synchronous tx_flush now and then
+                while out:
+                    complete_oldest()
+                xsum.tx_flush(13)
+                for m, k in items:
+                    np.testing.assert_array_equal(mb[m], rv[k])
+                    free.append(m)
+                checked += len(items)
+            else:
+                out.append((xsum.flush_submit(13), items))
+        while out:
+            complete_oldest()
+        assert checked > 30000
+        assert xsum.server_flushes(13) > 1000            # batches with a short frame go through the context
+        xsum.use_server(13, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+
+
+def test_server_tx_segments_random_groups(oracle):
+    """TX segment slots under a seeded random walk: 4,096 segments of 64 flows
+    (odd buffer bases and lengths, payloads of 0-1448 B, circular-buffer
+    wraps) handed over in groups of 1-90 (groups over 41 take several slots)
+    with 1-8 flushes in flight; every frame equals the oracle's flow_tx_read +
+    tcp_checksums."""
+    rng = np.random.default_rng(0x7E57)
+    n = 4096
+    pay = rng.integers(0, pktgen.TCP_MSS + 1, n)
+    pay[rng.random(n) < 0.2] = pktgen.TCP_MSS
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=64, odd=True, seed=0xA11,
+                                           room=pktgen.MBUF_ROOM)
+    exp_fr = fr.copy()
+    oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    xsum.server_start(0)
+    cx = _Ctxs([15])
+    try:
+        hf = xsum.PinnedBuffer(fr.size + 4096)
+        hs = xsum.PinnedBuffer(sl + 64)
+        cx.pins += [hf, hs]
+        hs.array[:sl] = shm[:sl]
+        hf.array[:] = 0
+        hf.array[:fr.size] = fr
+        xsum.register_frames(15, hf.addr, hf.nbytes)
+        xsum.register_shm(15, hs.addr, sl)
+        xsum.use_server(15)
+        out, i, depth = [], 0, 4
+        while i < n:
+            if rng.random() < 0.05:
+                depth = int(rng.integers(1, 9))
+            g = min(int(rng.integers(1, 91)), n - i)
+            while len(out) >= depth:
+                xsum.flush_wait(15, out.pop(0))
+            out.append(xsum.server_tx_segments(15, segs[i:i + g]))
+            i += g
+        for t in out:
+            xsum.flush_wait(15, t)
+        np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
+        xsum.use_server(15, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
