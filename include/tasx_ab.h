@@ -35,12 +35,14 @@
  *   45..48  RAW rows of 32 / 64 lanes and without the residency cap
  * The environment knobs, read once at load: TASX_TAS14_*_LDS and
  * TASX_WAVE_TCP4_LDS (KiB of reserved LDS for the A/B variants' launches),
- * TASX_TXSEG_DEBUG (TX segment diagnostics kernels; 29 =
- * tx_segment_wave_kernel, one segment per wave from aligned loads), TASX_XRUN
- * (XCD order of every grid), TASX_FEEDER_SWEEPS, and for the flush server
- * TASX_SRV_K (workgroups per ring), TASX_SRV_HOT_US / TASX_SRV_COLD_US (poll
- * backoff), TASX_SRV_SEGMAX (TX segments per slot), TASX_SRV_DIAG (its
- * timing form: tasx_ab_server_diag).
+ * TASX_XRUN (XCD order of every grid), TASX_FEEDER_SWEEPS, and for the flush
+ * server TASX_SRV_K (workgroups per ring), TASX_SRV_HOT_US / TASX_SRV_COLD_US
+ * (poll backoff), TASX_SRV_SEGMAX (TX segments per slot), TASX_SRV_DIAG (its
+ * timing form: tasx_ab_server_diag); read at each use: TASX_TXSEG_DEBUG (TX
+ * segment diagnostics kernels, at each TX launch; 29 = tx_segment_wave_kernel,
+ * one segment per wave from aligned loads) and TASX_SRV_ACQ (at each server
+ * start: 1 / 2 = the per-batch acquire at agent scope / left out, for pricing
+ * the server only -- not correct forms).
  */
 #ifndef TASX_AB_H_
 #define TASX_AB_H_
