@@ -2,7 +2,9 @@
 product), 12 and 24 loads per lane a round (A/B variants 49, 50: fewer bubbles
 between a 64 KB row's rounds), alternating rounds, beside the streaming read;
 each variant's results compared with the product's.  Run with
-TASX_LIB=$PWD/tas_amd/_lib/libtasx_ab.so.
+TASX_LIB=$PWD/tas_amd/_lib/libtasx_ab.so.  The record of profiles/r05 r05w:
+variants 49 / 50 were removed after it (no gain), so this no longer runs
+as is.
     python tools/tso_rows_probe.py [--rounds 3] [--launches 200]"""
 import argparse
 import json
