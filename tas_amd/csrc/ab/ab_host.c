@@ -47,6 +47,10 @@ __attribute__((constructor)) static void ab_hooks_init(void)
   g_hooks.srv_diag = getenv("TASX_SRV_DIAG") != NULL;          /* the server's timing sums */
   g_hooks.srv_hot_us = getenv("TASX_SRV_HOT_US") ? atoi(getenv("TASX_SRV_HOT_US")) : -1;
   g_hooks.srv_cold_us = getenv("TASX_SRV_COLD_US") ? atoi(getenv("TASX_SRV_COLD_US")) : -1;
+  if (env_u32("TASX_HOST_UC", 0u)) { /* frames and shm mapped MTYPE_UC: the L2 never caches them */
+    g_hooks.host_reg_flags = 0x80000000u;   /* hipExtHostRegisterUncached */
+    g_hooks.host_alloc_flags = 0x10000000u; /* hipHostMallocUncached */
+  }
   tasx_ext = &g_hooks;
 }
 

@@ -541,7 +541,8 @@ static int pin_acquire(uint8_t *base, size_t bytes, void **dev, int *owned)
     k++;
   if (k == MAX_PINS)
     rc = set_err(-ENOMEM, "more than %u pinned regions", MAX_PINS);
-  else if ((e = hipHostRegister(base, bytes, hipHostRegisterMapped)) != hipSuccess)
+  else if ((e = hipHostRegister(base, bytes, hipHostRegisterMapped | (tasx_ext ? tasx_ext->host_reg_flags : 0u))) !=
+           hipSuccess)
     rc = hip_err(e, "hipHostRegister");
   else if ((e = hipHostGetDevicePointer(dev, base, 0)) != hipSuccess) {
     hipHostUnregister(base);
@@ -2878,7 +2879,7 @@ int tasx_take_unfinished_segs(unsigned ctx_id, tasx_tx_seg *segs, uint32_t max)
 void *tasx_host_alloc(size_t bytes)
 {
   void *p = NULL;
-  unsigned flags = 0;
+  const unsigned flags = tasx_ext ? tasx_ext->host_alloc_flags : 0u;
   hipError_t e = hipHostMalloc(&p, bytes, flags);
   if (e != hipSuccess) {
     hip_err(e, "hipHostMalloc");

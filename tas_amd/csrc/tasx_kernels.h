@@ -188,6 +188,8 @@ typedef struct tasx_ext_hooks {
   uint32_t srv_segmax;    /* TX segments per server slot (TASX_SRV_SEGMAX), 0 = the product's */
   uint32_t srv_diag;      /* the server's timing sums (TASX_SRV_DIAG) */
   int32_t srv_hot_us, srv_cold_us; /* poll backoff times (TASX_SRV_HOT_US / _COLD_US), < 0 = the product's */
+  uint32_t host_reg_flags;   /* extra hipHostRegister flags for frame / shm regions (TASX_HOST_UC) */
+  uint32_t host_alloc_flags; /* extra hipHostMalloc flags of tasx_host_alloc (TASX_HOST_UC) */
 } tasx_ext_hooks;
 TASX_INTERNAL extern const tasx_ext_hooks *tasx_ext;
 /* test support for the A/B build's exports (tasx_ab_ctx_set_tickets,
