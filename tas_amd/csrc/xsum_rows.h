@@ -1177,12 +1177,12 @@ constexpr uint32_t kOccLds = 30u * 1024u;
 // XCD-ordered grids (xcd_run, round 5): from 16,384 blocks (a batch of 256K
 // frames or packets and up) each XCD works through runs of 256 consecutive
 // blocks (6 MB of 1500-byte packets), the 8 runs of a window adjacent.  In grid
-// order the 8 XCDs share every page of the ~30 MB the resident blocks span
-// (26.7K UTCL1 translation misses per 12.6 GB launch, the UTCL2 busy 1.1-1.6M
-// cycles); in runs each XCD's resident blocks lie in two or three 2 MB pages
-// (0-3.7K misses, UTCL2 busy 9K-230K).  8M x 1500 B RAW: 1.74-1.77 ms against
-// 1.87-2.00 (profiles/r05/INDEX.md r05a-r05c); 64K-frame batches (the headline)
-// are neutral to slower in any XCD order and stay in grid order.
+// order the 8 XCDs spread their L2 misses over every DRAM page in flight; in
+// runs each XCD's misses stay on few pages: 8M x 1500 B RAW 1.74-1.77 ms
+// against 1.87-2.00, the L2's DRAM credit stalls 0.25M against 1.48M and tag
+// stalls 0.29M against 1.52M per launch, translation misses about the same
+// (28K against 32K; profiles/r05/INDEX.md r05a-r05c, r05z).  64K-frame batches
+// (the headline) are neutral to slower in any XCD order and stay in grid order.
 constexpr uint32_t kXrunMinBlocks = 16384u;
 constexpr uint32_t kXrun = 9u; // runs of 2^(9 - 1) = 256 blocks
 
