@@ -867,21 +867,31 @@ def prewarm(run, seconds: float = 0.25):
 CTX2_MIN_STEPS = 200  # the two-context leg's minimum step count
 
 
-def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
+def timed_run(run, steps: int, warmup: int, ws: int, streams=None, spans: dict | None = None):
     """W untimed steps, then exactly K timed steps between barrier+sync pairs,
-    issued by one C loop.  A HIP event pair on the launch stream around the K
-    launches gives the average launch duration (no per-launch events, which
-    would add gaps of their own).  With several streams the event pair brackets
-    all of them (they wait on the start event; the current stream waits on each
-    one's end)."""
+    issued by one C loop.  HIP events on the launch stream give the average
+    launch duration (no per-launch events, which would add gaps of their
+    own): on one stream, from an event behind the FIRST timed launch to one
+    behind the last, over launches 2..K -- the first launch after the
+    synchronize also carries an idle GPU's dispatch of it (~6 us, which at the
+    driver's K = 20 read as 0.3 us on every launch against rocprofv3's own
+    kernel durations, profiles/r05 r05t); the start event sits before the
+    first launch all the same, and e0 -> e1 / K is returned in `spans`.  The
+    middle event costs the host a few us while the GPU runs launch 1, so the
+    timed region (GPU-bound) is unchanged.  With several streams one event
+    pair brackets all of them (they wait on the start event; the current
+    stream waits on each one's end)."""
     prewarm(run)
     run(0, warmup)
     torch.cuda.synchronize()
     cur = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    em = torch.cuda.Event(enable_timing=True)
+    mid = not streams and steps > 1
     # torch creates an event's HIP handle on its first record(): do that here,
     # not inside the timed region (10-44 us per event, profiles/r02/r02aw)
     e0.record(cur)
+    em.record(cur)
     e1.record(cur)
     torch.cuda.synchronize()
     barrier(ws)
@@ -893,7 +903,12 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
         s.wait_event(e0)
     t0 = time.perf_counter()
     ta = time.perf_counter()
-    run(warmup, steps)
+    if mid:
+        run(warmup, 1)
+        em.record(cur)
+        run(warmup + 1, steps - 1)
+    else:
+        run(warmup, steps)
     tb = time.perf_counter()
     for s in streams or []:
         cur.wait_stream(s)
@@ -910,7 +925,10 @@ def timed_run(run, steps: int, warmup: int, ws: int, streams=None):
                           "rec1_us": round((tc - tb) * 1e6, 2), "sync_us": round((t1 - tc) * 1e6, 2),
                           "host_us": round((t1 - t0) * 1e6, 2),
                           "event_us": round(e0.elapsed_time(e1) * 1e3, 2)}), file=sys.stderr)
-    return t1 - t0, e0.elapsed_time(e1) / steps
+    span = e0.elapsed_time(e1) / steps
+    if spans is not None:
+        spans["span_avg_us"] = round(span * 1e3, 3)
+    return t1 - t0, em.elapsed_time(e1) / (steps - 1) if mid else span
 
 
 def drop_rehearsal_fractions(obj):
@@ -933,12 +951,14 @@ def roofline(bytes_per_launch: int, avg_ms: float, traffic):
 
 
 def leg(run, bytes_per_step: int, args, ws, desc, kernel: str = "", streams=None):
-    dt, avg_ms = timed_run(run, args.steps, args.warmup, ws, streams)
+    spans = {}
+    dt, avg_ms = timed_run(run, args.steps, args.warmup, ws, streams, spans)
     per_rank = gather_over_ranks(bytes_per_step * args.steps / dt / GIB, ws)
     dtm = max_over_ranks(dt, ws)
     total = sum_over_ranks(float(bytes_per_step * args.steps), ws)
     r = {"value": total / dtm / GIB, "unit": "GiB/s", "ms_per_step": dtm / args.steps * 1e3,
          "workload": desc, "roofline": roofline(bytes_per_step, avg_ms, None), "seconds": dt}
+    r["roofline"]["span_avg_us"] = spans.get("span_avg_us")  # e0 -> e1 over all K launches
     if kernel:
         r["kernel"] = kernel
     if ws > 1:
