@@ -179,6 +179,25 @@ def numa_pin(bus_id: str) -> dict:
     return info
 
 
+def host_spin_wait(dev: int) -> str:
+    """Completion waits by spinning (hipDeviceScheduleSpin) on this rank's GPU,
+    set on the HIP runtime torch loaded before its context exists: the
+    timed region ends in a synchronize, and a waiting host thread that yields
+    adds its wake-up to every K-step interval.  TASX_BENCH_SCHED=auto keeps
+    the runtime's default."""
+    if os.environ.get("TASX_BENCH_SCHED", "spin") != "spin":
+        return "auto"
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so", mode=os.RTLD_NOLOAD)
+    except OSError:
+        return "auto (HIP runtime not loaded by name)"
+    if hip.hipSetDevice(dev) != 0:
+        return "auto (hipSetDevice failed)"
+    rc = hip.hipSetDeviceFlags(1)  # hipDeviceScheduleSpin
+    return "spin" if rc == 0 else f"auto (hipSetDeviceFlags rc {rc})"
+
+
 def dist_setup(args):
     """Rank setup.  WORLD_SIZE (from the launcher or spawn_ranks) must equal
     --gpus; each rank takes GPU LOCAL_RANK (distinct devices are checked), or
@@ -197,8 +216,10 @@ def dist_setup(args):
         if not rehearse and local >= ndev:
             raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, {ndev} visible (--rehearse to share)")
         dev = local % max(1, ndev)
+        sched = host_spin_wait(dev)
         torch.cuda.set_device(dev)
         info = numa_pin(pci_bus_id(dev))
+        info["host_wait"] = sched
     if ws > 1:
         if rehearse or args.control_selftest:
             dist.init_process_group("gloo")
@@ -1901,7 +1922,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             "frac_of_n_hbm": None if rehearse else round(head["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4),
             "per_rank_value": head.get("per_rank_value", [round(head["value"], 2)]),
             "ranks": {"bus_ids": info.get("all_bus_ids", [info.get("pci_bus_id")]),
-                      "numa_node_rank0": info.get("numa_node"), "rehearse": info.get("rehearse")},
+                      "numa_node_rank0": info.get("numa_node"), "rehearse": info.get("rehearse"),
+                      "host_wait": info.get("host_wait")},
             "cpu_baseline": extra.get("cpu_baseline"),
             "tcp4_nohint": nohint,
             "tcp4_frames_only": frames_only,
