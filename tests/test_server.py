@@ -828,7 +828,13 @@ def test_take_unfinished_without_a_failure(oracle):
         cx.close()
 
 
-def test_server_random_flushes(oracle):
+# seeds of the random-walk tests: one by default; TASX_STRESS_SEEDS=N runs N
+# (a stress run on the GPU box, profiles/r05 r05zd)
+STRESS_SEEDS = list(range(int(__import__("os").environ.get("TASX_STRESS_SEEDS", "1"))))
+
+
+@pytest.mark.parametrize("seed", STRESS_SEEDS)
+def test_server_random_flushes(oracle, seed):
     """A seeded random walk over the server's contract: 1,500 flushes of 1 to
     130 frames (batches over 64 frames take several slots), up to 1-8 in
     flight (the depth changing as it goes), mbufs refilled with new frames as
@@ -836,7 +842,7 @@ def test_server_random_flushes(oracle):
     be served again), a few frames the server does not take (their batches go
     through the context itself), submit or synchronous flush at random; every
     frame of every flush checked against the oracle when its ticket completes."""
-    rng = np.random.default_rng(0x5EED)
+    rng = np.random.default_rng(0x5EED + seed)
     nt, nmb = 1024, 600
     tmpl, _ = _frames(nt, 4242, short=True)              # templates: data segments, ACKs, a few short
     tmpl_arr = tmpl.array[:nt * 2048].copy()
@@ -898,17 +904,18 @@ def test_server_random_flushes(oracle):
         cx.close()
 
 
-def test_server_tx_segments_random_groups(oracle):
+@pytest.mark.parametrize("seed", STRESS_SEEDS)
+def test_server_tx_segments_random_groups(oracle, seed):
     """TX segment slots under a seeded random walk: 4,096 segments of 64 flows
     (odd buffer bases and lengths, payloads of 0-1448 B, circular-buffer
     wraps) handed over in groups of 1-90 (groups over 41 take several slots)
     with 1-8 flushes in flight; every frame equals the oracle's flow_tx_read +
     tcp_checksums."""
-    rng = np.random.default_rng(0x7E57)
+    rng = np.random.default_rng(0x7E57 + seed)
     n = 4096
     pay = rng.integers(0, pktgen.TCP_MSS + 1, n)
     pay[rng.random(n) < 0.2] = pktgen.TCP_MSS
-    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=64, odd=True, seed=0xA11,
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=64, odd=True, seed=0xA11 + seed,
                                            room=pktgen.MBUF_ROOM)
     exp_fr = fr.copy()
     oracle.tx_segment_batch(shm, sl, exp_fr, segs)
