@@ -1,7 +1,8 @@
 """bench.py's pricing helpers on the CPU: the roofline record, the data/ACK
 mixes' latency roofline (price_mix), the TX segment build's 128-byte block
-floor, and the rehearsal filter that drops any fraction above 1 when ranks
-share one GPU.  No GPU work."""
+floor, the rehearsal filter that drops any fraction above 1 when ranks
+share one GPU, the price leg's child process failing softly, and the host
+wait setting.  No GPU work."""
 import numpy as np
 
 import bench
@@ -90,3 +91,19 @@ def test_fastpath_mt_refuses_bad_shapes_before_any_gpu_call():
             assert e.code == -errno.EINVAL, (th, q, fl, mode, ctx0, e.code)
         else:
             raise AssertionError((th, q, fl, mode, ctx0))
+
+
+def test_server_cost_child_failure_is_reported_not_raised():
+    """The price leg runs in a child process (bench.py --server-cost-child); a
+    child that fails (here: no GPU) leaves an error record in the bench line
+    instead of ending the bench."""
+    import torch
+    if torch.cuda.is_available():
+        return  # on a GPU box the child runs for real (tests/test_bench_configs.py covers the legs)
+    r = bench.server_cost_child_leg(1)
+    assert set(r) == {"error"} and "server_cost child" in r["error"]
+
+
+def test_host_spin_wait_can_be_turned_off(monkeypatch):
+    monkeypatch.setenv("TASX_BENCH_SCHED", "auto")
+    assert bench.host_spin_wait(0) == "auto"
