@@ -75,7 +75,13 @@ def test_generator_wraps_and_flows():
 # tx_segment_tas_kernel (unaligned non-temporal window loads); "b128" = 41,
 # the product with its LDS windows read back by ds_read_b128; "ldsdma" = 44
 # (round 4), the product with its source chunks landed in the slice by LDS-DMA
-IMPLS = ["product", "r2", "b128", "ldsdma"]
+# The A/B forms run here beside the product: r2 (the round-2 kernel).  The
+# round-3/4 null results b128 (LDS windows by ds_read_b128, correct only where
+# the LDS runs in unaligned mode) and ldsdma (source chunks by LDS-DMA through
+# inline asm that moves M0) left this list in round 5: an illegal memory access
+# surfaced right after them in one full run (profiles/r05 r05end), and neither
+# is a product form; they stay in the A/B build (include/tasx_ab.h).
+IMPLS = ["product", "r2"]
 AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel"), "b128": ("41", "tx_segment_lds_kernel<b128>"),
             "ldsdma": ("44", "tx_segment_lds_kernel<ldsdma>")}
 
