@@ -25,10 +25,7 @@ def _lib():
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
     xsum.lib()
     yield
-    try:  # never leave a server running past the module
-        xsum.server_stop(0)
-    except xsum.TasxError:
-        pass
+    _stop_quietly_or_fail()  # never leave a server running past the module
 
 
 @pytest.fixture(autouse=True)
@@ -38,10 +35,42 @@ def _stop_server_after_each_test():
     finally blocks have destroyed its contexts, which detaches them) stop the
     server if one is still running."""
     yield
+    _stop_quietly_or_fail()
+
+
+def _stop_quietly_or_fail():
+    """Stop the server if one runs; "not running" (-EINVAL) is the normal case.
+    Anything else is reported, never swallowed: -EBUSY (contexts a failed test
+    left attached) aborts the server first so that later tests start clean,
+    and -EIO (its kernel did not leave within the bound: its memory stays
+    mapped, leaked) fails the teardown, as a kernel still running could fault
+    on regions later tests free."""
     try:
         xsum.server_stop(0)
-    except xsum.TasxError:
-        pass  # not running (the test stopped it)
+        return
+    except xsum.TasxError as e:
+        if e.code == -errno.EINVAL:
+            return
+        first = e
+    if first.code == -errno.EBUSY:
+        try:
+            xsum.server_abort(0)
+            xsum.server_stop(0)
+        except xsum.TasxError as e2:
+            pytest.fail(f"server left attached and not stoppable after abort: {first}; {e2}")
+        pytest.fail(f"server left with contexts attached (aborted and stopped): {first}")
+    pytest.fail(f"server stop after the test failed: {first}")
+
+
+def _stop_if_running():
+    """A test's own finally: stop the server if it still runs.  "Not running"
+    (-EINVAL) and "contexts still attached" (-EBUSY: the autouse fixture
+    aborts and reports it) pass; a kernel that did not leave (-EIO) raises."""
+    try:
+        xsum.server_stop(0)
+    except xsum.TasxError as e:
+        if e.code not in (-errno.EINVAL, -errno.EBUSY):
+            raise
 
 
 def _frames(nframes: int, seed: int, short: bool = True):
@@ -126,10 +155,7 @@ def test_server_interleaved_contexts(oracle):
             xsum.server_stop(0)                      # not running
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 def test_server_reused_mbufs_and_large_flush(oracle):
@@ -201,10 +227,7 @@ def test_server_refilled_mbufs_every_flush(oracle, mem):
         xsum.server_stop(0)
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
         del raw  # unregistered by the context's release (at the server's stop at the latest)
 
 
@@ -291,10 +314,7 @@ def test_server_reattach_keeps_ring_position(oracle):
         assert tmp.addr == 0
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 def test_server_frames_it_does_not_take(oracle):
@@ -336,10 +356,7 @@ def test_server_frames_it_does_not_take(oracle):
         xsum.server_stop(0)
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 def test_server_changed_frame_is_reported(oracle):
@@ -387,10 +404,7 @@ def test_server_changed_frame_is_reported(oracle):
         xsum.server_stop(0)
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 def test_server_threads(oracle):
@@ -477,10 +491,7 @@ def test_server_stop_is_bounded_and_restarts(oracle):
             xsum.feeder_stop(0)
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 @pytest.mark.parametrize("odd,shm_mem", [(False, "host_alloc"), (True, "host_alloc"), (True, "registered")])
@@ -547,10 +558,7 @@ def test_server_tx_segments(oracle, odd, shm_mem):
         xsum.server_stop(0)
     finally:
         cx.close()
-        try:
-            xsum.server_stop(0)
-        except xsum.TasxError:
-            pass
+        _stop_if_running()
 
 
 def test_server_beside_feeder_and_device_batches(oracle):
