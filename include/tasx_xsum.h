@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TASX_XSUM_ABI 8
+#define TASX_XSUM_ABI 9
 #define TASX_ABI_VERSION TASX_XSUM_ABI /* tasx_abi_version() */
 
 /* flags for the TCP4 batch entry points */
@@ -437,7 +437,19 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     hands the context's memory to the server (released at its stop), and
  *     tasx_host_free, tasx_host_unregister, tasx_dev_free and tasx_feeder_stop
  *     return -EBUSY; anything else in the process that frees device or pinned
- *     memory (e.g. torch.cuda.empty_cache) blocks until the stop
+ *     memory (hipFree, hipHostFree, hipHostUnregister, torch.cuda.empty_cache;
+ *     hipFreeAsync does not wait) blocks until the stop -- or, since ABI 9,
+ *     until a pause:
+ *   tasx_server_pause(device): the kernel leaves at its rings' current
+ *     positions (a batch being summed is finished first; at most 5 s, else
+ *     -EIO and the server runs on); contexts stay attached, submit as before
+ *     (the slots wait in the rings; a full ring waits inside the call) and
+ *     poll "not done"; frees do not wait, and the four calls above work.
+ *     -EALREADY when paused already, -EIO after an abort or a kernel exit.
+ *     Detaching (tasx_ctx_use_server(ctx, 0)) waits for the resume.
+ *   tasx_server_resume(device): launch the kernel again at those positions
+ *     (-EINVAL when not paused); the paused batches are served from there.
+ *     A server may also be stopped (once detached) or aborted while paused.
  *   tasx_server_stats: batches and frames submitted since start
  *   tasx_ctx_server_flushes: batches the context handed to the server */
 /* (ABI 7) The fused TX segment build through the flush server (the copy of
@@ -463,6 +475,8 @@ int tasx_ctx_register_shm(unsigned ctx_id, void *shm, size_t bytes);
 int tasx_server_tx_segments(unsigned ctx_id, const tasx_tx_seg *segs, uint32_t n, uint32_t *ticket);
 int tasx_server_start(int device);
 int tasx_server_stop(int device);
+int tasx_server_pause(int device);
+int tasx_server_resume(int device);
 int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames);
 int tasx_ctx_use_server(unsigned ctx_id, int on);
 int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);

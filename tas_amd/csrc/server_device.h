@@ -149,7 +149,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   if (DIAG && threadIdx.x < 6)
     s_d[threadIdx.x] = threadIdx.x == 5 ? wall_clock64() : 0ull;
   __syncthreads();
-  uint32_t p = blockIdx.x % K; // the server starts on a zeroed block: every ring at position 0
+  // a first launch starts on a zeroed block (every ring at position 0); a
+  // resumed one (tasx_server_resume) where this workgroup left off
+  uint32_t *const posw = (uint32_t *) (mem + TASX_SRV_POSW(blockIdx.x));
+  uint32_t p = P.resume ? __hip_atomic_load(posw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : blockIdx.x % K;
   uint64_t t_act = wall_clock64(), t_lease = t_act;
   uint32_t lease = 0u;
   uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
@@ -264,8 +267,11 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
     }
     __syncthreads();
-    if (s_cmd != 0u)
+    if (s_cmd != 0u) {
+      if (threadIdx.x == 0) // the position polled and not taken: where a resumed launch starts
+        st_sys32(posw, p);
       break;
+    }
     const uint32_t row = threadIdx.x >> 4;
     if (s_seg) {
       // TX segment slot: row r builds segment r (payload gathered from the

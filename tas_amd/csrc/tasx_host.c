@@ -2048,6 +2048,15 @@ struct fserver {
    * hipStreamQuery per poll from 8 cores serialised in the runtime's locks and
    * stalled the process's other HIP work, profiles/r05 r05o) */
   int launched, kstate;
+  /* launched and kstate change together under kmu (the keepalive thread's
+   * query and a pause or resume never interleave) */
+  pthread_mutex_t kmu;
+  /* tasx_server_pause: the kernel has left at its rings' positions and
+   * tasx_server_resume launches it again from them (prm.resume); set before
+   * the stop word is written and cleared after the new launch, so that a
+   * kernel found not running while paused is never taken for gone */
+  int paused;
+  tasx_srv_params prm;
 };
 
 struct grave {
@@ -2062,15 +2071,18 @@ static void ctx_settle(struct tasx_ctx *c);
 static int unf_seg(struct tasx_ctx *c, const tasx_tx_seg *g);
 
 /* HIP's frees wait for every stream of the device, the server's kernel too:
- * refused (-EBUSY) while any server runs, instead of waiting for its stop */
+ * refused (-EBUSY) while any server's kernel runs (a paused one does not),
+ * instead of waiting for its stop */
 static int server_blocks_free(const char *what)
 {
   int d, any = 0;
   pthread_mutex_lock(&g_server_mu);
   for (d = 0; d < MAX_DEVICES; d++)
-    any |= g_server[d] != NULL;
+    any |= g_server[d] != NULL && !__atomic_load_n(&g_server[d]->paused, __ATOMIC_ACQUIRE);
   pthread_mutex_unlock(&g_server_mu);
-  return any ? set_err(-EBUSY, "%s: a flush server is running (HIP frees wait for its kernel; tasx_server_stop first)",
+  return any ? set_err(-EBUSY,
+                       "%s: a flush server is running (HIP frees wait for its kernel; tasx_server_pause or "
+                       "tasx_server_stop first)",
                        what)
              : 0;
 }
@@ -2110,11 +2122,13 @@ static void *server_keepalive(void *arg)
   hipSetDevice(S->device);
   while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(lease, k++, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&S->kmu);
     if (__atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0) {
       const hipError_t e = hipStreamQuery(S->st);
       if (e != hipErrorNotReady)
         __atomic_store_n(&S->kstate, e == hipSuccess ? 1 : -(int) e, __ATOMIC_RELEASE);
     }
+    pthread_mutex_unlock(&S->kmu);
     nanosleep(&ts, NULL);
   }
   return NULL;
@@ -2135,11 +2149,26 @@ static void server_atexit(void)
 
 static void server_free(struct fserver *S)
 {
+  pthread_mutex_destroy(&S->kmu);
   if (S->h_mem)
     hipHostFree(S->h_mem);
   if (S->st)
     hipStreamDestroy(S->st);
   free(S);
+}
+
+/* 1 when the server's kernel has left for good: aborted, or not running and
+ * not paused (paused is read again after the query: a pause sets it before
+ * its kernel leaves) */
+static int server_gone(struct fserver *S)
+{
+  if (S->aborted)
+    return 1;
+  if (__atomic_load_n(&S->paused, __ATOMIC_ACQUIRE))
+    return 0;
+  if (hipStreamQuery(S->st) == hipErrorNotReady)
+    return 0;
+  return !__atomic_load_n(&S->paused, __ATOMIC_ACQUIRE);
 }
 
 /* 0 while the server kernel runs and has flagged no error */
@@ -2396,6 +2425,7 @@ int tasx_server_start(int device)
     return set_err(-ENOMEM, "server: out of host memory");
   }
   S->device = device;
+  pthread_mutex_init(&S->kmu, NULL);
   if ((e = hipSetDevice(device)) != hipSuccess ||
       (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking)) != hipSuccess ||
@@ -2416,6 +2446,7 @@ int tasx_server_start(int device)
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
     prm.diag = 0;
     prm.k = SRV_K;
+    prm.resume = 0;
     if (tasx_ext) { /* the A/B build's knobs: timing sums, workgroups per ring, poll backoff */
       prm.diag = tasx_ext->srv_diag;
       if (tasx_ext->srv_k)
@@ -2427,6 +2458,7 @@ int tasx_server_start(int device)
     }
     S->khz = (uint32_t) khz;
     S->k = prm.k;
+    S->prm = prm;
     if (prm.k == 0u || TASX_SRV_RING % prm.k != 0u || prm.k > TASX_SRV_KMAX)
       rc = set_err(-EINVAL, "server: %u workgroups per ring (a divisor of %u)", prm.k, TASX_SRV_RING);
   }
@@ -2441,7 +2473,9 @@ int tasx_server_start(int device)
       __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
       pthread_join(S->keep, NULL);
     } else {
+      pthread_mutex_lock(&S->kmu);
       __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
+      pthread_mutex_unlock(&S->kmu);
     }
   }
   if (rc) {
@@ -2564,7 +2598,7 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
       return rc;
     pthread_mutex_lock(&g_server_mu);
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
-    if (S && (S->aborted || hipStreamQuery(S->st) != hipErrorNotReady)) {
+    if (S && server_gone(S)) {
       pthread_mutex_unlock(&g_server_mu);
       return set_err(-EIO, "the flush server for device %d is not running (aborted, or its lease ran out): "
                      "tasx_server_stop it", c->device);
@@ -2644,6 +2678,106 @@ int tasx_server_abort(int device)
   if (e == hipErrorNotReady)
     return set_err(-EIO, "flush server for device %d did not stop within %u ms", device, SRV_STOP_WAIT_MS);
   return 0;
+}
+
+/* (ABI 9) HIP's frees (hipFree, hipHostFree, hipHostUnregister, and so
+ * torch.cuda.empty_cache) wait for every kernel of the device, the server's
+ * too (profiles/r05 r05free).  A pause lets them through without detaching
+ * anyone: every workgroup leaves at its next poll (a batch it is summing is
+ * finished first) and stores the position it polled; contexts keep
+ * submitting meanwhile (the slots wait in the rings) and their polls report
+ * "not done yet"; tasx_server_resume launches the kernel again at those
+ * positions. */
+int tasx_server_pause(int device)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "server: device %d out of range", device);
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = g_server[device];
+  int rc = 0;
+  if (!S)
+    rc = set_err(-EINVAL, "no flush server running for device %d", device);
+  else if (S->aborted)
+    rc = set_err(-EIO, "the flush server for device %d was aborted", device);
+  else if (S->paused)
+    rc = set_err(-EALREADY, "the flush server for device %d is paused already", device);
+  if (rc) {
+    pthread_mutex_unlock(&g_server_mu);
+    return rc;
+  }
+  pthread_mutex_lock(&S->kmu);
+  const int st = __atomic_load_n(&S->kstate, __ATOMIC_ACQUIRE);
+  if (st == 0) {
+    __atomic_store_n(&S->paused, 1, __ATOMIC_RELEASE);
+    __atomic_store_n(&S->launched, 0, __ATOMIC_RELEASE); /* the keepalive thread stops asking */
+  }
+  pthread_mutex_unlock(&S->kmu);
+  if (st != 0) {
+    pthread_mutex_unlock(&g_server_mu);
+    return st == 1 ? set_err(-EIO, "flush server: the kernel has exited (stopped, or its lease ran out)")
+                   : hip_err((hipError_t) -st, "flush server kernel");
+  }
+  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+  hipError_t e = hipErrorNotReady;
+  const struct timespec ts = {0, 100 * 1000};
+  for (uint32_t t = 0; t < SRV_STOP_WAIT_MS * 10u && (e = hipStreamQuery(S->st)) == hipErrorNotReady; t++)
+    nanosleep(&ts, NULL);
+  if (e != hipSuccess) {
+    /* still running after the bound, or failed: not paused; the keepalive
+     * thread watches the kernel again and the contexts see what it does */
+    pthread_mutex_lock(&S->kmu);
+    if (e != hipErrorNotReady)
+      __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
+    __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
+    __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&S->kmu);
+    pthread_mutex_unlock(&g_server_mu);
+    return e == hipErrorNotReady
+               ? set_err(-EIO, "flush server for device %d did not leave within %u ms", device, SRV_STOP_WAIT_MS)
+               : hip_err(e, "flush server kernel");
+  }
+  pthread_mutex_unlock(&g_server_mu);
+  return 0;
+}
+
+int tasx_server_resume(int device)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-ENODEV, "server: device %d out of range", device);
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = g_server[device];
+  int rc = 0;
+  if (!S)
+    rc = set_err(-EINVAL, "no flush server running for device %d", device);
+  else if (!S->paused)
+    rc = set_err(-EINVAL, "the flush server for device %d is not paused", device);
+  else if (S->aborted)
+    rc = set_err(-EIO, "the flush server for device %d was aborted", device);
+  if (rc) {
+    pthread_mutex_unlock(&g_server_mu);
+    return rc;
+  }
+  int prev = -1;
+  (void) hipGetDevice(&prev);
+  hipError_t e = hipSetDevice(S->device);
+  S->prm.resume = 1;
+  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 0u, __ATOMIC_RELEASE); /* the stop word; the lease goes on */
+  if (e == hipSuccess && tasx_launch_server(&S->prm, S->st) != 0) {
+    e = hipGetLastError();
+    if (e == hipSuccess)
+      e = hipErrorLaunchFailure;
+  }
+  pthread_mutex_lock(&S->kmu);
+  /* launched: the keepalive thread watches the new kernel; on a failed launch
+   * the contexts see the error (and settle, tasx_take_unfinished) */
+  __atomic_store_n(&S->kstate, e == hipSuccess ? 0 : -(int) e, __ATOMIC_RELEASE);
+  __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
+  __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
+  pthread_mutex_unlock(&S->kmu);
+  pthread_mutex_unlock(&g_server_mu);
+  if (prev >= 0)
+    (void) hipSetDevice(prev);
+  return e == hipSuccess ? 0 : hip_err(e, "flush server relaunch");
 }
 
 /* ---------------------------------------------------------------------- */
@@ -2729,13 +2863,13 @@ static int server_settle(struct tasx_ctx *c)
   int gone = 0;
   for (uint32_t k = 1; c->sv_done_pos != c->sv_pos; k++) {
     server_reap(c);
-    if ((k & 4095u) == 0 && hipStreamQuery(S->st) != hipErrorNotReady) {
+    if ((k & 4095u) == 0 && server_gone(S)) {
       server_reap(c);
       gone = c->sv_done_pos != c->sv_pos;
       break;
     }
   }
-  if (!gone && (S->aborted || hipStreamQuery(S->st) != hipErrorNotReady))
+  if (!gone && server_gone(S))
     gone = 1; /* idle, but nothing will serve this ring again */
   if (gone) {
     const uint32_t *done = srv_dline(S, id);

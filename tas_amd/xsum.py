@@ -99,6 +99,8 @@ SIGNATURES = {
     "tasx_take_unfinished": (_c_int, [_uns, _vp, _c_u32]),
     "tasx_take_unfinished_segs": (_c_int, [_uns, _vp, _c_u32]),
     "tasx_server_abort": (_c_int, [_c_int]),
+    "tasx_server_pause": (_c_int, [_c_int]),
+    "tasx_server_resume": (_c_int, [_c_int]),
     "tasx_set_kernel_variant": (_c_int, [_c_int]),
     "tasx_last_kernel": (ctypes.c_char_p, []),
     "tasx_host_alloc": (_vp, [_sz]),
@@ -551,6 +553,17 @@ def take_unfinished_segs(ctx_id: int, chunk: int = 64):
 def server_abort(device: int = 0) -> None:
     """Stop the flush server's kernel with contexts still attached (ABI 8)."""
     _check(lib().tasx_server_abort(device), "tasx_server_abort")
+
+
+def server_pause(device: int = 0) -> None:
+    """Let HIP frees through without stopping the flush server (ABI 9): its
+    kernel leaves at its rings' positions; contexts stay attached."""
+    _check(lib().tasx_server_pause(device), "tasx_server_pause")
+
+
+def server_resume(device: int = 0) -> None:
+    """Launch a paused flush server's kernel again at its rings' positions."""
+    _check(lib().tasx_server_resume(device), "tasx_server_resume")
 
 
 def server_flushes(ctx_id: int) -> int:

@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 8
+    assert L.tasx_abi_version() == 9
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -108,6 +108,11 @@ def test_abi_version_and_errors_without_gpu(L):
     assert L.tasx_take_unfinished_segs(3, None, 0) == -errno.EINVAL
     assert L.tasx_server_abort(0) == -errno.EINVAL
     assert L.tasx_server_abort(-1) == -errno.ENODEV
+    # ABI 9: pause / resume of a server that does not run
+    assert L.tasx_server_pause(0) == -errno.EINVAL
+    assert L.tasx_server_resume(0) == -errno.EINVAL
+    assert L.tasx_server_pause(-1) == -errno.ENODEV
+    assert L.tasx_server_resume(1 << 20) == -errno.ENODEV
     if L.tasx_device_count() <= 0:  # no GPU in this container: start fails, nothing launched
         assert L.tasx_server_start(0) in (-errno.EIO, -errno.ENODEV)
 

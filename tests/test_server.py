@@ -841,16 +841,31 @@ def test_take_unfinished_without_a_failure(oracle):
 STRESS_SEEDS = list(range(int(__import__("os").environ.get("TASX_STRESS_SEEDS", "1"))))
 
 
+def _pause_now(rng, drained: bool, submit):
+    """ABI 9 in a random walk: pause the server (with batches in flight unless
+    `drained`), and when drained hand it 1-3 batches while paused (their
+    tickets stay open until the resume), then resume."""
+    xsum.server_pause(0)
+    if drained:
+        for _ in range(int(rng.integers(1, 4))):
+            submit()
+    xsum.server_resume(0)
+
+
+@pytest.mark.parametrize("pauses", [False, True])
 @pytest.mark.parametrize("seed", STRESS_SEEDS)
-def test_server_random_flushes(oracle, seed):
+def test_server_random_flushes(oracle, seed, pauses):
     """A seeded random walk over the server's contract: 1,500 flushes of 1 to
     130 frames (batches over 64 frames take several slots), up to 1-8 in
     flight (the depth changing as it goes), mbufs refilled with new frames as
     soon as their flush completed (the lines an earlier batch read must never
     be served again), a few frames the server does not take (their batches go
     through the context itself), submit or synchronous flush at random; every
-    frame of every flush checked against the oracle when its ticket completes."""
-    rng = np.random.default_rng(0x5EED + seed)
+    frame of every flush checked against the oracle when its ticket completes.
+    With `pauses` (ABI 9) the server is paused and resumed about every 50
+    flushes, with batches in flight or with new ones handed over while it is
+    paused."""
+    rng = np.random.default_rng(0x5EED + seed + (1000 if pauses else 0))
     nt, nmb = 1024, 600
     tmpl, _ = _frames(nt, 4242, short=True)              # templates: data segments, ACKs, a few short
     tmpl_arr = tmpl.array[:nt * 2048].copy()
@@ -879,19 +894,38 @@ def test_server_random_flushes(oracle, seed):
                 free.append(m)
             checked += len(items)
 
-        for f in range(1500):
-            if f % 100 == 0:
-                depth = int(rng.integers(1, 9))
-            n = int(rng.integers(1, 33)) if rng.random() < 0.9 else int(rng.integers(33, 131))
-            while len(out) >= depth or len(free) < n:
-                complete_oldest()
+        # templates the server takes (a batch holding a short frame goes through
+        # the context after the server's tickets: while paused it would wait)
+        takes = np.array([k for k in range(nt) if k < 5 or (k - 5) % 97 != 0])
+
+        def record(n, pool=None):
             pick = [free.pop(int(rng.integers(0, len(free)))) for _ in range(n)]
             items = []
             for m in pick:
-                k = int(rng.integers(0, nt))
+                k = int(rng.integers(0, nt)) if pool is None else int(pool[rng.integers(0, len(pool))])
                 mb[m] = tv[k]
                 xsum.tcp_checksums(13, pin.addr + m * 2048)
                 items.append((m, k))
+            return items
+
+        def submit_small():  # one slot's worth, while paused: never waits for a free slot
+            items = record(int(rng.integers(1, 65)), takes)
+            out.append((xsum.flush_submit(13), items))
+
+        npause = 0
+        for f in range(1500):
+            if f % 100 == 0:
+                depth = int(rng.integers(1, 9))
+            if pauses and (rng.random() < 0.02 or f % 100 == 50):
+                drained = rng.random() < 0.5
+                while drained and out:
+                    complete_oldest()
+                _pause_now(rng, drained, submit_small)
+                npause += 1
+            n = int(rng.integers(1, 33)) if rng.random() < 0.9 else int(rng.integers(33, 131))
+            while len(out) >= depth or len(free) < n:
+                complete_oldest()
+            items = record(n)
             if rng.random() < 0.1:                       # a synchronous tx_flush now and then
                 while out:
                     complete_oldest()
@@ -906,19 +940,23 @@ def test_server_random_flushes(oracle, seed):
             complete_oldest()
         assert checked > 30000
         assert xsum.server_flushes(13) > 1000            # batches with a short frame go through the context
+        assert npause > 10 if pauses else npause == 0
         xsum.use_server(13, False)
         xsum.server_stop(0)
     finally:
         cx.close()
 
 
+@pytest.mark.parametrize("pauses", [False, True])
 @pytest.mark.parametrize("seed", STRESS_SEEDS)
-def test_server_tx_segments_random_groups(oracle, seed):
+def test_server_tx_segments_random_groups(oracle, seed, pauses):
     """TX segment slots under a seeded random walk: 4,096 segments of 64 flows
     (odd buffer bases and lengths, payloads of 0-1448 B, circular-buffer
     wraps) handed over in groups of 1-90 (groups over 41 take several slots)
     with 1-8 flushes in flight; every frame equals the oracle's flow_tx_read +
-    tcp_checksums."""
+    tcp_checksums.  With `pauses` (ABI 9) the server is paused and resumed
+    every ~12 groups, with groups in flight or with new ones (of one slot)
+    handed over while it is paused."""
     rng = np.random.default_rng(0x7E57 + seed)
     n = 4096
     pay = rng.integers(0, pktgen.TCP_MSS + 1, n)
@@ -939,10 +977,28 @@ def test_server_tx_segments_random_groups(oracle, seed):
         xsum.register_frames(15, hf.addr, hf.nbytes)
         xsum.register_shm(15, hs.addr, sl)
         xsum.use_server(15)
-        out, i, depth = [], 0, 4
+        out, i, depth, npause, since = [], 0, 4, 0, 0
+
+        def submit_small():  # one slot, while paused
+            nonlocal i
+            if i < n:
+                g = min(int(rng.integers(1, 42)), n - i)
+                out.append(xsum.server_tx_segments(15, segs[i:i + g]))
+                i += g
+
         while i < n:
             if rng.random() < 0.05:
                 depth = int(rng.integers(1, 9))
+            since += 1
+            if pauses and (rng.random() < 0.08 or since >= 15):
+                since = 0
+                drained = rng.random() < 0.5
+                while drained and out:
+                    xsum.flush_wait(15, out.pop(0))
+                _pause_now(rng, drained, submit_small)
+                npause += 1
+                if i >= n:
+                    break
             g = min(int(rng.integers(1, 91)), n - i)
             while len(out) >= depth:
                 xsum.flush_wait(15, out.pop(0))
@@ -951,7 +1007,79 @@ def test_server_tx_segments_random_groups(oracle, seed):
         for t in out:
             xsum.flush_wait(15, t)
         np.testing.assert_array_equal(hf.array[:fr.size], exp_fr)
+        assert npause >= 3 if pauses else npause == 0
         xsum.use_server(15, False)
         xsum.server_stop(0)
     finally:
         cx.close()
+
+
+def test_server_pause_lets_frees_through(oracle):
+    """ABI 9: HIP's frees wait for every kernel of the device, the server's
+    too (profiles/r05 r05free: hipFree, hipHostFree, hipHostUnregister and
+    torch.cuda.empty_cache each waited for the stop).  Paused, the server lets
+    them through with its context still attached: a torch empty_cache returns
+    at once, libtasx's own frees work instead of -EBUSY, batches handed over
+    meanwhile stay "not done", and after the resume they and later batches
+    come out bit-exact; pause/resume refuse what they cannot do."""
+    n, nb = 32, 6
+    xsum.server_start(0)
+    cx = _Ctxs([9])
+    try:
+        pin, frames = _frames(nb * n, 1900, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nb * n)
+        xsum.register_frames(9, pin.addr, pin.nbytes)
+        xsum.use_server(9)
+        extra = xsum.PinnedBuffer(1 << 20)
+        for i in range(n):                               # a batch before the pause
+            xsum.tcp_checksums(9, pin.addr + i * 2048)
+        xsum.tx_flush(9)
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.server_resume(0)                        # not paused
+        assert e.value.code == -errno.EINVAL
+        extra.free()
+        assert extra.addr != 0                           # refused (-EBUSY) while the kernel runs
+        xsum.server_pause(0)
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.server_pause(0)
+        assert e.value.code == -errno.EALREADY
+        x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+        x.fill_(1)
+        torch.cuda.synchronize()
+        del x
+        t0 = time.perf_counter()
+        torch.cuda.empty_cache()                         # hipFree: does not wait for the paused server
+        assert time.perf_counter() - t0 < 0.5
+        extra.free()
+        assert extra.addr == 0                           # libtasx's own free works while paused
+        tickets = []
+        for b in range(1, 4):                            # handed over while paused
+            for i in range(n):
+                xsum.tcp_checksums(9, pin.addr + (b * n + i) * 2048)
+            tickets.append(xsum.flush_submit(9))
+        time.sleep(0.05)
+        assert not any(xsum.flush_poll(9, t) for t in tickets)
+        assert not np.array_equal(pin.array[n * 2048:4 * n * 2048], ref[n * 2048:4 * n * 2048])
+        xsum.server_resume(0)
+        xsum.flush_wait(9, tickets[-1])
+        np.testing.assert_array_equal(pin.array[:4 * n * 2048], ref[:4 * n * 2048])
+        for b in range(4, nb):                           # and on as before
+            for i in range(n):
+                xsum.tcp_checksums(9, pin.addr + (b * n + i) * 2048)
+            xsum.tx_flush(9)
+        np.testing.assert_array_equal(pin.array[:ref.size], ref)
+        xsum.server_pause(0)                             # a paused server stops once detached
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.server_stop(0)                          # contexts attached
+        assert e.value.code == -errno.EBUSY
+        xsum.server_resume(0)
+        xsum.use_server(9, False)
+        xsum.server_pause(0)
+        xsum.server_stop(0)
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.server_pause(0)                         # not running
+        assert e.value.code == -errno.EINVAL
+    finally:
+        cx.close()
+        _stop_if_running()
