@@ -22,6 +22,7 @@
  *
  *   usage: boundary_test tests/golden/ref_frames.bin
  */
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -187,13 +188,30 @@ int main(int argc, char **argv)
     return 1;
   }
 
-  /* a failed flush: the flush server's kernel aborted while the context is
-   * attached, then a batch recorded and flushed.  tx_flush_checksums sees the
-   * error and finishes every frame on the CPU; TAS keeps running. */
+  /* the flush server (ABI 6), and a pause (ABI 9): HIP frees wait for the
+   * running kernel, so libtasx refuses its own (-EBUSY); paused, with the
+   * context still attached, they go through, and the resumed kernel takes the
+   * next flush */
   if (tasx_server_start(0) != 0 || tasx_ctx_use_server(TASX_CTX_SELF, 1) != 0) {
     fprintf(stderr, "server: %s\n", tasx_last_error());
     return 1;
   }
+  {
+    uint32_t sf0 = 0, sf1 = 0;
+    void *scratch = tasx_host_alloc(1u << 20);
+    CHECK(scratch != NULL, "tasx_host_alloc: %s", tasx_last_error());
+    CHECK(tasx_host_free(scratch) == -EBUSY, "a free went through beside the running server");
+    CHECK(tasx_server_pause(0) == 0, "server pause: %s", tasx_last_error());
+    CHECK(tasx_host_free(scratch) == 0, "free while paused: %s", tasx_last_error());
+    CHECK(tasx_server_resume(0) == 0, "server resume: %s", tasx_last_error());
+    tasx_ctx_server_flushes(TASX_CTX_SELF, &sf0);
+    run_batch("server-after-resume", pm, frames, r, 0, n, room);
+    tasx_ctx_server_flushes(TASX_CTX_SELF, &sf1);
+    CHECK(sf1 == sf0 + 1, "the flush after the resume did not go through the server (%u -> %u)", sf0, sf1);
+  }
+  /* a failed flush: the flush server's kernel aborted while the context is
+   * attached, then a batch recorded and flushed.  tx_flush_checksums sees the
+   * error and finishes every frame on the CPU; TAS keeps running. */
   CHECK(tasx_server_abort(0) == 0, "server abort: %s", tasx_last_error());
   unsigned recovered = 0;
   {
