@@ -1083,3 +1083,42 @@ def test_server_pause_lets_frees_through(oracle):
     finally:
         cx.close()
         _stop_if_running()
+
+
+def test_server_abort_while_paused_hands_back(oracle):
+    """ABI 8 across ABI 9: batches handed to a paused server that is then
+    aborted (never resumed) come back through tasx_take_unfinished, and
+    finished on the CPU every frame equals the oracle's; the batch finished
+    before the pause is not handed back; a resume after the abort is refused."""
+    n, nb = 32, 4
+    xsum.server_start(0)
+    cx = _Ctxs([10])
+    try:
+        pin, frames = _frames(nb * n, 2100, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, nb * n)
+        xsum.register_frames(10, pin.addr, pin.nbytes)
+        xsum.use_server(10)
+        for i in range(n):
+            xsum.tcp_checksums(10, pin.addr + i * 2048)
+        xsum.tx_flush(10)
+        xsum.server_pause(0)
+        for b in range(1, nb):
+            for i in range(n):
+                xsum.tcp_checksums(10, pin.addr + (b * n + i) * 2048)
+            xsum.flush_submit(10)
+        assert not xsum.flush_poll(10, nb)
+        xsum.server_abort(0)
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.server_resume(0)
+        assert e.value.code == -errno.EIO
+        with pytest.raises(xsum.TasxError):
+            xsum.flush_wait(10, nb)
+        back = xsum.take_unfinished(10)
+        offs = _finish_on_cpu(oracle, pin, back)
+        assert sorted(offs.tolist()) == [k * 2048 for k in range(n, nb * n)]
+        np.testing.assert_array_equal(pin.array[:ref.size], ref)
+        xsum.server_stop(0)                              # detached by the settle
+    finally:
+        cx.close()
+        _stop_if_running()
