@@ -442,7 +442,8 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     until a pause:
  *   tasx_server_pause(device): the kernel leaves at its rings' current
  *     positions (a batch being summed is finished first; at most 5 s, else
- *     -EIO and the server runs on); contexts stay attached, submit as before
+ *     -EIO: the stop word stays, so a kernel that leaves later is seen gone
+ *     by the contexts, tasx_take_unfinished); contexts stay attached, submit as before
  *     (the slots wait in the rings; a full ring waits inside the call) and
  *     poll "not done"; frees do not wait, and the four calls above work.
  *     -EALREADY when paused already, -EIO after an abort or a kernel exit.

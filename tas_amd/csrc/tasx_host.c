@@ -2724,7 +2724,9 @@ int tasx_server_pause(int device)
     nanosleep(&ts, NULL);
   if (e != hipSuccess) {
     /* still running after the bound, or failed: not paused; the keepalive
-     * thread watches the kernel again and the contexts see what it does */
+     * thread watches the kernel again and the contexts see what it does.  The
+     * stop word stays: cleared, workgroups that had already left would leave
+     * their rings unserved beside a kernel that still runs */
     pthread_mutex_lock(&S->kmu);
     if (e != hipErrorNotReady)
       __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
