@@ -1301,9 +1301,9 @@ def server_cost_child_leg(rot: int) -> dict:
         env.pop(k, None)
     cmd = [sys.executable, "-u", str(ROOT / "bench.py"), "--server-cost-child", "--rotate", str(rot)]
     try:
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     except subprocess.TimeoutExpired:
-        return {"error": "server_cost child: no answer within 400 s"}
+        return {"error": "server_cost child: no answer within 240 s"}
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if r.returncode != 0 or not lines:
         return {"error": f"server_cost child rc={r.returncode}: {r.stderr[-400:]}"}
