@@ -2048,9 +2048,13 @@ struct fserver {
    * hipStreamQuery per poll from 8 cores serialised in the runtime's locks and
    * stalled the process's other HIP work, profiles/r05 r05o) */
   int launched, kstate;
-  /* launched and kstate change together under kmu (the keepalive thread's
-   * query and a pause or resume never interleave) */
+  /* launched, kstate and kgen change together under kmu; the keepalive
+   * thread queries the stream outside it (a query can wait on the runtime's
+   * locks, e.g. behind a hipFree that waits for this very kernel, and a pause
+   * must still get to write the stop word) and keeps its answer only when no
+   * pause or resume (kgen) came in between */
   pthread_mutex_t kmu;
+  uint32_t kgen;
   /* tasx_server_pause: the kernel has left at its rings' positions and
    * tasx_server_resume launches it again from them (prm.resume); set before
    * the stop word is written and cleared after the new launch, so that a
@@ -2123,12 +2127,18 @@ static void *server_keepalive(void *arg)
   while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(lease, k++, __ATOMIC_RELEASE);
     pthread_mutex_lock(&S->kmu);
-    if (__atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0) {
-      const hipError_t e = hipStreamQuery(S->st);
-      if (e != hipErrorNotReady)
-        __atomic_store_n(&S->kstate, e == hipSuccess ? 1 : -(int) e, __ATOMIC_RELEASE);
-    }
+    const uint32_t gen = S->kgen;
+    const int watch = __atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0;
     pthread_mutex_unlock(&S->kmu);
+    if (watch) {
+      const hipError_t e = hipStreamQuery(S->st);
+      if (e != hipErrorNotReady) {
+        pthread_mutex_lock(&S->kmu);
+        if (S->kgen == gen && __atomic_load_n(&S->launched, __ATOMIC_ACQUIRE))
+          __atomic_store_n(&S->kstate, e == hipSuccess ? 1 : -(int) e, __ATOMIC_RELEASE);
+        pthread_mutex_unlock(&S->kmu);
+      }
+    }
     nanosleep(&ts, NULL);
   }
   return NULL;
@@ -2710,6 +2720,7 @@ int tasx_server_pause(int device)
   if (st == 0) {
     __atomic_store_n(&S->paused, 1, __ATOMIC_RELEASE);
     __atomic_store_n(&S->launched, 0, __ATOMIC_RELEASE); /* the keepalive thread stops asking */
+    S->kgen++;                                           /* and drops an answer it is getting now */
   }
   pthread_mutex_unlock(&S->kmu);
   if (st != 0) {
@@ -2732,6 +2743,7 @@ int tasx_server_pause(int device)
       __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
     __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
     __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
+    S->kgen++;
     pthread_mutex_unlock(&S->kmu);
     pthread_mutex_unlock(&g_server_mu);
     return e == hipErrorNotReady
@@ -2775,6 +2787,7 @@ int tasx_server_resume(int device)
   __atomic_store_n(&S->kstate, e == hipSuccess ? 0 : -(int) e, __ATOMIC_RELEASE);
   __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
   __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
+  S->kgen++;
   pthread_mutex_unlock(&S->kmu);
   pthread_mutex_unlock(&g_server_mu);
   if (prev >= 0)

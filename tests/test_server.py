@@ -1122,3 +1122,56 @@ def test_server_abort_while_paused_hands_back(oracle):
     finally:
         cx.close()
         _stop_if_running()
+
+
+def test_server_pause_unblocks_a_waiting_free(oracle):
+    """A free already waiting for the running server (torch.cuda.empty_cache
+    in another thread) is released by a pause: the pause writes the stop word
+    without waiting on anything the blocked free holds (the keepalive thread
+    asks the runtime outside the server's state lock), returns well inside
+    the 2 s lease, and the resumed server flushes as before."""
+    n = 32
+    # (made before the server starts: a device-wide synchronize waits for its kernel too)
+    x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    x.fill_(1)
+    torch.cuda.synchronize()
+    xsum.server_start(0)
+    cx = _Ctxs([11])
+    try:
+        pin, frames = _frames(2 * n, 2300, short=False)
+        cx.pins.append(pin)
+        ref = _ref(oracle, frames, 2 * n)
+        xsum.register_frames(11, pin.addr, pin.nbytes)
+        xsum.use_server(11)
+        for i in range(n):
+            xsum.tcp_checksums(11, pin.addr + i * 2048)
+        xsum.tx_flush(11)
+        del x                                            # back to torch's cache: empty_cache frees it
+        took = {}
+
+        def freer():
+            t = time.perf_counter()
+            torch.cuda.empty_cache()
+            took["s"] = time.perf_counter() - t
+
+        th = threading.Thread(target=freer)
+        th.start()
+        time.sleep(0.3)
+        assert th.is_alive()                             # the free waits for the running kernel
+        t0 = time.perf_counter()
+        xsum.server_pause(0)
+        tp = time.perf_counter() - t0
+        th.join(5.0)
+        assert not th.is_alive() and took["s"] < 1.5
+        assert tp < 1.0
+        xsum.server_resume(0)
+        for i in range(n):
+            xsum.tcp_checksums(11, pin.addr + (n + i) * 2048)
+        xsum.tx_flush(11)
+        np.testing.assert_array_equal(pin.array[:ref.size], ref)
+        assert xsum.server_flushes(11) == 2
+        xsum.use_server(11, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        _stop_if_running()
