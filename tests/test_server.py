@@ -1131,7 +1131,11 @@ def test_server_pause_unblocks_a_waiting_free(oracle):
     asks the runtime outside the server's state lock), returns well inside
     the 2 s lease, and the resumed server flushes as before."""
     n = 32
-    # (made before the server starts: a device-wide synchronize waits for its kernel too)
+    # (made before the server starts: a device-wide synchronize waits for its
+    # kernel too; torch's cache emptied first, so that x has a segment of its
+    # own and the empty_cache below has it to free)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
     x.fill_(1)
     torch.cuda.synchronize()
