@@ -87,6 +87,7 @@ def parse(argv=None):
     ap.add_argument("--no-raw", action="store_true")
     ap.add_argument("--no-txseg", action="store_true")
     ap.add_argument("--no-flow", action="store_true")
+    ap.add_argument("--no-config4", action="store_true", help="skip the BASELINE config 4 leg of the default line")
     ap.add_argument("--no-flushmix", action="store_true")
     ap.add_argument("--no-contexts", action="store_true", help="skip the two-context (two-stream) leg")
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
@@ -1744,6 +1745,34 @@ def rx_pass_leg(fw: FlowLookupWorkload, rot: int, args, ws: int, rank: int) -> d
     return r
 
 
+def config4_leg(args, ws: int, rank: int, info: dict) -> dict:
+    """BASELINE config 4 inside the default line: the
+    8,388,608 x 1500 B batch split over the ranks -- all of it on one GPU at
+    N = 1 (12.6 GB a step), 1,048,576 packets per GPU at N = 8 -- through the
+    same raw_sad_kernel<s32> call as `--workload shard8m`, with its live read
+    ceiling and (N = 1) its PMC traffic.  Parity: the whole batch on one GPU
+    through this call, tests/test_bench_configs.py::test_bench_config4_whole_on_one_gpu."""
+    wl = shard8m_workload(ws, rank)
+    r = leg(wl.loop(), wl.bytes_per_step, args, ws,
+            f"BASELINE config 4: 8,388,608 x 1500 B payloads split over {ws} GPU(s), {wl.n} packets on this "
+            "rank, rte_raw_cksum per packet, one launch a step", "raw_sad_kernel<s32>")
+    rehearse = bool(info.get("rehearse"))
+    r["packets_per_rank"] = [int(v) for v in gather_over_ranks(float(wl.n), ws)]
+    r["frac_of_n_hbm"] = None if rehearse else round(r["value"] * GIB / 1e9 / (ws * HBM_PEAK_GBS), 4)
+    r["parity"] = "tests/test_bench_configs.py::test_bench_config4_whole_on_one_gpu"
+    if rank == 0 and not rehearse:
+        torch.cuda.synchronize()
+        r["roofline"]["read_ceiling"] = read_ceiling(wl, r["roofline"]["launch_avg_us"], launches=40)
+    del wl
+    torch.cuda.empty_cache()
+    if rank == 0 and ws == 1 and not args.no_pmc:
+        p = pmc_leg("shard8m", "raw_sad_kernel", 4)
+        if p and "hbm_bytes_per_launch" in p:
+            r["roofline"]["traffic"] = int(p["hbm_bytes_per_launch"])
+        r["pmc"] = p
+    return r
+
+
 def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
     rot = max(1, args.rotate)
     wl = Tcp4Workload(rot, pktgen.SEED + rank)
@@ -1861,6 +1890,10 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
         del fw
         torch.cuda.empty_cache()
 
+    config4 = None
+    if not args.no_config4:
+        config4 = config4_leg(args, ws, rank, info)
+
     extra = {}
     if not args.no_server_cost and rank == 0 and ws == 1:
         extra["server_cost"] = server_cost_child_leg(rot)
@@ -1940,6 +1973,8 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
             line["flow_lookup"] = flow
         if rx_pass is not None:
             line["rx_pass"] = rx_pass
+        if config4 is not None:
+            line["config4"] = config4
         if "server_cost" in extra:
             line["server_cost"] = extra["server_cost"]
         if "e2e" in extra:

@@ -158,10 +158,7 @@ extern "C" TASX_INTERNAL int ab_launch_txseg(const tasx_txseg_params *p0, void *
   // 42 / 43: the access pattern alone (40) at 8 / 6 waves per SIMD (the pattern uses no LDS)
   case 42: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern,wpe8>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 8, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 43: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern,wpe6>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 6, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
-  case 41: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<b128>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 16>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 40: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<pattern>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 8>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
-  // 44 (round 4): the source chunks by LDS-DMA (the slice's LDS already caps residency at 6 waves per SIMD)
-  case 44: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<ldsdma>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 32>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   case 39: if (tas) { tasx_note_kernel("tx_segment_lds_kernel<nt_first>"); hipLaunchKernelGGL((tx_segment_lds_kernel<true, 6, 1, 4>), grid, block, 0, s, *p); return hipGetLastError() == hipSuccess ? 0 : -1; } break;
   // 35-38: the product with residency capped by dynamic LDS at 5 / 4 / 3 / 2 blocks per CU
   case 35: case 36: case 37: case 38: if (tas) {

@@ -180,6 +180,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     const bool seg = (h0 & TASX_SRV_SEG) != 0u;
     const uint32_t n = (uint32_t) (h0 & 0x7fffu), words = seg ? TASX_SRV_SEGW0 + 3u * n : n;
     const bool hdr = (h0 >> 48) == tag && (h1 >> 48) == tag && n >= 1u && n <= (seg ? TASX_SRV_SEGS : TASX_SRV_FB);
+    // the stop word first (a pause, a stop, an abort): a slot ready in this
+    // very read is left in the ring, and posw records it for a resumed launch
+    // (taking it first, a workgroup whose ring never runs empty would never
+    // see the stop word: ADVICE r05)
+    if ((uint32_t) c != 0u)
+      return 3;
     // a header-only read never takes the slot: unread entries (0) would match
     // the tag of every position p with p + 1 = 0 mod 2^16
     if (hdr && entries && __builtin_amdgcn_ballot_w64((uint32_t) lane < words && (v.e >> 48) != tag) == 0ull) {
@@ -218,8 +224,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     if constexpr (DIAG)
       if (lane == 0)
         s_d[4]++;
-    if ((uint32_t) c != 0u)
-      return 3;
     if ((uint32_t) (c >> 32) != lease) {
       lease = (uint32_t) (c >> 32);
       t_lease = now;

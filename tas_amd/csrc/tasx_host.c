@@ -530,6 +530,16 @@ static int pin_acquire(uint8_t *base, size_t bytes, void **dev, int *owned)
       pthread_mutex_unlock(&g_pins_mu);
       return rc;
     }
+    if (q->refs && base < q->base + q->bytes && base + bytes > q->base) {
+      /* overlapping a pin of this library without lying inside it: HIP would
+       * map the part inside the pin alone (hipHostGetDevicePointer succeeds
+       * for its start), and the pin's release would unmap it under this
+       * context */
+      pthread_mutex_unlock(&g_pins_mu);
+      return set_err(-EINVAL, "host range [%p, +%zu) overlaps a region pinned by another context ([%p, +%zu)) "
+                     "without lying inside it: register the larger region first", (void *) base, bytes,
+                     (void *) q->base, q->bytes);
+    }
   }
   if (hipHostGetDevicePointer(dev, base, 0) == hipSuccess) {
     pthread_mutex_unlock(&g_pins_mu);
@@ -687,7 +697,8 @@ int tasx_ctx_init(unsigned ctx_id, int device, size_t max_batch_bytes)
 
 static int flush_wait(struct tasx_ctx *c, uint32_t ticket);
 static int server_defer_release(struct tasx_ctx *c);
-static int server_blocks_free(const char *what);
+static int free_guard_enter(const char *what);
+static void free_guard_exit(void);
 
 int tasx_ctx_destroy(unsigned ctx_id)
 {
@@ -1913,7 +1924,7 @@ int tasx_feeder_stop(int device)
     pthread_mutex_unlock(&g_feeder_mu);
     return set_err(-EBUSY, "feeder for device %d still serves contexts", device);
   }
-  int rc = server_blocks_free("tasx_feeder_stop");
+  int rc = free_guard_enter("tasx_feeder_stop");
   if (rc) {
     pthread_mutex_unlock(&g_feeder_mu);
     return rc;
@@ -1925,6 +1936,7 @@ int tasx_feeder_stop(int device)
   hipSetDevice(device);
   hipStreamSynchronize(F->st);
   feeder_free(F);
+  free_guard_exit();
   pthread_mutex_unlock(&g_feeder_mu);
   return failed ? set_err(-EIO, "the feeder thread for device %d had failed", device) : 0;
 }
@@ -2041,7 +2053,8 @@ struct fserver {
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
-  int aborted;                     /* tasx_server_abort stopped the kernel (and the keepalive thread) */
+  int aborted; /* tasx_server_abort stopped the kernel (and the keepalive thread); read and written atomically:
+                * context threads read it (server_gone) outside g_server_mu */
   /* the kernel's state as the keepalive thread last saw it (hipStreamQuery
    * every 10 ms once launched): 0 running, 1 exited, < 0 -hipError_t.  The
    * fast-path cores read this word: their polls make no HIP call (a
@@ -2076,19 +2089,28 @@ static int unf_seg(struct tasx_ctx *c, const tasx_tx_seg *g);
 
 /* HIP's frees wait for every stream of the device, the server's kernel too:
  * refused (-EBUSY) while any server's kernel runs (a paused one does not),
- * instead of waiting for its stop */
-static int server_blocks_free(const char *what)
+ * instead of waiting for its stop.  On success g_server_mu stays held until
+ * free_guard_exit(), across the free itself: a resume (which takes the same
+ * lock to relaunch the kernel) cannot slip in between the check and the free
+ * and leave the free waiting for the relaunched kernel. */
+static int free_guard_enter(const char *what)
 {
   int d, any = 0;
   pthread_mutex_lock(&g_server_mu);
   for (d = 0; d < MAX_DEVICES; d++)
     any |= g_server[d] != NULL && !__atomic_load_n(&g_server[d]->paused, __ATOMIC_ACQUIRE);
+  if (!any)
+    return 0;
   pthread_mutex_unlock(&g_server_mu);
-  return any ? set_err(-EBUSY,
-                       "%s: a flush server is running (HIP frees wait for its kernel; tasx_server_pause or "
-                       "tasx_server_stop first)",
-                       what)
-             : 0;
+  return set_err(-EBUSY,
+                 "%s: a flush server is running (HIP frees wait for its kernel; tasx_server_pause or "
+                 "tasx_server_stop first)",
+                 what);
+}
+
+static void free_guard_exit(void)
+{
+  pthread_mutex_unlock(&g_server_mu);
 }
 
 /* tasx_ctx_destroy with a server running on the context's device: the
@@ -2172,7 +2194,7 @@ static void server_free(struct fserver *S)
  * its kernel leaves) */
 static int server_gone(struct fserver *S)
 {
-  if (S->aborted)
+  if (__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE))
     return 1;
   if (__atomic_load_n(&S->paused, __ATOMIC_ACQUIRE))
     return 0;
@@ -2517,7 +2539,7 @@ int tasx_server_stop(int device)
     return set_err(-EBUSY, "flush server for device %d still serves contexts", device);
   }
   __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
-  if (!S->aborted) {
+  if (!__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
     pthread_join(S->keep, NULL);
   }
@@ -2675,10 +2697,10 @@ int tasx_server_abort(int device)
     return set_err(-EINVAL, "no flush server running for device %d", device);
   }
   __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
-  if (!S->aborted) {
+  if (!__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE)) {
     __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
     pthread_join(S->keep, NULL);
-    S->aborted = 1;
+    __atomic_store_n(&S->aborted, 1, __ATOMIC_RELEASE);
   }
   hipError_t e = hipErrorNotReady;
   const struct timespec ts = {0, 100 * 1000};
@@ -2707,7 +2729,7 @@ int tasx_server_pause(int device)
   int rc = 0;
   if (!S)
     rc = set_err(-EINVAL, "no flush server running for device %d", device);
-  else if (S->aborted)
+  else if (__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE))
     rc = set_err(-EIO, "the flush server for device %d was aborted", device);
   else if (S->paused)
     rc = set_err(-EALREADY, "the flush server for device %d is paused already", device);
@@ -2765,7 +2787,7 @@ int tasx_server_resume(int device)
     rc = set_err(-EINVAL, "no flush server running for device %d", device);
   else if (!S->paused)
     rc = set_err(-EINVAL, "the flush server for device %d is not paused", device);
-  else if (S->aborted)
+  else if (__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE))
     rc = set_err(-EIO, "the flush server for device %d was aborted", device);
   if (rc) {
     pthread_mutex_unlock(&g_server_mu);
@@ -3039,11 +3061,12 @@ void *tasx_host_alloc(size_t bytes)
 
 int tasx_host_free(void *p)
 {
-  int rc = server_blocks_free("tasx_host_free");
+  int rc = free_guard_enter("tasx_host_free");
   if (rc)
     return rc;
-  HIPCHK(hipHostFree(p));
-  return 0;
+  const hipError_t e = hipHostFree(p);
+  free_guard_exit();
+  return e == hipSuccess ? 0 : hip_err(e, "hipHostFree");
 }
 
 void *tasx_host_device_pointer(void *p)
@@ -3065,11 +3088,12 @@ int tasx_host_register(void *p, size_t bytes)
 
 int tasx_host_unregister(void *p)
 {
-  int rc = server_blocks_free("tasx_host_unregister");
+  int rc = free_guard_enter("tasx_host_unregister");
   if (rc)
     return rc;
-  HIPCHK(hipHostUnregister(p));
-  return 0;
+  const hipError_t e = hipHostUnregister(p);
+  free_guard_exit();
+  return e == hipSuccess ? 0 : hip_err(e, "hipHostUnregister");
 }
 
 void *tasx_dev_alloc(int device, size_t bytes)
@@ -3087,11 +3111,12 @@ void *tasx_dev_alloc(int device, size_t bytes)
 
 int tasx_dev_free(void *p)
 {
-  int rc = server_blocks_free("tasx_dev_free");
+  int rc = free_guard_enter("tasx_dev_free");
   if (rc)
     return rc;
-  HIPCHK(hipFree(p));
-  return 0;
+  const hipError_t e = hipFree(p);
+  free_guard_exit();
+  return e == hipSuccess ? 0 : hip_err(e, "hipFree");
 }
 
 int tasx_memcpy_h2d(void *dst, const void *src, size_t bytes)

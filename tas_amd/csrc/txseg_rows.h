@@ -644,41 +644,19 @@ __device__ __forceinline__ u32x4 lds_window_at(const uint8_t *wp, uint32_t r)
 }
 
 // 16 bytes at LDS byte offset o of the slice: five dwords and a funnel shift
-// (B128: the first four by one ds_read_b128 at the dword-aligned address --
-// A/B only: it relies on the LDS running in unaligned mode)
-template <bool B128 = false>
 __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
 {
-  const uint32_t *w = (const uint32_t *) (sl + (o & ~3u));
-  const uint32_t r = o & 3u;
-  uint32_t w0, w1, w2, w3;
-  if constexpr (B128) {
-    const u32x4 q = *(const u32x4 *) w;
-    w0 = q.x, w1 = q.y, w2 = q.z, w3 = q.w;
-  } else {
-    w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
-  }
-  const uint32_t w4 = w[4];
-  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r), __builtin_amdgcn_alignbyte(w2, w1, r),
-               __builtin_amdgcn_alignbyte(w3, w2, r), __builtin_amdgcn_alignbyte(w4, w3, r)};
+  return lds_window_at(sl + (o & ~3u), o & 3u);
 }
 
-// OPT (A/B): 1 = no general-body fallback compiled in, 2 = wraps ignored
-// (piece A only) -- both timing only, results wrong -- 4 = the first block
-// stored non-temporal too (correct), 8 = the access pattern alone (timing
-// only: the aligned source chunks stored as loaded, no LDS realignment or
-// splice; bench.py's tx_segment pattern_ceiling), 16 = windows read back by
-// ds_read_b128 + ds_read_b32 (correct where the LDS runs in unaligned mode),
-// 32 = the source chunks land in the slice by LDS-DMA (global_load_lds_dwordx4,
-// round 4, VERDICT r03 item 4: no VGPR staging and no ds_write; one DMA per
-// row and slot, the row's lanes alone active, so that M0 -- per wave -- can
-// point at the row's own slice: the slice layout stays as it is)
-__device__ __forceinline__ void glds16_row(const void *gsrc, uint32_t lds_addr)
-{
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
-}
+// OPT (comparison forms of libtasx_ab.so): 1 = no general-body fallback
+// compiled in, 2 = wraps ignored (piece A only) -- both timing only, results
+// wrong -- 4 = the first block stored non-temporal too (correct), 8 = the
+// access pattern alone (timing only: the aligned source chunks stored as
+// loaded, no LDS realignment or splice; bench.py's tx_segment pattern_ceiling).
+// Round 6 deleted two forms: windows read back by ds_read_b128 at 4-byte
+// aligned LDS addresses, and the source chunks landed by LDS-DMA through
+// inline asm that moved M0 (profiles/r06/INDEX.md, r06a).
 template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
@@ -751,35 +729,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       const int nAB = max(nA + nB, 1);
       const uint32_t dB = nB > 0 ? cB - cA - 16u * (uint32_t) nA : 0u;
       u32x4 a[kLdsSlots];
-      if constexpr ((OPT & 32) != 0) { // A/B 44 (LDS-DMA staging, round 4: not taken)
-        // row q of the wave: its lanes alone write M0 + 256 q + 16 gl, so M0 =
-        // the row's slot address - 256 q puts chunk gl + 16u at slot 1 + gl + 16u
-        const uint32_t q = (threadIdx.x >> 4) & 3u;
-        const uint32_t slo = (uint32_t) (uintptr_t) (lds + (threadIdx.x / 16) * kLdsSlice + kLdsLead);
 #pragma unroll
-        for (int u = 0; u < kLdsSlots; ++u) {
-          const int v = min(gl + 16 * u, nAB - 1);
-          const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
-          const uint8_t *src = sbase + min(ro, hi_ok);
-#pragma unroll
-          for (uint32_t qq = 0; qq < 4u; ++qq)
-            if (q == qq)
-              glds16_row(src, __builtin_amdgcn_readfirstlane(slo + 256u * (uint32_t) u - 256u * qq));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMAs have landed in LDS
-      } else {
-#pragma unroll
-        for (int u = 0; u < kLdsSlots; ++u) {
-          const int v = min(gl + 16 * u, nAB - 1);
-          const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
-          a[u] = ld16_off(sbase, min(ro, hi_ok));
-        }
+      for (int u = 0; u < kLdsSlots; ++u) {
+        const int v = min(gl + 16 * u, nAB - 1);
+        const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
+        a[u] = ld16_off(sbase, min(ro, hi_ok));
       }
-      if constexpr ((OPT & 32) != 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else if constexpr (!(OPT & 8)) {
+      if constexpr (!(OPT & 8)) {
 #pragma unroll
         for (int u = 0; u < kLdsSlots; ++u)
           *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
@@ -798,7 +754,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       for (int u = 0; u < 6; ++u) {
         const int j0 = 16 * (16 * u + kh) - 66;
         const int o = min(o0 + 256 * u + (j0 >= wrapc ? dW : 0), kLdsSlice - 20);
-        w[u] = (OPT & 8) ? a[u] : lds_window<(OPT & 16) != 0>(sl, (uint32_t) o);
+        w[u] = (OPT & 8) ? a[u] : lds_window(sl, (uint32_t) o);
       }
       // the chunk holding the wrap (a row whose payload wraps off a chunk
       // boundary): its bytes from wrapc - j0 on are piece B's
@@ -809,7 +765,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         for (int u = 0; u < 6; ++u) {
           const int j0 = 16 * (16 * u + kh) - 66;
           if (strad && u == (ks >> 4))
-            w[u] = splice(w[u], lds_window<(OPT & 16) != 0>(sl, (uint32_t) min(max(oB + j0 - wrapc, 0), kLdsSlice - 20)),
+            w[u] = splice(w[u], lds_window(sl, (uint32_t) min(max(oB + j0 - wrapc, 0), kLdsSlice - 20)),
                           wrapc - j0, 16);
         }
       }

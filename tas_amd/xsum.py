@@ -319,12 +319,15 @@ FLOW_NONE = 0xFFFFFFFF
 def flow_lookup_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst: torch.Tensor, fs_num: int, *,
                       offsets: torch.Tensor | None = None, stride: int = 0, ip_off: int = TAS_IP_OFF,
                       l4_off: int = TAS_L4_OFF, fs_stride: int = 128, fs_key_off: int = 32,
-                      want_hash: bool = True, stream=None):
+                      want_hash: bool = True, ht_entries: int | None = None, stream=None):
     """RX flow lookup (fast_flows_packet_fss, tas/fast/fast_flows.c:1084-1163):
-    returns (hashes int32 or None, flow ids int32; FLOW_NONE = no flow)."""
-    fid = torch.empty(n, dtype=torch.int32, device=frames.device)
-    h = torch.empty(n, dtype=torch.int32, device=frames.device) if want_hash else None
-    ent = flowht.numel() * flowht.element_size() // 8
+    returns (hashes int32 or None, flow ids int32; FLOW_NONE = no flow).
+    frames / flowht / flowst may be device addresses (ints); an int flowht
+    needs ht_entries."""
+    dev = frames.device if isinstance(frames, torch.Tensor) else "cuda"
+    fid = torch.empty(n, dtype=torch.int32, device=dev)
+    h = torch.empty(n, dtype=torch.int32, device=dev) if want_hash else None
+    ent = ht_entries if ht_entries is not None else flowht.numel() * flowht.element_size() // 8
     _check(lib().tasx_flow_lookup_batch_dev(_ptr(frames), _ptr(offsets), stride, n, ip_off, l4_off, _ptr(flowht),
                                             ent, _ptr(flowst), fs_num, fs_stride, fs_key_off, _ptr(h), _ptr(fid),
                                             _stream(stream)), "tasx_flow_lookup_batch_dev")
@@ -335,7 +338,7 @@ def rx_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst: torch.T
              offsets: torch.Tensor | None = None, stride: int = 0, ip_off: int = TAS_IP_OFF,
              l4_off: int = TAS_L4_OFF, frame_len: torch.Tensor | int | None = None, room: int = 0,
              fs_stride: int = 128, fs_key_off: int = 32, want_hash: bool = True, flags=None, fid=None, h=None,
-             stream=None):
+             ht_entries: int | None = None, stream=None):
     """One RX pass: tcp4_verify_batch and flow_lookup_batch of the same frames
     (tasx_rx_batch_dev).  Returns (flags uint8, hashes int32 or None, flow
     ids int32)."""
@@ -347,7 +350,7 @@ def rx_batch(frames: torch.Tensor, n: int, flowht: torch.Tensor, flowst: torch.T
     if offsets is not None:
         assert offsets.dtype == torch.int64 and offsets.numel() >= n
     flen, flen0 = _hints(frame_len, n) if frame_len is not None else (None, 0)
-    ent = flowht.numel() * flowht.element_size() // 8
+    ent = ht_entries if ht_entries is not None else flowht.numel() * flowht.element_size() // 8
     _check(lib().tasx_rx_batch_dev(_ptr(frames), _ptr(offsets), stride, _ptr(flen), flen0, room, n, ip_off, l4_off,
                                    _ptr(flags), _ptr(flowht), ent, _ptr(flowst), fs_num, fs_stride, fs_key_off,
                                    _ptr(h), _ptr(fid), _stream(stream)), "tasx_rx_batch_dev")

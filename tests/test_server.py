@@ -1179,3 +1179,81 @@ def test_server_pause_unblocks_a_waiting_free(oracle):
     finally:
         cx.close()
         _stop_if_running()
+
+
+def test_server_pause_under_tight_submission(oracle):
+    """the kernel looks at the stop word before it takes a ready
+    slot, so a pause returns while fast-path threads keep every ring busy
+    (taking first, a workgroup whose ring never ran empty never saw the stop
+    word and the pause ran into its 5 s bound).  Four threads submit 32-frame
+    batches back to back with up to 4 in flight; the main thread pauses and
+    resumes the server three times meanwhile; every frame comes out bit-exact."""
+    ids, n, nb = (4, 5, 6, 7), 32, 48
+    xsum.server_start(0)
+    cx = _Ctxs(ids)
+    try:
+        refs, pins = {}, {}
+        for k, c in enumerate(ids):
+            pin, frames = _frames(nb * n, 2500 + k, short=False)
+            cx.pins.append(pin)
+            pins[c], refs[c] = pin, _ref(oracle, frames, nb * n)
+            xsum.register_frames(c, pin.addr, pin.nbytes)
+            xsum.use_server(c)
+        errs, started = [], threading.Barrier(len(ids) + 1)
+
+        def body(c):
+            try:
+                started.wait()
+                last = None
+                for b in range(nb):
+                    for i in range(n):
+                        xsum.tcp_checksums(c, pins[c].addr + (b * n + i) * 2048)
+                    last = xsum.flush_submit(c)      # completes the oldest when 4 are out
+                xsum.flush_wait(c, last)
+            except Exception as e:  # reported below
+                errs.append(repr(e))
+        ths = [threading.Thread(target=body, args=(c,)) for c in ids]
+        for t in ths:
+            t.start()
+        started.wait()
+        pauses = []
+        for _ in range(3):
+            time.sleep(0.01)
+            t0 = time.perf_counter()
+            xsum.server_pause(0)                     # refused with -EIO if a workgroup never saw the stop word
+            pauses.append(time.perf_counter() - t0)
+            time.sleep(0.01)
+            xsum.server_resume(0)
+        for t in ths:
+            t.join(60)
+        assert not errs, errs
+        assert max(pauses) < 1.0, pauses
+        for c in ids:
+            np.testing.assert_array_equal(pins[c].array[:refs[c].size], refs[c])
+            xsum.use_server(c, False)
+        xsum.server_stop(0)
+    finally:
+        cx.close()
+        _stop_if_running()
+
+
+def test_pin_overlapping_another_context_refused():
+    """a frame region that starts inside a region another context
+    pinned but runs past its end is refused (-EINVAL): HIP would map only the
+    part inside the pin, and that pin's release would unmap it under the second
+    context.  A region lying inside the pin shares it (counted)."""
+    cx = _Ctxs([3, 8])
+    raw = np.zeros(6 * 4096, np.uint8)
+    try:
+        base = raw.ctypes.data + (-raw.ctypes.data) % 4096
+        xsum.register_frames(3, base, 2 * 4096)
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.register_frames(8, base, 4 * 4096)
+        assert e.value.code == -errno.EINVAL
+        with pytest.raises(xsum.TasxError) as e:
+            xsum.register_frames(8, base + 4096, 2 * 4096)
+        assert e.value.code == -errno.EINVAL
+        xsum.register_frames(8, base + 4096, 4096)      # inside: the same pin, counted
+    finally:
+        cx.close()
+    del raw

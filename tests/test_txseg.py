@@ -70,20 +70,13 @@ def test_generator_wraps_and_flows():
 # ---------------------------------------------------------------------------
 # GPU parity
 
-# A/B variants of libtasx_ab.so (TASX_TXSEG_DEBUG) run on the same cases as
-# the product (tx_segment_lds_kernel): "r2" = 30, the round-2 product
-# tx_segment_tas_kernel (unaligned non-temporal window loads); "b128" = 41,
-# the product with its LDS windows read back by ds_read_b128; "ldsdma" = 44
-# (round 4), the product with its source chunks landed in the slice by LDS-DMA
-# The A/B forms run here beside the product: r2 (the round-2 kernel).  The
-# round-3/4 null results b128 (LDS windows by ds_read_b128, correct only where
-# the LDS runs in unaligned mode) and ldsdma (source chunks by LDS-DMA through
-# inline asm that moves M0) left this list in round 5: an illegal memory access
-# surfaced right after them in one full run (profiles/r05 r05end), and neither
-# is a product form; they stay in the A/B build (include/tasx_ab.h).
+# The comparison form of libtasx_ab.so (TASX_TXSEG_DEBUG) that runs here beside
+# the product (tx_segment_lds_kernel) on every case: "r2" = 30, the round-2
+# product tx_segment_tas_kernel (unaligned non-temporal window loads).  Round 6
+# deleted the two forms that left this list in round 5 (ds_read_b128 windows,
+# LDS-DMA staging through inline asm that moved M0): profiles/r06/INDEX.md.
 IMPLS = ["product", "r2"]
-AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel"), "b128": ("41", "tx_segment_lds_kernel<b128>"),
-            "ldsdma": ("44", "tx_segment_lds_kernel<ldsdma>")}
+AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel")}
 
 
 def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):
