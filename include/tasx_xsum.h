@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define TASX_XSUM_ABI 9
+#define TASX_XSUM_ABI 10
 #define TASX_ABI_VERSION TASX_XSUM_ABI /* tasx_abi_version() */
 
 /* flags for the TCP4 batch entry points */
@@ -405,8 +405,7 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
 /* Flush server (ABI 6): a persistent kernel per GPU takes the flushes of
  * every attached context from pinned host memory, so a fast-path core's
  * tasx_flush_submit(), _poll() and _wait() make NO HIP call (the server's
- * keepalive thread watches the kernel, every 10 ms) and the GPU pays no launch
- * per batch.
+ * epoch thread watches the kernel) and the GPU pays no launch per batch.
  * Each context has a ring of TASX_SRV_RING (8) descriptor slots, up to 64
  * frames each: submit writes the frames' offsets in the context's registered
  * region and their ip.total_length into the next slot, the header last, and
@@ -425,21 +424,27 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * still detaches and returns -EIO once.  The TAS path this replaces: tx_flush
  * (tas/fast/fastemu.c:544-566) after tcp_checksums (fast_flows.c:1058-1069).
  *   tasx_server_start(device): launch the server kernel (2 * TASX_MAX_CTX
- *     workgroups of 1024 threads) and its keepalive thread; the kernel also
- *     leaves by itself 2 s after the process stops refreshing it
+ *     workgroups of 1024 threads) and its epoch thread.  (ABI 10) The kernel
+ *     runs in epochs of 5 ms: each launch leaves at its rings' positions after
+ *     its period and the epoch thread keeps the next launch queued behind it
+ *     on the server's stream, so a HIP call elsewhere in the process that
+ *     waits for all of the device's work -- hipDeviceSynchronize
+ *     (torch.cuda.synchronize), the frees (hipFree, hipHostFree,
+ *     hipHostUnregister, torch.cuda.empty_cache), synchronous copies, waits on
+ *     the null stream -- waits for the epochs queued when it was made (about
+ *     10 ms), not for the server's stop; and a process that is gone queues no
+ *     further epoch (INTEGRATION.md 4f lists the calls, measured)
  *   tasx_server_stop(device): -EBUSY while contexts are attached; waits up
  *     to 5 s for the kernel to leave, else -EIO
  *   tasx_ctx_use_server(ctx, 1 / 0): attach (needs a running server and a
  *     registered frame region below 4 GiB; not together with the feeder) /
  *     detach (waits for the context's tickets; the ring's position is kept
  *     for the next context attached under that id)
- *   While a server runs, HIP's frees would wait for its kernel: tasx_ctx_destroy
- *     hands the context's memory to the server (released at its stop), and
- *     tasx_host_free, tasx_host_unregister, tasx_dev_free and tasx_feeder_stop
- *     return -EBUSY; anything else in the process that frees device or pinned
- *     memory (hipFree, hipHostFree, hipHostUnregister, torch.cuda.empty_cache;
- *     hipFreeAsync does not wait) blocks until the stop -- or, since ABI 9,
- *     until a pause:
+ *   While a server runs, HIP's frees wait for its queued epochs:
+ *     tasx_ctx_destroy hands the context's memory to the server (released at
+ *     its stop), and tasx_host_free, tasx_host_unregister, tasx_dev_free and
+ *     tasx_feeder_stop return -EBUSY (a fast-path core must never wait on
+ *     the GPU); a pause lets every free through at once:
  *   tasx_server_pause(device): the kernel leaves at its rings' current
  *     positions (a batch being summed is finished first; at most 5 s, else
  *     -EIO: the stop word stays, so a kernel that leaves later is seen gone
@@ -452,6 +457,10 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  *     (-EINVAL when not paused); the paused batches are served from there.
  *     A server may also be stopped (once detached) or aborted while paused.
  *   tasx_server_stats: batches and frames submitted since start
+ *   tasx_server_epochs (ABI 10): epochs completed, and the epoch thread's
+ *     waits longer than 50 ms (a HIP call of its, or an epoch overdue: another
+ *     thread in a device-wide wait) with the longest in ms; the first is also
+ *     reported once on stderr (TASX_SERVER_QUIET=1 silences it)
  *   tasx_ctx_server_flushes: batches the context handed to the server */
 /* (ABI 7) The fused TX segment build through the flush server (the copy of
  * flow_tx_segment's payload from the app's TX buffer plus tcp_checksums,
@@ -479,6 +488,7 @@ int tasx_server_stop(int device);
 int tasx_server_pause(int device);
 int tasx_server_resume(int device);
 int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames);
+int tasx_server_epochs(int device, uint64_t *epochs, uint32_t *slow_waits, uint32_t *max_wait_ms);
 int tasx_ctx_use_server(unsigned ctx_id, int on);
 int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);
 

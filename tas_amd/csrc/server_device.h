@@ -153,8 +153,11 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // resumed one (tasx_server_resume) where this workgroup left off
   uint32_t *const posw = (uint32_t *) (mem + TASX_SRV_POSW(blockIdx.x));
   uint32_t p = P.resume ? __hip_atomic_load(posw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : blockIdx.x % K;
-  uint64_t t_act = wall_clock64(), t_lease = t_act;
-  uint32_t lease = 0u;
+  uint64_t *const tactw = (uint64_t *) (mem + TASX_SRV_TACT(blockIdx.x));
+  const uint64_t t_launch = wall_clock64();
+  // the last batch's time carries over from the previous epoch: an idle ring
+  // stays on header-only polls across epochs (the wall clock is the device's)
+  uint64_t t_act = P.resume ? __hip_atomic_load(tactw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : t_launch;
   uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // A read of position p: 1 = the batch is complete (taken: its descriptors
   // into LDS), 0 = nothing yet, 2 = the header without all its entries (the
   // host still writing them, or a header-only poll: read the whole slot at
-  // once), 3 = stop, 4 = the lease ran out
+  // once), 3 = stop, 4 = the epoch is over
   auto judge = [&](const SlotRead &v, bool entries, uint64_t now) -> int {
     const uint64_t tag = (uint64_t) ((p + 1u) & 0xffffu);
     const uint64_t h0 = rlane64(v.hw, 0), h1 = rlane64(v.hw, 1), c = rlane64(v.hw, 2);
@@ -186,6 +189,12 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     // see the stop word: ADVICE r05)
     if ((uint32_t) c != 0u)
       return 3;
+    // the epoch's end, checked before a slot is taken as well: the next
+    // epoch, queued behind this launch, takes it (an epoch bounds how long a
+    // device-wide synchronize or a free elsewhere in the process waits for
+    // this kernel; server_epochs in tasx_host.c)
+    if (now - t_launch >= P.period_ticks)
+      return 4;
     // a header-only read never takes the slot: unread entries (0) would match
     // the tag of every position p with p + 1 = 0 mod 2^16
     if (hdr && entries && __builtin_amdgcn_ballot_w64((uint32_t) lane < words && (v.e >> 48) != tag) == 0ull) {
@@ -224,12 +233,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     if constexpr (DIAG)
       if (lane == 0)
         s_d[4]++;
-    if ((uint32_t) (c >> 32) != lease) {
-      lease = (uint32_t) (c >> 32);
-      t_lease = now;
-    } else if (now - t_lease > P.lease_ticks) { // no keepalive: the host process is gone
-      return 4;
-    }
     return hdr ? 2 : 0;
   };
   for (;;) {
@@ -272,8 +275,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
     }
     __syncthreads();
     if (s_cmd != 0u) {
-      if (threadIdx.x == 0) // the position polled and not taken: where a resumed launch starts
+      if (threadIdx.x == 0) { // the position polled and not taken: where the next launch starts
         st_sys32(posw, p);
+        st_sys64(tactw, t_act);
+      }
       break;
     }
     const uint32_t row = threadIdx.x >> 4;

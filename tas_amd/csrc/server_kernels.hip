@@ -38,10 +38,16 @@
 // TX buffer into the frame, both checksums -- with plain stores, and one lane
 // issues a system-scope release (buffer_wbl2 sc0 sc1) before the done word.
 //
-// Exit: every wave of every workgroup leaves when the host sets the stop word,
-// or when the lease word has not changed for lease_ticks of the GPU's wall
-// clock (the host's keepalive thread bumps it every 10 ms while the server is
-// started, so this only ends a server whose process is gone).
+// Epochs (round 6): one launch serves for P.period_ticks of the GPU's wall
+// clock, then every workgroup leaves at its next poll (a batch it is summing
+// is finished first), storing its ring position and the time of its last
+// batch; the host's epoch thread keeps the next launch queued behind it on the
+// same stream, and that launch resumes at those positions.  A HIP call that
+// waits for all of the device's work (hipDeviceSynchronize, the frees, a
+// synchronous copy) therefore waits for at most the launches queued when it
+// was made -- about two periods -- instead of for a kernel that never ends.
+// Every wave also leaves at once when the host sets the stop word (stop,
+// pause, abort); a process that is gone queues no further epoch.
 #include "server_device.h"
 
 extern "C" int tasx_launch_server(const tasx_srv_params *p, void *stream)

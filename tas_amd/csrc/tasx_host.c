@@ -2030,15 +2030,29 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
  * (release) -- and returns: no HIP call, no lock, no launch.  SRV_K
  * workgroups of the kernel poll ring r (workgroup k the positions k mod
  * SRV_K), checksum the frames in place over PCIe and post each slot's done
- * word; tasx_flush_poll/_wait reap those in position order.  A keepalive
- * thread bumps the lease word every 10 ms; the kernel leaves on the stop word
- * or, when the lease has not moved for 2 s, on its own (the process is gone). */
+ * word; tasx_flush_poll/_wait reap those in position order.
+ *
+ * Epochs (round 6): a launch serves for SRV_PERIOD_US, then leaves at its
+ * rings' positions; the server's epoch thread keeps the next launch queued
+ * behind the running one on the server's stream (two outstanding, each with
+ * an event), so service goes on while any HIP call that waits for all of the
+ * device's work -- hipDeviceSynchronize (torch.cuda.synchronize), the frees
+ * (torch.cuda.empty_cache), synchronous copies, waits on the null stream --
+ * waits for at most the epochs queued when it was made (about two periods)
+ * instead of hanging on a kernel that never ends (the
+ * round-5 server had a 2 s lease and no end).  A process that is gone queues
+ * no further epoch, so the server also ends with it.  The epoch thread makes
+ * the server's only routine HIP calls (hipEventQuery, the launches); a call
+ * of its that waits longer than SRV_SLOW_MS, or an epoch overdue by as long,
+ * is counted and reported once on stderr (tasx_server_epochs has the counts). */
 
-#define SRV_LEASE_S 2u
+#define SRV_PERIOD_US 5000u
+#define SRV_SLOW_MS 50u
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
 #define SRV_COLD_US 2000u /* idle time from which a ring's header alone is polled */
 #define SRV_K 2u          /* workgroups per ring (tasx_srv_params.k): profiles/r04/r04g */
+#define SRV_QUEUED 2u     /* epochs outstanding on the server's stream */
 
 struct fserver {
   int device;
@@ -2046,32 +2060,30 @@ struct fserver {
   uint8_t *h_mem, *d_mem; /* coherent pinned block (tasx_kernels.h TASX_SRV_*) */
   uint8_t *h_ring, *d_ring; /* the host-written lines (control word, slots): h_mem / d_mem */
   uint32_t attached;      /* bit r: ring r serves a context */
-  int keep_run;
+  int keep_run;           /* the epoch thread runs */
   pthread_t keep;
   uint64_t batches, frames; /* submitted by contexts since detached (statistics) */
   uint32_t khz;             /* wall clock rate (the A/B build's timing sums) */
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
-  int aborted; /* tasx_server_abort stopped the kernel (and the keepalive thread); read and written atomically:
+  int aborted; /* tasx_server_abort stopped the kernel (and the epoch thread); read and written atomically:
                 * context threads read it (server_gone) outside g_server_mu */
-  /* the kernel's state as the keepalive thread last saw it (hipStreamQuery
-   * every 10 ms once launched): 0 running, 1 exited, < 0 -hipError_t.  The
-   * fast-path cores read this word: their polls make no HIP call (a
-   * hipStreamQuery per poll from 8 cores serialised in the runtime's locks and
-   * stalled the process's other HIP work, profiles/r05 r05o) */
+  /* kstate: 0 while the epochs run (or are paused), < 0 -hipError_t when an
+   * epoch failed to launch or faulted.  The fast-path cores read this word:
+   * their polls make no HIP call (a hipStreamQuery per poll from 8 cores
+   * serialised in the runtime's locks, profiles/r05 r05o).  launched: the
+   * epoch thread keeps epochs queued (cleared by a pause).  launched, kstate,
+   * paused and the epoch queue (ev, qhead, nq, nlaunch) change under kmu. */
   int launched, kstate;
-  /* launched, kstate and kgen change together under kmu; the keepalive
-   * thread queries the stream outside it (a query can wait on the runtime's
-   * locks, e.g. behind a hipFree that waits for this very kernel, and a pause
-   * must still get to write the stop word) and keeps its answer only when no
-   * pause or resume (kgen) came in between */
   pthread_mutex_t kmu;
-  uint32_t kgen;
+  hipEvent_t ev[SRV_QUEUED];
+  uint64_t qhead, nlaunch; /* epochs completed / launched */
+  uint32_t nq;             /* outstanding: nlaunch - qhead */
+  uint32_t slow_calls, max_wait_ms, warned; /* the epoch thread's waits (tasx_server_epochs) */
   /* tasx_server_pause: the kernel has left at its rings' positions and
    * tasx_server_resume launches it again from them (prm.resume); set before
-   * the stop word is written and cleared after the new launch, so that a
-   * kernel found not running while paused is never taken for gone */
+   * the stop word is written and cleared after the new launch */
   int paused;
   tasx_srv_params prm;
 };
@@ -2139,35 +2151,99 @@ static uint32_t *srv_dline(const struct fserver *S, unsigned r)
   return (uint32_t *) (S->h_mem + TASX_SRV_DONE(r));
 }
 
-static void *server_keepalive(void *arg)
+static uint64_t mono_ns(void)
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t) t.tv_sec * 1000000000ull + (uint64_t) t.tv_nsec;
+}
+
+/* the epoch thread's report of a long wait (once per server; the counts stay
+ * in tasx_server_epochs) */
+static void server_slow(struct fserver *S, const char *what, uint64_t ns)
+{
+  const uint32_t ms = (uint32_t) (ns / 1000000u);
+  S->slow_calls++;
+  if (ms > S->max_wait_ms)
+    S->max_wait_ms = ms;
+  if (!S->warned && !getenv("TASX_SERVER_QUIET")) {
+    S->warned = 1;
+    fprintf(stderr,
+            "tasx: flush server (device %d): %s took %u ms -- another thread is in a HIP call that waits for all "
+            "of the device's work (hipDeviceSynchronize / torch.cuda.synchronize, a free, a synchronous copy, a "
+            "wait on the null stream).  The server's epochs bound that wait to about %u ms each time; "
+            "tasx_server_pause() around such calls avoids it (INTEGRATION.md 4f)\n",
+            S->device, what, ms, 2u * SRV_PERIOD_US / 1000u);
+  }
+}
+
+/* launch the next epoch and record its event (kmu held) */
+static hipError_t server_launch_epoch(struct fserver *S)
+{
+  S->prm.resume = S->nlaunch > 0u ? 1u : 0u;
+  if (tasx_launch_server(&S->prm, S->st) != 0) {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? hipErrorLaunchFailure : e;
+  }
+  const hipError_t e = hipEventRecord(S->ev[S->nlaunch % SRV_QUEUED], S->st);
+  if (e != hipSuccess)
+    return e;
+  S->nlaunch++;
+  S->nq++;
+  return hipSuccess;
+}
+
+/* The epoch thread: every 200 us, retire the epochs that have completed and
+ * queue new ones up to SRV_QUEUED (unless paused or failed). */
+static void *server_epochs(void *arg)
 {
   struct fserver *S = arg;
-  uint32_t *lease = (uint32_t *) (S->h_ring + TASX_SRV_CTL) + 1;
-  uint32_t k = 1;
-  const struct timespec ts = {0, 10 * 1000 * 1000};
+  const struct timespec ts = {0, 200 * 1000};
+  const uint64_t slow = (uint64_t) SRV_SLOW_MS * 1000000u;
+  uint64_t t_head = mono_ns(); /* when the oldest outstanding epoch became the oldest */
   hipSetDevice(S->device);
   while (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE)) {
-    __atomic_store_n(lease, k++, __ATOMIC_RELEASE);
     pthread_mutex_lock(&S->kmu);
-    const uint32_t gen = S->kgen;
-    const int watch = __atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0;
-    pthread_mutex_unlock(&S->kmu);
-    if (watch) {
-      const hipError_t e = hipStreamQuery(S->st);
-      if (e != hipErrorNotReady) {
-        pthread_mutex_lock(&S->kmu);
-        if (S->kgen == gen && __atomic_load_n(&S->launched, __ATOMIC_ACQUIRE))
-          __atomic_store_n(&S->kstate, e == hipSuccess ? 1 : -(int) e, __ATOMIC_RELEASE);
-        pthread_mutex_unlock(&S->kmu);
+    if (__atomic_load_n(&S->launched, __ATOMIC_ACQUIRE) && __atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0) {
+      while (S->nq > 0u) {
+        const uint64_t t0 = mono_ns();
+        const hipError_t e = hipEventQuery(S->ev[S->qhead % SRV_QUEUED]);
+        const uint64_t t1 = mono_ns();
+        if (t1 - t0 > slow)
+          server_slow(S, "hipEventQuery of an epoch", t1 - t0);
+        if (e == hipErrorNotReady) {
+          /* an epoch lasts SRV_PERIOD_US and its successor waits behind it:
+           * the oldest should retire within about two periods */
+          if (t1 - t_head > slow + 2000ull * SRV_PERIOD_US)
+            server_slow(S, "an epoch past its period", t1 - t_head), t_head = t1;
+          break;
+        }
+        if (e != hipSuccess) {
+          __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
+          break;
+        }
+        S->qhead++;
+        S->nq--;
+        t_head = t1;
+      }
+      while (__atomic_load_n(&S->kstate, __ATOMIC_RELAXED) == 0 && S->nq < SRV_QUEUED) {
+        const uint64_t t0 = mono_ns();
+        const hipError_t e = server_launch_epoch(S);
+        const uint64_t t1 = mono_ns();
+        if (t1 - t0 > slow)
+          server_slow(S, "an epoch's launch", t1 - t0);
+        if (e != hipSuccess)
+          __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
       }
     }
+    pthread_mutex_unlock(&S->kmu);
     nanosleep(&ts, NULL);
   }
   return NULL;
 }
 
 /* process exit with a server still started: stop the kernel first (the
- * runtime's own teardown would otherwise wait for it until the lease ran out) */
+ * runtime's own teardown would otherwise wait for the queued epochs) */
 static void server_atexit(void)
 {
   for (int d = 0; d < MAX_DEVICES; d++) {
@@ -2182,6 +2258,9 @@ static void server_atexit(void)
 static void server_free(struct fserver *S)
 {
   pthread_mutex_destroy(&S->kmu);
+  for (uint32_t q = 0; q < SRV_QUEUED; q++)
+    if (S->ev[q])
+      hipEventDestroy(S->ev[q]);
   if (S->h_mem)
     hipHostFree(S->h_mem);
   if (S->st)
@@ -2189,18 +2268,20 @@ static void server_free(struct fserver *S)
   free(S);
 }
 
-/* 1 when the server's kernel has left for good: aborted, or not running and
- * not paused (paused is read again after the query: a pause sets it before
- * its kernel leaves) */
+/* 1 when the server has gone for good: aborted, an epoch failed, or stopped
+ * with its last launch finished.  A paused server, and one whose epoch thread
+ * runs, has not (between two epochs the stream may be idle for a moment). */
 static int server_gone(struct fserver *S)
 {
   if (__atomic_load_n(&S->aborted, __ATOMIC_ACQUIRE))
     return 1;
   if (__atomic_load_n(&S->paused, __ATOMIC_ACQUIRE))
     return 0;
-  if (hipStreamQuery(S->st) == hipErrorNotReady)
+  if (__atomic_load_n(&S->kstate, __ATOMIC_ACQUIRE) < 0)
+    return 1;
+  if (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE))
     return 0;
-  return !__atomic_load_n(&S->paused, __ATOMIC_ACQUIRE);
+  return hipStreamQuery(S->st) != hipErrorNotReady;
 }
 
 /* 0 while the server kernel runs and has flagged no error */
@@ -2217,7 +2298,7 @@ static int server_alive(const struct tasx_ctx *c)
   int st = __atomic_load_n(&S->kstate, __ATOMIC_ACQUIRE);
   if (st == 0) {
     if (__atomic_load_n(&S->keep_run, __ATOMIC_ACQUIRE))
-      return 0; /* the keepalive thread watches the kernel */
+      return 0; /* the epoch thread keeps it going */
     /* it has stopped (an abort or a stop under way): ask the runtime */
     const hipError_t e = hipStreamQuery(S->st);
     if (e == hipErrorNotReady)
@@ -2225,8 +2306,8 @@ static int server_alive(const struct tasx_ctx *c)
     st = e == hipSuccess ? 1 : -(int) e;
   }
   if (st == 1)
-    return set_err(-EIO, "flush server: the kernel has exited (stopped, or its lease ran out)");
-  return hip_err((hipError_t) -st, "flush server: hipStreamQuery");
+    return set_err(-EIO, "flush server: the kernel has exited (stopped)");
+  return hip_err((hipError_t) -st, "flush server: an epoch");
 }
 
 /* 0 while the server kernel runs and has flagged no frame of this context */
@@ -2462,7 +2543,9 @@ int tasx_server_start(int device)
       (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void **) &S->h_mem, TASX_SRV_BYTES, hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void **) &S->d_mem, S->h_mem, 0)) != hipSuccess)
+      (e = hipHostGetDevicePointer((void **) &S->d_mem, S->h_mem, 0)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&S->ev[0], hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&S->ev[1], hipEventDisableTiming)) != hipSuccess)
     rc = hip_err(e, "server allocation");
   if (!rc && khz <= 0)
     rc = set_err(-ENODEV, "server: device %d reports no wall clock", device);
@@ -2473,7 +2556,7 @@ int tasx_server_start(int device)
     S->d_ring = S->d_mem;
     prm.mem = S->d_mem;
     prm.ring = S->d_ring;
-    prm.lease_ticks = (uint64_t) khz * 1000u * SRV_LEASE_S;
+    prm.period_ticks = (uint64_t) khz * SRV_PERIOD_US / 1000u;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
     prm.diag = 0;
@@ -2495,19 +2578,19 @@ int tasx_server_start(int device)
       rc = set_err(-EINVAL, "server: %u workgroups per ring (a divisor of %u)", prm.k, TASX_SRV_RING);
   }
   if (!rc) {
-    S->keep_run = 1;
-    __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL) + 1, 1u, __ATOMIC_RELEASE);
-    if (pthread_create(&S->keep, NULL, server_keepalive, S) != 0) {
-      S->keep_run = 0;
-      rc = set_err(-ENOMEM, "server: pthread_create failed");
-    } else if (tasx_launch_server(&prm, S->st) != 0) {
-      rc = hip_err(hipGetLastError(), "server kernel launch");
-      __atomic_store_n(&S->keep_run, 0, __ATOMIC_RELEASE);
-      pthread_join(S->keep, NULL);
+    /* the first epoch here (a launch error is the caller's), the rest from
+     * the epoch thread */
+    if ((e = server_launch_epoch(S)) != hipSuccess) {
+      rc = hip_err(e, "server kernel launch");
     } else {
-      pthread_mutex_lock(&S->kmu);
-      __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
-      pthread_mutex_unlock(&S->kmu);
+      S->launched = 1;
+      S->keep_run = 1;
+      if (pthread_create(&S->keep, NULL, server_epochs, S) != 0) {
+        S->keep_run = 0;
+        __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
+        (void) hipStreamSynchronize(S->st); /* the first epoch leaves on the stop word */
+        rc = set_err(-ENOMEM, "server: pthread_create failed");
+      }
     }
   }
   if (rc) {
@@ -2560,6 +2643,26 @@ int tasx_server_stop(int device)
   }
   server_free(S);
   return e == hipSuccess ? 0 : hip_err(e, "flush server kernel");
+}
+
+int tasx_server_epochs(int device, uint64_t *epochs, uint32_t *slow_waits, uint32_t *max_wait_ms)
+{
+  if (device < 0 || device >= MAX_DEVICES)
+    return set_err(-EINVAL, "no flush server running for device %d", device);
+  pthread_mutex_lock(&g_server_mu);
+  struct fserver *S = g_server[device];
+  if (S) {
+    pthread_mutex_lock(&S->kmu);
+    if (epochs)
+      *epochs = S->qhead;
+    if (slow_waits)
+      *slow_waits = S->slow_calls;
+    if (max_wait_ms)
+      *max_wait_ms = S->max_wait_ms;
+    pthread_mutex_unlock(&S->kmu);
+  }
+  pthread_mutex_unlock(&g_server_mu);
+  return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
 }
 
 int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
@@ -2632,7 +2735,7 @@ int tasx_ctx_use_server(unsigned ctx_id, int on)
     struct fserver *S = c->device < MAX_DEVICES ? g_server[c->device] : NULL;
     if (S && server_gone(S)) {
       pthread_mutex_unlock(&g_server_mu);
-      return set_err(-EIO, "the flush server for device %d is not running (aborted, or its lease ran out): "
+      return set_err(-EIO, "the flush server for device %d is not running (aborted, or an epoch failed): "
                      "tasx_server_stop it", c->device);
     }
     if (S) {
@@ -2737,42 +2840,43 @@ int tasx_server_pause(int device)
     pthread_mutex_unlock(&g_server_mu);
     return rc;
   }
+  /* under kmu: the epoch thread queues nothing more once launched is clear */
   pthread_mutex_lock(&S->kmu);
   const int st = __atomic_load_n(&S->kstate, __ATOMIC_ACQUIRE);
   if (st == 0) {
     __atomic_store_n(&S->paused, 1, __ATOMIC_RELEASE);
-    __atomic_store_n(&S->launched, 0, __ATOMIC_RELEASE); /* the keepalive thread stops asking */
-    S->kgen++;                                           /* and drops an answer it is getting now */
+    __atomic_store_n(&S->launched, 0, __ATOMIC_RELEASE);
   }
   pthread_mutex_unlock(&S->kmu);
   if (st != 0) {
     pthread_mutex_unlock(&g_server_mu);
-    return st == 1 ? set_err(-EIO, "flush server: the kernel has exited (stopped, or its lease ran out)")
-                   : hip_err((hipError_t) -st, "flush server kernel");
+    return hip_err((hipError_t) -st, "flush server: an epoch");
   }
+  /* every queued epoch leaves at once on the stop word */
   __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 1u, __ATOMIC_RELEASE);
   hipError_t e = hipErrorNotReady;
   const struct timespec ts = {0, 100 * 1000};
   for (uint32_t t = 0; t < SRV_STOP_WAIT_MS * 10u && (e = hipStreamQuery(S->st)) == hipErrorNotReady; t++)
     nanosleep(&ts, NULL);
-  if (e != hipSuccess) {
-    /* still running after the bound, or failed: not paused; the keepalive
-     * thread watches the kernel again and the contexts see what it does.  The
-     * stop word stays: cleared, workgroups that had already left would leave
-     * their rings unserved beside a kernel that still runs */
-    pthread_mutex_lock(&S->kmu);
+  pthread_mutex_lock(&S->kmu);
+  if (e == hipSuccess) { /* drained: every outstanding epoch has completed */
+    S->qhead += S->nq;
+    S->nq = 0;
+  } else {
+    /* still running after the bound, or failed: not paused.  The stop word
+     * stays: cleared, workgroups that had already left would leave their
+     * rings unserved beside a launch that still runs */
     if (e != hipErrorNotReady)
       __atomic_store_n(&S->kstate, -(int) e, __ATOMIC_RELEASE);
     __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
     __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
-    S->kgen++;
-    pthread_mutex_unlock(&S->kmu);
-    pthread_mutex_unlock(&g_server_mu);
+  }
+  pthread_mutex_unlock(&S->kmu);
+  pthread_mutex_unlock(&g_server_mu);
+  if (e != hipSuccess)
     return e == hipErrorNotReady
                ? set_err(-EIO, "flush server for device %d did not leave within %u ms", device, SRV_STOP_WAIT_MS)
                : hip_err(e, "flush server kernel");
-  }
-  pthread_mutex_unlock(&g_server_mu);
   return 0;
 }
 
@@ -2796,20 +2900,16 @@ int tasx_server_resume(int device)
   int prev = -1;
   (void) hipGetDevice(&prev);
   hipError_t e = hipSetDevice(S->device);
-  S->prm.resume = 1;
-  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 0u, __ATOMIC_RELEASE); /* the stop word; the lease goes on */
-  if (e == hipSuccess && tasx_launch_server(&S->prm, S->st) != 0) {
-    e = hipGetLastError();
-    if (e == hipSuccess)
-      e = hipErrorLaunchFailure;
-  }
+  __atomic_store_n((uint32_t *) (S->h_ring + TASX_SRV_CTL), 0u, __ATOMIC_RELEASE); /* the stop word */
   pthread_mutex_lock(&S->kmu);
-  /* launched: the keepalive thread watches the new kernel; on a failed launch
-   * the contexts see the error (and settle, tasx_take_unfinished) */
+  /* one epoch here (resuming at the positions the last one left), the rest
+   * from the epoch thread; on a failed launch the contexts see the error (and
+   * settle, tasx_take_unfinished) */
+  if (e == hipSuccess)
+    e = server_launch_epoch(S);
   __atomic_store_n(&S->kstate, e == hipSuccess ? 0 : -(int) e, __ATOMIC_RELEASE);
   __atomic_store_n(&S->launched, 1, __ATOMIC_RELEASE);
   __atomic_store_n(&S->paused, 0, __ATOMIC_RELEASE);
-  S->kgen++;
   pthread_mutex_unlock(&S->kmu);
   pthread_mutex_unlock(&g_server_mu);
   if (prev >= 0)

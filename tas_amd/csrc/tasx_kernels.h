@@ -91,15 +91,17 @@ typedef struct tasx_flow_params {
 
 /* The persistent flush server (server_kernels.hip): one block of coherent
  * pinned host memory per GPU, host-written lines apart from GPU-written ones.
- *   [TASX_SRV_CTL]     u64: stop (low word, host) | lease (high word, host keepalive)
+ *   [TASX_SRV_CTL]     u64: stop (low word, host); the high word is unused
  *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 done[TASX_SRV_RING]
  *                      (done[p mod RING] = p + 1 once position p is finished),
  *                      u32 error at word TASX_SRV_ERRW (sticky)
  *   [TASX_SRV_DIAG(b)] A/B builds: workgroup b's 5 u64 timing sums
  *                      (tasx_ab_server_diag); every build: u32 at
  *                      TASX_SRV_POSW(b) = the ring position workgroup b
- *                      polled when it left (a paused server's launch
- *                      resumes there, tasx_server_resume)
+ *                      polled when it left, and u64 at TASX_SRV_TACT(b) =
+ *                      the wall-clock time of its last batch (the next
+ *                      epoch's launch, and a paused server's, resumes
+ *                      there: tasx_server_resume, server_epochs)
  *   [TASX_SRV_SLOTP(r, p)] ring r, position p: a 1 KiB descriptor slot,
  *     u64 h0 = n | min(region bytes, 2^32 - 1) << 16 | tag << 48,
  *     u64 h1 = region device address (48 bits) | tag << 48,
@@ -132,6 +134,7 @@ typedef struct tasx_flow_params {
 #define TASX_SRV_ERRW TASX_SRV_RING
 #define TASX_SRV_DIAG(b) (4096u + 64u * (b))
 #define TASX_SRV_POSW(b) (TASX_SRV_DIAG(b) + 48u)
+#define TASX_SRV_TACT(b) (TASX_SRV_DIAG(b) + 56u)
 #define TASX_SRV_RINGS (4096u + 64u * TASX_MAX_CTX * TASX_SRV_KMAX)
 #define TASX_SRV_SLOTP(r, p) (TASX_SRV_RINGS + ((r) * TASX_SRV_RING + (p) % TASX_SRV_RING) * TASX_SRV_SLOT)
 #define TASX_SRV_BYTES (TASX_SRV_RINGS + TASX_MAX_CTX * TASX_SRV_RING * TASX_SRV_SLOT)
@@ -139,13 +142,14 @@ typedef struct tasx_flow_params {
 typedef struct tasx_srv_params {
   uint8_t *mem;          /* device view of the server's pinned block (the GPU-written lines) */
   uint8_t *ring;         /* device view of the host-written lines (control word, slots): mem */
-  uint64_t lease_ticks;  /* wall-clock ticks without a lease change before the kernel exits */
+  uint64_t period_ticks; /* an epoch: wall-clock ticks from its launch after which each workgroup
+                            leaves at its next poll (the host has the next epoch queued behind it) */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
   uint32_t diag;         /* the A/B build's timing form: per-batch timing sums (tasx_ab_server_diag) */
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
   uint32_t resume;       /* 0: every ring at position 0 (a zeroed block); 1: each workgroup at the
-                            position it left at (TASX_SRV_POSW), after tasx_server_pause */
+                            position it left at (TASX_SRV_POSW): every epoch after the first */
 } tasx_srv_params;
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */

@@ -94,6 +94,7 @@ SIGNATURES = {
     "tasx_server_tx_segments": (_c_int, [_uns, _vp, _c_u32, ctypes.POINTER(ctypes.c_uint32)]),
     "tasx_server_stop": (_c_int, [_c_int]),
     "tasx_server_stats": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u64)]),
+    "tasx_server_epochs": (_c_int, [_c_int, ctypes.POINTER(_c_u64), ctypes.POINTER(_c_u32), ctypes.POINTER(_c_u32)]),
     "tasx_ctx_use_server": (_c_int, [_uns, _c_int]),
     "tasx_ctx_server_flushes": (_c_int, [_uns, ctypes.POINTER(_c_u32)]),
     "tasx_take_unfinished": (_c_int, [_uns, _vp, _c_u32]),
@@ -501,6 +502,13 @@ def server_stats(device: int = 0) -> tuple[int, int]:
     b, fr = ctypes.c_uint64(), ctypes.c_uint64()
     _check(lib().tasx_server_stats(device, ctypes.byref(b), ctypes.byref(fr)), "tasx_server_stats")
     return b.value, fr.value
+
+
+def server_epochs(device: int = 0) -> tuple[int, int, int]:
+    """(epochs completed, the epoch thread's waits over 50 ms, the longest in ms)."""
+    e, n, m = _c_u64(), _c_u32(), _c_u32()
+    _check(lib().tasx_server_epochs(device, ctypes.byref(e), ctypes.byref(n), ctypes.byref(m)), "tasx_server_epochs")
+    return e.value, n.value, m.value
 
 
 def register_shm(ctx_id: int, base_addr: int, nbytes: int) -> None:

@@ -71,7 +71,7 @@ def test_gfx950_code_object(libpath):
 
 
 def test_abi_version_and_errors_without_gpu(L):
-    assert L.tasx_abi_version() == 9
+    assert L.tasx_abi_version() == 10
     # argument errors are reported before any HIP call
     rc = L.tasx_raw_cksum_batch_dev(None, None, 0, None, 10, 5, None, None)
     assert rc == -errno.EINVAL
@@ -98,6 +98,7 @@ def test_abi_version_and_errors_without_gpu(L):
     # flush server (ABI 6): nothing running, no context
     assert L.tasx_server_stop(0) == -errno.EINVAL
     assert L.tasx_server_stats(0, None, None) == -errno.EINVAL
+    assert L.tasx_server_epochs(0, None, None, None) == -errno.EINVAL   # ABI 10
     assert L.tasx_server_stop(-1) == -errno.ENODEV
     assert L.tasx_ctx_use_server(3, 1) == -errno.EINVAL
     assert L.tasx_ctx_server_flushes(3, None) == -errno.EINVAL

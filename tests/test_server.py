@@ -1124,57 +1124,63 @@ def test_server_abort_while_paused_hands_back(oracle):
         _stop_if_running()
 
 
-def test_server_pause_unblocks_a_waiting_free(oracle):
-    """A free already waiting for the running server (torch.cuda.empty_cache
-    in another thread) is released by a pause: the pause writes the stop word
-    without waiting on anything the blocked free holds (the keepalive thread
-    asks the runtime outside the server's state lock), returns well inside
-    the 2 s lease, and the resumed server flushes as before."""
-    n = 32
-    # (made before the server starts: a device-wide synchronize waits for its
-    # kernel too; torch's cache emptied first, so that x has a segment of its
-    # own and the empty_cache below has it to free)
+def test_server_epochs_bound_device_wide_waits(oracle):
+    """ABI 10: the server runs in epochs of
+    5 ms with the next launch queued behind the running one, so the HIP calls
+    that wait for all of the device's work -- a device-wide synchronize, a
+    free (torch.cuda.empty_cache), a copy to pageable host memory -- return
+    while it serves (no pause), even with a fast-path thread flushing through
+    it the whole time; the epochs go on, and every frame is right."""
+    n, nb = 32, 400
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
-    x = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
-    x.fill_(1)
-    torch.cuda.synchronize()
     xsum.server_start(0)
-    cx = _Ctxs([11])
+    cx = _Ctxs([12])
     try:
-        pin, frames = _frames(2 * n, 2300, short=False)
+        pin, frames = _frames(nb * n, 2600, short=False)
         cx.pins.append(pin)
-        ref = _ref(oracle, frames, 2 * n)
-        xsum.register_frames(11, pin.addr, pin.nbytes)
-        xsum.use_server(11)
-        for i in range(n):
-            xsum.tcp_checksums(11, pin.addr + i * 2048)
-        xsum.tx_flush(11)
-        del x                                            # back to torch's cache: empty_cache frees it
-        took = {}
+        ref = _ref(oracle, frames, nb * n)
+        xsum.register_frames(12, pin.addr, pin.nbytes)
+        xsum.use_server(12)
+        err = []
 
-        def freer():
-            t = time.perf_counter()
-            torch.cuda.empty_cache()
-            took["s"] = time.perf_counter() - t
-
-        th = threading.Thread(target=freer)
+        def flusher():
+            try:
+                last = None
+                for b in range(nb):
+                    for i in range(n):
+                        xsum.tcp_checksums(12, pin.addr + (b * n + i) * 2048)
+                    last = xsum.flush_submit(12)
+                    time.sleep(0.0005)
+                xsum.flush_wait(12, last)
+            except Exception as e:  # reported below
+                err.append(repr(e))
+        th = threading.Thread(target=flusher)
         th.start()
-        time.sleep(0.3)
-        assert th.is_alive()                             # the free waits for the running kernel
-        t0 = time.perf_counter()
-        xsum.server_pause(0)
-        tp = time.perf_counter() - t0
-        th.join(5.0)
-        assert not th.is_alive() and took["s"] < 1.5
-        assert tp < 1.0
-        xsum.server_resume(0)
-        for i in range(n):
-            xsum.tcp_checksums(11, pin.addr + (n + i) * 2048)
-        xsum.tx_flush(11)
+        took = {}
+        for k in range(20):
+            x = torch.empty(16 << 20, dtype=torch.uint8, device="cuda")
+            x.fill_(k)
+            t = time.perf_counter()
+            torch.cuda.synchronize()                     # hipDeviceSynchronize
+            took.setdefault("synchronize", []).append(time.perf_counter() - t)
+            t = time.perf_counter()
+            h = x[:1 << 20].cpu()                        # a copy to pageable memory
+            took.setdefault("copy", []).append(time.perf_counter() - t)
+            assert int(h[0]) == k
+            del x, h
+            t = time.perf_counter()
+            torch.cuda.empty_cache()                     # hipFree of the segment
+            took.setdefault("free", []).append(time.perf_counter() - t)
+        th.join(60)
+        assert not err, err
+        assert not th.is_alive()
         np.testing.assert_array_equal(pin.array[:ref.size], ref)
-        assert xsum.server_flushes(11) == 2
-        xsum.use_server(11, False)
+        worst = {k: max(v) for k, v in took.items()}
+        assert all(v < 0.5 for v in worst.values()), worst
+        epochs, slow, max_ms = xsum.server_epochs(0)
+        assert epochs >= 2, epochs
+        xsum.use_server(12, False)
         xsum.server_stop(0)
     finally:
         cx.close()
