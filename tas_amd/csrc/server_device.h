@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
   __shared__ uint64_t s_w[TASX_SRV_WORDS]; // a TX segment slot's entry words
-  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg;
+  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg, s_pair;
   __shared__ uint64_t s_base;
   // DIAG sums, kept in LDS (registers are the TX rows' budget: in registers
   // they spilled): detection -> loaded, loaded -> acked, gap, batches, empty
@@ -161,16 +161,21 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
-  // (lanes 0-1) and the control word (lane 2).
+  // (lanes 0-1), the control word (lane 2) and, with the entries, the two
+  // header words of the workgroup's next position p + K (lanes 3-4: the pair
+  // below).
   struct SlotRead {
     uint64_t e, hw;
   };
   auto read_slot = [&](bool entries) {
     const uint8_t *slot = ring + TASX_SRV_SLOTP(r, p);
+    const uint8_t *next = ring + TASX_SRV_SLOTP(r, p + K);
     SlotRead v;
     v.e = entries ? ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane) : 0ull;
-    v.hw = lane < 2 ? ld_sys64((const uint64_t *) slot + lane)
-                    : lane == 2 ? ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL)) : 0ull;
+    v.hw = lane < 2    ? ld_sys64((const uint64_t *) slot + lane)
+           : lane == 2 ? ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL))
+           : (lane < 5 && entries) ? ld_sys64((const uint64_t *) next + (lane - 3))
+                                   : 0ull;
     return v;
   };
   // A read of position p: 1 = the batch is complete (taken: its descriptors
@@ -219,9 +224,36 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         if (mine)
           s_w[TASX_SRV_FB + lane] = w2;
       }
+      // The pair (round 6): when this workgroup's next
+      // position p + K is queued too -- a checksum slot of the same frame
+      // region whose frames fit the 64 rows beside these -- it is taken in the
+      // same poll round, so ONE system-scope acquire (below) covers both
+      // batches and the rows sum them at once.  Its header came with this
+      // read; its entries take one more round trip (the host wrote them before
+      // that header), tags checked; anything else is left for the next round.
+      uint32_t n2 = 0u;
+      if (!seg && !torn) {
+        const uint64_t tag2 = (uint64_t) ((p + K + 1u) & 0xffffu);
+        const uint64_t g0 = rlane64(v.hw, 3), g1 = rlane64(v.hw, 4);
+        const uint32_t m = (uint32_t) (g0 & 0x7fffu);
+        if ((g0 >> 48) == tag2 && (g1 >> 48) == tag2 && !(g0 & TASX_SRV_SEG) && m >= 1u && n + m <= TASX_SRV_FB &&
+            ((g0 ^ h0) & 0xffffffff0000ull) == 0ull && ((g1 ^ h1) & 0xffffffffffffull) == 0ull) {
+          const uint64_t e2 = (uint32_t) lane < m
+                                  ? ld_sys64((const uint64_t *) (ring + TASX_SRV_SLOTP(r, p + K) + TASX_SRV_HDR) + lane)
+                                  : 0ull;
+          if (__builtin_amdgcn_ballot_w64((uint32_t) lane < m && (e2 >> 48) != tag2) == 0ull) {
+            n2 = m;
+            if ((uint32_t) lane < m) {
+              s_off[n + lane] = (uint32_t) e2;
+              s_tl[n + lane] = (uint32_t) (e2 >> 32) & 0xffffu;
+            }
+          }
+        }
+      }
       if (lane == 0) {
         s_seg = seg ? 1u : 0u;
-        s_n = torn ? 0u : n; // a slot still torn is not built, and flags the ring
+        s_n = torn ? 0u : n + n2; // a slot still torn is not built, and flags the ring
+        s_pair = n2 ? 1u : 0u;
         if (torn)
           s_bad = 1u;
         s_bytes = (uint32_t) (h0 >> 16);
@@ -332,18 +364,20 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         s_bad = 0u; // (the rows of the next batch set it only after the next barrier)
       }
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
+      if (s_pair)
+        st_sys32(dline + (p + K) % TASX_SRV_RING, p + K + 1u);
       if constexpr (DIAG) {
         const uint64_t t_acked = wall_clock64();
         s_d[0] += t_loaded - t_act;
         s_d[1] += t_acked - t_loaded;
         s_d[2] += t_act - s_d[5];
-        s_d[3]++;
+        s_d[3] += 1u + s_pair;
         s_d[5] = t_acked;
         for (int k = 0; k < 5; ++k)
           st_sys64(dd + k, s_d[k]);
       }
     }
-    p += K;
+    p += s_pair ? 2u * K : K; // (s_pair is rewritten only by the next take, after the next barrier)
   }
 }
 

@@ -92,16 +92,25 @@ class Guarded:
         self.nbytes = nbytes
         # the data: flush against the mapping's end or its start
         self.addr = self.map_base + (self.mapped - nbytes if at == "end" else 0)
+        # (hipMemset is asynchronous for device memory, and a copy into a
+        # virtual-memory mapping is not ordered behind it: each step waits)
         _ok(h.hipMemset(self.map_base, 0, self.mapped), "hipMemset")
+        _ok(h.hipDeviceSynchronize(), "hipDeviceSynchronize")
 
     def upload(self, a: np.ndarray, offset: int = 0) -> None:
         a = np.ascontiguousarray(a)
         assert offset + a.nbytes <= self.nbytes
         _ok(hip().hipMemcpy(self.addr + offset, a.ctypes.data, a.nbytes, 1), "hipMemcpy H2D")
+        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        # the data as the kernels will see it (a mismatch later is theirs)
+        back = self.download()[offset:offset + a.nbytes]
+        assert np.array_equal(back, a.reshape(-1).view(np.uint8)), "upload into the guarded mapping did not land"
 
     def download(self) -> np.ndarray:
         out = np.empty(self.nbytes, np.uint8)
+        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         _ok(hip().hipMemcpy(out.ctypes.data, self.addr, self.nbytes, 2), "hipMemcpy D2H")
+        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
         return out
 
     def free(self) -> None:
