@@ -93,7 +93,8 @@ def parse(argv=None):
     ap.add_argument("--pmc", action="store_true", help=argparse.SUPPRESS)  # default now; kept for old command lines
     ap.add_argument("--no-pmc", action="store_true", help="skip the HBM-traffic rocprofv3 child runs")
     ap.add_argument("--server-cost-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx", "flushmix", "tso", "shard8m"], help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", choices=["tcp4", "raw", "txseg", "mixed", "rx", "flushmix", "tso", "shard8m", "readceil"],
+                    help=argparse.SUPPRESS)
     ap.add_argument("--control-selftest", action="store_true", help=argparse.SUPPRESS)  # CPU test of the rank plumbing
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     return ap.parse_args(argv)
@@ -479,37 +480,30 @@ class TxSegWorkload:
 
 def txseg_pattern_ceiling(tw: "TxSegWorkload", avg_us: float, launches: int = 100) -> dict:
     """The TX segment build's access pattern alone, timed live over the same
-    rotation: the product kernel with TASX_TXSEG_DEBUG=40 (A/B build) -- the
-    same descriptor, header and aligned source loads, the same frame stores,
-    the loaded chunks stored as they are (no LDS realignment, no splice)."""
+    rotation: tasx_ab_tx_segment_form(40) of the comparison build -- the
+    product's descriptor, header and aligned source loads and its frame
+    stores, the loaded chunks stored as they are (no LDS realignment, no
+    splice)."""
     ab = xsum._load(xsum.AB_LIB_PATH)
     s = torch.cuda.current_stream().cuda_stream
     R = len(tw.shms)
-    old = os.environ.get("TASX_TXSEG_DEBUG")
-    os.environ["TASX_TXSEG_DEBUG"] = "40"  # read by the A/B build at each call
 
     # the same rotation of shm regions and frame buffers as the leg (the
     # pattern stores unrealigned bytes: the leg's frames are not checked after it)
     def pat(k):
-        rc = ab.tasx_tx_segment_batch_dev(tw.shms[k % R].data_ptr(), tw.shm_len, tw.bufs[k % R].data_ptr(),
-                                          tw.segs.data_ptr(), tw.n, IP_OFF, L4_OFF, tw.outs[k % R].data_ptr(), s)
+        rc = ab.tasx_ab_tx_segment_form(40, tw.shms[k % R].data_ptr(), tw.shm_len, tw.bufs[k % R].data_ptr(),
+                                        tw.segs.data_ptr(), tw.n, IP_OFF, L4_OFF, tw.outs[k % R].data_ptr(), s)
         if rc:
-            raise xsum.TasxError(rc, "tasx_tx_segment_batch_dev (pattern)")
-    try:
-        for k in range(10):
-            pat(k)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
-        e0.record()
-        for k in range(launches):
-            pat(k)
-        e1.record()
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            os.environ.pop("TASX_TXSEG_DEBUG", None)
-        else:
-            os.environ["TASX_TXSEG_DEBUG"] = old
+            raise xsum.TasxError(rc, "tasx_ab_tx_segment_form(40)")
+    for k in range(10):
+        pat(k)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for k in range(launches):
+        pat(k)
+    e1.record()
+    torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / launches
     return {"bound": "the access pattern", "us": round(us, 3), "frac": round(us / avg_us, 4),
             "kernel": "tx_segment_lds_kernel<pattern> (libtasx_ab.so): the product's loads and stores, "
@@ -721,20 +715,20 @@ def tcp4_pattern_ceiling(wl: "Tcp4Workload", avg_us: float, launches: int = 200)
                       "residency, words xor-folded instead of summed"}
 
 
-# tasx_ab_stream_read paths: 0 register loads in grid order, 1 LDS-DMA, 2 + k
-# register loads with the blocks in XCD runs of 2^k (round 5, xcd_run: runs of
-# 64 read config 4's 12.6 GB fastest, profiles/r05/INDEX.md r05b)
-READ_PATHS = {"register": 0, "lds_dma": 1, "register_xcd64": 8, "register_xcd256": 10}
+# tasx_ab_stream_read paths: 0 register loads in grid order, 2 + k register
+# loads with the blocks in XCD runs of 2^k (round 5, xcd_run: runs of 64 read
+# config 4's 12.6 GB fastest, profiles/r05/INDEX.md r05b).  LDS-DMA (path 1)
+# was slower at every size (profiles/r04/INDEX.md r04a) and left the line in
+# round 6 with the other inline-asm M0 code.
+READ_PATHS = {"register": 0, "register_xcd64": 8, "register_xcd256": 10}
 
 
 def read_ceiling(wl, avg_us: float, launches: int = 200) -> dict:
     """A pure streaming read of a leg's algorithmic bytes per launch, over the
-    same buffer rotation (wl.bufs), by each load path of tasx_ab_stream_read
-    (the A/B build): register loads in grid order and in XCD runs, LDS-DMA
-    (global_load_lds_dwordx4 nt).  The fastest is the read ceiling; the pattern
-    ceiling above is the register path, LDS-DMA being the slower one
-    (profiles/r04/INDEX.md r04a).  Launch counts shrink with the size (about
-    0.1 s of reads per path)."""
+    same buffer rotation (wl.bufs), by tasx_ab_stream_read of the comparison
+    build: register loads in grid order and in XCD runs.  The fastest is the
+    read ceiling.  Launch counts shrink with the size (about 0.1 s of reads per
+    path)."""
     ab = xsum._load(xsum.AB_LIB_PATH)
     s = torch.cuda.current_stream().cuda_stream
     R = len(wl.bufs)
@@ -763,7 +757,7 @@ def read_ceiling(wl, avg_us: float, launches: int = 200) -> dict:
     return {"bound": "a pure streaming read of the same bytes", "bytes": nbytes, "launches": launches,
             **{f"{k}_us": round(v, 3) for k, v in per.items()}, "us": round(us, 3), "path": best,
             "frac": round(us / avg_us, 4), "achieved_gbs": round(nbytes / us / 1e3, 1),
-            "kernels": "stream_read_reg_kernel (grid order / XCD runs) / stream_read_glds_kernel (libtasx_ab.so)"}
+            "kernels": "stream_read_reg_kernel in grid order / XCD runs (libtasx_ab.so)"}
 
 
 def mix_bounds(mw: "FlushMixWorkload", launches: int = 200) -> dict:
@@ -1296,7 +1290,7 @@ def server_cost_child_leg(rot: int) -> dict:
     run inside the full bench process after the two-context and flush-mix
     legs, the busy pass's first synchronize blocked until the flush run had
     ended (profiles/r05 r05q), so that process measured nothing busy; a fresh
-    process measures the leg as tools/price_leg.py does."""
+    process measures the leg alone."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -1540,6 +1534,23 @@ def pmc_child(mode: str, steps: int):
         run = tso_workload(0).loop(HINT)
     elif mode == "shard8m":
         run = shard8m_workload(1, 0).loop()
+    elif mode == "readceil":
+        # the headline's read ceiling (read_ceiling): a streaming read of the
+        # headline's algorithmic bytes over the same 16 buffers, by the
+        # tasx_ab_stream_read path TASX_READ_PATH (default 0: grid order) --
+        # the counter comparison of tools/pmc_read_compare.sh
+        wl = Tcp4Workload(16, pktgen.SEED)
+        ab = xsum._load(xsum.AB_LIB_PATH)
+        path = int(os.environ.get("TASX_READ_PATH", "0"))
+        nbytes = wl.bytes_per_step // 1024 * 1024
+        sink = torch.zeros(1, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+
+        def run(_, k):
+            for j in range(k):
+                rc = ab.tasx_ab_stream_read(wl.bufs[j % 16].data_ptr(), nbytes, path, sink.data_ptr(), st)
+                if rc:
+                    raise xsum.TasxError(rc, "tasx_ab_stream_read")
     else:
         run = mixed_workload().loop()
     run(0, steps)
@@ -1931,12 +1942,12 @@ def run_tcp4(args, ws: int, rank: int, info: dict) -> None:
                         cc["traffic_frac_of_copy"] = round(rate / cc["GBps"], 4)
                 txseg["pmc"] = pt
             if mix is not None:  # tcp4_tas14_kernel<hints>: MODE kHintArr = 5, TX, 8 waves per SIMD, stride mode
-                pm = pmc_leg("flushmix", "<6, 5, false, 8, false,", 48)
+                pm = pmc_leg("flushmix", "<6, 5, false, 8, false, 0>", 48)
                 if pm and "hbm_bytes_per_launch" in pm:
                     mix["roofline"]["traffic"] = int(pm["hbm_bytes_per_launch"])
                 mix["pmc"] = pm
-            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplitX = 5, LOPT 0>)
-                prx = pmc_leg("rx", "256, false, 5, 0>", 48)
+            if rx_pass is not None:  # the one-pass RX kernel (per-frame lengths: tcp4_tas14_kernel<..., kFlowSplitX = 5>)
+                prx = pmc_leg("rx", "<6, 5, true, 8, false, 5>", 48)
                 if prx and "hbm_bytes_per_launch" in prx:
                     rx_pass["roofline"]["traffic"] = int(prx["hbm_bytes_per_launch"])
                 rx_pass["pmc"] = prx

@@ -536,7 +536,7 @@ int tasx_take_unfinished_segs(unsigned ctx_id, tasx_tx_seg *segs, uint32_t max);
 int tasx_server_abort(int device);
 
 /* ---------------------------------------------------------------------- */
-/* Kernel selection, for tests and A/B runs.  Per calling thread (TAS runs one
+/* Kernel selection, for tests.  Per calling thread (TAS runs one
  * fast-path core, i.e. one context, per thread); set it before launching.
  *   0 automatic: RAW -> 7 with per-packet lengths, else raw_sad_kernel; TCP4 ->
  *     6 when it applies, else 3 for the TAS layout in stride mode with a hint,
@@ -553,8 +553,8 @@ int tasx_server_abort(int device);
  *     Otherwise as 0.  RAW: as 0 without lengths.
  *   7 RAW: raw_wave_kernel (a wave's 4 packets summed as one chunk sequence:
  *     mixed lengths keep every lane loading); TCP4 as 0
- * Variants 1, 4, 5 and 8-11 exist only in the A/B build (libtasx_ab.so,
- * include/tasx_ab.h); this library rejects them with -EINVAL. */
+ * Any other number is rejected with -EINVAL (the comparison variants of
+ * rounds 1-5 were retired in round 6). */
 int tasx_set_kernel_variant(int variant);
 /* Name of the kernel the calling thread's last batch call launched (its entry
  * kernel; rows it cannot take are redone inside it by a general body), "" if

@@ -9,7 +9,7 @@
  * C ABI exactly as a TAS integration would call it: same entry point, same
  * arguments, one call per step.
  */
-#define _GNU_SOURCE /* RTLD_DEFAULT (mt_server_diag) */
+#define _GNU_SOURCE
 #include <stdint.h>
 #include <time.h>
 
@@ -219,7 +219,6 @@ int tasxb_flush_loop(unsigned ctx, uint8_t *base, uint64_t stride, uint32_t n, i
  *   out[3] median core time per flush: record + submit + polls (us)
  * keep (optional, keep_bytes): thread 0's mempool after the run, for the
  * caller's check against the device kernel. */
-#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -239,8 +238,6 @@ struct mt_thr {
   double *lat, *lat2, *core;
   const int *go; /* 1: start, 2: leave at once */
 };
-
-static void mt_server_diag(int device, const struct mt_thr *T, int threads, const char *what);
 
 static void mt_frame(uint8_t *f, unsigned k, uint64_t *rng)
 {
@@ -427,8 +424,6 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
     if (keep && T[0].pool)
       memcpy(keep, T[0].pool, keep_bytes < pool_bytes ? keep_bytes : pool_bytes);
   }
-  if (mode == 2)
-    mt_server_diag(device, T, threads, "server");
   for (int k = 0; k < threads; k++) {
     if (mode == 1 && T[k].inited)
       tasx_ctx_use_feeder(T[k].ctx, 0);
@@ -449,27 +444,6 @@ int tasxb_fastpath_mt(int device, unsigned ctx0, int threads, unsigned inflight,
     free(T[k].core);
   }
   return rc;
-}
-
-/* A/B build with TASX_SRV_DIAG set: the server's timing sums per batch over
- * the threads' rings (tasx_ab_server_diag, looked up at run time: the product
- * library has no such symbol), one JSON line on stderr */
-static void mt_server_diag(int device, const struct mt_thr *T, int threads, const char *what)
-{
-  if (!getenv("TASX_SRV_DIAG"))
-    return;
-  int (*diag)(int, unsigned, double *) = (int (*)(int, unsigned, double *)) dlsym(RTLD_DEFAULT, "tasx_ab_server_diag");
-  double s[5] = {0, 0, 0, 0, 0};
-  for (int k = 0; diag && k < threads; k++) {
-    double d[5];
-    if (T[k].inited && diag(device, T[k].ctx, d) == 0)
-      for (int j = 0; j < 5; j++)
-        s[j] += d[j];
-  }
-  if (s[3] > 0)
-    fprintf(stderr, "{\"server_diag\": \"%s\", \"threads\": %d, \"batches\": %.0f, \"detect_to_loaded_us\": %.3f, "
-            "\"loaded_to_acked_us\": %.3f, \"gap_us\": %.3f, \"empty_polls_per_batch\": %.2f}\n",
-            what, threads, s[3], s[0] / s[3], s[1] / s[3], s[2] / s[3], s[4] / s[3]);
 }
 
 /* The fused TX segment build through the flush server from several fast-path
@@ -580,7 +554,6 @@ int tasxb_txseg_server_mt(int device, unsigned ctx0, int threads, unsigned infli
     free(all);
     free(core);
   }
-  mt_server_diag(device, T, threads, "txseg_server");
   for (int k = 0; k < threads; k++)
     if (T[k].inited)
       tasx_ctx_use_server(T[k].ctx, 0);

@@ -17,17 +17,17 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "tas_amd" / "csrc"
 OUT_DIR = ROOT / "tas_amd" / "_lib"
 LIB = OUT_DIR / "libtasx.so"
-# the A/B build: the product's own objects plus tas_amd/csrc/ab/ (the kernels
-# and knobs kept for comparisons, include/tasx_ab.h), which hook in through
-# tasx_ext (tasx_kernels.h); used by tools/, bench.py's ceilings and the
-# variant tests only
+# the comparison build: the product's own objects plus tas_amd/csrc/ab/ (the
+# ceiling kernels bench.py prices the product against, the round-2 TX kernel
+# the tests run beside the product, one test hook: include/tasx_ab.h); the
+# product sources know nothing of it
 LIB_AB = OUT_DIR / "libtasx_ab.so"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
 HIP_SRCS = ["xsum_kernels.hip", "txseg_kernels.hip", "flow_kernels.hip", "server_kernels.hip"]
 C_SRCS = ["tasx_host.c"]
-AB_HIP_SRCS = ["ab/ab_xsum.hip", "ab/ab_txseg.hip", "ab/ab_flow.hip", "ab/ab_server.hip"]
+AB_HIP_SRCS = ["ab/ab_xsum.hip", "ab/ab_txseg.hip", "ab/ab_flow.hip"]
 AB_C_SRCS = ["ab/ab_host.c"]
 
 

@@ -10,9 +10,9 @@
 // load of a phase is issued before any is used (both frames' keys, then their
 // eight bucket entries together, then the candidates' keys together, clamped
 // to flow 0 when not a candidate), and the kernel keeps few registers so many
-// chains are in flight per CU.  CRC32C is computed bit by bit on the VALU by default (a
-// slice-by-4 variant from LDS tables built at compile time measured the same:
-// the CRC is not on the critical path).
+// chains are in flight per CU.  CRC32C is computed bit by bit on the VALU (a
+// slice-by-4 form from LDS tables measured the same: the CRC is not on the
+// critical path).
 #include "flow_device.h"
 
 extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, void *stream)
@@ -20,17 +20,9 @@ extern "C" int tasx_launch_flow_lookup(const tasx_flow_params *p, int variant, v
   if (p->n == 0)
     return 0;
   hipStream_t s = (hipStream_t) stream;
-  // A/B variants (libtasx_ab.so, ab/ab_flow.hip: CRC forms, frames per
-  // lane, key cache policies, the partitioned lookup): the lookup is bound by
-  // its dependent load chain (frame header -> bucket -> flow state), not by
-  // the CRC arithmetic (profiles/r01_flow_variants.jsonl, profiles/r04)
-  if (variant != 0 && tasx_ext && tasx_ext->flow) {
-    const int r = tasx_ext->flow(p, variant, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   // two frames per lane: 256K lookups 11.85 us against 12.53 with one and
   // 12.98 with four (register pressure; profiles/r02/r02ca); the frame keys
   // non-temporal (round 4, above)
-  return launch_flow_f<kFlowFramesPerLane, true>("flow_lookup_kernel", p, s);
+  (void) variant; // one form (tasx_set_kernel_variant selects none here)
+  return launch_flow_f<kFlowFramesPerLane>("flow_lookup_kernel", p, s);
 }

@@ -1,6 +1,5 @@
 // server_device.h -- the persistent flush server's kernel (round 4; see
-// server_kernels.hip for the protocol), shared by the product launcher and the
-// A/B build's timing form (ab/ab_server.hip: DIAG = true).
+// server_kernels.hip for the protocol, and the epochs of round 6).
 #ifndef TASX_SERVER_DEVICE_H_
 #define TASX_SERVER_DEVICE_H_
 
@@ -116,29 +115,17 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 // 1 x 1, profiles/r04/r04z); 128 VGPRs, no scratch.
 constexpr int kSrvTxU = 6;
 
-// DIAG (the A/B build's timing form, ab/ab_server.hip): per workgroup, running
-// sums of the detection -> frames loaded and frames loaded -> stores
-// acknowledged times, the gap between a batch's completion and the next
-// detection, and the empty polls, in its diagnostics line after every batch
-// (tasx_ab_server_diag).  The frame-load cache policies measured in round 4
-// (A/B 1-14: no acquire, system-scope loads, write-through TX stores, no
-// release, ...; profiles/r04/INDEX.md r04g-r04v) lost to this form and are
-// gone from the source.
-// ACQ: the per-batch acquire -- 0 system scope (the product), and in the A/B
-// build's price diagnostics only (TASX_SRV_ACQ, profiles/r05 r05l) 1 agent
-// scope (this CU's L1 alone) and 2 none, to tell what the server costs the
-// device-resident work beside it.
-template <bool DIAG, int ACQ = 0>
+// The frame-load cache policies measured in round 4 (no acquire, system-scope
+// loads, write-through TX stores, no release, ...; profiles/r04/INDEX.md
+// r04g-r04v), the per-batch timing form (profiles/r05 r05h) and the acquire at
+// agent scope or left out for pricing (profiles/r05 r05l) were measured
+// against this form and are gone from the source (round 6).
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
   __shared__ uint64_t s_w[TASX_SRV_WORDS]; // a TX segment slot's entry words
   __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg, s_pair;
   __shared__ uint64_t s_base;
-  // DIAG sums, kept in LDS (registers are the TX rows' budget: in registers
-  // they spilled): detection -> loaded, loaded -> acked, gap, batches, empty
-  // polls, the last batch's end
-  __shared__ uint64_t s_d[6];
   const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
   uint8_t *const mem = P.mem;
@@ -146,8 +133,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
   if (threadIdx.x == 0)
     s_bad = 0u;
-  if (DIAG && threadIdx.x < 6)
-    s_d[threadIdx.x] = threadIdx.x == 5 ? wall_clock64() : 0ull;
   __syncthreads();
   // a first launch starts on a zeroed block (every ring at position 0); a
   // resumed one (tasx_server_resume) where this workgroup left off
@@ -158,7 +143,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // the last batch's time carries over from the previous epoch: an idle ring
   // stays on header-only polls across epochs (the wall clock is the device's)
   uint64_t t_act = P.resume ? __hip_atomic_load(tactw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : t_launch;
-  uint64_t *const dd = (uint64_t *) (mem + TASX_SRV_DIAG(blockIdx.x));
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
   // (lanes 0-1), the control word (lane 2) and, with the entries, the two
@@ -262,9 +246,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       t_act = wall_clock64();
       return 1;
     }
-    if constexpr (DIAG)
-      if (lane == 0)
-        s_d[4]++;
     return hdr ? 2 : 0;
   };
   for (;;) {
@@ -295,15 +276,10 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
       if (lane == 0)
         s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
-      // a batch taken: this CU's L1 and the XCD's L2 drop their non-coherent
-      // lines before any frame load (A/B: policies 1-4 and 7 without)
+      // a batch taken (one or a pair): this CU's L1 and the XCD's L2 drop
+      // their non-coherent lines before any frame load
       if (st == 1)
-      {
-        if constexpr (ACQ == 0)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        else if constexpr (ACQ == 1)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     if (s_cmd != 0u) {
@@ -335,7 +311,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         tp.n = s_n;
         tp.ip_off = (uint32_t) (s_w[1] >> 32) & 0xffu;
         tp.l4_off = (uint32_t) (s_w[1] >> 40) & 0xffu;
-        tp.dbg = 0u;
         // reads stay inside the region the host validated the frame against
         // (s_bytes from the frame region's start, the frame 16-byte aligned in it)
         const uint32_t rb = s_bytes > (uint32_t) wa ? s_bytes - (uint32_t) wa : 0u;
@@ -353,7 +328,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       if (gl == 15 && !ok)
         atomicOr(&s_bad, 1u);
     }
-    const uint64_t t_loaded = DIAG ? wall_clock64() : 0ull; // thread 0: its row's loads are in (its sums used them)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -366,16 +340,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
       if (s_pair)
         st_sys32(dline + (p + K) % TASX_SRV_RING, p + K + 1u);
-      if constexpr (DIAG) {
-        const uint64_t t_acked = wall_clock64();
-        s_d[0] += t_loaded - t_act;
-        s_d[1] += t_acked - t_loaded;
-        s_d[2] += t_act - s_d[5];
-        s_d[3] += 1u + s_pair;
-        s_d[5] = t_acked;
-        for (int k = 0; k < 5; ++k)
-          st_sys64(dd + k, s_d[k]);
-      }
     }
     p += s_pair ? 2u * K : K; // (s_pair is rewritten only by the next take, after the next barrier)
   }

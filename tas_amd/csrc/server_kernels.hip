@@ -54,12 +54,7 @@ extern "C" int tasx_launch_server(const tasx_srv_params *p, void *stream)
 {
   if (p->k == 0u || TASX_SRV_RING % p->k != 0u || p->k > TASX_SRV_KMAX)
     return -1;
-  if (tasx_ext && tasx_ext->server) { // the A/B build's forms (timing sums, price diagnostics)
-    const int r = tasx_ext->server(p, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
-  hipLaunchKernelGGL(flush_server_kernel<false>, dim3(TASX_MAX_CTX * p->k), dim3(kSrvBlock), 0, (hipStream_t) stream,
+  hipLaunchKernelGGL(flush_server_kernel, dim3(TASX_MAX_CTX * p->k), dim3(kSrvBlock), 0, (hipStream_t) stream,
                      *p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

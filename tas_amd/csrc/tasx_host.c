@@ -71,16 +71,10 @@ int tasx_device_count(void)
  * 0 = automatic */
 static __thread int g_variant = 0;
 
-/* the A/B build's hooks (tasx_kernels.h); NULL in libtasx.so */
-const tasx_ext_hooks *tasx_ext = NULL;
-
 int tasx_set_kernel_variant(int variant)
 {
-  const int maxv = tasx_ext ? tasx_ext->max_variant : 7;
-  if (variant < 0 || variant > maxv)
-    return set_err(-EINVAL, "kernel variant %d out of range", variant);
-  if (!tasx_ext && (variant == 1 || variant == 4 || variant == 5))
-    return set_err(-EINVAL, "kernel variant %d is an A/B build variant (libtasx_ab.so)", variant);
+  if (variant < 0 || variant > 7 || variant == 1 || variant == 4 || variant == 5)
+    return set_err(-EINVAL, "kernel variant %d does not exist (0, 2, 3, 6, 7)", variant);
   g_variant = variant;
   return 0;
 }
@@ -165,7 +159,6 @@ int tasx_tcp4_cksum_batch_dev_room(void *base, const uint64_t *off,
   p.flen = flen;
   p.flen0 = flen0;
   p.room = room;
-  p.diag = tasx_ext ? tasx_ext->diag : NULL;
   r = tasx_launch_tcp4(&p, g_variant, stream);
   if (r != 0)
     return hip_err(hipGetLastError(), "tcp4_cksum_kernel launch");
@@ -285,7 +278,6 @@ int tasx_tx_segment_batch_dev(const void *shm, uint64_t shm_len, void *frames,
   p.n = n;
   p.ip_off = ip_off;
   p.l4_off = l4_off;
-  p.dbg = 0u;  /* the A/B build's txseg hook sets its diagnostics form */
   if (tasx_launch_txseg(&p, stream) != 0)
     return hip_err(hipGetLastError(), "tx segment kernel launch");
   return 0;
@@ -551,7 +543,7 @@ static int pin_acquire(uint8_t *base, size_t bytes, void **dev, int *owned)
     k++;
   if (k == MAX_PINS)
     rc = set_err(-ENOMEM, "more than %u pinned regions", MAX_PINS);
-  else if ((e = hipHostRegister(base, bytes, hipHostRegisterMapped | (tasx_ext ? tasx_ext->host_reg_flags : 0u))) !=
+  else if ((e = hipHostRegister(base, bytes, hipHostRegisterMapped)) !=
            hipSuccess)
     rc = hip_err(e, "hipHostRegister");
   else if ((e = hipHostGetDevicePointer(dev, base, 0)) != hipSuccess) {
@@ -1338,7 +1330,7 @@ int tasx_ctx_stats(unsigned ctx_id, uint32_t *zerocopy_flushes, uint32_t *staged
   return 0;
 }
 
-/* Test support (the A/B build exports it as tasx_ab_ctx_set_tickets):
+/* Test support (libtasx_ab.so exports it as tasx_ab_ctx_set_tickets):
  * restart the context's tickets at `start` (nothing in flight), so a test can
  * run flushes across the 2^32 wrap.  Every completion word holds `start`,
  * which no upcoming ticket equals (as 0 does after tasx_ctx_init). */
@@ -1642,7 +1634,7 @@ int tasx_flush(unsigned ctx_id)
 #define FB_MAX 1024u     /* frames per queued batch */
 #define SWEEP_MAX 32768u /* frames per launch */
 #define SWEEP_REC 256u   /* (context, ticket) records per sweep */
-#define NSWEEP 2u     /* sweeps in flight (the A/B build: TASX_FEEDER_SWEEPS = 2 or 4) */
+#define NSWEEP 2u     /* sweeps in flight (4 measured no better: profiles/r02) */
 #define NSWEEP_MAX 4u /* a power of two: sweep s uses buffer s % nsweep across the uint32 wrap */
 #define MAX_DEVICES 64
 
@@ -1669,7 +1661,7 @@ struct feeder {
   hipStream_t st;
   uint32_t *h_done, *d_done; /* one completion word per sweep buffer */
   uint32_t *d_count;         /* per sweep buffer: blocks finished (device memory) */
-  uint32_t nsweep;           /* NSWEEP, or 4 (A/B) */
+  uint32_t nsweep;           /* NSWEEP */
   struct fsweep sw[NSWEEP_MAX];
   uint64_t sweeps, frames;   /* statistics */
 };
@@ -1878,8 +1870,6 @@ int tasx_feeder_start(int device)
   F->device = device;
   F->running = 1;
   F->nsweep = NSWEEP;
-  if (tasx_ext && tasx_ext->feeder_sweeps == 4u) /* the A/B build: 4 sweeps in flight */
-    F->nsweep = 4u;
   if ((e = hipSetDevice(device)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&F->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void **) &F->h_done, 4u * DONE_STRIDE * NSWEEP_MAX, hipHostMallocCoherent)) != hipSuccess ||
@@ -2063,7 +2053,6 @@ struct fserver {
   int keep_run;           /* the epoch thread runs */
   pthread_t keep;
   uint64_t batches, frames; /* submitted by contexts since detached (statistics) */
-  uint32_t khz;             /* wall clock rate (the A/B build's timing sums) */
   uint32_t k;               /* workgroups per ring */
   uint32_t ring_pos[TASX_MAX_CTX]; /* next position of a ring no context is attached to */
   struct grave *graves;            /* contexts destroyed while the server ran: released at stop */
@@ -2413,11 +2402,10 @@ static int server_submit(struct tasx_ctx *c)
   return 0;
 }
 
-/* segments per TX slot: TASX_SRV_SEGS (the A/B build: TASX_SRV_SEGMAX, e.g. round 4's 20) */
+/* segments per TX slot */
 static uint32_t srv_segs_max(void)
 {
-  return tasx_ext && tasx_ext->srv_segmax && tasx_ext->srv_segmax <= TASX_SRV_SEGS ? tasx_ext->srv_segmax
-                                                                                     : TASX_SRV_SEGS;
+  return TASX_SRV_SEGS;
 }
 
 /* TX segment batches through the server: validated up front (nothing is
@@ -2559,19 +2547,8 @@ int tasx_server_start(int device)
     prm.period_ticks = (uint64_t) khz * SRV_PERIOD_US / 1000u;
     prm.hot_ticks = (uint64_t) khz * SRV_HOT_US / 1000u;
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
-    prm.diag = 0;
     prm.k = SRV_K;
     prm.resume = 0;
-    if (tasx_ext) { /* the A/B build's knobs: timing sums, workgroups per ring, poll backoff */
-      prm.diag = tasx_ext->srv_diag;
-      if (tasx_ext->srv_k)
-        prm.k = tasx_ext->srv_k;
-      if (tasx_ext->srv_hot_us >= 0)
-        prm.hot_ticks = (uint64_t) khz * (uint64_t) tasx_ext->srv_hot_us / 1000u;
-      if (tasx_ext->srv_cold_us >= 0)
-        prm.cold_ticks = (uint64_t) khz * (uint64_t) tasx_ext->srv_cold_us / 1000u;
-    }
-    S->khz = (uint32_t) khz;
     S->k = prm.k;
     S->prm = prm;
     if (prm.k == 0u || TASX_SRV_RING % prm.k != 0u || prm.k > TASX_SRV_KMAX)
@@ -2682,32 +2659,6 @@ int tasx_server_stats(int device, uint64_t *batches, uint64_t *frames)
       *batches = b;
     if (frames)
       *frames = f;
-  }
-  pthread_mutex_unlock(&g_server_mu);
-  return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
-}
-
-/* Test support (the A/B build exports it as tasx_ab_server_diag): ring r's
- * timing sums over its workgroups (the timing form, TASX_SRV_DIAG=1 at
- * tasx_server_start), in us: out[0] detection -> frames loaded, [1] frames
- * loaded -> stores acknowledged, [2] a workgroup's completion -> its next
- * detection, summed over out[3] batches; out[4] empty polls */
-int tasx_server_diag_internal(int device, unsigned r, double *out)
-{
-  if (device < 0 || device >= MAX_DEVICES || r >= TASX_MAX_CTX || !out)
-    return set_err(-EINVAL, "server diag: bad argument");
-  pthread_mutex_lock(&g_server_mu);
-  const struct fserver *S = g_server[device];
-  if (S) {
-    for (int k = 0; k < 5; k++)
-      out[k] = 0.0;
-    for (uint32_t w = 0; w < S->k; w++) {
-      const uint64_t *dd = (const uint64_t *) (S->h_mem + TASX_SRV_DIAG(r * S->k + w));
-      for (int k = 0; k < 5; k++) {
-        const uint64_t v = __atomic_load_n(dd + k, __ATOMIC_ACQUIRE);
-        out[k] += (k < 3 && S->khz) ? (double) v * 1000.0 / S->khz : (double) v;
-      }
-    }
   }
   pthread_mutex_unlock(&g_server_mu);
   return S ? 0 : set_err(-EINVAL, "no flush server running for device %d", device);
@@ -3150,7 +3101,7 @@ int tasx_take_unfinished_segs(unsigned ctx_id, tasx_tx_seg *segs, uint32_t max)
 void *tasx_host_alloc(size_t bytes)
 {
   void *p = NULL;
-  const unsigned flags = tasx_ext ? tasx_ext->host_alloc_flags : 0u;
+  const unsigned flags = 0u;
   hipError_t e = hipHostMalloc(&p, bytes, flags);
   if (e != hipSuccess) {
     hip_err(e, "hipHostMalloc");

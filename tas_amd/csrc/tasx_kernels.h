@@ -40,14 +40,6 @@ typedef struct tasx_tcp4_params {
   uint32_t flen0;        /* uniform hint; 0 = none */
   uint32_t room;         /* bytes from each frame's start that may be read (the
                           * mbuf data room); 0 = unknown */
-  uint64_t *diag;        /* diagnostic timestamp buffer (the A/B build's wave-timeline variant) */
-  /* completion posted by the kernel itself (tcp4_tas14_kernel<..., DONE>: the
-   * last block to finish resets *done_count and stores done_seq into
-   * *done_word, system scope); the product posts completion words with
-   * tasx_launch_post_done and leaves these NULL (round 2: no faster) */
-  uint32_t *done_word;
-  uint32_t *done_count;  /* device memory, 0 between launches */
-  uint32_t done_seq;
   /* the RX flow lookup fused into verification (tasx_rx_batch_dev) */
   const uint32_t *flowht; /* {flow_id, flow_hash} pairs */
   const uint8_t *flowst;
@@ -69,7 +61,6 @@ typedef struct tasx_txseg_params {
   uint32_t n;
   uint32_t ip_off;
   uint32_t l4_off;
-  uint32_t dbg;            /* the A/B build's TASX_TXSEG_DEBUG diagnostics forms (0 = product) */
 } tasx_txseg_params;
 
 typedef struct tasx_flow_params {
@@ -95,13 +86,12 @@ typedef struct tasx_flow_params {
  *   [TASX_SRV_DONE(r)] ring r's GPU-written line: u32 done[TASX_SRV_RING]
  *                      (done[p mod RING] = p + 1 once position p is finished),
  *                      u32 error at word TASX_SRV_ERRW (sticky)
- *   [TASX_SRV_DIAG(b)] A/B builds: workgroup b's 5 u64 timing sums
- *                      (tasx_ab_server_diag); every build: u32 at
- *                      TASX_SRV_POSW(b) = the ring position workgroup b
- *                      polled when it left, and u64 at TASX_SRV_TACT(b) =
- *                      the wall-clock time of its last batch (the next
- *                      epoch's launch, and a paused server's, resumes
- *                      there: tasx_server_resume, server_epochs)
+ *   [TASX_SRV_WGL(b)]  workgroup b's line: u32 at TASX_SRV_POSW(b) = the
+ *                      ring position it polled when it left, u64 at
+ *                      TASX_SRV_TACT(b) = the wall-clock time of its last
+ *                      batch (the next epoch's launch, and a paused
+ *                      server's, resumes there: tasx_server_resume,
+ *                      server_epochs)
  *   [TASX_SRV_SLOTP(r, p)] ring r, position p: a 1 KiB descriptor slot,
  *     u64 h0 = n | min(region bytes, 2^32 - 1) << 16 | tag << 48,
  *     u64 h1 = region device address (48 bits) | tag << 48,
@@ -132,9 +122,9 @@ typedef struct tasx_flow_params {
 #define TASX_SRV_CTL 0u
 #define TASX_SRV_DONE(r) (128u * (1u + (r)))
 #define TASX_SRV_ERRW TASX_SRV_RING
-#define TASX_SRV_DIAG(b) (4096u + 64u * (b))
-#define TASX_SRV_POSW(b) (TASX_SRV_DIAG(b) + 48u)
-#define TASX_SRV_TACT(b) (TASX_SRV_DIAG(b) + 56u)
+#define TASX_SRV_WGL(b) (4096u + 64u * (b))
+#define TASX_SRV_POSW(b) (TASX_SRV_WGL(b))
+#define TASX_SRV_TACT(b) (TASX_SRV_WGL(b) + 8u)
 #define TASX_SRV_RINGS (4096u + 64u * TASX_MAX_CTX * TASX_SRV_KMAX)
 #define TASX_SRV_SLOTP(r, p) (TASX_SRV_RINGS + ((r) * TASX_SRV_RING + (p) % TASX_SRV_RING) * TASX_SRV_SLOT)
 #define TASX_SRV_BYTES (TASX_SRV_RINGS + TASX_MAX_CTX * TASX_SRV_RING * TASX_SRV_SLOT)
@@ -146,7 +136,6 @@ typedef struct tasx_srv_params {
                             leaves at its next poll (the host has the next epoch queued behind it) */
   uint64_t hot_ticks;    /* ticks after a batch during which a ring is polled without backoff */
   uint64_t cold_ticks;   /* ticks after a batch from which only the header is polled */
-  uint32_t diag;         /* the A/B build's timing form: per-batch timing sums (tasx_ab_server_diag) */
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
   uint32_t resume;       /* 0: every ring at position 0 (a zeroed block); 1: each workgroup at the
                             position it left at (TASX_SRV_POSW): every epoch after the first */
@@ -175,37 +164,9 @@ TASX_INTERNAL int tasx_launch_server(const tasx_srv_params *p, void *stream);
 /* record the name of the kernel the calling thread launches (tasx_last_kernel) */
 TASX_INTERNAL void tasx_note_kernel(const char *name);
 
-/* The extension point the A/B build uses.  libtasx_ab.so is the product's objects
- * plus tas_amd/csrc/ab/ (kernels and knobs kept for comparisons, include/
- * tasx_ab.h): a constructor there points tasx_ext at its hooks.  In libtasx.so
- * it stays NULL and no hook is ever called.  A launch hook returns
- * TASX_EXT_PASS for a variant it does not own: the product path runs. */
-#define TASX_EXT_PASS 1
-typedef struct tasx_ext_hooks {
-  int max_variant; /* the highest tasx_set_kernel_variant value */
-  int (*raw)(const tasx_raw_params *p, int variant, void *stream);
-  int (*tcp4)(const tasx_tcp4_params *p, int variant, void *stream);
-  int (*verify)(const tasx_tcp4_params *p, int variant, void *stream);
-  int (*rx)(const tasx_tcp4_params *p, int variant, void *stream);
-  int (*flow)(const tasx_flow_params *p, int variant, void *stream);
-  int (*txseg)(const tasx_txseg_params *p, void *stream);
-  int (*server)(const tasx_srv_params *p, void *stream); /* the server's other forms (timing sums, price diagnostics) */
-  int (*xrun)(uint64_t blocks); /* >= 0: the XCD order of a grid of `blocks` blocks */
-  /* host knobs (from the environment, read once by the A/B build) */
-  uint64_t *diag;         /* p.diag of TCP4 launches (the wave-timeline variant) */
-  uint32_t feeder_sweeps; /* sweeps in flight (TASX_FEEDER_SWEEPS: 2 or 4), 0 = the product's */
-  uint32_t srv_k;         /* workgroups per ring (TASX_SRV_K), 0 = the product's */
-  uint32_t srv_segmax;    /* TX segments per server slot (TASX_SRV_SEGMAX), 0 = the product's */
-  uint32_t srv_diag;      /* the server's timing sums (TASX_SRV_DIAG) */
-  int32_t srv_hot_us, srv_cold_us; /* poll backoff times (TASX_SRV_HOT_US / _COLD_US), < 0 = the product's */
-  uint32_t host_reg_flags;   /* extra hipHostRegister flags for frame / shm regions (TASX_HOST_UC) */
-  uint32_t host_alloc_flags; /* extra hipHostMalloc flags of tasx_host_alloc (TASX_HOST_UC) */
-} tasx_ext_hooks;
-TASX_INTERNAL extern const tasx_ext_hooks *tasx_ext;
-/* test support for the A/B build's exports (tasx_ab_ctx_set_tickets,
- * tasx_ab_server_diag): library-internal, never exported */
+/* test support for the comparison build's export tasx_ab_ctx_set_tickets:
+ * library-internal, never exported */
 TASX_INTERNAL int tasx_ctx_set_tickets_internal(unsigned ctx_id, uint32_t start);
-TASX_INTERNAL int tasx_server_diag_internal(int device, unsigned r, double *out);
 
 #ifdef __cplusplus
 }

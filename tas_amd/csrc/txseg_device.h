@@ -22,7 +22,7 @@ __device__ __forceinline__ u32x4 put_byte(u32x4 v, int b, uint32_t x)
 // dwords as dword stores, the rest as byte stores (constant offsets from one
 // address)
 // write-through (sc0 sc1) vector stores: they reach host memory without an
-// L2 write-back (the flush server's TX segment slots, A/B 13)
+// L2 write-back (the flush server's TX segment slots)
 __device__ __forceinline__ void wt_store16(uint8_t *p, u32x4 v)
 {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");

@@ -6,10 +6,11 @@
 // then the checksum loop); here each payload byte is read once from the TX
 // buffer, written once into the frame, and summed from registers.
 //
-// Kernels (tasx_launch_txseg): tx_segment_tas_kernel (the default for TAS's
-// layout: one unaligned window load per frame chunk, fixed header geometry),
-// tx_segment_u_kernel (any layout, same load scheme: txseg_row), and the
-// first-generation aligned-gather kernel below (TASX_TXSEG_DEBUG=4, A/B).
+// Kernels (tasx_launch_txseg): tx_segment_lds_kernel for TAS's layout (aligned
+// source loads realigned through a per-row LDS slice), tx_segment_u_kernel
+// (any layout: one unaligned window load per frame chunk, txseg_row), and the
+// aligned-gather kernel below for checksum fields past the frame's first 256
+// bytes.
 //
 // Aligned-gather kernel layout: one 16-lane group (a DPP row) per segment, as in the checksum
 // kernels.  The group walks the frame's address-aligned 16-byte chunks
@@ -40,16 +41,10 @@ extern "C" int tasx_launch_txseg(const tasx_txseg_params *p, void *stream)
   const bool u_ok = p->l4_off + 18u + 15u <= 256u && p->ip_off + 12u + 15u <= 256u && p->shm_len >= 16u;
   // the TAS kernel: IPv4 at 14, TCP at 34 (its other segments go to the general body)
   const bool tas = p->ip_off == 14u && p->l4_off == 34u;
-  // diagnostics forms of the A/B build (TASX_TXSEG_DEBUG, tools/txseg_probe.py; ab/ab_txseg.hip)
-  if (tasx_ext && tasx_ext->txseg) {
-    const int r = tasx_ext->txseg(p, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   if (!u_ok) {
     // checksum fields beyond the frame's first 256 bytes: the aligned-gather build
     tasx_note_kernel("tx_segment_kernel");
-    hipLaunchKernelGGL((tx_segment_kernel<6, 0>), grid, block, 0, s, *p);
+    hipLaunchKernelGGL((tx_segment_kernel<6>), grid, block, 0, s, *p);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   if (tas) {

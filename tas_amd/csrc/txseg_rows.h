@@ -1,8 +1,10 @@
 // txseg_rows.h -- the fused TX segment build's kernels (SURVEY.md section 8f
 // row 1; flow_tx_read + tcp_checksums of flow_tx_segment,
-// /root/reference/tas/fast/fast_flows.c:833-846, :930-936), shared by the
-// product launcher (txseg_kernels.hip, which describes them) and the A/B
-// build's diagnostics forms (ab/ab_txseg.hip).
+// /root/reference/tas/fast/fast_flows.c:833-846, :930-936), launched by
+// txseg_kernels.hip (which describes them): tx_segment_lds_kernel (TAS's
+// layout), tx_segment_u_kernel (any layout with both checksum fields in the
+// frame's first 256 bytes) and tx_segment_kernel (any other layout); the
+// general row body is txseg_device.h's.
 #ifndef TASX_TXSEG_ROWS_H_
 #define TASX_TXSEG_ROWS_H_
 
@@ -58,10 +60,7 @@ __device__ __forceinline__ void window_pair(uintptr_t S, int lo, int hi, const u
 // both (the first payload chunk) is summed and stored in two parts.  All
 // loads of a round are issued before any is consumed, so a segment costs one
 // memory latency after its descriptor (plus one per extra 96-chunk round).
-// MODE (diagnostics, TASX_TXSEG_DEBUG): bit 0 = no full-chunk payload stores,
-// bit 1 = temporal instead of non-temporal stores, bit 3 = no header
-// write-back, bit 4 = no partial-chunk stores.
-template <int U, int MODE = 0>
+template <int U>
 __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
 {
   const int gl = threadIdx.x & 15;
@@ -187,12 +186,8 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
       if (c == cs) // bytes from the wrap on come from the buffer start
         v = merge_at(v, funnel16(xa2, xb2, (int) ((s2 + (uint32_t) j0) & 15u)), wrap - j0);
       uint8_t *const cp = (uint8_t *) (c0p + c);
-      if (valid && blo == 0 && bhi == 16) {
-        if (MODE & 2)
-          *(__attribute__((address_space(1))) u32x4 *) cp = v;
-        else if (!(MODE & 1))
-          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
-      }
+      if (valid && blo == 0 && bhi == 16)
+        __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
       // the (at most two) partial payload chunks are stored after the loop
       if (valid && c == cp0)
         vfirst = v;
@@ -204,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
       acc += (uint64_t) v.x + v.y + v.z + v.w;
     }
   }
-  if (!(MODE & 16) && nend > cp0) {
+  if (nend > cp0) {
     // partial first / last payload chunks, on the lanes that own them
     if (lane_of(cp0) == (uint32_t) gl) {
       const int o = 16 * (int) cp0 - head;
@@ -258,8 +253,7 @@ __global__ __launch_bounds__(kBlock) void tx_segment_kernel(tasx_txseg_params p)
     v = put_byte(v, fi + 1 - b0, res >> 8);
     v = put_byte(v, ft - b0, res >> 16);
     v = put_byte(v, ft + 1 - b0, res >> 24);
-    if (!(MODE & 8))
-      store_range((uint8_t *) (f0p + k), v, max(fh - b0, 0), min(fh + (int) hl - b0, 16), false);
+    store_range((uint8_t *) (f0p + k), v, max(fh - b0, 0), min(fh + (int) hl - b0, 16), false);
   }
 }
 
@@ -303,298 +297,6 @@ __device__ __forceinline__ uint32_t row_ror(uint32_t x)
 }
 
 // ---------------------------------------------------------------------------
-// tx_segment_tas_kernel: TAS data segments as flow_tx_segment() builds them
-// (fast_flows.c:877-955): IPv4 at frame + 14, TCP at + 34 (host-checked for
-// the batch), hdrs_len 66 (TCP header + 12-byte timestamp option, :887-888),
-// frames 16-byte aligned (the mbuf data room).  The header geometry is then
-// fixed and the per-chunk work is the copy itself: frame chunk k >= 5 holds
-// payload [16k - 66, 16k - 50), one unaligned window load, one store, four
-// v_sad_u16.  Chunks 0..4 (ethernet + IPv4 + TCP + option, and chunk 4's
-// first 14 payload bytes) are read from the frame and written back whole at
-// the end with both checksums inserted; the IPv4 / pseudo-header channels
-// come from chunks 0..2 as in tcp4_tas14_kernel (xsum_kernels.hip).  A
-// segment with another hdrs_len or frame alignment, or whose ip.total_length
-// is not 52 + payload (:897), is done by the general body (txseg_row), which
-// rewrites the same payload bytes and then the checksums.  When the
-// descriptor's room (the mbuf data room) covers the frame's last 16-byte
-// chunk, that chunk is written whole, its bytes past the frame with their own
-// values, instead of by dword and byte stores.
-// OPT: how the frame's first block is written, and A/B ablations.
-//   kTxHeaderFirst (the product): chunks 0..4 (headers with stale checksum
-//     fields, chunk 4's payload) are stored right after the first round's loads
-//     are issued, every payload chunk as soon as it lands, and at the end only
-//     the two 16-bit checksum fields -- into lines the kernel has just written,
-//     merged in L2 (44.9-45.0 against 46.0 us, traffic 1.126 against 1.143 x
-//     algorithmic; profiles/r02/r02ar).
-//   kTxDppTail (the product, with kTxHeaderFirst): the row total reaches every
-//     lane by row rotations and the lane holding chunk 1 finishes and writes
-//     both fields, instead of four ds_bpermute round trips to and from lane 15
-//     (0.1-0.3 us better in 4 of 4 same-box pairs; profiles/r02/r02ax, r02ay).
-//     Occupancy: the kernel holds 105 VGPRs (4 waves per SIMD); 5 waves
-//     (WPE 5: 96 VGPRs, a small spill) costs 48 us and residency capped at 3
-//     or 2 blocks per CU 46 / 50 us.
-//   0: the round-1 form -- the first 256-byte block (headers with both
-//     checksums + the payload chunks kept in vfb) written by one instruction
-//     at the end; kTxLineKeep: keep only chunk 4's 128-byte line; kTxFieldsOnly:
-//     keep nothing, write back chunks 1, 3, 4; kTxSimple: branch-free loop for
-//     the common case (profiles/r02/r02v, r02x).
-//   Ablations (timing only, results wrong; profiles/r02/r02u): kTxNoScratch,
-//     kTxNoWriteBack, kTxNoWindows (chunk-4 / piece-2 window loads),
-//     kTxNoFallback (general body not compiled in), kTxNoPayloadStores.
-enum : int {
-  kTxNoScratch = 1, kTxNoWriteBack = 2, kTxNoWindows = 4, kTxNoFallback = 8, kTxNoPayloadStores = 16,
-  kTxLineKeep = 32, kTxFieldsOnly = 64, kTxSimple = 128, kTxHeaderFirst = 256, kTxDppTail = 512,
-  kTxNoHeaderStore = 1024, kTxNoFields = 2048, kTxNoSums = 4096 // timing-only ablations (profiles/r02/r02az)
-};
-template <int U, bool NTS, int WPE = 1, int OPT = kTxHeaderFirst | kTxDppTail>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_tas_kernel(tasx_txseg_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return; // whole 16-lane group leaves together
-  const u32x4 d0 = ld16((const u32x4 *) p.segs, 2 * i), d1 = ld16((const u32x4 *) p.segs, 2 * i + 1);
-  const uint64_t frame_off = d0.x | ((uint64_t) d0.y << 32);
-  const uint64_t tx_base = d0.z | ((uint64_t) d0.w << 32);
-  const uint32_t tx_len = d1.x, pos = d1.y, pay_ = d1.z & 0xffffu, hl_ = d1.z >> 16;
-  const bool ok = (pay_ == 0 || pos < tx_len) && pay_ <= tx_len && tx_base <= p.shm_len &&
-                  tx_len <= p.shm_len - tx_base && hl_ >= p.l4_off + 20;
-  uint8_t *const f = p.frames + frame_off;
-  bool fast = ok && hl_ == 66u && ((uintptr_t) f & 15u) == 0;
-  if (fast) {
-    const int pay = (int) pay_, fend = 66 + pay;
-    const int K = (fend + 15) >> 4;
-    // the descriptor's room covers the last chunk: write it whole, the bytes
-    // past the frame with their own values (sub-dword stores cost ~10% here).
-    // A scratch room (TASX_TXSEG_SCRATCH) also lets the build write the frame's
-    // last 128-byte block whole, with zeros past the frame: no read of the last
-    // chunk and no partial-line write for the memory side to merge.
-    const uint32_t room = d1.w & ~TASX_TXSEG_SCRATCH;
-    const bool scratch = (d1.w & TASX_TXSEG_SCRATCH) != 0u && room >= 16u * (uint32_t) K;
-    const bool whole = room >= 16u * (uint32_t) K;
-    int kend = K; // chunks [K, kend): scratch zeros up to the block's end
-    if (scratch) {
-      const uint64_t be = (frame_off + (uint64_t) fend + 127u) & ~127ull;
-      kend = max(K, min((int) ((be - frame_off + 15u) >> 4), (int) (room >> 4)));
-    }
-    const int aoff = (int) (((uintptr_t) f >> 4) & 15u);
-    const int kh = (gl - aoff) & 15; // this lane's chunk in the frame's first 256-byte block
-    const uint8_t *const shm = p.shm;
-    const uint32_t s1 = (uint32_t) (tx_base + pos);
-    const int wrap = (int) tx_len - (int) pos;
-    const int wrapc = (pay > 0 && wrap < pay) ? wrap : 0x7fffffff; // payload index where piece 2 starts
-    const uint32_t smax = (uint32_t) (p.shm_len - 16u);
-    auto woff = [&](int j0) -> uint32_t { return s1 + (uint32_t) j0 - (j0 >= wrapc ? tx_len : 0u); };
-    const bool straddle = wrapc < pay && ((66 + wrap) & 15);
-    const int ks = straddle ? (66 + wrap) >> 4 : -1;
-    const uint32_t xoff = straddle ? s1 - tx_len + (uint32_t) (16 * ks - 66) : s1;
-    // up front: the header chunk, chunk 4's window (payload [-2, 14)), the piece-2 window
-    const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4));
-    const uint32_t o4 = s1 - 2u;
-    const u32x4 w4 = (OPT & kTxNoWindows) ? hv : ld16u(shm, min(o4, smax));
-    const u32x4 xw = (OPT & kTxNoWindows) ? hv : ld16u(shm, min(xoff, smax));
-    u32x4 tv = {0u, 0u, 0u, 0u};
-    if (!scratch)
-      tv = ld16((const u32x4 *) f, (uint32_t) (K - 1)); // the frame's last chunk as it is
-
-    // whole payload chunks 5..K-1; each store instruction covers whole 256-byte
-    // blocks.  The payload chunks of the frame's first block (k < fbe) are kept
-    // in vfb and stored at the end together with the header chunks, so the
-    // block's lines are written whole by one instruction (a line written in two
-    // parts at different times costs an HBM read-modify-write).
-    int fbe = aoff <= 10 ? 16 - aoff : 0;
-    if (OPT & kTxLineKeep) { // A/B: keep only the payload chunks of chunk 4's 128-byte line
-      const int lo8 = aoff & 7;
-      fbe = min(fbe, 8 * ((lo8 + 4) / 8 + 1) - lo8);
-    }
-    if (OPT & (kTxFieldsOnly | kTxHeaderFirst)) // A/B: keep nothing (64: the write-back stores chunks 1, 3, 4 only;
-      fbe = 0;          // 256: chunks 0..4 stored early, the two checksum fields at the end)
-    // chunks 0..4 (tcp4_tas14_kernel's map for 0..3; chunk 4 = option pad + payload [0, 14))
-    auto header_chunk = [&]() -> u32x4 {
-      u32x4 h = hv;
-      if (kh == 4) {
-        u32x4 win = o4 <= smax ? w4 : gather16(shm, o4, p.shm_len);
-        if (ks == 4)
-          win = splice(win, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap + 2, 16);
-        h = splice(hv, win, 2, fend - 64);
-      }
-      return h;
-    };
-    auto store_header = [&](const u32x4 &h) {
-      uint8_t *const cp = f + 16 * kh;
-      const int hi = fend - 16 * kh;
-      if (kh < 5 && hi >= 16)
-        *(__attribute__((address_space(1))) u32x4 *) cp = h;
-      else if (kh < 5 && whole && kh < K) // h holds the frame's own bytes past its end
-        *(__attribute__((address_space(1))) u32x4 *) cp = h;
-      else if (kh < 5)
-        store_range(cp, h, 0, hi, false);
-    };
-    u32x4 vfb = hv;
-    uint32_t acc = 0;
-    const int base0 = 5 - ((5 + aoff) & 15);
-    // the common case, wave-wide: every row a fast one with no wrap inside its
-    // payload, every window inside the region, one round of chunks.  Its loop
-    // has no per-chunk branches but the store's predicate (sums by select)
-    const bool simple_row = fast && wrapc == 0x7fffffff && o4 <= smax && base0 + 16 * U >= K &&
-                            s1 + (uint32_t) (16 * (K - 1) - 66) <= smax;
-    const bool simple = (OPT & kTxSimple) && __builtin_amdgcn_ballot_w64(!simple_row) == 0ull;
-    if (simple) {
-      u32x4 a[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = min(max(base0 + gl + 16 * u, 5), K - 1);
-        a[u] = ld16u(shm, s1 + (uint32_t) (16 * k - 66));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = base0 + gl + 16 * u, hi = fend - 16 * k;
-        const u32x4 v = a[u];
-        const bool in = k >= 5 && k < K, full = in && hi >= 16;
-        const bool keep = u == 0 && k < fbe;
-        if (full && !keep)
-          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
-        if (u == 0)
-          vfb = full && keep ? v : vfb;
-        const uint32_t sv = sad4(v, 0u);
-        acc += full ? sv : 0u;
-        if (in && hi < 16) { // the frame's last chunk (one lane per row)
-          acc += sad_below(v, (uint32_t) hi);
-          uint8_t *const cp = f + 16 * k;
-          if (whole)
-            *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
-          else
-            store_range(cp, v, 0, hi, false);
-        }
-      }
-    }
-    for (int base = base0; !simple && base < K; base += 16 * U) {
-      u32x4 a[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = min(max(base + gl + 16 * u, 5), K - 1);
-        a[u] = ld16u(shm, min(woff(16 * k - 66), smax));
-      }
-      if ((OPT & kTxHeaderFirst) && !(OPT & kTxNoHeaderStore) && base == base0) // the header chunks (stale checksum fields) go out first
-        store_header(header_chunk());
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int k = base + gl + 16 * u, j0 = 16 * k - 66;
-        if (k < 5 || k >= K)
-          continue;
-        u32x4 v = a[u];
-        const uint32_t off = woff(j0);
-        if (off > smax) // a window reaching past the region's end: byte by byte
-          v = gather16(shm, off, p.shm_len);
-        if (k == ks)
-          v = splice(v, xoff <= smax ? xw : gather16(shm, xoff, p.shm_len), wrap - j0, 16);
-        uint8_t *const cp = f + 16 * k;
-        const int hi = fend - 16 * k;
-        if (u == 0 && k < fbe && hi >= 16) {
-          vfb = v;
-          acc = sad4(v, acc);
-        } else if (hi >= 16) {
-          if (OPT & kTxNoPayloadStores)
-            ;
-          else if (NTS)
-            __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
-          else
-            *(__attribute__((address_space(1))) u32x4 *) cp = v;
-          if (!(OPT & kTxNoSums))
-            acc = sad4(v, acc);
-        } else {
-          acc += sad_below(v, (uint32_t) hi);
-          if (whole)
-            *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
-          else
-            store_range(cp, v, 0, hi, false);
-        }
-      }
-    }
-
-    if (scratch && !(OPT & kTxNoScratch)) { // the scratch chunks past the frame outside its first block
-      const int k = K + gl;
-      if (k < kend && k >= fbe)
-        __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
-    }
-
-    u32x4 h = header_chunk();
-    const uint32_t m0 = kh == 2 ? 0xffff0000u : (kh == 3 ? 0x0000ffffu : 0xffffffffu);
-    uint32_t l4 = sad4(u32x4{h.x & m0, h.y, h.z, h.w}, 0u);
-    if (kh == 4 && fend < 80)
-      l4 = sad_below(h, (uint32_t) (fend - 64));
-    acc += (kh >= 2 && kh <= 4) ? l4 : 0u;
-    const uint32_t c0d3 = row_ror<1>(h.w), c2d0 = row_ror<15>(h.x);
-    const uint32_t addrs = sadw(h.z & 0xffff0000u, sadw(h.w, sadw(c2d0 & 0xffffu, 0u)));
-    const uint32_t ph = sadw(h.y & 0xff000000u, addrs);
-    const uint32_t ipsum = sadw(c0d3 & 0xffff0000u, sadw(h.x, sadw(h.y, addrs)));
-    const int l1 = (int) ((threadIdx.x & 63u) & ~15u) + ((1 + aoff) & 15); // lane holding chunk 1
-    if ((OPT & kTxDppTail) && (OPT & kTxHeaderFirst)) {
-      // no LDS round trips: every lane gets the row total by row rotations,
-      // and the lane holding chunk 1 (ip.len, the IP header and pseudo-header
-      // sums) finishes both checksums and writes both fields itself
-      acc += row_ror<8>(acc);
-      acc += row_ror<4>(acc);
-      acc += row_ror<2>(acc);
-      acc += row_ror<1>(acc);
-      const bool ok1 = kh == 1 && bswap16(h.x & 0xffffu) == 52u + (uint32_t) pay;
-      fast = (__builtin_amdgcn_ballot_w64(ok1) >> l1) & 1ull; // otherwise the general body redoes the segment
-      if (ok1) {
-        const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
-        const uint32_t tcpc = inv_result(
-            residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph) + bswap16(32u + (uint32_t) pay))));
-        if (p.out)
-          stg(p.out, i, ipc | (tcpc << 16));
-        if (!(OPT & kTxNoFields)) {
-          *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
-          *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
-        }
-      }
-    } else {
-    acc = row_sum16(acc);
-    const uint32_t ip1 = (uint32_t) __shfl((int) ipsum, l1, 64), ph1 = (uint32_t) __shfl((int) ph, l1, 64);
-    const uint32_t tl = bswap16((uint32_t) __shfl((int) (h.x & 0xffffu), l1, 64));
-    fast = tl == 52u + (uint32_t) pay; // otherwise the general body redoes the segment
-    const uint32_t ipc = inv_result(residue(fold32_to_16(ip1)));
-    const uint32_t len = 32u + (uint32_t) pay;
-    const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(acc) + fold32_to_16(ph1) + bswap16(len))));
-    const uint32_t res = (uint32_t) __shfl((int) (ipc | (tcpc << 16)), (int) ((threadIdx.x & 63u) | 15u), 64);
-    if ((OPT & kTxHeaderFirst) && fast) { // only the two fields are left to write
-      if (gl == 15 && p.out)
-        stg(p.out, i, res);
-      if (kh == 1)
-        *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) res;
-      if (kh == 3)
-        *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) (res >> 16);
-    } else if (fast && !(OPT & kTxNoWriteBack)) {
-      if (gl == 15 && p.out)
-        stg(p.out, i, res);
-      // the first block: header chunks with the checksums inserted (ip.chksum:
-      // chunk 1 bytes 8-9, tcp.chksum: chunk 3 bytes 2-3) and the kept payload chunks
-      if (kh == 1)
-        h.z = (h.z & 0xffff0000u) | (res & 0xffffu);
-      if (kh == 3)
-        h.x = (h.x & 0x0000ffffu) | (res & 0xffff0000u);
-      uint8_t *const cp = f + 16 * kh;
-      const int hi = fend - 16 * kh;
-      if ((OPT & kTxFieldsOnly) && (kh == 0 || kh == 2))
-        ; // unchanged header chunks
-      else if ((kh < 5 || kh < fbe) && hi >= 16)
-        *(__attribute__((address_space(1))) u32x4 *) cp = kh < 5 ? h : vfb;
-      else if (kh < 5 && whole && kh < K) // h holds the frame's own bytes past its end
-        *(__attribute__((address_space(1))) u32x4 *) cp = h;
-      else if (kh < 5)
-        store_range(cp, h, 0, hi, false);
-      else if (!(OPT & kTxNoScratch) && kh >= K && kh < kend && kh < fbe) // scratch chunks inside the first block
-        *(__attribute__((address_space(1))) u32x4 *) cp = u32x4{0u, 0u, 0u, 0u};
-    }
-    }
-  }
-  if (!(OPT & kTxNoFallback) && !fast) // (3 chunks per lane and round: keeps the fallback's registers below the fast path's)
-    txseg_row<3, NTS>(p, i, gl);
-}
-
-// ---------------------------------------------------------------------------
 // tx_segment_lds_kernel (round 3, the product for TAS's layout): the same
 // segment build, one 16-lane row per segment, with the payload read by
 // ALIGNED, L2-allocating 16-byte loads and realigned through a per-row LDS
@@ -625,13 +327,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 //   Rows that are not TAS data segments (hdrs_len != 66, a frame off 16-byte
 //   alignment, total_length != 52 + payload, a rejected descriptor) go to the
 //   general body (txseg_row), as before.
-// SLOTS load slots per lane: 6 (96 aligned chunks: piece A from its 16-byte
-// chunk on, 25.3 KiB of LDS per block, 6 blocks per CU) or 7 (112: piece A from
-// its 128-byte line on, so lanes own whole lines; 29.4 KiB, 5 blocks per CU).
-// A window's bytes [o, o + 16) lie in the loaded chunks; its fifth dword, read
+// 6 load slots per lane: 96 aligned chunks, piece A from its 16-byte chunk on;
+// 25.3 KiB of LDS per block, 6 blocks per CU.  A window's bytes [o, o + 16) lie in the loaded chunks; its fifth dword, read
 // past them, lies in the same aligned chunk as byte o + 15.
 constexpr int kLdsLead = 64; // lead bytes: chunk 0's window (payload index -66) stays in the slice
-template <int SLOTS>
+constexpr int kLdsSlots = 6;
+template <int SLOTS = kLdsSlots>
 constexpr int lds_slice() { return kLdsLead + 16 * 16 * SLOTS + 32; } // lead, the slots, tail slack
 
 // 16 bytes at a dword-aligned LDS address shifted by r bytes: five dwords and a funnel shift
@@ -649,19 +350,13 @@ __device__ __forceinline__ u32x4 lds_window(const uint8_t *sl, uint32_t o)
   return lds_window_at(sl + (o & ~3u), o & 3u);
 }
 
-// OPT (comparison forms of libtasx_ab.so): 1 = no general-body fallback
-// compiled in, 2 = wraps ignored (piece A only) -- both timing only, results
-// wrong -- 4 = the first block stored non-temporal too (correct), 8 = the
-// access pattern alone (timing only: the aligned source chunks stored as
-// loaded, no LDS realignment or splice; bench.py's tx_segment pattern_ceiling).
-// Round 6 deleted two forms: windows read back by ds_read_b128 at 4-byte
-// aligned LDS addresses, and the source chunks landed by LDS-DMA through
-// inline asm that moved M0 (profiles/r06/INDEX.md, r06a).
-template <bool NTS, int SLOTS = 6, int WPE = 1, int OPT = 0>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tx_segment_lds_kernel(tasx_txseg_params p)
+// (The comparison build keeps this kernel's round-3 options, among them the
+// access pattern alone that bench.py prices it against: ab/ab_txseg_rows.h.)
+template <bool NTS>
+__global__ __launch_bounds__(kBlock) void tx_segment_lds_kernel(tasx_txseg_params p)
 {
-  constexpr int kLdsSlots = SLOTS, kLdsSlice = lds_slice<SLOTS>();
-  constexpr uintptr_t kAlignA = SLOTS >= 7 ? 127u : 15u;
+  constexpr int kLdsSlice = lds_slice();
+  constexpr uintptr_t kAlignA = 15u;
   __shared__ __attribute__((aligned(16))) uint8_t lds[(kBlock / 16) * kLdsSlice];
   const int gl = threadIdx.x & 15;
   const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
@@ -707,7 +402,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const uint32_t hi_ok = (uint32_t) ((sb + p.shm_len - 1u) & ~(uintptr_t) 15) - (uint32_t) (sb & ~(uintptr_t) 15);
     const uint32_t t0 = sh0 + (uint32_t) tx_base, s1 = t0 + pos; // ring start, payload index 0
     const int wrap = (int) tx_len - (int) pos;
-    const int wrapc = (pay > 0 && wrap < pay && !(OPT & 2)) ? wrap : 0x7fffffff; // payload index where piece B starts
+    const int wrapc = (pay > 0 && wrap < pay) ? wrap : 0x7fffffff; // payload index where piece B starts
     const u32x4 hv = ld16((const u32x4 *) f, (uint32_t) min(kh, 4)); // header chunks 0..4
     uint32_t acc = 0;
     u32x4 vlast = hv; // the frame's last chunk when it is partial (its lane: kh == (K - 1) & 15)
@@ -735,14 +430,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const uint32_t ro = cA + 16u * (uint32_t) v + (v >= nA ? dB : 0u);
         a[u] = ld16_off(sbase, min(ro, hi_ok));
       }
-      if constexpr (!(OPT & 8)) {
 #pragma unroll
-        for (int u = 0; u < kLdsSlots; ++u)
-          *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
+      for (int u = 0; u < kLdsSlots; ++u)
+        *(u32x4 *) (sl + kLdsLead + 16 * (gl + 16 * u)) = a[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // LDS byte offsets: payload index 0 in piece A, piece B's first byte;
       // window u at o0 + 256u (+ dW for a window in piece B)
       const int oA = kLdsLead + (int) (s1 - cA);
@@ -754,12 +447,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       for (int u = 0; u < 6; ++u) {
         const int j0 = 16 * (16 * u + kh) - 66;
         const int o = min(o0 + 256 * u + (j0 >= wrapc ? dW : 0), kLdsSlice - 20);
-        w[u] = (OPT & 8) ? a[u] : lds_window(sl, (uint32_t) o);
+        w[u] = lds_window(sl, (uint32_t) o);
       }
       // the chunk holding the wrap (a row whose payload wraps off a chunk
       // boundary): its bytes from wrapc - j0 on are piece B's
       const int ks = wrapc < pay ? (66 + wrapc) >> 4 : -1;
-      const bool strad = !(OPT & 8) && ks >= 0 && ((66 + wrapc) & 15) != 0 && kh == (ks & 15);
+      const bool strad = ks >= 0 && ((66 + wrapc) & 15) != 0 && kh == (ks & 15);
       if (__builtin_amdgcn_ballot_w64(strad) != 0ull) {
 #pragma unroll
         for (int u = 0; u < 6; ++u) {
@@ -784,10 +477,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         // every row of the wave holds at least 81 chunks: slots 0..4 are whole
         // frame chunks, only slot 5 holds the frame's end
         acc = sad4(u32x4{w[0].x & mx, w[0].y & mr, w[0].z & mr, w[0].w & mr}, acc);
-        if (OPT & 4)
-          __builtin_nontemporal_store(w[0], (__attribute__((address_space(1))) u32x4 *) (f + 16 * kh));
-        else
-          *(__attribute__((address_space(1))) u32x4 *) (f + 16 * kh) = w[0];
+        *(__attribute__((address_space(1))) u32x4 *) (f + 16 * kh) = w[0];
 #pragma unroll
         for (int u = 1; u < 5; ++u) {
           acc = sad4(w[u], acc);
@@ -813,7 +503,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           // whole chunks, and scratch zeros past the frame to its block's end
           if (full || (k >= K && k < kend)) {
             const u32x4 sv = k < K ? v : u32x4{0u, 0u, 0u, 0u};
-            if (u == 0 && !(OPT & 4))
+            if (u == 0)
               *(__attribute__((address_space(1))) u32x4 *) (f + 16 * k) = sv;
             else
               __builtin_nontemporal_store(sv, (__attribute__((address_space(1))) u32x4 *) (f + 16 * k));
@@ -852,201 +542,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
     }
   }
-  if (!(OPT & 1) && !fast)
+  if (!fast)
     txseg_row<3, NTS>(p, i, gl);
-}
-
-// ---------------------------------------------------------------------------
-// tx_segment_wave_kernel: the TAS-layout build with ONE segment per wave.  The
-// segment's geometry is wave-uniform, so the descriptor comes in by scalar
-// loads and every branch on it is uniform.  The payload is read by ALIGNED
-// 16-byte loads: lane L holds the aligned source chunks under frame chunks L
-// and L + 64 and gets the next aligned chunk from lane L + 1 by DPP wave_rol:1
-// (lane 63: lane 0's second chunk by readlane), then funnel-shifts the pair
-// by the segment's source shift (a uniform dword select + v_alignbyte).  The
-// bare copy pattern measured 36.6 us this way against 38.6 us for unaligned
-// window loads on 16-lane rows (tools/copy_unaligned.hip, profiles/r02/r02bp).
-// A segment whose payload wraps in its circular buffer, or whose aligned
-// span leaves the shm region, takes unaligned window loads (the row kernel's
-// woff / splice / gather scheme) on the same lanes; one that is not TAS's
-// data-segment geometry goes to the general row body (txseg_row, lanes 0-15).
-// Frame chunk k of lane L, round r: k = L + 64 r.  Chunks 0..3 are headers
-// read from the frame, chunk 4 = header bytes 64-65 + payload [0, 14), chunks
-// 5.. K-1 payload [16k - 66, +16).  Header-first stores as the row kernel's
-// product form: every chunk stored as soon as it is built (stale checksum
-// fields), the two 16-bit fields at the end.
-__device__ __forceinline__ uint32_t wave_rol1(uint32_t x)
-{
-  return (uint32_t) __builtin_amdgcn_update_dpp(0, (int) x, 0x134, 0xf, 0xf, false); // lane L <- lane L + 1
-}
-__device__ __forceinline__ u32x4 wave_rol1_4(u32x4 v)
-{
-  return u32x4{wave_rol1(v.x), wave_rol1(v.y), wave_rol1(v.z), wave_rol1(v.w)};
-}
-__device__ __forceinline__ u32x4 readlane0_4(u32x4 v)
-{
-  return u32x4{(uint32_t) __builtin_amdgcn_readlane((int) v.x, 0), (uint32_t) __builtin_amdgcn_readlane((int) v.y, 0),
-               (uint32_t) __builtin_amdgcn_readlane((int) v.z, 0), (uint32_t) __builtin_amdgcn_readlane((int) v.w, 0)};
-}
-// bytes [sh, sh + 16) of a:b, sh wave-uniform
-__device__ __forceinline__ u32x4 funnel_uniform(u32x4 a, u32x4 b, uint32_t sh)
-{
-  const uint32_t r8 = sh & 3u;
-  uint32_t w0, w1, w2, w3, w4;
-  switch (sh >> 2) {
-  case 0: w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; break;
-  case 1: w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; break;
-  case 2: w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; break;
-  default: w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; break;
-  }
-  return u32x4{__builtin_amdgcn_alignbyte(w1, w0, r8), __builtin_amdgcn_alignbyte(w2, w1, r8),
-               __builtin_amdgcn_alignbyte(w3, w2, r8), __builtin_amdgcn_alignbyte(w4, w3, r8)};
-}
-__device__ __forceinline__ uint32_t rl(uint32_t v, int lane)
-{
-  return (uint32_t) __builtin_amdgcn_readlane((int) v, lane);
-}
-
-template <bool NTS>
-__global__ __launch_bounds__(kBlock) void tx_segment_wave_kernel(tasx_txseg_params p)
-{
-  const uint32_t L = threadIdx.x & 63u;
-  const uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * (kBlock / 64u) + threadIdx.x / 64u);
-  if (i >= p.n)
-    return; // the whole wave
-  const uint32_t *sd = (const uint32_t *) p.segs + 8u * i; // scalar loads: i is uniform
-  const uint64_t frame_off = sd[0] | ((uint64_t) sd[1] << 32);
-  const uint64_t tx_base = sd[2] | ((uint64_t) sd[3] << 32);
-  const uint32_t tx_len = sd[4], pos = sd[5], pay = sd[6] & 0xffffu, hl = sd[6] >> 16, roomw = sd[7];
-  const bool ok = (pay == 0 || pos < tx_len) && pay <= tx_len && tx_base <= p.shm_len &&
-                  tx_len <= p.shm_len - tx_base && hl >= p.l4_off + 20;
-  uint8_t *const f = p.frames + frame_off;
-  bool fast = ok && hl == 66u && ((uintptr_t) f & 15u) == 0 && p.shm_len >= 16u;
-  if (fast) {
-    const uint32_t fend = 66u + pay, K = (fend + 15u) >> 4;
-    const uint32_t room = roomw & ~TASX_TXSEG_SCRATCH;
-    const bool whole = room >= 16u * K, scratch = (roomw & TASX_TXSEG_SCRATCH) != 0u && whole;
-    uint32_t kend = K; // scratch zeros in chunks [K, kend): up to the frame's last 128-byte block end
-    if (scratch) {
-      const uint64_t be = (frame_off + fend + 127u) & ~127ull;
-      kend = max(K, min((uint32_t) ((be - frame_off + 15u) >> 4), room >> 4));
-    }
-    const uint8_t *const shm = p.shm;
-    const uint64_t s1 = tx_base + pos;
-    const uint32_t wrap = tx_len - pos;                     // payload index where piece 2 starts
-    const bool wraps = pay > 0 && wrap < pay;
-    // aligned span: frame chunk k >= 4 reads source [s1 - 2 + 16 (k - 4), +16)
-    const uint64_t a0 = s1 - 2u, abase = a0 & ~15ull;
-    const uint32_t sh = (uint32_t) (a0 & 15u);
-    const uint32_t na = K - 3u;                              // aligned chunks abase .. abase + 16 (na - 1)
-    const bool aligned = !wraps && s1 >= 2u && abase + 16ull * na <= p.shm_len;
-    // the frame's header chunks (lanes 0..4) and, if kept, its last chunk
-    const u32x4 hv = ld16((const u32x4 *) f, min(L, 4u));
-    const u32x4 tv = (!scratch && whole) ? ld16((const u32x4 *) f, K - 1u) : u32x4{0u, 0u, 0u, 0u};
-    // unaligned windows: payload index j at s1 + j before the wrap, at
-    // s1 + j - tx_len (= tx_base + j - wrap) from it on; a window outside
-    // the region is gathered byte by byte (bytes outside it as 0)
-    const int64_t smax = (int64_t) p.shm_len - 16;
-    auto load_at = [&](int64_t off) -> u32x4 {
-      if (off >= 0 && off <= smax)
-        return __builtin_nontemporal_load((gcu4u *) (shm + off));
-      return gather16(shm, (uint32_t) off, p.shm_len);
-    };
-    auto window = [&](uint32_t k) -> u32x4 {
-      const int j0 = 16 * (int) k - 66;
-      const bool in2 = wraps && j0 >= (int) wrap;
-      u32x4 v = load_at((int64_t) s1 + j0 - (in2 ? (int64_t) tx_len : 0));
-      if (wraps && j0 < (int) wrap && j0 + 16 > (int) wrap) // the straddle chunk: piece 2 from byte wrap - j0 on
-        v = splice(v, load_at((int64_t) s1 + j0 - (int64_t) tx_len), (int) wrap - j0, 16);
-      return v;
-    };
-    auto aload = [&](uint32_t c) -> u32x4 { // aligned source chunk c (clamped to the span)
-      return __builtin_nontemporal_load(
-          (const __attribute__((address_space(1))) u32x4 *) (shm + abase + 16ull * min(c, na - 1u)));
-    };
-    // build, store and sum frame chunk k from its payload window v
-    uint32_t acc = 0u;
-    auto emit = [&](uint32_t k, u32x4 v) {
-      if (k >= kend)
-        return;
-      uint8_t *const cp = f + 16u * k;
-      if (k >= K) { // scratch past the frame
-        __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (__attribute__((address_space(1))) u32x4 *) cp);
-        return;
-      }
-      const int hi = (int) fend - 16 * (int) k; // frame bytes in this chunk (>= 1)
-      if (k < 4u) {
-        // L4 bytes of the header chunks: chunk 2 from byte 34, chunk 3 without tcp.chksum
-        const uint32_t m0 = k == 2u ? 0xffff0000u : (k == 3u ? 0x0000ffffu : 0u);
-        if (k >= 2u)
-          acc = sad4(u32x4{hv.x & m0, hv.y, hv.z, hv.w}, acc);
-        *(__attribute__((address_space(1))) u32x4 *) cp = hv;
-        return;
-      }
-      if (k == 4u)
-        v = splice(hv, v, 2, hi); // header bytes 64-65, payload [0, 14); past the frame: its own bytes
-      if (hi >= 16) {
-        acc = sad4(v, acc);
-        if (k == 4u || !NTS)
-          *(__attribute__((address_space(1))) u32x4 *) cp = v;
-        else
-          __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *) cp);
-      } else { // the frame's last chunk
-        acc += sad_below(v, (uint32_t) hi);
-        if (k == 4u && whole)
-          *(__attribute__((address_space(1))) u32x4 *) cp = v;
-        else if (whole)
-          *(__attribute__((address_space(1))) u32x4 *) cp = splice(tv, v, 0, hi);
-        else
-          store_range(cp, v, 0, hi, false);
-      }
-    };
-    // 128 frame chunks per round: lane L builds chunks base + L and base + 64 + L
-    for (uint32_t base = 0; base < kend; base += 128u) {
-      const uint32_t k0 = base + L, k1 = base + 64u + L;
-      u32x4 w0, w1;
-      if (aligned) { // frame chunk k >= 4 = aligned chunks k - 4 and k - 3 funnelled by sh
-        const u32x4 v0 = aload(k0 >= 4u ? k0 - 4u : 0u), v1 = aload(k1 - 4u);
-        const u32x4 vx = aload(base + 124u); // under chunk base + 128: lane 63's second neighbour
-        u32x4 n0 = wave_rol1_4(v0), n1 = wave_rol1_4(v1);
-        const u32x4 l0 = readlane0_4(v1);
-        if (L == 63u) {
-          n0 = l0;
-          n1 = vx;
-        }
-        w0 = funnel_uniform(v0, n0, sh);
-        w1 = funnel_uniform(v1, n1, sh);
-      } else {
-        w0 = window(max(k0, 4u));
-        w1 = window(min(k1, K - 1u));
-      }
-      emit(k0, w0);
-      emit(k1, w1);
-    }
-    // wave totals: 16-lane rows by DPP, the four rows by readlane
-    acc += row_ror<8>(acc);
-    acc += row_ror<4>(acc);
-    acc += row_ror<2>(acc);
-    acc += row_ror<1>(acc);
-    const uint32_t l4 = rl(acc, 0) + rl(acc, 16) + rl(acc, 32) + rl(acc, 48);
-    // the IPv4 header (bytes 14..33, ip.chksum as 0) and pseudo-header from chunks 0..2
-    const uint32_t h0w = rl(hv.w, 0), h1x = rl(hv.x, 1), h1y = rl(hv.y, 1), h1z = rl(hv.z, 1), h1w = rl(hv.w, 1),
-                   h2x = rl(hv.x, 2);
-    const uint32_t addrs = sadw(h1z & 0xffff0000u, sadw(h1w, sadw(h2x & 0xffffu, 0u)));
-    const uint32_t ph = sadw(h1y & 0xff000000u, addrs);
-    const uint32_t ipsum = sadw(h0w & 0xffff0000u, sadw(h1x, sadw(h1y, addrs)));
-    fast = bswap16(h1x & 0xffffu) == 52u + pay; // otherwise the general body redoes the segment
-    if (fast && L == 0u) {
-      const uint32_t ipc = inv_result(residue(fold32_to_16(ipsum)));
-      const uint32_t tcpc = inv_result(residue(fold32_to_16(fold32_to_16(l4) + fold32_to_16(ph) + bswap16(32u + pay))));
-      if (p.out)
-        stg(p.out, i, ipc | (tcpc << 16));
-      *(__attribute__((address_space(1))) uint16_t *) (f + 24) = (uint16_t) ipc;
-      *(__attribute__((address_space(1))) uint16_t *) (f + 50) = (uint16_t) tcpc;
-    }
-  }
-  if (!fast && L < 16u)
-    txseg_row<3, NTS>(p, i, (int) L);
 }
 
 } // namespace

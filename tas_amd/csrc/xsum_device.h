@@ -381,37 +381,15 @@ __device__ __forceinline__ uint32_t tas_flow_hash(uint32_t lip, uint32_t rip, ui
   return crc32c_u32(crc32c_u32(crc32c_u32(0u, lip), rip), ports);
 }
 
-// slice-by-4 tables (built at compile time): t[k][x] = CRC of byte x followed
-// by k zero bytes (init 0); a word step is four independent table reads
 constexpr uint32_t kPoly = 0x82f63b78u; // CRC32C (Castagnoli), reflected
-struct CrcTables {
-  uint32_t t[4][256];
-};
-constexpr CrcTables make_crc_tables()
-{
-  CrcTables T{};
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k)
-      c = (c & 1u) ? (c >> 1) ^ kPoly : c >> 1;
-    T.t[0][i] = c;
-  }
-  for (int k = 1; k < 4; ++k)
-    for (uint32_t i = 0; i < 256; ++i)
-      T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xffu];
-  return T;
-}
-__constant__ CrcTables kCrc = make_crc_tables();
 
-// SSE4.2 crc32 on one 32-bit little-endian word from a (LDS) copy of kCrc
+// SSE4.2 crc32 on one 32-bit little-endian word from slice-by-4 tables in LDS
+// (t[k][x] = CRC of byte x followed by k zero bytes, init 0)
 __device__ __forceinline__ uint32_t crc32c_u32_tab(const uint32_t (*t)[256], uint32_t crc, uint32_t w)
 {
   crc ^= w;
   return t[3][crc & 0xffu] ^ t[2][(crc >> 8) & 0xffu] ^ t[1][(crc >> 16) & 0xffu] ^ t[0][crc >> 24];
 }
-
-template <int F, int BS, int LOPT = 0, typename P>
-__device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F]);
 
 // fast_flows_packet_fss lookups (fast_flows.c:1084-1163), F frames per lane:
 // lookup block `blk` of BS lanes takes frames blk * BS * F + f * BS + lane,
@@ -420,12 +398,7 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
 // before any is used.  The split-grid blocks of tcp4_tas14_kernel<...,flow>
 // (xsum_kernels.hip) run it; flow_kernels.hip's flow_lookup_kernel is the same
 // arithmetic for any layout.  P: tasx_tcp4_params or tasx_flow_params.
-// LOPT (A/B, timing only: results wrong): 1 = no frame key load (the key made
-// from the frame index), 2 = no CRC (the key's words xor-folded), 4 = no
-// flow-state key load (the first valid hash match wins), 8 = no bucket loads
-// (entry j made valid with the frame's hash, flow id (h + j) % fs_num); 1024
-// (correct) = the flow-state key loads non-temporal
-template <int F, int BS, int LOPT, typename P>
+template <int F, int BS, typename P>
 __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t (&i0)[F])
 {
   static_assert(BS == 256, "one table entry per lane");
@@ -438,11 +411,7 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
   for (int f = 0; f < F; ++f) {
     i[f] = min(i0[f], p.n - 1u); // lanes past the batch repeat the last frame (no store)
     const uint8_t *fr = p.base + pkt_offset(p.off, p.stride, i[f]);
-    u32x3u k;
-    if (LOPT & 1)
-      k = u32x3u{i[f] * 2654435761u, i[f] ^ 0x5bd1e995u, i[f] * 40503u};
-    else
-      k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
+    const u32x3u k = *(__attribute__((address_space(1))) const u32x3u *) (fr + p.ip_off + 12);
     rip[f] = k.x;
     lip[f] = k.y;
     ports[f] = (k.z >> 16) | (k.z << 16); // tcp.dest | tcp.src << 16
@@ -465,15 +434,13 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
   }
 #pragma unroll
   for (int f = 0; f < F; ++f)
-    h[f] = (LOPT & 2) ? lip[f] ^ rip[f] ^ ports[f]
-                      : crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, lip[f]), rip[f]), ports[f]);
+    h[f] = crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, lip[f]), rip[f]), ports[f]);
   uint64_t e[F][kNb];
 #pragma unroll
   for (int f = 0; f < F; ++f)
 #pragma unroll
     for (uint32_t j = 0; j < kNb; ++j)
-      e[f][j] = (LOPT & 8) ? (((uint64_t) h[f] << 32) | TASX_FLOWHTE_VALID | ((h[f] + j) % p.fs_num))
-                           : ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
+      e[f][j] = ldg((const uint64_t *) p.flowht, (h[f] + j) % p.ht_entries);
   bool cand[F][kNb];
   uint32_t fid[F][kNb];
   u32x3 key[F][kNb];
@@ -485,12 +452,7 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
       fid[f][j] = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
       cand[f][j] = (ef & TASX_FLOWHTE_VALID) && eh == h[f] && fid[f][j] < p.fs_num;
       const uint8_t *fsk = p.flowst + (uint64_t) (cand[f][j] ? fid[f][j] : 0u) * p.fs_stride + p.fs_key_off;
-      if (LOPT & 4)
-        key[f][j] = u32x3{lip[f], rip[f], ports[f]};
-      else if (LOPT & 1024) // A/B: the flow-state key lines streamed (evicted first), the buckets kept
-        key[f][j] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x3 *) fsk);
-      else
-        key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) fsk;
+      key[f][j] = *(__attribute__((address_space(1))) const u32x3 *) fsk;
     }
 #pragma unroll
   for (int f = 0; f < F; ++f) {
@@ -505,17 +467,6 @@ __device__ __forceinline__ void flow_lookup_lanes_at(const P &p, const uint32_t 
         stg(p.hash_out, i[f], h[f]);
     }
   }
-}
-
-// lookup block `blk` of BS lanes: frames blk * BS * F + f * BS + lane
-template <int F, int BS, int LOPT = 0, typename P>
-__device__ __forceinline__ void flow_lookup_lanes(const P &p, uint32_t blk)
-{
-  uint32_t i0[F];
-#pragma unroll
-  for (int f = 0; f < F; ++f)
-    i0[f] = blk * (uint32_t) (BS * F) + (uint32_t) (BS * f) + threadIdx.x;
-  flow_lookup_lanes_at<F, BS, LOPT>(p, i0);
 }
 
 } // namespace

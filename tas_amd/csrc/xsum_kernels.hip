@@ -34,11 +34,7 @@
 //       a uniform frame-length hint; per-row total_length modes otherwise),
 //   7 = raw_wave_kernel (RAW with per-packet lengths: a wave's 4 packets as one
 //       chunk sequence).
-// The device code lives in xsum_rows.h.  The A/B build (libtasx_ab.so =
-// these objects plus ab/, include/tasx_ab.h) adds its variants through the
-// tasx_ext hooks (tasx_kernels.h): the first-generation group-per-packet
-// kernels, wave-timeline stamps, 32-lane groups, tcp4_wave_kernel, forced row
-// modes, block sizes, the RX pass's split and ablation forms.
+// The device code lives in xsum_rows.h.
 #include "xsum_rows.h"
 
 // ---------------------------------------------------------------------------
@@ -124,11 +120,6 @@ extern "C" int tasx_launch_tcp4_offload(const tasx_tcp4_params *p, void *stream)
 extern "C" int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  if (variant != 0 && tasx_ext && tasx_ext->raw) { // the A/B build's variants
-    const int r = tasx_ext->raw(p, variant, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   switch (variant) {
   case 2: // the general form
     return launch_groups("raw_sad_kernel", raw_sad_kernel<6>, *p, s, kOccLds);
@@ -157,8 +148,7 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s)
   // (64K frames, 0 / 50 / 100 % ACKs: 17.4 / 12.1 / 7.7-7.9 us against 18.3-18.6
   // / 12.8-12.9 / 8.8-9.0 for lookup blocks over consecutive frames, and 16.9 /
   // 13.0 / 7.1-7.3 with two frames per lane; profiles/r03/INDEX.md r03b)
-  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr, kFlowSplitX>(p, s, 0u)
-                          : launch_rx_rows<OFFS, kTlFirst, kFlowSplitX>(p, s, 0u);
+  return mode == kHintArr ? launch_rx_rows<OFFS, kHintArr>(p, s) : launch_rx_rows<OFFS, kTlFirst>(p, s);
 }
 
 // RX verification + flow lookup: the row kernels' selection (as
@@ -168,11 +158,6 @@ static int launch_tas14_rx(const tasx_tcp4_params &p, int mode, hipStream_t s)
 extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  if (variant != 0 && tasx_ext && tasx_ext->rx) { // the A/B build's split and ablation forms
-    const int r = tasx_ext->rx(p, variant, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
   if (auto6 && tas14_ok(*p)) {
     // a uniform received length is a data burst: two frames per lookup lane,
@@ -180,7 +165,7 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
     // (64K frames: 16.8 against 17.1 us with one frame per lane and 17.6-17.9
     // with lookup blocks over consecutive frames; profiles/r03/INDEX.md r03b)
     return launch_splitx<2>("tcp4_tas14_kernel<hint,verify,flow>",
-                            tcp4_tas14_kernel<6, kHint, true, 1, false, kBlock, false, kFlowSplitX2>, *p, s, kOccLds);
+                            tcp4_tas14_kernel<6, kHint, true, 1, false, kFlowSplitX2>, *p, s, kOccLds);
   }
   if (auto6 && (tas14_nohint_ok(*p) || tas14_offs_ok(*p))) {
     const int mode = p->flen ? kHintArr : kTlFirst;
@@ -212,11 +197,6 @@ extern "C" int tasx_launch_tcp4_rx(const tasx_tcp4_params *p, int variant, void 
 extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  if (variant != 0 && tasx_ext && tasx_ext->verify) { // the A/B build's row forms
-    const int r = tasx_ext->verify(p, variant, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   const bool auto6 = variant == 0 || variant == 6 || variant >= 7;
   if (auto6 && tas14_ok(*p))
     return launch_groups("tcp4_tas14_kernel<hint,verify>", tcp4_tas14_kernel<6, kHint, true>, *p, s, kOccLds);
@@ -239,13 +219,8 @@ extern "C" int tasx_launch_tcp4_verify(const tasx_tcp4_params *p, int variant, v
 extern "C" int tasx_launch_tcp4(const tasx_tcp4_params *p, int variant, void *stream)
 {
   hipStream_t s = (hipStream_t) stream;
-  if (variant != 0 && tasx_ext && tasx_ext->tcp4) { // the A/B build's variants
-    const int r = tasx_ext->tcp4(p, variant, stream);
-    if (r != TASX_EXT_PASS)
-      return r;
-  }
   if (variant != 2 && variant != 3)
-    variant = 0; // 6 = the automatic choice; RAW-only and A/B-only numbers run it too
+    variant = 0; // 6 = the automatic choice; the RAW-only number runs it too
   if (variant == 0) {
     // TAS frames in 16-byte rooms: a uniform hint, per-frame hints or none ->
     // tcp4_tas14_kernel; frames by offsets -> its OFFS form

@@ -1,9 +1,9 @@
 // xsum_rows.h -- the checksum kernels' device code (SURVEY.md section 8a:
 // rte_raw_cksum, rte_ipv4_cksum, rte_ipv4_udptcp_cksum as tcp_checksums()
 // calls them, /root/reference/tas/fast/fast_flows.c:1058-1069) and the
-// launch helpers, shared by the product launchers (xsum_kernels.hip, whose
-// header comment gives the layout and arithmetic) and the A/B build's
-// variants (ab/ab_xsum.hip).
+// launch helpers, used by the product launchers (xsum_kernels.hip, whose
+// header comment gives the layout and arithmetic) and by the comparison
+// build's access-pattern kernels (ab/ab_xsum.hip).
 #ifndef TASX_XSUM_ROWS_H_
 #define TASX_XSUM_ROWS_H_
 
@@ -31,14 +31,12 @@ namespace {
 // offsets from the block's first packet (a uniform 64-bit base: 16 strides
 // from a 16-byte aligned base stay 16-byte aligned), so each load is
 // global_load_dwordx4 v, v_off, s[base] (one VGPR per address) at any batch size.
-// G (A/B, round 4): lanes per packet -- 16 (the product: one DPP row), 32 or
-// 64 with U = 3 / 2 loads per lane for a 1500-byte packet: fewer loads in
-// flight per lane and more packets' worth of short-lived waves, the shape of
-// the fastest trivial streaming read at config 4's sizes (profiles/r04/INDEX.md
-// r04b); lane G - 1 holds the last chunk and the group total (group_total<G>).
-template <int U, bool S32 = false, int G = 16>
+// (32- and 64-lane packet groups measured no faster at config 4's sizes,
+// profiles/r04/INDEX.md r04b.)
+template <int U, bool S32 = false>
 __global__ __launch_bounds__(kBlock) void raw_sad_kernel(tasx_raw_params p)
 {
+  constexpr int G = 16;
   const int gl = threadIdx.x & (G - 1);
   const uint32_t blk = xcd_run(blockIdx.x, gridDim.x, p.xrun);
   const uint32_t i = blk * (kBlock / G) + threadIdx.x / G;
@@ -407,17 +405,6 @@ __device__ __forceinline__ uint32_t in_range(int base, int lo, int hi)
   return (uint32_t) (((1ull << (8 * bh)) - 1ull) & ~((1ull << (8 * bl)) - 1ull));
 }
 
-template <int BS>
-__device__ __forceinline__ void diag_stamp(const tasx_tcp4_params &p, int slot)
-{
-  // 100 MHz global clock; one record of 4 stamps per wave
-  const uint64_t t = __builtin_amdgcn_s_memrealtime();
-  if ((threadIdx.x & 63) == 0) {
-    const uint64_t w = ((uint64_t) blockIdx.x * (BS / 64) + threadIdx.x / 64);
-    p.diag[w * 4 + slot] = t;
-  }
-}
-
 // TCP4, TAS frame layout (tcp = ip + 20), stride mode: one chunk range
 // [ip, ip + 20 + L4 length) carries the IPv4 header, the pseudo-header fields
 // and the segment, so no byte loads are issued at all.  The (up to 4) lanes
@@ -449,11 +436,13 @@ __device__ __forceinline__ uint32_t pat_bits(uint64_t pat, int s)
 }
 
 
-// one frame (i) per G-lane group; lane gl, group's first lane gbase in the wave.
-// VERIFY: the receive-side flags of tcp4_frame_kernel<U, true> instead.
-template <int U, int DIAG = 0, int G = 16, bool VERIFY = false>
+// one frame (i) per 16-lane group (a DPP row); lane gl, the row's first lane
+// gbase in the wave.  VERIFY: the receive-side flags of tcp4_frame_kernel<U,
+// true> instead.
+template <int U, bool VERIFY = false>
 __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, int gl, int gbase)
 {
+  constexpr int G = 16;
   constexpr uint64_t pat_ip = VERIFY ? kPatIPV : kPatIP, pat_nl4 = VERIFY ? kPatNL4V : kPatNL4;
   const uint8_t *base = p.base; // 16-byte aligned, batch span < 4 GiB (host-checked)
   const uint32_t fo = (uint32_t) pkt_offset(p.off, p.stride, i);
@@ -473,8 +462,6 @@ __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, i
   const uint32_t ba = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 2) & 15), gbase + ca, 64);
   const uint32_t bb = (uint32_t) __shfl((int) chunk_byte(v[0], (hb + 3) & 15), gbase + cb, 64);
   const uint32_t tl = (ba << 8) | bb;
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 1);
   const uint32_t len = tl >= 20 ? tl - 20 : 0;
   int E = 20 + (int) len;
   bool trunc = false; // RX: the datagram reaches past the frame's bound (rx_bound)
@@ -536,8 +523,6 @@ __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, i
   }
   uint32_t c_ip = fold64_to_18(acc_ip);
   uint32_t c_ph = fold64_to_18(acc_ph);
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 2);
   part = group_total<G>(part);
   c_ip = group_total<G>(c_ip);
   c_ph = group_total<G>(c_ph);
@@ -583,19 +568,15 @@ __device__ __forceinline__ void tcp4_tas_frame(tasx_tcp4_params p, uint32_t i, i
       st8(ip + 37, tcpc >> 8);
     }
   }
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 3);
 }
 
-template <int U, int DIAG = 0, int G = 16>
+template <int U>
 __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 {
-  if constexpr (DIAG)
-    diag_stamp<kBlock>(p, 0);
-  const uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  const uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
-  tcp4_tas_frame<U, DIAG, G>(p, i, threadIdx.x & (G - 1), (threadIdx.x & 63) & ~(G - 1));
+  tcp4_tas_frame<U>(p, i, threadIdx.x & 15, (threadIdx.x & 63) & ~15);
 }
 
 // TCP4 headline kernel: TAS frames in 16-byte aligned mbuf rooms (IPv4 header
@@ -627,31 +608,24 @@ __global__ __launch_bounds__(kBlock) void tcp4_tas_kernel(tasx_tcp4_params p)
 //            [ip_off + 38, ip_off + 1522] or beyond the room, is redone by
 //            the general body).  One dependent latency after the hint load,
 //            which 4 rows share a line of.
-//   kHead5   chunks 0..4 (a whole pure ACK, ip.len 52) are loaded with the
-//            total_length, the rest after it: ACK rows take one latency, data
-//            rows two.  Needs a room of 80 B (the chunk-4 read).
 //   kRoom    all 96 chunks of the frame's room at once, masked per row by its
 //            total_length after the loads: one latency for every frame, at the
 //            price of reading whole rooms.  Needs a room of 1536 B.
-// Rows with total_length outside [38 (51 for kHead5), 1522], or beyond the RX
+// Rows with total_length outside [38, 1522], or beyond the RX
 // read bound, take the general body (tcp4_tas_frame; tcp4_frame_row with OFFS).
 // OFFS (not kHint): frames at base + off[i] instead of i * stride; a row whose
 // frame start (base + off[i] + (ip_off & ~15)) is not 16-byte aligned loads
 // only the aligned chunk holding the IPv4 header start and is redone by the
 // general row body.
-enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kHead5 = 2, kRoom = 3, kMix = 4 /* tcp4_mix_kernel, A/B */,
-                       kHintArr = 5 /* per-frame hints as the geometry */,
-                       kHintArrP = 6 /* the same, lanes past the last chunk load nothing (A/B) */,
-                       kHintArrS = 7 /* kHintArr, a block's rows sorted long frames first (A/B, variant 28):
-                                        bit-exact, slower at every ACK fraction (64K frames, 0 / 50 / 100 %
-                                        ACKs: 16.7-17.0 / 10.9-11.1 / 7.9-8.0 us against 16.5 / 10.2 / 7.1-7.2;
-                                        profiles/r02/r02cg) -- the block's 16 hints and two ballots per
-                                        row cost more than the loads pure-ACK waves skip */ };
+// (Round 6: the head-5 mode, tcp4_mix_kernel's, the per-frame-hint rows that
+// leave lanes past the last chunk idle and the sorted-rows form -- all measured
+// slower, profiles/r02 -- are gone from the source.)
+enum Tas14Mode : int { kHint = 0, kTlFirst = 1, kRoom = 3, kHintArr = 5 /* per-frame hints as the geometry */ };
 
 // The row body after the loads: v[] holds the row's chunks (lane gl: chunks
 // gl + 16u), hend the datagram extent it assumed; sums, results, stores, and
 // the general body for a row the fast path cannot take.
-template <int U, int MODE, bool VERIFY, bool OFFS, bool FALLBACK = true, bool ROWFB = false>
+template <int U, int MODE, bool VERIFY, bool OFFS>
 __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t i, int gl, const uint8_t *fb,
                                              uint32_t a0, uint32_t hend, bool in_range, const u32x4 (&v)[U])
 {
@@ -689,7 +663,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
     }
     u32x4 t = v[U - 1];
     uint32_t tlane = 15u;
-    if constexpr (MODE == kRoom || MODE == kHintArrP) {
+    if constexpr (MODE == kRoom) {
       const uint32_t ut = last >> 4;
       t = v[0];
 #pragma unroll
@@ -702,7 +676,7 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
   }
   acc = row_sum16(acc);
   const uint32_t ip15 = row_shr<14>(ipsum), ph15 = row_shr<14>(ph), tl15 = bswap16(row_shr<14>(tlw));
-  constexpr bool kArr = MODE == kHintArr || MODE == kHintArrP || MODE == kHintArrS;
+  constexpr bool kArr = MODE == kHintArr;
   const bool bad = MODE == kHint ? tl15 != hend : kArr ? (tl15 != hend || !in_range) : !in_range; // kHint*: meaningful on lane 15
   if constexpr (VERIFY) {
     const uint32_t vihl = row_shr<14>(c0d3 >> 16); // ip[0]: version / IHL
@@ -729,172 +703,54 @@ __device__ __forceinline__ void tas14_finish(const tasx_tcp4_params &p, uint32_t
       st8(ip + 37, tcpc >> 8);
     }
   }
-  if (FALLBACK && __builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
+  if (__builtin_amdgcn_ballot_w64(gl == 15 && bad) != 0ull) {
     const int gbase = (threadIdx.x & 63) & ~15;
     const bool rbad = (MODE == kHint || kArr) ? (bool) __shfl((int) bad, gbase + 15, 64) : bad;
     if (rbad) {
-      if constexpr (OFFS || ROWFB) // ROWFB (A/B): the any-layout row body in stride mode too
+      if constexpr (OFFS)
         tcp4_frame_row<3, VERIFY>(p, i, gl);
       else
-        tcp4_tas_frame<U, 0, 16, VERIFY>(p, i, gl, gbase);
-    }
-  }
-}
-
-// DONE (round 2, not taken; no launcher selects it since round 5): the
-// kernel's own completion word for the flush forms.  Measured against the
-// product's second one-lane
-// launch: the submitting core pays less (5.5 -> 3.4 us per 32-frame flush) and
-// a synchronous flush is ~2 us shorter, but every block's agent-scope release
-// writes back L2 (gfx950: agent scope spans the XCDs' separate L2s), and the
-// feeder's sweeps and concurrent flushes get slower (8 threads: 26 against 31
-// M frames/s; profiles/r02/r02am).  Every block makes its stores visible at
-// agent scope and counts itself in (acquire-release on a device-memory
-// counter); the last one resets the counter and release-stores the sequence
-// number into the pinned word the host polls, at system scope.  Vector atomics
-// on device memory only.
-__device__ __forceinline__ void block_done(const tasx_tcp4_params &p)
-{
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(p.done_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1u) {
-      __hip_atomic_store(p.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.done_word, p.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        tcp4_tas_frame<U, VERIFY>(p, i, gl, gbase);
     }
   }
 }
 
 // FLOW (RX, with VERIFY): the frames' flow lookup (fast_flows_packet_fss,
 // tas/fast/fast_flows.c:1084-1163) in the same launch.
-//  kFlowSplit / kFlowSplit1 (the round-2 product, A/B 36 / 27): the grid's first blocks run
-//   flow_lookup_lanes, F frames per lane (F BS consecutive frames per block),
-//   the rest are the verify blocks.  The lookup's dependent chain (key ->
-//   bucket -> flow key) is the long one, so its blocks start first and
-//   overlap the verify rows instead of forming the grid's tail.  64K received
-//   frames: 1.24-1.40x the two kernels in turn.
-//  kFlowRow (A/B variant 26): lanes 0..3 of each verify row load the 12-byte
-//   key before the chunk loads, hash it, probe bucket entry h + lane and load
-//   that candidate's key while the chunks land.  Each wave of 4 rows pays a
-//   whole bitwise CRC for 4 frames, and the bucket (issued after the chunks,
-//   vector loads return in order) waits for all of them: slower wherever
-//   ACKs are present.  Measured and not taken either: lookup blocks
-//   interleaved one per BS frames (their chains end the grid), and the key
-//   hashed beside the row's first load with the bucket issued before the
-//   chunks (the per-row CRC stays).
-//  kFlowSplit / kFlowSplit1: two / one frames per lookup lane -- two for
-//   uniform-length (data) bursts, one for the row forms (data/ACK mixes),
-//   the other choice as A/B variant 27.
-//  kFlowInter (round 3): groups of 128 verify blocks followed by 8 lookup
-//   blocks (136 = 17 x 8 blocks, so every block keeps blockIdx % 8: its XCD
-//   under round-robin placement).  Lookup block x of a group takes the 256
-//   frames of the group's verify blocks on its own XCD (x, x + 8, ...), one per
-//   lane, after them; those rows load their first 256 bytes L2-allocating, so
-//   the lookup reads each frame's 12-byte key from that XCD's L2 instead of
-//   fetching the line again.
 //  kFlowSplitX (round 3, the product for the row forms; kFlowSplitX2 for a
 //   uniform received length): the split grid with the lookup blocks first, one
 //   frame per lane, each lookup block taking the frames of the 16 verify blocks
 //   that land on its own XCD (blocks are placed round-robin over the 8 XCDs
 //   by blockIdx; the lookup block count is a multiple of 8, so verify block vb
-//   keeps vb % 8).  The lookup's plain key load leaves the frame's first line in
-//   that XCD's L2, where the verify row's chunk-0 load then finds it.
-//   kFlowSplitX2: the same with two frames per lookup lane (32 verify blocks
-//   per lookup block).
-// LOPT bit of tcp4_tas14_kernel<kHintArr> (A/B): prefetch the hint line one
-// generation ahead; a generation = 256 CUs x 8 blocks of 16 rows (gfx950 at 8
-// waves per SIMD)
-constexpr int kHintPrefetch = 16;
-// LOPT bit (A/B): a stride-mode row the fast path cannot take is redone by the
-// any-layout row body (tcp4_frame_row, as the OFFS forms) instead of
-// tcp4_tas_frame, whose registers spill at 8 waves per SIMD
-constexpr int kRowFallback = 32;
-// LOPT bit (A/B, timing only): a split grid's verify blocks exit at once
-constexpr int kLookupOnly = 64;
-// LOPT bit (A/B, timing only): a split grid's lookup blocks exit at once
-constexpr int kVerifyOnly = 128;
-// LOPT bit (A/B): a split grid's lookup waves run at the highest issue priority
-constexpr int kLookupPrio = 256;
-// LOPT bit (A/B, kHintArr): rows of the second generation of resident blocks
-// take the other half of the hint lines the first generation read (block b
-// and block b + kGenBlocks, same XCD), so their hint loads hit L2 -- no extra
-// instruction, unlike kHintPrefetch.  A generation = 256 CUs x 8 blocks.
-constexpr int kLinePair = 512;
-constexpr uint32_t kGenBlocks = 256u * 8u;
-// frame of row `row` (of 16) in verify block vb of nblk, kLinePair order:
-// blocks 2kG + r and (2k + 1)G + r share hint line kG + r (32 frames); blocks
-// past the last whole pair of generations keep the identity order
-__device__ __forceinline__ uint32_t line_pair_frame(uint32_t vb, uint32_t row, uint32_t nblk)
-{
-  constexpr uint32_t G = kGenBlocks;
-  const uint32_t P = nblk / (2u * G);
-  if (vb >= 2u * G * P)
-    return vb * 16u + row;
-  const uint32_t g = vb / G, r = vb % G;
-  return 32u * ((g / 2u) * G + r) + 16u * (g & 1u) + row;
-}
-constexpr uint32_t kPrefetchRows = 256u * 8u * 16u;
-enum { kFlowNone = 0, kFlowRow = 1, kFlowSplit = 2, kFlowSplit1 = 3, kFlowInter = 4, kFlowSplitX = 5, kFlowSplitX2 = 6 };
+//   keeps vb % 8).  The lookup's dependent chain (key -> bucket -> flow key)
+//   is the long one, so its blocks start first and overlap the verify rows
+//   instead of forming the grid's tail; its plain key load leaves the frame's
+//   first line in that XCD's L2, where the verify row's chunk-0 load then
+//   finds it.  kFlowSplitX2: the same with two frames per lookup lane (32
+//   verify blocks per lookup block).
+//  Measured and not taken (profiles/r02-r04; gone from the source in round 6):
+//   the lookup inside the verify rows, lookup blocks over consecutive frames
+//   (the round-2 product) or interleaved with the verify blocks, hint
+//   prefetch, line-paired generations, issue priority, streamed flow-state keys.
+enum { kFlowNone = 0, kFlowSplitX = 5, kFlowSplitX2 = 6 };
 // lookup blocks of a kFlowSplitX* grid over nv verify blocks (16 F of them per lookup block)
 template <uint32_t F>
 __host__ __device__ constexpr uint32_t splitx_lookup_blocks(uint32_t nv) { return ((nv + 16u * F - 1u) / (16u * F) + 7u) & ~7u; }
-constexpr uint32_t kInterV = 128u, kInterL = 8u; // verify / lookup blocks per group
-// frames per lane of a split grid's lookup blocks
-template <int FLOW>
-constexpr uint32_t split_frames() { return FLOW == kFlowSplit1 ? 1u : 2u; }
-template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int BS = kBlock, bool DONE = false,
-          int FLOW = kFlowNone, int LOPT = 0>
-__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
+template <int U, int MODE, bool VERIFY = false, int WPE = 1, bool OFFS = false, int FLOW = kFlowNone>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_kernel(tasx_tcp4_params p)
 {
+  constexpr int BS = kBlock;
   static_assert(U == 6, "one round of 96 chunks covers the 1522-byte datagram bound");
   static_assert(!(OFFS && MODE == kHint), "uniform hints are a stride-mode form");
   static_assert(FLOW == kFlowNone || VERIFY, "the fused flow lookup is an RX form");
-  static_assert((FLOW != kFlowSplit && FLOW != kFlowSplit1 && FLOW != kFlowSplitX && FLOW != kFlowSplitX2) || !DONE,
-                "split grids post no completion word");
   const int gl = threadIdx.x & 15;
   // this block's verify block (split grids: below); large batches XCD-ordered
   uint32_t vb = FLOW == kFlowNone ? xcd_run(blockIdx.x, gridDim.x, p.xrun) : blockIdx.x;
-  // kFlowRow: CRC32C from slice-by-4 tables the block builds in LDS first (before
-  // any row leaves: every wave reaches the barriers; the bitwise CRC cost every
-  // verify wave ~300 VALU)
-  __shared__ uint32_t lt[FLOW == kFlowRow ? 4 : 1][256];
-  if constexpr (FLOW == kFlowRow) {
-    static_assert(BS == 256, "one table entry per thread");
-    uint32_t c = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      c = (c >> 1) ^ (kPoly & (0u - (c & 1u)));
-    lt[0][threadIdx.x] = c;
-    __syncthreads();
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      c = (c >> 8) ^ lt[0][c & 0xffu];
-      lt[k][threadIdx.x] = c;
-    }
-    __syncthreads();
-  }
-  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1) {
-    // the lookup blocks first: their dependent chains are the long ones, so
-    // they start at once and overlap the verify blocks instead of forming the
-    // grid's tail (interleaved one per BS frames they did: DESIGN.md 5.2)
-    constexpr uint32_t kF = split_frames<FLOW>(); // frames per lookup lane (flow_kernels.hip: kFlowFramesPerLane)
-    const uint32_t nl = (uint32_t) (((uint64_t) p.n + BS * kF - 1u) / (BS * kF)); // 64-bit: n near 2^32
-    if (blockIdx.x < nl) {
-      flow_lookup_lanes<kF, BS, LOPT>(p, blockIdx.x);
-      return;
-    }
-    vb = blockIdx.x - nl;
-  }
   if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2) {
     static_assert(BS == 256, "16 verify rows per block, one lookup lane per row of 16 blocks");
     constexpr uint32_t kF = FLOW == kFlowSplitX2 ? 2u : 1u;
     const uint32_t nl = splitx_lookup_blocks<kF>((uint32_t) (((uint64_t) p.n + BS / 16 - 1u) / (BS / 16)));
     if (blockIdx.x < nl) {
-      if constexpr ((LOPT & kVerifyOnly) != 0)
-        return; // A/B timing: the verify blocks alone
-      if constexpr ((LOPT & kLookupPrio) != 0)
-        __builtin_amdgcn_s_setprio(3); // A/B: the lookup waves' instructions issue first
       // lane t, frame f: row t % 16 of verify block 8 (16 F (b / 8) + 16 f + t / 16) + b % 8 (past the batch: no store)
       const uint32_t b = blockIdx.x;
       uint32_t i0[kF];
@@ -902,56 +758,16 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (uint32_t f = 0; f < kF; ++f) {
         const uint32_t vbk = 8u * (16u * kF * (b / 8u) + 16u * f + threadIdx.x / 16u) + (b & 7u);
         i0[f] = vbk * (BS / 16) + (threadIdx.x & 15u);
-        if constexpr ((LOPT & kLinePair) != 0) // the verify rows' frame order (past the batch: still >= n)
-          i0[f] = line_pair_frame(vbk, threadIdx.x & 15u, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
       }
-      flow_lookup_lanes_at<kF, BS, LOPT>(p, i0);
+      flow_lookup_lanes_at<kF, BS>(p, i0);
       return;
     }
-    if constexpr ((LOPT & kLookupOnly) != 0)
-      return; // A/B timing: the lookup blocks alone
     vb = blockIdx.x - nl;
   }
-  if constexpr (FLOW == kFlowInter) {
-    static_assert(BS == 256, "16 verify rows per block, one lookup lane per frame of 16 blocks");
-    const uint32_t g = blockIdx.x / (kInterV + kInterL), r = blockIdx.x % (kInterV + kInterL);
-    if (r >= kInterV) {
-      // lane t: row t % 16 of the group's verify block x + 8 (t / 16)
-      const uint32_t x = r - kInterV;
-      const uint32_t i0[1] = {(g * kInterV + x + kInterL * (threadIdx.x / 16u)) * (BS / 16) + (threadIdx.x & 15u)};
-      flow_lookup_lanes_at<1, BS, LOPT>(p, i0);
-      return;
-    }
-    vb = g * kInterV + r;
-  }
-  uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
-  if constexpr ((LOPT & kLinePair) != 0 && MODE == kHintArr && BS == 256)
-    i = line_pair_frame(vb, threadIdx.x / 16, (uint32_t) (((uint64_t) p.n + 15u) / 16u));
-  uint32_t hs = 0; // kHintArrS: the row's hint
-  if constexpr (MODE == kHintArrS) {
-    // The block's rows take its frames long ones first (stable), so that the
-    // frames that fit in one chunk per lane (pure ACKs) share waves, and those
-    // waves issue one load instead of U.  Every row reads the block's BS / 16
-    // hints, one per lane, and computes the same permutation: no LDS, no barrier.
-    static_assert(BS / 16 <= 16, "one lane per frame of the block");
-    const uint32_t f0 = vb * (BS / 16), fi = f0 + (uint32_t) gl;
-    const bool mine = gl < BS / 16 && fi < p.n;
-    const uint32_t hh = mine ? ldg(p.flen, fi) : 0u;
-    const bool lng = mine && hh > p.ip_off + 242u; // more than one chunk per lane of a row
-    const uint32_t sh = (threadIdx.x & 63u) & ~15u;
-    const uint32_t lm = (uint32_t) (__builtin_amdgcn_ballot_w64(lng) >> sh) & 0xffffu;
-    const uint32_t below = __builtin_popcount(lm & ((1u << gl) - 1u));
-    const uint32_t dest = lng ? below : (uint32_t) __builtin_popcount(lm) + (uint32_t) gl - below;
-    const uint32_t row = threadIdx.x / 16u;
-    const uint32_t fm = (uint32_t) (__builtin_amdgcn_ballot_w64(dest == row && gl < BS / 16) >> sh) & 0xffffu;
-    const int f = fm ? __builtin_ctz(fm) : 0;
-    hs = (uint32_t) __shfl((int) hh, (int) sh + f, 64);
-    i = f0 + (uint32_t) f;
-  }
+  const uint32_t i = vb * (BS / 16) + threadIdx.x / 16;
   if (i >= p.n)
     return;
   const uint8_t *fb = p.base; // loads at fb + 32-bit offsets
-  const uint8_t *ipp;         // the IPv4 header (FLOW)
   uint32_t a0;
   bool row_ok = true;
   if constexpr (OFFS) {
@@ -959,37 +775,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     row_ok = (fo & 15u) == 0u;
     fb = (const uint8_t *) (uintptr_t) (row_ok ? fo : ((fo + 14u) & ~15ull)); // else: the chunk holding ip[0]
     a0 = 0;
-    ipp = (const uint8_t *) (uintptr_t) (fo + 14u);
   } else {
     a0 = i * (uint32_t) p.stride + (p.ip_off & ~15u);
-    ipp = fb + a0 + 14u;
-  }
-  constexpr int kNb = (int) TASX_FLOWHT_NBSZ;
-  u32x3 fkey = {0u, 0u, 0u};
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) // ip.src, ip.dst, tcp.src | tcp.dst << 16 (little-endian dwords)
-      fkey = *(__attribute__((address_space(1))) const u32x3u *) (ipp + 12);
   }
   // RX: datagram bytes this row may read (rx_bound); TX trusts total_length
   uint32_t have = 65535u;
   if constexpr (VERIFY && MODE != kHint) {
-    const uint32_t b = rx_bound(p, MODE == kHintArrS ? hs : p.flen ? ldg(p.flen, i) : p.flen0);
+    const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
     have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-  }
-  // FLOW (kFlowRow): the key arrived with the hint, so the hash and the bucket
-  // probe go out BEFORE the chunk loads (vector loads complete in order: a
-  // bucket issued after the chunks could be used only once they all landed)
-  uint32_t fh = 0;
-  uint64_t fe = 0;
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) {
-      fh = crc32c_u32_tab(lt, crc32c_u32_tab(lt, crc32c_u32_tab(lt, 0u, fkey.y), fkey.x), (fkey.z >> 16) | (fkey.z << 16));
-      const uint32_t ht = p.ht_entries;
-      const uint32_t hb = (ht & (ht - 1u)) == 0u ? (fh & (ht - 1u)) : fh % ht; // the bucket's first entry
-      const uint32_t ej = hb + (uint32_t) gl;
-      // one subtraction wraps ej < ht + kNb; tables smaller than a bucket take the modulo
-      fe = ldg((const uint64_t *) p.flowht, ht >= (uint32_t) kNb ? (ej >= ht ? ej - ht : ej) : ej % ht);
-    }
   }
   // the datagram [ip, ip + hend): uniform from the hint, or per row from the
   // frame's own total_length; loads clamped to its last chunk (kRoom: to the room)
@@ -1015,7 +808,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
     for (int u = 0; u < U; ++u)
       v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-  } else if constexpr (MODE == kHintArr || MODE == kHintArrP) {
+  } else if constexpr (MODE == kHintArr) {
     // the row's own hint (mbuf data_len) fixes its geometry; lane 15 checks
     // it against total_length afterwards, as kHint does for a uniform hint
     const uint32_t h = ldg(p.flen, i);
@@ -1024,51 +817,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     hend = in_range ? hl : (row_ok ? 20u : 1u);
     const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if constexpr (MODE == kHintArrP) {
-        v[u] = u32x4{0u, 0u, 0u, 0u};
-        if ((uint32_t) gl + 16u * u <= last) // the tail comes from v[last / 16] on lane last % 16
-          v[u] = ld16nt_off(fb, lo + 256u * u);
-      } else if (FLOW == kFlowInter && u == 0) { // the key's line stays in L2 for the lookup block
-        v[u] = ld16_off(fb, min(lo, lastoff));
-      } else {
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-      }
-    }
-  } else if constexpr (MODE == kHintArrS) {
-    const uint32_t hl = hs > p.ip_off ? hs - p.ip_off : 0u;
-    in_range = row_ok && hl >= 38u && hl <= 1522u && hs <= slot_bound(p);
-    hend = in_range ? hl : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4, lastoff = a0 + 16u * last;
-    v[0] = ld16nt_off(fb, min(lo, lastoff));
-    if (__builtin_amdgcn_ballot_w64(last >= 16u) != 0ull) { // a wave-uniform branch
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    } else { // every row of the wave ends in its first 256 bytes; lane 15's v[U-1] = the last chunk
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = v[0];
-    }
-  } else if constexpr (MODE == kHead5) {
-    v[0] = ld16nt_off(fb, row_ok ? a0 + 16u * min((uint32_t) gl, 4u) : a0);
-    const uint32_t tl0 = bswap16(row_newbcast<1>(v[0].x) & 0xffffu);
-    // from 51: the last chunk is chunk 4 or later, so lane 15 holds it
-    in_range = row_ok && tl0 >= 51u && tl0 <= 1522u && tl0 <= have;
-    hend = in_range ? tl0 : (row_ok ? 20u : 1u);
-    const uint32_t last = (14u + hend - 1u) >> 4;
-    if (last > 4u) { // the datagram goes on past chunk 4
-      const uint32_t lastoff = a0 + 16u * last;
-      if (gl > 4)
-        v[0] = ld16nt_off(fb, min(lo, lastoff));
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    } else {
-#pragma unroll
-      for (int u = 1; u < U; ++u)
-        v[u] = v[0]; // excluded below; lane 15's v[U-1] = chunk 4, the last one
-    }
+    for (int u = 0; u < U; ++u)
+      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
   } else { // kRoom
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1077,85 +827,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     in_range = row_ok && tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
     hend = in_range ? tl0 : (row_ok ? 20u : 1u);
   }
-  // LOPT & kHintPrefetch (A/B, kHintArr): after its chunk loads, one lane per
-  // hint line (32 rows) loads the line of the row one generation of resident
-  // rows later, so that row's first load (its hint) is an L2 hit (block b and
-  // block b + kPrefetchRows / 16 run on the same XCD)
-  uint32_t pf = 0;
-  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS) {
-    const uint32_t j = i + kPrefetchRows;
-    if (gl == 0 && (i & 31u) == 0u && j < p.n)
-      pf = ldg(p.flen, j);
-  }
-  // FLOW: the flow-state key load goes out while the chunks are in flight (the
-  // bucket, issued before them, has returned first)
-  uint32_t ffid = 0;
-  u32x3 ck = {0u, 0u, 0u};
-  bool fcand = false;
-  if constexpr (FLOW == kFlowRow) {
-    if (gl < kNb) {
-      const uint32_t ef = (uint32_t) fe, eh = (uint32_t) (fe >> 32);
-      ffid = ef & ((1u << TASX_FLOWHTE_POSSHIFT) - 1u);
-      fcand = (ef & TASX_FLOWHTE_VALID) && eh == fh && ffid < p.fs_num;
-      ck = *(__attribute__((address_space(1))) const u32x3 *) (p.flowst +
-                                                              (uint64_t) (fcand ? ffid : 0u) * p.fs_stride +
-                                                              p.fs_key_off);
-    }
-  }
-  tas14_finish<U, MODE, VERIFY, OFFS, true, (LOPT & kRowFallback) != 0>(p, i, gl, fb, a0, hend, in_range, v);
-  if constexpr ((LOPT & kHintPrefetch) != 0 && MODE == kHintArr && !OFFS)
-    asm volatile("" ::"v"(pf)); // the prefetch is not dead code
-  if constexpr (FLOW == kFlowRow) {
-    const uint32_t ports = (fkey.z >> 16) | (fkey.z << 16);
-    const bool match = gl < kNb && fcand && ck.x == fkey.y && ck.y == fkey.x && ck.z == ports;
-    const uint32_t rm = (uint32_t) (__builtin_amdgcn_ballot_w64(match) >> ((threadIdx.x & 63u) & ~15u)) & 0xfu;
-    const int first = rm ? __builtin_ctz(rm) : 0; // the first matching entry wins
-    if (gl == first)
-      stg(p.fid_out, i, rm ? ffid : TASX_FLOW_NONE);
-    if (gl == 0 && p.hash_out)
-      stg(p.hash_out, i, fh);
-  }
-  if constexpr (DONE)
-    block_done(p);
-}
-
-
-// tcp4_tas14_kernel's total_length-first rows as a persistent loop: row r
-// takes frames r, r + R, r + 2R, ... (R rows in the grid) and loads the next
-// frame's total_length while the current frame's data is in flight, so in the
-// steady state a frame costs one dependent memory latency instead of two
-// (stride mode; TX and RX as tcp4_tas14_kernel<kTlFirst>).
-template <int U, bool VERIFY = false, int WPE = 8>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void tcp4_tas14_rows_kernel(tasx_tcp4_params p)
-{
-  const int gl = threadIdx.x & 15;
-  const uint32_t R = gridDim.x * (kBlock / 16);
-  uint32_t i = blockIdx.x * (kBlock / 16) + threadIdx.x / 16;
-  if (i >= p.n)
-    return;
-  const uint8_t *fb = p.base;
-  const uint32_t ipa = p.ip_off & ~15u;
-  uint32_t tln = bswap16(ldg((const uint32_t *) (fb + i * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
-  for (; i < p.n; i += R) { // row-uniform
-    const uint32_t a0 = i * (uint32_t) p.stride + ipa;
-    uint32_t have = 65535u;
-    if constexpr (VERIFY) {
-      const uint32_t b = rx_bound(p, p.flen ? ldg(p.flen, i) : p.flen0);
-      have = b > p.ip_off + 20u ? min(b - p.ip_off, 65535u) : 20u;
-    }
-    const uint32_t tl0 = tln;
-    const bool in_range = tl0 >= 38u && tl0 <= 1522u && tl0 <= have;
-    const uint32_t hend = in_range ? tl0 : 20u;
-    const uint32_t lo = a0 + 16u * (uint32_t) gl, lastoff = a0 + 16u * ((14u + hend - 1u) >> 4);
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = ld16nt_off(fb, min(lo + 256u * u, lastoff));
-    const uint32_t inext = i + R;
-    if (inext < p.n) // the next frame's total_length, in flight with this frame's data
-      tln = bswap16(ldg((const uint32_t *) (fb + inext * (uint32_t) p.stride + ipa + 16u), 0u) & 0xffffu);
-    tas14_finish<U, kTlFirst, VERIFY, false>(p, i, gl, fb, a0, hend, in_range, v);
-  }
+  tas14_finish<U, MODE, VERIFY, OFFS>(p, i, gl, fb, a0, hend, in_range, v);
 }
 
 // Dynamic LDS reserved (never used) by the v_sad_u16 kernels to cap residency
@@ -1189,21 +861,17 @@ constexpr uint32_t kXrun = 9u; // runs of 2^(9 - 1) = 256 blocks
 
 static uint32_t xrun_for(uint64_t blocks)
 {
-  if (tasx_ext && tasx_ext->xrun) { // the A/B build's override (tasx_ab_set_xrun, TASX_XRUN)
-    const int x = tasx_ext->xrun(blocks);
-    if (x >= 0)
-      return (uint32_t) x;
-  }
   return blocks >= kXrunMinBlocks ? kXrun : 0u;
 }
 
-template <int G = 16, int BS = kBlock, typename K, typename Prm>
+template <typename K, typename Prm>
 int launch_groups(const char *name, K kern, const Prm &p, hipStream_t s, uint32_t lds = 0)
 {
-  // one G-lane group per packet, BS / G groups per block: the grid covers
-  // the batch once (measured faster than persistent grids at these batch
-  // sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
-  constexpr uint64_t fpb = BS / G;
+  // one 16-lane group per packet, kBlock / 16 groups per block: the grid
+  // covers the batch once (measured faster than persistent grids at these
+  // batch sizes: no uneven drain, the dispatcher refills CUs within ~0.5 us)
+  constexpr int BS = kBlock;
+  constexpr uint64_t fpb = BS / 16;
   const uint64_t blocks = ((uint64_t) p.n + fpb - 1) / fpb;
   if (blocks == 0)
     return 0;
@@ -1263,7 +931,7 @@ static bool tas14_offs_ok(const tasx_tcp4_params &p)
 // reads cost every ACK row 1.5 KB (16.0 us at any ACK share) and total_length
 // first wins (25 / 50 / 75 % ACKs: 13.6 / 10.6 / 8.5 us); the head-5 mode
 // (an ACK's 80 bytes with the total_length) lost to it everywhere but all-ACK
-// batches (6.3 against 6.8 us) and is an A/B variant (10).  With per-frame
+// batches (6.3 against 6.8 us).  With per-frame
 // hints each row takes its own hint as its geometry (kHintArr: no dependent
 // total_length read; 0 / 25 / 50 / 75 % ACKs 16.5 / 13.2 / 10.4-10.5 / 8.3 us
 // against 17.0 / 13.6-13.7 / 10.6-10.8 / 8.6 us, all-ACK 7.2 against 6.9).
@@ -1290,37 +958,6 @@ static int launch_tas14_verify(const tasx_tcp4_params &p, int mode, hipStream_t 
   }
 }
 
-// the split grid of tcp4_tas14_kernel<..., kFlowSplit*>: one lookup block per
-// F * BS frames, then the verify blocks
-template <uint32_t F = 2, int BS = kBlock, typename K>
-static int launch_split(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  const uint64_t nv = ((uint64_t) p.n + BS / 16 - 1) / (BS / 16), nl = ((uint64_t) p.n + F * BS - 1) / (F * BS);
-  if (nv == 0)
-    return 0;
-  if (nv + nl > 0x7fffffffull)
-    return -2;
-  tasx_note_kernel(name);
-  hipLaunchKernelGGL(kern, dim3((uint32_t) (nv + nl)), dim3(BS), lds, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// the grid of tcp4_tas14_kernel<..., kFlowInter>: per group of kInterV verify
-// blocks, kInterL lookup blocks after them
-template <typename K>
-static int launch_inter(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
-{
-  const uint64_t nv = ((uint64_t) p.n + kBlock / 16 - 1) / (kBlock / 16);
-  const uint64_t groups = (nv + kInterV - 1) / kInterV, blocks = groups * (kInterV + kInterL);
-  if (nv == 0)
-    return 0;
-  if (blocks > 0x7fffffffull)
-    return -2;
-  tasx_note_kernel(name);
-  hipLaunchKernelGGL(kern, dim3((uint32_t) blocks), dim3(kBlock), lds, s, p);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 // the grid of tcp4_tas14_kernel<..., kFlowSplitX*>: the XCD-matched lookup blocks, then the verify blocks
 template <uint32_t F = 1, typename K>
 static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
@@ -1336,33 +973,16 @@ static int launch_splitx(const char *name, K kern, const tasx_tcp4_params &p, hi
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <bool OFFS, int MODE, int FLOW>
-static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s, uint32_t lds)
+// the RX pass's row forms (no uniform received length): one lookup lane per
+// frame (kFlowSplitX)
+template <bool OFFS, int MODE>
+static int launch_rx_rows(const tasx_tcp4_params &p, hipStream_t s)
 {
-  // kernel names by FLOW: kFlowRow, kFlowSplit, kFlowSplit1, kFlowSplitX (the product), kFlowSplitX2
-  static const char *const names[2][2][5] = {
-      {{"tcp4_tas14_kernel<tl_first,verify,flow_row>", "tcp4_tas14_kernel<tl_first,verify,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,flow>",
-        "tcp4_tas14_kernel<tl_first,verify,flow_xcd2>"},
-       {"tcp4_tas14_kernel<tl_first,verify,offs,flow_row>", "tcp4_tas14_kernel<tl_first,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<tl_first,verify,offs,flow_split1>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>",
-        "tcp4_tas14_kernel<tl_first,verify,offs,flow_xcd2>"}},
-      {{"tcp4_tas14_kernel<hints,verify,flow_row>", "tcp4_tas14_kernel<hints,verify,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,flow_split1>", "tcp4_tas14_kernel<hints,verify,flow>",
-        "tcp4_tas14_kernel<hints,verify,flow_xcd2>"},
-       {"tcp4_tas14_kernel<hints,verify,offs,flow_row>", "tcp4_tas14_kernel<hints,verify,offs,flow_f2>",
-        "tcp4_tas14_kernel<hints,verify,offs,flow_split1>", "tcp4_tas14_kernel<hints,verify,offs,flow>",
-        "tcp4_tas14_kernel<hints,verify,offs,flow_xcd2>"}}};
-  static_assert(FLOW == kFlowRow || FLOW == kFlowSplit || FLOW == kFlowSplit1 || FLOW == kFlowSplitX ||
-                    FLOW == kFlowSplitX2, "a row form of the RX pass");
-  const int fi = FLOW == kFlowRow ? 0 : FLOW == kFlowSplit ? 1 : FLOW == kFlowSplit1 ? 2 : FLOW == kFlowSplitX ? 3 : 4;
-  const char *name = names[MODE == kHintArr][OFFS][fi];
-  auto kern = tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kBlock, false, FLOW>;
-  if constexpr (FLOW == kFlowSplit || FLOW == kFlowSplit1)
-    return launch_split<split_frames<FLOW>()>(name, kern, p, s, lds);
-  if constexpr (FLOW == kFlowSplitX || FLOW == kFlowSplitX2)
-    return launch_splitx<FLOW == kFlowSplitX2 ? 2u : 1u>(name, kern, p, s, lds);
-  return launch_groups(name, kern, p, s, lds);
+  static const char *const names[2][2] = {
+      {"tcp4_tas14_kernel<tl_first,verify,flow>", "tcp4_tas14_kernel<tl_first,verify,offs,flow>"},
+      {"tcp4_tas14_kernel<hints,verify,flow>", "tcp4_tas14_kernel<hints,verify,offs,flow>"}};
+  return launch_splitx<1u>(names[MODE == kHintArr][OFFS], tcp4_tas14_kernel<6, MODE, true, 8, OFFS, kFlowSplitX>, p,
+                           s, 0u);
 }
 
 // tcp4_tas14_kernel without a uniform hint, in the mode the room allows.  Built for 8 waves per SIMD (64 VGPRs; the
@@ -1381,9 +1001,6 @@ static int launch_tas14_rows(const tasx_tcp4_params &p, int mode, hipStream_t s)
   case kRoom:
     return launch_groups(OFFS ? "tcp4_tas14_kernel<room,offs>" : "tcp4_tas14_kernel<room>",
                          tcp4_tas14_kernel<6, kRoom, false, 8, OFFS>, p, s, lds);
-  case kHead5:
-    return launch_groups(OFFS ? "tcp4_tas14_kernel<head5,offs>" : "tcp4_tas14_kernel<head5>",
-                         tcp4_tas14_kernel<6, kHead5, false, 8, OFFS>, p, s, lds);
   default:
     return launch_groups(OFFS ? "tcp4_tas14_kernel<tl_first,offs>" : "tcp4_tas14_kernel<tl_first>",
                          tcp4_tas14_kernel<6, kTlFirst, false, 8, OFFS>, p, s, lds);

@@ -25,8 +25,8 @@ from pathlib import Path
 import torch  # noqa: F401  -- must be imported first: libtasx then binds torch's HIP runtime
 
 _LIB_DIR = Path(__file__).resolve().parent / "_lib"
-# TASX_LIB: another in-tree build of the library (the A/B build
-# tas_amd/_lib/libtasx_ab.so, or a kernel revision from tools/ab_lib.sh)
+# TASX_LIB: another in-tree build of the library (e.g. the comparison build
+# tas_amd/_lib/libtasx_ab.so)
 _LIB_PATH = Path(os.environ.get("TASX_LIB") or _LIB_DIR / "libtasx.so")
 AB_LIB_PATH = _LIB_DIR / "libtasx_ab.so"
 _lib = None
@@ -117,16 +117,15 @@ SIGNATURES = {
 }
 
 
-# A/B build only (include/tasx_ab.h)
+# the comparison build only (include/tasx_ab.h)
 AB_SIGNATURES = {
-    "tasx_set_diag_buffer": (_c_int, [_vp]),
     "tasx_ab_flow_pattern": (_c_int, [_vp, _c_u64, _c_u32, _c_u32, _vp, _c_u32, _vp, _c_u32, _c_u32, _c_u32, _vp,
                                       _vp]),
     "tasx_ab_tcp4_pattern": (_c_int, [_vp, _c_u64, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ab_tcp4_mix_pattern": (_c_int, [_vp, _c_u64, _c_u32, _vp, _c_u32, _c_int, _vp, _vp]),
     "tasx_ab_stream_copy": (_c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
     "tasx_ab_stream_read": (_c_int, [_vp, ctypes.c_size_t, _c_int, _vp, _vp]),
-    "tasx_ab_set_xrun": (_c_int, [_c_int]),
+    "tasx_ab_tx_segment_form": (_c_int, [_c_int, _vp, _c_u64, _vp, _vp, _c_u32, _c_u32, _c_u32, _vp, _vp]),
     "tasx_ab_ctx_set_tickets": (_c_int, [_uns, _c_u32]),
 }
 
@@ -172,8 +171,8 @@ def lib() -> ctypes.CDLL:
 
 class using_library:
     """Route this module's calls through another build of the library for the
-    duration of a with-block (the A/B build for variant tests:
-    ``with xsum.using_library(xsum.AB_LIB_PATH): ...``).  Both builds are
+    duration of a with-block (``with xsum.using_library(xsum.AB_LIB_PATH):
+    ...``: the comparison build behaves as the product).  Both builds are
     linked -Bsymbolic and loaded RTLD_LOCAL, so they coexist in one process."""
 
     def __init__(self, path):

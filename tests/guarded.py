@@ -53,14 +53,26 @@ def hip():
             "hipMemUnmap": [vp, sz],
             "hipMemRelease": [vp],
             "hipMemAddressFree": [vp, sz],
-            "hipMemcpy": [vp, vp, sz, ctypes.c_int],
-            "hipMemset": [vp, ctypes.c_int, sz],
             "hipDeviceSynchronize": [],
         }.items():
             f = getattr(h, name)
             f.argtypes, f.restype = args, ctypes.c_int
         _HIP = h
     return _HIP
+
+
+class _Cai:
+    """A device range as __cuda_array_interface__ (torch.as_tensor wraps it
+    without a copy)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
+def _view(ptr: int, nbytes: int, device: int):
+    import torch
+    return torch.as_tensor(_Cai(ptr, nbytes), device=f"cuda:{device}")
 
 
 def _ok(rc: int, what: str) -> None:
@@ -92,30 +104,34 @@ class Guarded:
         self.nbytes = nbytes
         # the data: flush against the mapping's end or its start
         self.addr = self.map_base + (self.mapped - nbytes if at == "end" else 0)
-        # (hipMemset is asynchronous for device memory, and a copy into a
-        # virtual-memory mapping is not ordered behind it: each step waits)
-        _ok(h.hipMemset(self.map_base, 0, self.mapped), "hipMemset")
-        _ok(h.hipDeviceSynchronize(), "hipDeviceSynchronize")
+        # Data moves in and out by device kernels through torch views of the
+        # mapping (never by hipMemset / hipMemcpy into it: those copies went
+        # around the L2, and kernels then read stale lines of the mapping --
+        # results wrong in a 64 KiB stretch, profiles/r06/INDEX.md r06a-r06b)
+        self._all = _view(self.map_base, self.mapped, device)
+        self._all.zero_()
+        self.data = self._all[self.addr - self.map_base:self.addr - self.map_base + nbytes]
 
     def upload(self, a: np.ndarray, offset: int = 0) -> None:
-        a = np.ascontiguousarray(a)
+        import torch
+        a = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
         assert offset + a.nbytes <= self.nbytes
-        _ok(hip().hipMemcpy(self.addr + offset, a.ctypes.data, a.nbytes, 1), "hipMemcpy H2D")
-        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        self.data[offset:offset + a.nbytes].copy_(torch.from_numpy(a.copy()).cuda())
+        torch.cuda.synchronize()
         # the data as the kernels will see it (a mismatch later is theirs)
-        back = self.download()[offset:offset + a.nbytes]
-        assert np.array_equal(back, a.reshape(-1).view(np.uint8)), "upload into the guarded mapping did not land"
+        assert np.array_equal(self.download()[offset:offset + a.nbytes], a), "upload into the guarded mapping"
 
     def download(self) -> np.ndarray:
-        out = np.empty(self.nbytes, np.uint8)
-        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
-        _ok(hip().hipMemcpy(out.ctypes.data, self.addr, self.nbytes, 2), "hipMemcpy D2H")
-        _ok(hip().hipDeviceSynchronize(), "hipDeviceSynchronize")
+        import torch
+        torch.cuda.synchronize()
+        out = self.data.clone().cpu().numpy()
+        torch.cuda.synchronize()
         return out
 
     def free(self) -> None:
         if self.va:
             h = hip()
+            self.data = self._all = None
             h.hipDeviceSynchronize()
             h.hipMemUnmap(self.map_base, self.mapped)
             h.hipMemRelease(self.handle)

@@ -169,10 +169,14 @@ def test_room_contract_errors(L):
 
 
 def test_both_builds_coexist_in_one_process(L):
-    """The A/B build loads next to the product (-Bsymbolic, RTLD_LOCAL): each
-    keeps its own variant range."""
+    """The comparison build loads next to the product (-Bsymbolic, RTLD_LOCAL):
+    each keeps its own error state, and only it has the comparison entry points."""
     from tas_amd import xsum
+    assert L.tasx_set_kernel_variant(-1) == -errno.EINVAL
     with xsum.using_library(xsum.AB_LIB_PATH) as ab:
-        assert ab.tasx_set_kernel_variant(8) == 0
+        assert ab.tasx_set_kernel_variant(5) == -errno.EINVAL
+        assert b"variant 5" in ab.tasx_last_error()
         assert ab.tasx_set_kernel_variant(0) == 0
-    assert L.tasx_set_kernel_variant(8) == -errno.EINVAL
+        assert ab.tasx_ab_stream_read(None, 1024, 0, None, None) == -errno.EINVAL
+    assert b"variant -1" in L.tasx_last_error()
+    assert not hasattr(L, "tasx_ab_stream_read")

@@ -102,35 +102,22 @@ def _gpu(frames, n, flowht, flowst, fs_num, stride=0, offsets=None, want_hash=Tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 13])
-def test_gpu_flow_golden(flow_golden, variant):
-    """Every kernel variant (CRC bitwise / LDS slice-by-4, key by bytes /
-    chunks, 2 / 4 frames per lane, L2-allocating keys (9: the round-3
-    product), non-temporal flow-state keys (10)) on the fixture."""
+def test_gpu_flow_golden(flow_golden):
+    """The lookup on the fixture (round 6 retired the comparison variants:
+    CRC forms, frames per lane, key cache policies, the partitioned lookup)."""
     from tas_amd import xsum
     g = flow_golden
     n = len(g["expected_fid"])
-    import contextlib
-    # the CRC / key-load variants are A/B-build kernels (include/tasx_ab.h)
-    with (xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()):
-        xsum.set_kernel_variant(variant)
-        try:
-            h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
-            assert xsum.last_kernel().startswith("flow_route_kernel" if variant == 11 else "flow_lookup_kernel")
-        finally:
-            xsum.set_kernel_variant(0)
+    h, fid = _gpu(g["frames"], n, g["flowht"], g["flowst"], int(g["fs_num"]), stride=int(g["stride"]))
+    assert xsum.last_kernel() == "flow_lookup_kernel"
     np.testing.assert_array_equal(h, g["expected_hash"])
     np.testing.assert_array_equal(fid, g["expected_fid"])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 6, 7, 9, 10, 11, 12, 13])
-def test_gpu_flow_vs_oracle_large(oracle, variant):
+def test_gpu_flow_vs_oracle_large(oracle):
     """64K flows in a TAS-sized table (2x entries), 256K frames: hits in random
-    order, misses (unknown keys), hash-out off; the product and the 2 / 4
-    frames-per-lane forms (A/B 6, 7), 9-13, with a ragged batch end."""
-    import contextlib
-    from tas_amd import xsum
+    order, misses (unknown keys), hash-out off, with a ragged batch end."""
     nflows, ent, n = 65536, 131072, 262144
     keys = pktgen.flow_keys(nflows, seed=5)
     fs = pktgen.flow_state(keys, seed=5)
@@ -145,21 +132,16 @@ def test_gpu_flow_vs_oracle_large(oracle, variant):
     fkeys[miss, 4] ^= 0x5A  # unknown remote ip
     fr = pktgen.rx_frames(fkeys, stride=128, seed=6)
     eh, ef = oracle.flow_lookup_batch(fr, n, ht, fs, fs_num=nflows, stride=128)
-    with (xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()):
-        xsum.set_kernel_variant(variant)
-        try:
-            h, fid = _gpu(fr, n, ht, fs, nflows, stride=128)
-            np.testing.assert_array_equal(h, eh)
-            np.testing.assert_array_equal(fid, ef)
-            assert (fid[miss] == 0xFFFFFFFF).all()
-            _, fid2 = _gpu(fr, n, ht, fs, nflows, stride=128, want_hash=False)
-            np.testing.assert_array_equal(fid2, ef)
-            m = n - 777                                          # ragged end
-            h3, fid3 = _gpu(fr, m, ht, fs, nflows, stride=128)
-            np.testing.assert_array_equal(fid3, ef[:m])
-            np.testing.assert_array_equal(h3, eh[:m])
-        finally:
-            xsum.set_kernel_variant(0)
+    h, fid = _gpu(fr, n, ht, fs, nflows, stride=128)
+    np.testing.assert_array_equal(h, eh)
+    np.testing.assert_array_equal(fid, ef)
+    assert (fid[miss] == 0xFFFFFFFF).all()
+    _, fid2 = _gpu(fr, n, ht, fs, nflows, stride=128, want_hash=False)
+    np.testing.assert_array_equal(fid2, ef)
+    m = n - 777                                          # ragged end
+    h3, fid3 = _gpu(fr, m, ht, fs, nflows, stride=128)
+    np.testing.assert_array_equal(fid3, ef[:m])
+    np.testing.assert_array_equal(h3, eh[:m])
 
 
 @pytest.mark.gpu

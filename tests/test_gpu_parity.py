@@ -27,21 +27,19 @@ def _lib():
     torch.cuda.synchronize()
 
 
-# variants that exist only in the A/B build (include/tasx_ab.h)
-AB_VARIANTS = set(range(8, 26)) | {1, 4, 5} | set(range(45, 49))
+# the product's kernel selections (tasx_set_kernel_variant; round 6 retired the
+# comparison build's variants)
+VARIANTS = (0, 2, 3, 6, 7)
 
 
 @contextlib.contextmanager
 def kernel_variant(v: int):
-    """Run the block with kernel variant v selected -- through the A/B build
-    (tas_amd/_lib/libtasx_ab.so) for the variants only it carries."""
-    ctx = xsum.using_library(xsum.AB_LIB_PATH) if v in AB_VARIANTS else contextlib.nullcontext()
-    with ctx:
-        xsum.set_kernel_variant(v)
-        try:
-            yield
-        finally:
-            xsum.set_kernel_variant(0)
+    """Run the block with kernel variant v selected."""
+    xsum.set_kernel_variant(v)
+    try:
+        yield
+    finally:
+        xsum.set_kernel_variant(0)
 
 
 def to_dev(a: np.ndarray) -> torch.Tensor:
@@ -83,7 +81,7 @@ def test_kat_ipv4_header_public(oracle):
     frame[14:34] = np.frombuffer(bytes.fromhex(kat["header_hex"]), np.uint8)
     frame[34:14 + 115] = np.arange(95, dtype=np.uint8) * 7
     exp = oracle.tcp4_batch(frame.copy(), 1, stride=2048)
-    for v in (0, 1, 2, 3, 6):
+    for v in (0, 2, 3, 6):
         with kernel_variant(v):
             for hint in (None, 14 + 115):
                 got = u16(xsum.tcp4_cksum_batch(to_dev(frame), 1, stride=2048, frame_len=hint))
@@ -340,7 +338,7 @@ def test_tcp4_nonstandard_offsets(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 8])
+@pytest.mark.parametrize("variant", [0])
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 4099])
 @pytest.mark.parametrize("ack_frac", [0.0, 0.5, 0.9])
 def test_tcp4_flush_mix_per_frame_hints(oracle, n, ack_frac, variant):
@@ -383,13 +381,13 @@ def test_tcp4_wave_odd_offsets(oracle):
         big[offs[i]:offs[i] + 2048] = frames[i * 2048:(i + 1) * 2048]
     exp = oracle.tcp4_batch(big, n, offsets=offs)
     hint = (14 + 52 + pay).astype(np.int32)
-    for v in (0, 8):
+    for v in (0, 2):
         with kernel_variant(v):
             got = u16(xsum.tcp4_cksum_batch(to_dev(big), n, offsets=to_dev(offs), frame_len=to_dev(hint)))
         np.testing.assert_array_equal(got, exp, err_msg=f"variant {v}")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_tcp4_all_variants_and_hints(oracle, variant):
     """Every kernel variant, with and without frame-length hints (exact, short,
     long, zero, garbage): results follow ip.total_length only."""
@@ -414,7 +412,7 @@ def test_tcp4_all_variants_and_hints(oracle, variant):
             np.testing.assert_array_equal(got, exp, err_msg=f"variant {variant} hint {hint if isinstance(hint, (int, type(None))) else 'array'}")
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 6, 7, 8])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_raw_all_variants(oracle, variant):
     buf, offs, lens = pktgen.raw_mixed(6000, seed=57, sizes=(0, 1, 3, 64, 255, 576, 1500, 1501, 9000), odd=True)
     n = len(lens)
@@ -425,29 +423,7 @@ def test_raw_all_variants(oracle, variant):
         np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [45, 46, 47, 48])
-def test_raw_stride_lane_groups(oracle, variant):
-    """A/B 45-48 (round 4): RAW stride mode with 32 / 64 lanes per packet (3 /
-    2 loads per lane) and without the residency cap -- odd strides and lengths,
-    packets longer than one round (9000 B: several rounds of G*U chunks),
-    empty packets, and config 2's 64K x 1500 B batch."""
-    for L, stride in ((1500, 1500), (1499, 1501), (0, 16), (1, 17), (9000, 9000), (4097, 4112)):
-        n = 2500
-        buf = pktgen.random_bytes(L * 3 + stride + variant, n * stride + 16)
-        exp = oracle.raw_batch(buf, n, stride=stride, len0=L)
-        with kernel_variant(variant):
-            got = u16(xsum.raw_cksum_batch(to_dev(buf), n, stride=stride, len0=L))
-            assert xsum.last_kernel().startswith("raw_sad_kernel<s32,"), xsum.last_kernel()
-        np.testing.assert_array_equal(got, exp, err_msg=f"L={L} stride={stride}")
-    n, L = 65536, 1500
-    d = dev_random(n * L, 2)
-    exp = oracle.raw_batch(d.cpu().numpy(), n, stride=L, len0=L)
-    with kernel_variant(variant):
-        got = u16(xsum.raw_cksum_batch(d, n, stride=L, len0=L))
-    np.testing.assert_array_equal(got, exp)
-
-
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 3])
 def test_tso_with_hints(oracle, variant):
     n, stride = 512, 65552
     frames = pktgen.tcp4_frames(n, payload=0, stride=stride, seed=58,
@@ -1099,13 +1075,15 @@ def test_verify_uniform_hint(oracle, variant):
 # rooms: rows that load ahead of their total_length (tasx_tcp4_cksum_batch_dev_room)
 
 @pytest.mark.parametrize("room", [80, 1536, 2048])
-@pytest.mark.parametrize("variant", [0, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 25])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 def test_tcp4_rooms_every_row_mode(oracle, room, variant):
-    """Stride-mode TAS frames in 2048 B rooms with a room contract: automatic
-    selection and every forced row mode (9 total_length first, 10 head-5, 11
-    whole room, 19 the mix kernel) over data segments, ACKs, total_length 0..90 and 1523..2034
-    (rows the fast path hands to the general body), with no hint, per-frame
-    hints (exact, short, long) and a uniform hint; out of place and in place."""
+    """Stride-mode TAS frames in 2048 B rooms with a room contract: the
+    automatic selection (each row mode the room and the hints select: whole
+    room, total_length first, per-frame hints, the uniform hint) and the
+    general kernels, over data segments, ACKs, total_length 0..90 and
+    1523..2034 (rows the fast path hands to the general body), with no hint,
+    per-frame hints (exact, short, long) and a uniform hint; out of place and
+    in place."""
     n = 5000
     rng = np.random.default_rng(room + variant)
     pay = np.where(rng.random(n) < 0.4, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
@@ -1158,45 +1136,6 @@ def test_tcp4_room_selects_row_mode():
         xsum.tcp4_cksum_batch(frames, n, **kw)
         assert xsum.last_kernel() == name, (kw, xsum.last_kernel())
     torch.cuda.synchronize()
-
-
-@pytest.mark.parametrize("ip_off", [14, 30])
-@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 64, 65, 4099])
-def test_tcp4_mix_kernel_edges(oracle, ip_off, n):
-    """tcp4_mix_kernel (A/B variant 19: per-frame hints + room): batches that end inside a
-    wave's 16 frames, the IPv4 header at 14 and at 30 (the frame start 16 B
-    into the stride slot), every total_length from 0 to 1600 (short frames
-    38..66 done by one lane, data frames 67..1522 by rows, the rest by the
-    general body) and waves with 0..16 data frames; out of place and in place."""
-    stride = 2048
-    rng = np.random.default_rng(1000 + n + ip_off)
-    tl = rng.permutation(np.arange(n) % 1601) if n > 1 else np.array([52])
-    if n >= 64:  # whole waves of one kind: all short, all data, all general
-        tl[:16], tl[16:32], tl[32:48] = 52, 1500, 1600
-    pay = np.clip(tl - 52, 0, pktgen.TCP_MSS).astype(np.int64)
-    base = pktgen.tcp4_frames(n, payload=pay, stride=stride, seed=n)
-    frames = np.zeros_like(base)
-    sh = ip_off - 14
-    frames.reshape(n, stride)[:, sh:] = base.reshape(n, stride)[:, :stride - sh]
-    f = frames.reshape(n, stride)
-    f[:, ip_off + 2] = (tl >> 8) & 0xFF
-    f[:, ip_off + 3] = tl & 0xFF
-    exp = oracle.tcp4_batch(frames.copy(), n, stride=stride, ip_off=ip_off, l4_off=ip_off + 20)
-    hint = to_dev((ip_off + tl).astype(np.int32))
-    kw = dict(stride=stride, ip_off=ip_off, l4_off=ip_off + 20, frame_len=hint, room=stride)
-    d = to_dev(frames)
-    with kernel_variant(19):
-        got = u16(xsum.tcp4_cksum_batch(d, n, **kw))
-        assert xsum.last_kernel() == "tcp4_mix_kernel"
-        np.testing.assert_array_equal(got, exp)
-        xsum.tcp4_cksum_batch(d, n, inplace=True, want_out=False, **kw)
-    h = d.cpu().numpy().reshape(n, stride)
-    np.testing.assert_array_equal(h[:, ip_off + 10:ip_off + 12].copy().view(np.uint16).ravel(), exp[0::2])
-    np.testing.assert_array_equal(h[:, ip_off + 36:ip_off + 38].copy().view(np.uint16).ravel(), exp[1::2])
-    # nothing but the two fields changed
-    h[:, ip_off + 10:ip_off + 12] = f[:, ip_off + 10:ip_off + 12]
-    h[:, ip_off + 36:ip_off + 38] = f[:, ip_off + 36:ip_off + 38]
-    np.testing.assert_array_equal(h, f)
 
 
 @pytest.mark.parametrize("ip_off", [14, 30])
@@ -1256,7 +1195,7 @@ def test_tcp4_room_tso_rows(oracle):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("variant", [0, 9])
+@pytest.mark.parametrize("variant", [0])
 @pytest.mark.parametrize("offs", [False, True])
 @pytest.mark.parametrize("bound", ["len", "room", "none"])
 def test_verify_mix_received_lengths(oracle, variant, offs, bound):
@@ -1265,8 +1204,8 @@ def test_verify_mix_received_lengths(oracle, variant, offs, bound):
     truncated frames, corrupted bytes and checksum fields; stride mode and an
     offsets array; bounded by each frame's received length (its hint: row mode
     <hints,verify>), by a 2048 B room or by nothing but the stride slot / the
-    frame's own total_length (both <tl_first,verify>); A/B variant
-    9 forces total_length-first rows.  Bit-exact against the bounded oracle."""
+    frame's own total_length (both <tl_first,verify>).  Bit-exact against the
+    bounded oracle."""
     n, stride = 8192, 2048
     rng = np.random.default_rng(17 + variant + 2 * offs)
     pay = np.where(rng.random(n) < 0.5, 0, rng.integers(1, pktgen.TCP_MSS + 1, n)).astype(np.int64)
@@ -1295,7 +1234,7 @@ def test_verify_mix_received_lengths(oracle, variant, offs, bound):
     exp = oracle.tcp4_verify_batch_bounded(frames, n, b, stride=stride)
     with kernel_variant(variant):
         got = xsum.tcp4_verify_batch(to_dev(frames), n, **kw)
-        name = f"tcp4_tas14_kernel<{'tl_first' if variant == 9 else mode},verify{',offs' if offs else ''}>"
+        name = f"tcp4_tas14_kernel<{mode},verify{',offs' if offs else ''}>"
         assert xsum.last_kernel() == name
         np.testing.assert_array_equal(got.cpu().numpy(), exp)
 

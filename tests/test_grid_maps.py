@@ -1,13 +1,11 @@
 """The RX pass's grid arithmetic, restated on the CPU (no GPU work): the
-XCD-matched split grid (tcp4_tas14_kernel<..., kFlowSplitX / kFlowSplitX2>,
+XCD-matched split grid (tcp4_tas14_kernel<..., flow>,
 tas_amd/csrc/xsum_kernels.hip, and launch_splitx) must look every frame up
 exactly once, from a lookup block on the same XCD (blockIdx % 8) as the
-frame's verify block, and the line-paired row order (A/B kLinePair,
-line_pair_frame) must be a permutation of the batch; and the XCD-run block
-order of large grids (xcd_run, tas_amd/csrc/xsum_device.h, round 5) must sum
-every block once and give each XCD runs of consecutive blocks.  The GPU tests check the
-kernels at a few batch sizes (tests/test_rx_fused.py, tools/ab_check.py);
-these sweep the formulas over many."""
+frame's verify block; and the XCD-run block order of large grids (xcd_run,
+tas_amd/csrc/xsum_device.h, round 5) must sum every block once and give each
+XCD runs of consecutive blocks.  The GPU tests check the kernels at a few
+batch sizes (tests/test_rx_fused.py); these sweep the formulas over many."""
 import numpy as np
 import pytest
 
@@ -43,36 +41,6 @@ def test_splitx_covers_every_frame_once_on_its_xcd(n, f):
     # the frame's verify block runs at blockIdx nl + vb: same XCD as its lookup block
     vb = frames // ROWS
     assert np.array_equal((nl + vb) % 8, blk[live] % 8)
-
-
-def line_pair_frame(vb, row, nblk, g=256 * 8):
-    """line_pair_frame (xsum_kernels.hip): blocks 2kG + r and (2k + 1)G + r share hint line kG + r."""
-    vb = np.asarray(vb)
-    p = nblk // (2 * g)
-    paired = vb < 2 * g * p
-    gen, r = vb // g, vb % g
-    out = np.where(paired, 32 * ((gen // 2) * g + r) + 16 * (gen & 1) + row, vb * ROWS + row)
-    return out
-
-
-@pytest.mark.parametrize("n", [1, 4096, 65535, 65536, 65537, 70007, 131072, 135000, 262144 + 33])
-def test_line_pair_order_is_a_permutation(n):
-    nblk = (n + ROWS - 1) // ROWS
-    vb = np.repeat(np.arange(nblk), ROWS)
-    row = np.tile(np.arange(ROWS), nblk)
-    frames = line_pair_frame(vb, row, nblk)
-    live = frames[frames < n]
-    assert np.array_equal(np.sort(live), np.arange(n))
-    assert (frames >= n).sum() == nblk * ROWS - n  # only the last block's spare rows fall outside
-
-
-def test_line_pair_shares_hint_lines_across_generations():
-    g, nblk = 256 * 8, 4096  # 64K frames: one pair of generations
-    for vb in (0, 5, g - 1):
-        a = line_pair_frame(np.full(ROWS, vb), np.arange(ROWS), nblk)
-        b = line_pair_frame(np.full(ROWS, vb + g), np.arange(ROWS), nblk)
-        assert set(a // 32) == set(b // 32) and len(set(a // 32)) == 1  # one 128-byte line of 4-byte hints
-        assert vb % 8 == (vb + g) % 8  # the same XCD
 
 
 def xcd_run(b, nb, xrun):

@@ -127,48 +127,11 @@ def test_rx_fused_ragged_and_errors():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("form", ["hint", "hints", "tl_first", "tl_first_offs"])
-def test_rx_fused_row_variant_ab(oracle, form):
-    """A/B variant 26 (libtasx_ab.so): the lookup inside the verify rows
-    instead of in lookup blocks ahead of them -- the same results."""
-    import torch
-    from tas_amd import xsum
-    stride, offs, bound, uniform, kernel = FORMS[form]
-    kernel = kernel.replace(",flow>", ",flow_row>")
-    n = 4096
-    frames, rcv, ht, fs, nflows, _ = _burst(oracle, n, stride, seed=700 + len(form), uniform=uniform)
-    dev = "cuda:0"
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-    kw = dict(offsets=t(np.arange(n, dtype=np.int64) * stride)) if offs else dict(stride=stride)
-    if bound == "uniform":
-        kw["frame_len"] = int(rcv[0])
-        b = int(rcv[0])
-    elif bound == "len":
-        kw["frame_len"] = t(rcv.astype(np.int32))
-        b = rcv.astype(np.uint32)
-    else:
-        b = 0 if offs else stride
-    exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, b, stride=stride)
-    exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=stride)
-    with xsum.using_library(xsum.AB_LIB_PATH):
-        xsum.set_kernel_variant(26)
-        try:
-            flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nflows, **kw)
-            torch.cuda.synchronize()
-            assert xsum.last_kernel() == kernel
-        finally:
-            xsum.set_kernel_variant(0)
-    np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
-    np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
-    np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("ent", [1, 2, 3, 5])
-def test_rx_fused_row_variant_tiny_tables(oracle, ent):
-    """A/B 26 probes bucket entries (h + j) % ht_entries in
-    the verify rows; tables smaller than a bucket (1-3 entries) wrap more
-    than once, and every probe stays inside the table."""
+def test_rx_fused_tiny_tables(oracle, ent):
+    """ADVICE r3 (low): the lookup probes bucket entries (h + j) % ht_entries;
+    tables smaller than a bucket (1-3 entries) wrap more than once, and every
+    probe stays inside the table."""
     import torch
     from tas_amd import xsum
     n, stride = 600, 2048
@@ -181,13 +144,8 @@ def test_rx_fused_row_variant_tiny_tables(oracle, ent):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=stride)
     exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, stride, stride=stride)
-    with xsum.using_library(xsum.AB_LIB_PATH):
-        xsum.set_kernel_variant(26)
-        try:
-            flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nflows, stride=stride)
-            torch.cuda.synchronize()
-        finally:
-            xsum.set_kernel_variant(0)
+    flags, h, fid = xsum.rx_batch(t(frames), n, t(ht), t(fs), nflows, stride=stride)
+    torch.cuda.synchronize()
     np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
     np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
     np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
@@ -195,13 +153,9 @@ def test_rx_fused_row_variant_tiny_tables(oracle, ent):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 27, 32, 36])
-def test_rx_fused_uniform_batch_edges(oracle, variant):
-    """the uniform-received-length grids at the same batch
-    edges -- the product's XCD-matched lookup blocks with two frames per lane,
-    A/B 32 (XCD-matched, one frame per lookup lane), 27 and 36 (lookup blocks
-    over consecutive frames, one / two per lane)."""
-    import contextlib
+def test_rx_fused_uniform_batch_edges(oracle):
+    """the uniform-received-length grid (XCD-matched lookup
+    blocks with two frames per lane) at the same batch edges."""
     import torch
     from tas_amd import xsum
     frames, rcv, ht, fs, nflows, _ = _burst(oracle, 4200, 2048, seed=913, uniform=True)
@@ -209,62 +163,36 @@ def test_rx_fused_uniform_batch_edges(oracle, variant):
     dev = "cuda:0"
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     fr = t(frames)
-    ctx = xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()
-    kernel = {0: "tcp4_tas14_kernel<hint,verify,flow>", 27: "tcp4_tas14_kernel<hint,verify,flow_f1>",
-              32: "tcp4_tas14_kernel<hint,verify,flow_xcd>", 36: "tcp4_tas14_kernel<hint,verify,flow_split2>"}[variant]
-    with ctx:
-        xsum.set_kernel_variant(variant)
-        try:
-            for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096,
-                      4097, 4200):
-                exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
-                exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, int(rcv[0]), stride=2048)
-                flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048, frame_len=int(rcv[0]))
-                torch.cuda.synchronize()
-                assert xsum.last_kernel() == kernel
-                np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
-                np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
-                np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
-        finally:
-            xsum.set_kernel_variant(0)
+    for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096, 4097, 4200):
+        exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
+        exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, int(rcv[0]), stride=2048)
+        flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048, frame_len=int(rcv[0]))
+        torch.cuda.synchronize()
+        assert xsum.last_kernel() == "tcp4_tas14_kernel<hint,verify,flow>"
+        np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+        np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+        np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 26, 27, 28, 35, 36])
-def test_rx_fused_batch_edges(oracle, variant):
+def test_rx_fused_batch_edges(oracle):
     """Batch sizes around row, block and lookup-block boundaries (16 frames
     per verify block, 256 / 512 frames per lookup block, 2048 / 4096 frames per
     8 XCD-matched lookup blocks or per 128-block group): every frame verified
     and looked up once, in the product's split grid (lookup blocks first, each
-    over the frames of the verify blocks on its own XCD), the row form (A/B
-    26), lookup blocks over consecutive frames with two / one frames per lane
-    (A/B 27, and 36 = the round-2 product), lookup blocks after their verify
-    blocks (A/B 28) and the product's grid with two frames per lookup lane (A/B
-    35)."""
-    import contextlib
+    over the frames of the verify blocks on its own XCD)."""
     import torch
     from tas_amd import xsum
     frames, rcv, ht, fs, nflows, _ = _burst(oracle, 4200, 2048, seed=911)
     dev = "cuda:0"
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     fr = t(frames)
-    ctx = xsum.using_library(xsum.AB_LIB_PATH) if variant else contextlib.nullcontext()
-    kernel = {0: "tcp4_tas14_kernel<hints,verify,flow>", 26: "tcp4_tas14_kernel<hints,verify,flow_row>",
-              27: "tcp4_tas14_kernel<hints,verify,flow_f2>", 28: "tcp4_tas14_kernel<hints,verify,flow_inter>",
-              35: "tcp4_tas14_kernel<hints,verify,flow_xcd2>", 36: "tcp4_tas14_kernel<hints,verify,flow_split1>"}[variant]
-    with ctx:
-        xsum.set_kernel_variant(variant)
-        try:
-            for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096,
-                      4097, 4200):
-                exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
-                exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, rcv[:n].astype(np.uint32), stride=2048)
-                flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048,
-                                              frame_len=t(rcv[:n].astype(np.int32)))
-                torch.cuda.synchronize()
-                assert xsum.last_kernel() == kernel
-                np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
-                np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
-                np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)
-        finally:
-            xsum.set_kernel_variant(0)
+    for n in (1, 15, 16, 17, 255, 256, 257, 511, 512, 513, 1024, 1300, 2047, 2048, 2049, 4095, 4096, 4097, 4200):
+        exp_h, exp_fid = oracle.flow_lookup_batch(frames, n, ht, fs, fs_num=nflows, stride=2048)
+        exp_flags = oracle.tcp4_verify_batch_bounded(frames, n, rcv[:n].astype(np.uint32), stride=2048)
+        flags, h, fid = xsum.rx_batch(fr, n, t(ht), t(fs), nflows, stride=2048, frame_len=t(rcv[:n].astype(np.int32)))
+        torch.cuda.synchronize()
+        assert xsum.last_kernel() == "tcp4_tas14_kernel<hints,verify,flow>"
+        np.testing.assert_array_equal(flags.cpu().numpy(), exp_flags)
+        np.testing.assert_array_equal(h.cpu().numpy().view(np.uint32), exp_h)
+        np.testing.assert_array_equal(fid.cpu().numpy().view(np.uint32), exp_fid)

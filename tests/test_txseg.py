@@ -70,33 +70,22 @@ def test_generator_wraps_and_flows():
 # ---------------------------------------------------------------------------
 # GPU parity
 
-# The comparison form of libtasx_ab.so (TASX_TXSEG_DEBUG) that runs here beside
-# the product (tx_segment_lds_kernel) on every case: "r2" = 30, the round-2
-# product tx_segment_tas_kernel (unaligned non-temporal window loads).  Round 6
-# deleted the two forms that left this list in round 5 (ds_read_b128 windows,
-# LDS-DMA staging through inline asm that moved M0): profiles/r06/INDEX.md.
+# The comparison form of libtasx_ab.so that runs here beside the product
+# (tx_segment_lds_kernel) on every TAS-layout case: "r2" =
+# tasx_ab_tx_segment_form(30, ...), the round-2 product tx_segment_tas_kernel
+# (unaligned non-temporal window loads).  Round 6 deleted the two forms that
+# left this list in round 5 (ds_read_b128 windows, LDS-DMA staging through
+# inline asm that moved M0): profiles/r06/INDEX.md.
 IMPLS = ["product", "r2"]
-AB_IMPLS = {"r2": ("30", "tx_segment_tas_kernel")}
 
 
 def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, impl="product"):
-    import os
-    from tas_amd import xsum
-    if impl == "product":
+    if impl == "product" or (ip_off, l4_off) != (14, 34):
         return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
-    dbg, kernel = AB_IMPLS[impl]
-    os.environ["TASX_TXSEG_DEBUG"] = dbg
-    try:
-        with xsum.using_library(xsum.AB_LIB_PATH):
-            r = _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift)
-            if ip_off == 14 and l4_off == 34:
-                assert xsum.last_kernel() == kernel, xsum.last_kernel()
-            return r
-    finally:
-        del os.environ["TASX_TXSEG_DEBUG"]
+    return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift, form=30)
 
 
-def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
+def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, form=None):
     import torch
     from tas_amd import xsum
     dev = "cuda:0"
@@ -107,7 +96,15 @@ def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0):
     s = segs.copy()
     s["frame_off"] += np.uint64(frame_shift)
     dsegs = torch.from_numpy(s.view(np.uint8).copy()).to(dev)
-    out = xsum.tx_segment_batch(dshm[:shm_len], dfr, dsegs, len(s), ip_off=ip_off, l4_off=l4_off)
+    if form is None:
+        out = xsum.tx_segment_batch(dshm[:shm_len], dfr, dsegs, len(s), ip_off=ip_off, l4_off=l4_off)
+    else:
+        out = torch.zeros(max(len(s), 1), dtype=torch.int32, device=dev)
+        with xsum.using_library(xsum.AB_LIB_PATH) as ab:
+            rc = ab.tasx_ab_tx_segment_form(form, dshm.data_ptr(), shm_len, dfr.data_ptr(), dsegs.data_ptr(), len(s),
+                                            ip_off, l4_off, out.data_ptr(), xsum._stream(None))
+            assert rc == 0, ab.tasx_last_error()
+            assert xsum.last_kernel() == "tx_segment_tas_kernel", xsum.last_kernel()
     torch.cuda.synchronize()
     got = dfr.cpu().numpy()
     assert not got[:frame_shift].any() and not got[frame_shift + fr.size:].any(), "wrote outside the frames"

@@ -36,9 +36,6 @@
 
 #include "tasx_xsum.h"
 #include "tasx_oracle.h"
-#ifdef FEEDER_AB /* built against libtasx_ab.so: the flush server's timing sums (TASX_SRV_DIAG=1) */
-#include "tasx_ab.h"
-#endif
 
 #define STRIDE 2048u
 #define BATCH 32u
@@ -262,23 +259,6 @@ int main(int argc, char **argv)
         lat2_all[k] = median(T[k].lat2, T[k].nlat);
         stall += T[k].stall / flushes;
       }
-#ifdef FEEDER_AB
-      if (mode == 2 && getenv("TASX_SRV_DIAG")) {
-        static double prev[MAXT][5]; /* cumulative per ring: report this run's part */
-        double dsum[5] = {0, 0, 0, 0, 0};
-        for (int k = 0; k < n; k++) {
-          double d[5];
-          if (tasx_ab_server_diag(0, (unsigned) k, d) == 0)
-            for (int j = 0; j < 5; j++) {
-              dsum[j] += d[j] - prev[k][j];
-              prev[k][j] = d[j];
-            }
-        }
-        printf("{\"mode\": \"server_diag\", \"threads\": %d, \"in_flight\": %u, \"batches\": %.0f, "
-               "\"detect_to_loaded_us\": %.3f, \"loaded_to_acked_us\": %.3f, \"gap_us\": %.3f, \"empty_polls_per_batch\": %.2f}\n",
-               n, INFLIGHT, dsum[3], dsum[0] / dsum[3], dsum[1] / dsum[3], dsum[2] / dsum[3], dsum[4] / dsum[3]);
-      }
-#endif
       printf("{\"mode\": \"%s\", \"threads\": %d, \"in_flight\": %u, \"flushes_per_thread\": %d, \"frames_per_flush\": %u, "
              "\"core_us_per_flush\": %.3f, \"stall_us_per_flush\": %.3f, \"latency_us\": %.2f, \"latency_from_submit_us\": %.2f, "
              "\"frames_per_s\": %.0f, \"sweeps\": %llu, \"frames_per_sweep\": %.1f}\n",
