@@ -172,6 +172,32 @@ def main():
     ]
     for name, prep, call in cases:
         case(name, prep, call)
+    # HIP maps streams onto at most GPU_MAX_HW_QUEUES (4) hardware queues; a
+    # stream that shares the server's queue waits behind the server's queued
+    # launches (round 5: one long kernel, so such a stream waited until the
+    # stop: profiles/r05 r05q / r05r).  Eight fresh streams, a small kernel
+    # and that stream's synchronize on each.
+    keep_streams = []
+    waits = []
+    fired = []
+    dog = threading.Timer(3 * HOLD, lambda: (fired.append(1), xsum.server_pause(0)))
+    dog.start()
+    for _ in range(8):
+        st = torch.cuda.Stream()
+        keep_streams.append(st)
+        with torch.cuda.stream(st):
+            x = torch.ones(1024, device="cuda")
+            x.add_(1)
+        t = time.perf_counter()
+        st.synchronize()
+        waits.append(round(time.perf_counter() - t, 5))
+        keep.append(x)
+    dog.cancel()
+    dog.join()
+    if fired:
+        xsum.server_resume(0)
+    print(json.dumps({"call": "a small kernel + hipStreamSynchronize on each of 8 fresh streams",
+                      "seconds_per_stream": waits, "waited_until_pause": bool(fired)}), flush=True)
     stop.set()
     ft.join()
     ep = xsum.server_epochs(0)
