@@ -2041,7 +2041,13 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
 #define SRV_COLD_US 2000u /* idle time from which a ring's header alone is polled */
-#define SRV_K 2u          /* workgroups per ring (tasx_srv_params.k): profiles/r04/r04g */
+/* workgroups per ring (tasx_srv_params.k).  One since round 6: with 8 cores
+ * flushing 3 batches in flight, two per ring (round 4, profiles/r04/r04g)
+ * cost a device-resident batch on the same GPU 1.42-1.53x its time, one per
+ * ring 1.13x, at the same flush rate (profiles/r06/INDEX.md r06d): the frame
+ * reads in flight through the XCDs' L2s are what the tax is made of, and a
+ * ring's next queued slot is paired with the one taken anyway. */
+#define SRV_K 1u
 #define SRV_QUEUED 2u     /* epochs outstanding on the server's stream */
 
 struct fserver {
