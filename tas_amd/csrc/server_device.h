@@ -114,6 +114,9 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 // against 16.5-16.6 M segments/s at 8 x 3, 18.6-19.6 against 16.8-17.8 us at
 // 1 x 1, profiles/r04/r04z); 128 VGPRs, no scratch.
 constexpr int kSrvTxU = 6;
+// frames of a paired slot (its entries come with the poll: TAS flushes
+// TXBUF_SIZE = 32 frames at most, /root/reference/tas/include/fastpath.h:38)
+constexpr uint32_t kSrvPairFB = 32u;
 
 // The frame-load cache policies measured in round 4 (no acquire, system-scope
 // loads, write-through TX stores, no release, ...; profiles/r04/INDEX.md
@@ -146,10 +149,11 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
   // (lanes 0-1), the control word (lane 2) and, with the entries, the two
-  // header words of the workgroup's next position p + K (lanes 3-4: the pair
-  // below).
+  // header words of the workgroup's next position p + K (lanes 3-4) and that
+  // slot's first kSrvPairFB entry words (lanes 0-31), all in the same round
+  // trip: the pair below costs no extra one.
   struct SlotRead {
-    uint64_t e, hw;
+    uint64_t e, hw, e2;
   };
   auto read_slot = [&](bool entries) {
     const uint8_t *slot = ring + TASX_SRV_SLOTP(r, p);
@@ -160,6 +164,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
            : lane == 2 ? ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL))
            : (lane < 5 && entries) ? ld_sys64((const uint64_t *) next + (lane - 3))
                                    : 0ull;
+    v.e2 = (entries && lane < (int) kSrvPairFB) ? ld_sys64((const uint64_t *) (next + TASX_SRV_HDR) + lane) : 0ull;
     return v;
   };
   // A read of position p: 1 = the batch is complete (taken: its descriptors
@@ -210,21 +215,20 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
       // The pair (round 6): when this workgroup's next
       // position p + K is queued too -- a checksum slot of the same frame
-      // region whose frames fit the 64 rows beside these -- it is taken in the
-      // same poll round, so ONE system-scope acquire (below) covers both
-      // batches and the rows sum them at once.  Its header came with this
-      // read; its entries take one more round trip (the host wrote them before
-      // that header), tags checked; anything else is left for the next round.
+      // region, at most kSrvPairFB frames (TAS's TXBUF_SIZE), that fit the 64
+      // rows beside these -- it is taken in the same poll round, so ONE
+      // system-scope acquire (below) covers both batches and the rows sum them
+      // at once.  Its header and entries came with this read; an entry read
+      // before the host wrote it carries an older tag, and then the slot is
+      // left for the next round.
       uint32_t n2 = 0u;
       if (!seg && !torn) {
         const uint64_t tag2 = (uint64_t) ((p + K + 1u) & 0xffffu);
         const uint64_t g0 = rlane64(v.hw, 3), g1 = rlane64(v.hw, 4);
         const uint32_t m = (uint32_t) (g0 & 0x7fffu);
-        if ((g0 >> 48) == tag2 && (g1 >> 48) == tag2 && !(g0 & TASX_SRV_SEG) && m >= 1u && n + m <= TASX_SRV_FB &&
-            ((g0 ^ h0) & 0xffffffff0000ull) == 0ull && ((g1 ^ h1) & 0xffffffffffffull) == 0ull) {
-          const uint64_t e2 = (uint32_t) lane < m
-                                  ? ld_sys64((const uint64_t *) (ring + TASX_SRV_SLOTP(r, p + K) + TASX_SRV_HDR) + lane)
-                                  : 0ull;
+        if ((g0 >> 48) == tag2 && (g1 >> 48) == tag2 && !(g0 & TASX_SRV_SEG) && m >= 1u && m <= kSrvPairFB &&
+            n + m <= TASX_SRV_FB && ((g0 ^ h0) & 0xffffffff0000ull) == 0ull && ((g1 ^ h1) & 0xffffffffffffull) == 0ull) {
+          const uint64_t e2 = v.e2;
           if (__builtin_amdgcn_ballot_w64((uint32_t) lane < m && (e2 >> 48) != tag2) == 0ull) {
             n2 = m;
             if ((uint32_t) lane < m) {

@@ -30,3 +30,38 @@ def raw_golden():
 def tcp4_golden():
     with np.load(GOLDEN / "tcp4_vectors.npz") as z:
         return {k: z[k] for k in z.files}
+
+
+# Contexts a GPU test leaves initialised keep their pinned frame / shm regions
+# registered with HIP (tasx_ctx_register_frames); if the test's host memory
+# is then freed, HIP still maps the old range.  Reported per test at the end
+# of the session (round 6: the r06e illegal address surfaced at a plain D2H
+# copy after a clean synchronize).
+_CTX_LEAKS = []
+
+
+@pytest.fixture(autouse=True)
+def _ctx_leak_check(request):
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    try:
+        from tas_amd import xsum
+    except Exception:
+        return
+    if getattr(xsum, "_lib", None) is None:
+        return
+    left = []
+    for c in range(16):
+        try:
+            xsum.ctx_stats(c)
+            left.append(c)
+        except Exception:
+            pass
+    if left:
+        _CTX_LEAKS.append((request.node.nodeid, left))
+
+
+def pytest_terminal_summary(terminalreporter):
+    for nodeid, left in _CTX_LEAKS:
+        terminalreporter.write_line(f"CTX LEAK after {nodeid}: contexts {left} still initialised")

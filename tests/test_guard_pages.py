@@ -56,8 +56,10 @@ def _sync_u32(t: torch.Tensor) -> np.ndarray:
 # ---------------------------------------------------------------------------
 # TX segment build
 
-def _txseg_fenced(oracle, shm, sl, fr, segs, frames_at, shm_at):
-    """fr trimmed to its furthest frame byte, all three buffers fenced."""
+def _txseg_fenced(oracle, shm, sl, fr, segs, frames_at, shm_at, impl="product"):
+    """fr trimmed to its furthest frame byte, all three buffers fenced.
+    impl "r2": the comparison build's round-2 kernel (tx_segment_tas_kernel,
+    tasx_ab_tx_segment_form 30), the form r06e's fault surfaced after."""
     fend = int((segs["frame_off"].astype(np.int64) + segs["hdrs_len"] + segs["payload"]).max())
     fr = np.ascontiguousarray(fr[:fend])
     exp_fr = fr.copy()
@@ -65,18 +67,29 @@ def _txseg_fenced(oracle, shm, sl, fr, segs, frames_at, shm_at):
     with _fenced(fr, frames_at) as gf, _fenced(np.ascontiguousarray(shm[:sl]), shm_at) as gs, \
             _fenced(segs.view(np.uint8), "end") as gd:
         assert gd.addr % 16 == 0
-        out = xsum.tx_segment_batch(gs.addr, gf.addr, gd.addr, len(segs), shm_len=sl)
-        got_out = _sync_u32(out)
-        got_fr = gf.download()
-        kernel = xsum.last_kernel()
+        if impl == "product":
+            out = xsum.tx_segment_batch(gs.addr, gf.addr, gd.addr, len(segs), shm_len=sl)
+            got_out = _sync_u32(out)
+            got_fr = gf.download()
+            kernel = xsum.last_kernel()
+        else:
+            out = torch.zeros(len(segs), dtype=torch.int32, device=DEV)
+            with xsum.using_library(xsum.AB_LIB_PATH) as ab:
+                rc = ab.tasx_ab_tx_segment_form(30, gs.addr, sl, gf.addr, gd.addr, len(segs), 14, 34, out.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream)
+                assert rc == 0, ab.tasx_last_error()
+                got_out = _sync_u32(out)
+                got_fr = gf.download()
+                kernel = xsum.last_kernel()
     np.testing.assert_array_equal(got_out, exp)
     np.testing.assert_array_equal(got_fr, exp_fr)
     return kernel
 
 
+@pytest.mark.parametrize("impl", ["product", "r2"])
 @pytest.mark.parametrize("frames_at", ["start", "end"])
 @pytest.mark.parametrize("shm_at", ["start", "end"])
-def test_guard_txseg_packed_odd_frames(oracle, frames_at, shm_at):
+def test_guard_txseg_packed_odd_frames(oracle, frames_at, shm_at, impl):
     """r05end's failing input: frames packed at stride 1515 (15 of 16 off
     16-byte alignment: the general body; 1 of 16 aligned: the LDS rows)."""
     n, stride = 1024, 1515
@@ -90,11 +103,13 @@ def test_guard_txseg_packed_odd_frames(oracle, frames_at, shm_at):
         s = segs.copy()
         s["frame_off"] += np.uint64(shift)
         f = np.concatenate([np.zeros(shift, np.uint8), fr])
-        assert _txseg_fenced(oracle, shm, sl, f, s, frames_at, shm_at) == "tx_segment_lds_kernel"
+        kernel = _txseg_fenced(oracle, shm, sl, f, s, frames_at, shm_at, impl)
+        assert kernel == ("tx_segment_lds_kernel" if impl == "product" else "tx_segment_tas_kernel")
 
 
+@pytest.mark.parametrize("impl", ["product", "r2"])
 @pytest.mark.parametrize("shm_at", ["start", "end"])
-def test_guard_txseg_wraps_and_region_edges(oracle, shm_at):
+def test_guard_txseg_wraps_and_region_edges(oracle, shm_at, impl):
     """Every buffer wrap after 1..60 payload bytes, payloads at the very start
     and the very end of the shm region, other header lengths (general body)."""
     tx_len, nfl = 1600, 64
@@ -123,16 +138,17 @@ def test_guard_txseg_wraps_and_region_edges(oracle, shm_at):
     segs[-1], segs[-4] = segs[-4].copy(), segs[-1].copy()
     f[[-1, -4]] = f[[-4, -1]]
     segs["frame_off"] = np.arange(n, dtype=np.uint64) * np.uint64(2048)
-    _txseg_fenced(oracle, shm, shm_len, fr, segs, "end", shm_at)
+    _txseg_fenced(oracle, shm, shm_len, fr, segs, "end", shm_at, impl)
 
 
+@pytest.mark.parametrize("impl", ["product", "r2"])
 @pytest.mark.parametrize("odd,tx_len,nflows", [(True, 1500, 7), (False, 16384, 512)])
-def test_guard_txseg_random(oracle, odd, tx_len, nflows):
+def test_guard_txseg_random(oracle, odd, tx_len, nflows, impl):
     n = 4096
     pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 131) % 1449, pktgen.TCP_MSS)
     pay = np.minimum(pay, tx_len - (7 if odd else 0))
     shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=tx_len, nflows=nflows, odd=odd, seed=0xFE11 + tx_len)
-    _txseg_fenced(oracle, shm, sl, fr, segs, "end", "end")
+    _txseg_fenced(oracle, shm, sl, fr, segs, "end", "end", impl)
 
 
 def test_guard_txseg_tso(oracle):

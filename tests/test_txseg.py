@@ -85,6 +85,25 @@ def _gpu_run(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, im
     return _gpu_run1(shm, shm_len, frames, segs, ip_off, l4_off, frame_shift, form=30)
 
 
+def _download(t):
+    """t's bytes on the host, in three steps that each name themselves when a
+    GPU fault surfaces in them (r05end and r06e saw hipErrorIllegalAddress at
+    this copy after a clean synchronize): the synchronize after the kernel, a
+    second one 50 ms later (a fault in the kernel reported late surfaces here),
+    and the device-to-host copy itself."""
+    import time
+    import torch
+    for stage in ("synchronize after the kernel", "synchronize 50 ms later", "device-to-host copy"):
+        try:
+            if stage == "device-to-host copy":
+                return t.cpu().numpy()
+            if stage == "synchronize 50 ms later":
+                time.sleep(0.05)
+            torch.cuda.synchronize()
+        except Exception as e:
+            raise AssertionError(f"GPU error surfaced at the {stage}: {e}") from e
+
+
 def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, form=None):
     import torch
     from tas_amd import xsum
@@ -105,8 +124,7 @@ def _gpu_run1(shm, shm_len, frames, segs, ip_off=14, l4_off=34, frame_shift=0, f
                                             ip_off, l4_off, out.data_ptr(), xsum._stream(None))
             assert rc == 0, ab.tasx_last_error()
             assert xsum.last_kernel() == "tx_segment_tas_kernel", xsum.last_kernel()
-    torch.cuda.synchronize()
-    got = dfr.cpu().numpy()
+    got = _download(dfr)
     assert not got[:frame_shift].any() and not got[frame_shift + fr.size:].any(), "wrote outside the frames"
     return out.cpu().numpy().view(np.uint32), got[frame_shift:frame_shift + fr.size]
 
