@@ -134,6 +134,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint8_t *const mem = P.mem;
   const uint8_t *const ring = P.ring;
   uint32_t *const dline = (uint32_t *) (mem + TASX_SRV_DONE(r));
+  uint32_t *const tokw = P.tok + r * TASX_SRV_TOKW;
   if (threadIdx.x == 0)
     s_bad = 0u;
   __syncthreads();
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       // before the host wrote it carries an older tag, and then the slot is
       // left for the next round.
       uint32_t n2 = 0u;
-      if (!seg && !torn) {
+      if (!seg && !torn && K == 1u) { // (with K > 1 the read token orders the ring's positions one by one)
         const uint64_t tag2 = (uint64_t) ((p + K + 1u) & 0xffffu);
         const uint64_t g0 = rlane64(v.hw, 3), g1 = rlane64(v.hw, 4);
         const uint32_t m = (uint32_t) (g0 & 0x7fffu);
@@ -276,6 +277,30 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
           __builtin_amdgcn_s_sleep(32);
         } else {
           __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      // The ring's read token (K > 1): the workgroups of a ring poll and take
+      // their positions independently, but read frames one position at a
+      // time, in ring order -- a busy server's frame reads in flight through
+      // the XCDs' L2s are what it costs device-resident work on the same GPU
+      // (profiles/r06/INDEX.md r06d).  The slot has only been read (nothing
+      // is posted before its rows ran), so a stop or the epoch's end while
+      // waiting leaves it in the ring for the next launch, as in judge().
+      if (st == 1 && K > 1u) {
+        for (uint32_t sp = 1;; ++sp) {
+          if (__hip_atomic_load(tokw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p)
+            break;
+          if ((sp & 7u) == 0u) {
+            if ((uint32_t) ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL)) != 0u) {
+              st = 3;
+              break;
+            }
+            if (wall_clock64() - t_launch >= P.period_ticks) {
+              st = 4;
+              break;
+            }
+          }
+          __builtin_amdgcn_s_sleep(2);
         }
       }
       if (lane == 0)
@@ -341,6 +366,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         st_sys32(dline + TASX_SRV_ERRW, 1u);
         s_bad = 0u; // (the rows of the next batch set it only after the next barrier)
       }
+      if (K > 1u) // every row's loads have completed: the ring's next position may read
+        __hip_atomic_store(tokw, p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
       if (s_pair)
         st_sys32(dline + (p + K) % TASX_SRV_RING, p + K + 1u);

@@ -2041,19 +2041,21 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes)
 #define SRV_HOT_US 200u
 #define SRV_STOP_WAIT_MS 5000u
 #define SRV_COLD_US 2000u /* idle time from which a ring's header alone is polled */
-/* workgroups per ring (tasx_srv_params.k).  One since round 6: with 8 cores
- * flushing 3 batches in flight, two per ring (round 4, profiles/r04/r04g)
- * cost a device-resident batch on the same GPU 1.42-1.53x its time, one per
- * ring 1.13x, at the same flush rate (profiles/r06/INDEX.md r06d): the frame
- * reads in flight through the XCDs' L2s are what the tax is made of, and a
- * ring's next queued slot is paired with the one taken anyway. */
-#define SRV_K 1u
+/* workgroups per ring (tasx_srv_params.k).  Two, so that one polls the
+ * ring's next position while the other sums (profiles/r04/r04g), but taking
+ * turns at reading frames (the ring's read token, server_device.h): the frame
+ * reads a busy server keeps in flight through the XCDs' L2s are what it costs
+ * device-resident work on the same GPU (two workgroups reading at once:
+ * 1.30-1.53x a batch's time; one per ring 1.12-1.15x, with a lower rate and
+ * a longer lone flush; profiles/r06/INDEX.md r06d-r06f). */
+#define SRV_K 2u
 #define SRV_QUEUED 2u     /* epochs outstanding on the server's stream */
 
 struct fserver {
   int device;
   hipStream_t st;
   uint8_t *h_mem, *d_mem; /* coherent pinned block (tasx_kernels.h TASX_SRV_*) */
+  uint32_t *d_tok;        /* device memory: each ring's read token (tasx_srv_params.tok) */
   uint8_t *h_ring, *d_ring; /* the host-written lines (control word, slots): h_mem / d_mem */
   uint32_t attached;      /* bit r: ring r serves a context */
   int keep_run;           /* the epoch thread runs */
@@ -2258,6 +2260,8 @@ static void server_free(struct fserver *S)
       hipEventDestroy(S->ev[q]);
   if (S->h_mem)
     hipHostFree(S->h_mem);
+  if (S->d_tok)
+    hipFree(S->d_tok);
   if (S->st)
     hipStreamDestroy(S->st);
   free(S);
@@ -2539,7 +2543,9 @@ int tasx_server_start(int device)
       (e = hipHostMalloc((void **) &S->h_mem, TASX_SRV_BYTES, hipHostMallocCoherent)) != hipSuccess ||
       (e = hipHostGetDevicePointer((void **) &S->d_mem, S->h_mem, 0)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&S->ev[0], hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&S->ev[1], hipEventDisableTiming)) != hipSuccess)
+      (e = hipEventCreateWithFlags(&S->ev[1], hipEventDisableTiming)) != hipSuccess ||
+      (e = hipMalloc((void **) &S->d_tok, TASX_MAX_CTX * TASX_SRV_TOKW * sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMemsetAsync(S->d_tok, 0, TASX_MAX_CTX * TASX_SRV_TOKW * sizeof(uint32_t), S->st)) != hipSuccess)
     rc = hip_err(e, "server allocation");
   if (!rc && khz <= 0)
     rc = set_err(-ENODEV, "server: device %d reports no wall clock", device);
@@ -2555,6 +2561,7 @@ int tasx_server_start(int device)
     prm.cold_ticks = (uint64_t) khz * SRV_COLD_US / 1000u;
     prm.k = SRV_K;
     prm.resume = 0;
+    prm.tok = S->d_tok;
     S->k = prm.k;
     S->prm = prm;
     if (prm.k == 0u || TASX_SRV_RING % prm.k != 0u || prm.k > TASX_SRV_KMAX)

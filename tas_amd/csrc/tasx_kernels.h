@@ -139,7 +139,10 @@ typedef struct tasx_srv_params {
   uint32_t k;            /* workgroups per ring (a divisor of TASX_SRV_RING, <= TASX_SRV_KMAX) */
   uint32_t resume;       /* 0: every ring at position 0 (a zeroed block); 1: each workgroup at the
                             position it left at (TASX_SRV_POSW): every epoch after the first */
+  uint32_t *tok;         /* device memory, one 128-byte line per ring (TASX_SRV_TOKW words apart):
+                            the ring position whose frames may be read next (k > 1) */
 } tasx_srv_params;
+#define TASX_SRV_TOKW 32u
 
 /* variant: see tasx_set_kernel_variant (0 = automatic).  0 on success. */
 TASX_INTERNAL int tasx_launch_raw(const tasx_raw_params *p, int variant, void *stream);

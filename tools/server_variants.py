@@ -4,8 +4,10 @@ each in server_device.h / tasx_host.c, linked with the product's other objects
 into tools/bin/exp_<name>/libtasx.so (soname libtasx.so, so bench.py's loop
 library binds to it under TASX_LIB).  None of these is a product form:
 
-  prod    the product as it is (one workgroup per ring)
-  k2      two workgroups per ring (the round 4-5 product)
+  prod    the product as it is (two workgroups per ring taking turns at
+          reading frames: the ring's read token)
+  k1      one workgroup per ring (taking a queued next slot with its own)
+  notok   two workgroups per ring reading frames at once (round 4-5)
   rows8   a batch's frames summed 8 (rows16: 16) at a time
   sysld   system-scope frame loads and no acquire for checksum slots
   noacq   no acquire for checksum slots (serves stale lines: pricing only)
@@ -20,7 +22,8 @@ VARS = {
   "prod": {},
   "rows8": {"rows": 8},
   "rows16": {"rows": 16},
-  "k2": {"k": 2},
+  "k1": {"k": 1},
+  "notok": {"notok": 1},
   "sysld": {"sys": 1},
   "noacq": {"noacq": 1},
 }
@@ -42,6 +45,10 @@ for name, v in VARS.items():
         a = "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n    }\n    asm volatile"
         assert a in s
         s = s.replace(a, "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n     }\n    }\n    asm volatile")
+    if "notok" in v:
+        a = "      if (st == 1 && K > 1u) {\n        for (uint32_t sp = 1;; ++sp) {"
+        assert a in s
+        s = s.replace(a, "      if (st == 1 && K > 1u && false) {\n        for (uint32_t sp = 1;; ++sp) {")
     if "sys" in v:
         a = "      ok = ok && srv_row(rs, fo, tl, gl);"
         assert a in s
@@ -53,7 +60,7 @@ for name, v in VARS.items():
     open(f"{d}/server_device.h", "w").write(s)
     h = open(f"{d}/tasx_host.c").read()
     if "k" in v:
-        h = h.replace("#define SRV_K 1u", f"#define SRV_K {v['k']}u"); assert f"SRV_K {v['k']}u" in h
+        h = h.replace("#define SRV_K 2u", f"#define SRV_K {v['k']}u"); assert f"SRV_K {v['k']}u" in h
     open(f"{d}/tasx_host.c", "w").write(h)
     o = f"{R}/tools/bin/exp_{name}"
     os.makedirs(o, exist_ok=True)
