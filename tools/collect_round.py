@@ -1,7 +1,9 @@
-"""Copy one gpu_round.sh pass (gpurun_out/TAG) into profiles/: the bench lines
-as pretty JSON and the rocprofv3 kernel-stats summary; prints a summary.
+"""Copy one gpu_round.sh pass (gpurun_out/TAG) into profiles/DIR/TAG/: the
+logs, the bench lines as pretty JSON and the rocprofv3 kernel-stats summary
+(whichever of them the pass produced: PART=a has no rocprof run); prints a
+summary.
 
-    python tools/collect_round.py TAG [--prefix r01]
+    python tools/collect_round.py TAG [--dir r06]
 """
 from __future__ import annotations
 
@@ -23,21 +25,28 @@ def last_json(log: Path) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--prefix", default="r01")
+    ap.add_argument("--dir", default="r06")
     a = ap.parse_args()
     src = ROOT / "gpurun_out" / a.tag
-    dst = ROOT / "profiles"
-    for name, out in (("bench", "bench"), ("bench_mixed", "bench_mixed"), ("bench_shard8m", "bench_shard8m"),
-                      ("bench_tso", "bench_tso")):
+    dst = ROOT / "profiles" / a.dir / a.tag
+    dst.mkdir(parents=True, exist_ok=True)
+    for log in sorted(src.glob("*.log")):
+        shutil.copy(log, dst / log.name)
+    for name in ("bench", "bench_k20", "bench_mixed", "bench_shard8m", "bench_tso", "bench_n2"):
+        if not (src / f"{name}.log").exists():
+            continue
         d = last_json(src / f"{name}.log")
         d["source"] = f"gpurun_out/{a.tag}/{name}.log (tools/gpu_round.sh {a.tag})"
-        (dst / f"{a.prefix}_{out}.json").write_text(json.dumps(d, indent=4) + "\n")
+        (dst / f"{name}.json").write_text(json.dumps(d, indent=4) + "\n")
         r = d["roofline"]
-        print(f"{out:14s} {d['value']:9.2f} GiB/s  frac {r['frac']:.4f}  launch {r['launch_avg_us']:.2f} us")
-    shutil.copy(src / "prof" / "run_kernel_stats.csv", dst / f"{a.prefix}_rocprof_kernel_stats.csv")
-    shutil.copy(src / "prof" / "run_agent_info.csv", dst / f"{a.prefix}_rocprof_agent_info.csv")
+        print(f"{name:14s} {d['value']:9.2f} GiB/s  frac {r['frac']:.4f}  launch {r['launch_avg_us']:.2f} us")
+    stats = src / "prof" / "run_kernel_stats.csv"
+    if not stats.exists():
+        return
+    shutil.copy(stats, dst / "rocprof_kernel_stats.csv")
+    shutil.copy(src / "prof" / "run_agent_info.csv", dst / "rocprof_agent_info.csv")
     import csv
-    for row in csv.DictReader(open(src / "prof" / "run_kernel_stats.csv")):
+    for row in csv.DictReader(open(stats)):
         if "tasx" in row["Name"] or "_kernel<" in row["Name"] and "at::" not in row["Name"]:
             print(f"  rocprof {row['Name'][:78]:78s} calls {row['Calls']:>6s} avg {float(row['AverageNs']) / 1e3:7.2f} us")
 
