@@ -357,6 +357,18 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       if (gl == 15 && !ok)
         atomicOr(&s_bad, 1u);
     }
+    if (K > 1u) {
+      // every row has issued its stores, and a store is issued only once the
+      // loads it is made of have landed: the ring's next position may read
+      // while these stores are still on their way (a barrier without a
+      // memory fence: nothing here waits for them)
+      __builtin_amdgcn_s_barrier();
+      // (by the last wave: its rows are past every batch TAS flushes, 32
+      // frames or 41 segments, so the wait for its own memory operations the
+      // compiler puts before the store has nothing to wait for)
+      if (threadIdx.x == kSrvBlock - 1)
+        __hip_atomic_store(tokw, p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's field stores have completed
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -366,8 +378,6 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         st_sys32(dline + TASX_SRV_ERRW, 1u);
         s_bad = 0u; // (the rows of the next batch set it only after the next barrier)
       }
-      if (K > 1u) // every row's loads have completed: the ring's next position may read
-        __hip_atomic_store(tokw, p + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
       if (s_pair)
         st_sys32(dline + (p + K) % TASX_SRV_RING, p + K + 1u);
