@@ -42,9 +42,9 @@ for name, v in VARS.items():
         s = s.replace(a, f"    }} else if (row < {n}u) {{\n     for (uint32_t jr = row; jr < s_n; jr += {n}u) {{\n      const uint64_t base = s_base;")
         a = "      const uint32_t fo = s_off[row], tl = s_tl[row];"
         s = s.replace(a, "      const uint32_t fo = s_off[jr], tl = s_tl[jr];")
-        a = "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n    }\n    asm volatile"
+        a = "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n    }\n    if (K > 1u) {"
         assert a in s
-        s = s.replace(a, "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n     }\n    }\n    asm volatile")
+        s = s.replace(a, "      if (gl == 15 && !ok)\n        atomicOr(&s_bad, 1u);\n     }\n    }\n    if (K > 1u) {")
     if "notok" in v:
         a = "      if (st == 1 && K > 1u) {\n        for (uint32_t sp = 1;; ++sp) {"
         assert a in s
