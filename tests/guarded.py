@@ -86,7 +86,13 @@ class Guarded:
     def __init__(self, nbytes: int, at: str = "end", device: int = 0):
         assert at in ("start", "end") and nbytes > 0
         h = hip()
-        prop = _Prop(type=1, requestedHandleType=0, location=_Loc(1, device))
+        # Uncached physical memory (hipMemAllocationTypeUncached): the XCDs'
+        # L2s do not keep lines of it, so what one kernel (or copy) wrote is
+        # what the next one reads on every XCD.  Cached VMM memory (type
+        # Pinned) was not kept coherent across XCDs between kernels here: data
+        # moved in by a copy read back wrong on another XCD (r06a, r06b, r06i
+        # in profiles/r06/INDEX.md), a harness problem, not the kernels'.
+        prop = _Prop(type=0x40000000, requestedHandleType=0, location=_Loc(1, device))
         g = ctypes.c_size_t(0)
         _ok(h.hipMemGetAllocationGranularity(ctypes.byref(g), ctypes.byref(prop), 0), "granularity")
         self.gran = g.value
@@ -96,7 +102,7 @@ class Guarded:
         _ok(h.hipMemAddressReserve(ctypes.byref(va), self.total, self.gran, None, 0), "hipMemAddressReserve")
         self.va = va.value
         self.handle = ctypes.c_void_p(0)
-        _ok(h.hipMemCreate(ctypes.byref(self.handle), self.mapped, ctypes.byref(prop), 0), "hipMemCreate")
+        _ok(h.hipMemCreate(ctypes.byref(self.handle), self.mapped, ctypes.byref(prop), 0), "hipMemCreate (uncached)")
         self.map_base = self.va + self.gran
         _ok(h.hipMemMap(self.map_base, self.mapped, 0, self.handle, 0), "hipMemMap")
         acc = _Access(location=_Loc(1, device), flags=3)
@@ -105,9 +111,7 @@ class Guarded:
         # the data: flush against the mapping's end or its start
         self.addr = self.map_base + (self.mapped - nbytes if at == "end" else 0)
         # Data moves in and out by device kernels through torch views of the
-        # mapping (never by hipMemset / hipMemcpy into it: those copies went
-        # around the L2, and kernels then read stale lines of the mapping --
-        # results wrong in a 64 KiB stretch, profiles/r06/INDEX.md r06a-r06b)
+        # mapping
         self._all = _view(self.map_base, self.mapped, device)
         self._all.zero_()
         self.data = self._all[self.addr - self.map_base:self.addr - self.map_base + nbytes]
