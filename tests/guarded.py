@@ -75,6 +75,9 @@ def _view(ptr: int, nbytes: int, device: int):
     return torch.as_tensor(_Cai(ptr, nbytes), device=f"cuda:{device}")
 
 
+_PARKED = []  # (va, total, map_base, mapped, handle) of every freed buffer: see Guarded.free
+
+
 def _ok(rc: int, what: str) -> None:
     if rc != 0:
         raise RuntimeError(f"{what}: hipError {rc}")
@@ -133,13 +136,14 @@ class Guarded:
         return out
 
     def free(self) -> None:
+        # The mapping is kept (parked until the process exits), never unmapped
+        # and reserved again: a range unmapped and handed to the next buffer
+        # at the same virtual address was read stale by a later kernel on
+        # this stack (r06j: 9 of 70 sums wrong with every upload verified), so
+        # every guarded buffer of a session lives at an address of its own.
         if self.va:
-            h = hip()
             self.data = self._all = None
-            h.hipDeviceSynchronize()
-            h.hipMemUnmap(self.map_base, self.mapped)
-            h.hipMemRelease(self.handle)
-            h.hipMemAddressFree(self.va, self.total)
+            _PARKED.append((self.va, self.total, self.map_base, self.mapped, self.handle))
             self.va = 0
 
     def __enter__(self):
