@@ -123,7 +123,11 @@ class Guarded:
         import torch
         a = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
         assert offset + a.nbytes <= self.nbytes
-        self.data[offset:offset + a.nbytes].copy_(torch.from_numpy(a.copy()).cuda())
+        # (the host-to-device copy of a whole buffer whose size is a multiple
+        # of 16; the odd-sized part moves device to device)
+        h = np.zeros((a.nbytes + 15) // 16 * 16, np.uint8)
+        h[:a.nbytes] = a
+        self.data[offset:offset + a.nbytes].copy_(torch.from_numpy(h).cuda()[:a.nbytes])
         torch.cuda.synchronize()
         # the data as the kernels will see it (a mismatch later is theirs)
         assert np.array_equal(self.download()[offset:offset + a.nbytes], a), "upload into the guarded mapping"
@@ -131,7 +135,9 @@ class Guarded:
     def download(self) -> np.ndarray:
         import torch
         torch.cuda.synchronize()
-        out = self.data.clone().cpu().numpy()
+        pad = torch.zeros((self.nbytes + 15) // 16 * 16, dtype=torch.uint8, device=self.data.device)
+        pad[:self.nbytes].copy_(self.data)
+        out = pad.cpu().numpy()[:self.nbytes]
         torch.cuda.synchronize()
         return out
 
