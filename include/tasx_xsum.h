@@ -410,9 +410,11 @@ int tasx_ctx_feeder_flushes(unsigned ctx_id, uint32_t *feeder_flushes);
  * frames each: submit writes the frames' offsets in the context's registered
  * region and their ip.total_length into the next slot, the header last, and
  * returns; two workgroups of the server kernel poll that ring over PCIe
- * (each every other position, so two of a context's queued batches are
- * summed at once), sum the frames in place and store both checksum fields
- * into them, then post each slot's done word, which tasx_flush_poll/_wait
+ * (each every other position: one takes the next batch while the other sums
+ * the current one, and they read frames in turn, which bounds what a busy
+ * server costs other device work on the GPU), sum the frames in place and
+ * store both checksum fields into them, then post each slot's done word,
+ * which tasx_flush_poll/_wait
  * reap in position order (ticket order as before; submit spins only when 8
  * batches are in flight).  A ring idle for 2 ms is polled by its header alone.  Frames
  * the server does not take -- outside the registered region, not TAS layout,
