@@ -96,9 +96,10 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 }
 
 // K = P.k workgroups serve ring r (context r): workgroup k takes the ring's
-// positions p = k, k + K, k + 2K, ..., so up to K of the ring's queued batches
-// are summed at once (one workgroup per ring summed its batches one after the
-// other: 14-15 M frames/s at 8 threads x 7 in flight, profiles/r04/r04d) and
+// positions p = k, k + K, k + 2K, ..., so one takes the ring's next batch
+// while another sums the current one (one workgroup per ring summed its
+// batches one after the other: 14-15 M frames/s at 8 threads x 7 in flight,
+// profiles/r04/r04d), reading frames in turn (the read token, below), and
 // each posts its own slot's done word.  Wave 0 polls the workgroup's next
 // position: lanes read the 64 entry words, lanes 0-1 the two header words,
 // lane 2 the control word, all system scope, in one round trip; a slot is
@@ -114,20 +115,19 @@ __device__ __forceinline__ bool srv_row(__amdgpu_buffer_rsrc_t rs, uint32_t fo, 
 // against 16.5-16.6 M segments/s at 8 x 3, 18.6-19.6 against 16.8-17.8 us at
 // 1 x 1, profiles/r04/r04z); 128 VGPRs, no scratch.
 constexpr int kSrvTxU = 6;
-// frames of a paired slot (its entries come with the poll: TAS flushes
-// TXBUF_SIZE = 32 frames at most, /root/reference/tas/include/fastpath.h:38)
-constexpr uint32_t kSrvPairFB = 32u;
 
 // The frame-load cache policies measured in round 4 (no acquire, system-scope
 // loads, write-through TX stores, no release, ...; profiles/r04/INDEX.md
-// r04g-r04v), the per-batch timing form (profiles/r05 r05h) and the acquire at
-// agent scope or left out for pricing (profiles/r05 r05l) were measured
-// against this form and are gone from the source (round 6).
+// r04g-r04v), the per-batch timing form (profiles/r05 r05h), the acquire at
+// agent scope or left out for pricing (profiles/r05 r05l) and a workgroup
+// taking its next queued slot under the same acquire (round 6, r06b: no
+// effect on what a busy server costs other work) were measured against this
+// form and are gone from the source.
 __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params P)
 {
   __shared__ uint32_t s_off[TASX_SRV_FB], s_tl[TASX_SRV_FB];
   __shared__ uint64_t s_w[TASX_SRV_WORDS]; // a TX segment slot's entry words
-  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg, s_pair;
+  __shared__ uint32_t s_cmd, s_n, s_bytes, s_bad, s_seg;
   __shared__ uint64_t s_base;
   const uint32_t K = P.k, r = blockIdx.x / K;
   const int lane = threadIdx.x & 63, gl = threadIdx.x & 15;
@@ -149,23 +149,17 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
   uint64_t t_act = P.resume ? __hip_atomic_load(tactw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : t_launch;
   // The poller's reads of ring r's slot at position p: the entry words (every
   // lane; skipped when only the header is polled), the two header words
-  // (lanes 0-1), the control word (lane 2) and, with the entries, the two
-  // header words of the workgroup's next position p + K (lanes 3-4) and that
-  // slot's first kSrvPairFB entry words (lanes 0-31), all in the same round
-  // trip: the pair below costs no extra one.
+  // (lanes 0-1) and the control word (lane 2), all in one round trip.
   struct SlotRead {
-    uint64_t e, hw, e2;
+    uint64_t e, hw;
   };
   auto read_slot = [&](bool entries) {
     const uint8_t *slot = ring + TASX_SRV_SLOTP(r, p);
-    const uint8_t *next = ring + TASX_SRV_SLOTP(r, p + K);
     SlotRead v;
     v.e = entries ? ld_sys64((const uint64_t *) (slot + TASX_SRV_HDR) + lane) : 0ull;
     v.hw = lane < 2    ? ld_sys64((const uint64_t *) slot + lane)
            : lane == 2 ? ld_sys64((const uint64_t *) (ring + TASX_SRV_CTL))
-           : (lane < 5 && entries) ? ld_sys64((const uint64_t *) next + (lane - 3))
-                                   : 0ull;
-    v.e2 = (entries && lane < (int) kSrvPairFB) ? ld_sys64((const uint64_t *) (next + TASX_SRV_HDR) + lane) : 0ull;
+                       : 0ull;
     return v;
   };
   // A read of position p: 1 = the batch is complete (taken: its descriptors
@@ -214,35 +208,9 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         if (mine)
           s_w[TASX_SRV_FB + lane] = w2;
       }
-      // The pair (round 6): when this workgroup's next
-      // position p + K is queued too -- a checksum slot of the same frame
-      // region, at most kSrvPairFB frames (TAS's TXBUF_SIZE), that fit the 64
-      // rows beside these -- it is taken in the same poll round, so ONE
-      // system-scope acquire (below) covers both batches and the rows sum them
-      // at once.  Its header and entries came with this read; an entry read
-      // before the host wrote it carries an older tag, and then the slot is
-      // left for the next round.
-      uint32_t n2 = 0u;
-      if (!seg && !torn && K == 1u) { // (with K > 1 the read token orders the ring's positions one by one)
-        const uint64_t tag2 = (uint64_t) ((p + K + 1u) & 0xffffu);
-        const uint64_t g0 = rlane64(v.hw, 3), g1 = rlane64(v.hw, 4);
-        const uint32_t m = (uint32_t) (g0 & 0x7fffu);
-        if ((g0 >> 48) == tag2 && (g1 >> 48) == tag2 && !(g0 & TASX_SRV_SEG) && m >= 1u && m <= kSrvPairFB &&
-            n + m <= TASX_SRV_FB && ((g0 ^ h0) & 0xffffffff0000ull) == 0ull && ((g1 ^ h1) & 0xffffffffffffull) == 0ull) {
-          const uint64_t e2 = v.e2;
-          if (__builtin_amdgcn_ballot_w64((uint32_t) lane < m && (e2 >> 48) != tag2) == 0ull) {
-            n2 = m;
-            if ((uint32_t) lane < m) {
-              s_off[n + lane] = (uint32_t) e2;
-              s_tl[n + lane] = (uint32_t) (e2 >> 32) & 0xffffu;
-            }
-          }
-        }
-      }
       if (lane == 0) {
         s_seg = seg ? 1u : 0u;
-        s_n = torn ? 0u : n + n2; // a slot still torn is not built, and flags the ring
-        s_pair = n2 ? 1u : 0u;
+        s_n = torn ? 0u : n; // a slot still torn is not built, and flags the ring
         if (torn)
           s_bad = 1u;
         s_bytes = (uint32_t) (h0 >> 16);
@@ -305,7 +273,7 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
       }
       if (lane == 0)
         s_cmd = st == 1 ? 0u : st == 3 ? 1u : 2u;
-      // a batch taken (one or a pair): this CU's L1 and the XCD's L2 drop
+      // a batch taken: this CU's L1 and the XCD's L2 drop
       // their non-coherent lines before any frame load
       if (st == 1)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -379,10 +347,8 @@ __global__ __launch_bounds__(kSrvBlock) void flush_server_kernel(tasx_srv_params
         s_bad = 0u; // (the rows of the next batch set it only after the next barrier)
       }
       st_sys32(dline + p % TASX_SRV_RING, p + 1u);
-      if (s_pair)
-        st_sys32(dline + (p + K) % TASX_SRV_RING, p + K + 1u);
     }
-    p += s_pair ? 2u * K : K; // (s_pair is rewritten only by the next take, after the next barrier)
+    p += K;
   }
 }
 

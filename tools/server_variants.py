@@ -6,7 +6,7 @@ library binds to it under TASX_LIB).  None of these is a product form:
 
   prod    the product as it is (two workgroups per ring taking turns at
           reading frames: the ring's read token)
-  k1      one workgroup per ring (taking a queued next slot with its own)
+  k1      one workgroup per ring
   notok   two workgroups per ring reading frames at once (round 4-5)
   rows8   a batch's frames summed 8 (rows16: 16) at a time
   sysld   system-scope frame loads and no acquire for checksum slots
