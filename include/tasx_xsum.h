@@ -508,7 +508,7 @@ int tasx_ctx_server_flushes(unsigned ctx_id, uint32_t *server_flushes);
  *     context: it waits for in-flight work whose path is still healthy, then
  *     collects every recorded frame whose checksum fields the GPU did not
  *     store -- batches of a server whose kernel has gone (stopped by
- *     tasx_server_abort, its lease ran out, a fault), of a failed feeder, of a
+ *     tasx_server_abort, an epoch that failed, a fault), of a failed feeder, of a
  *     failed or stalled stream, and frames recorded but not submitted -- marks
  *     every ticket complete, and detaches the context from a dead server or
  *     feeder.  Each call then writes up to max of them ({ip, l4} as recorded)
