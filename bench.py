@@ -1020,15 +1020,68 @@ def txseg_host_leg(ws: int, rank: int, reps: int) -> dict:
         torch.cuda.synchronize()
         t = time.perf_counter() - t0
         tm = max_over_ranks(t, ws)
+        kernel = xsum.last_kernel()
         hdr = pktgen.HDRS_LEN - pktgen.ETH_LEN - pktgen.IP_LEN
         alg = n * (2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4)
-        return {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s (algorithmic, as tx_segment)",
-                "ms_per_batch": tm / reps * 1e3, "segments_per_s": sum_over_ranks(n * reps, ws) / tm,
-                "pcie_h2d_bytes_per_rank": n * (pktgen.TCP_MSS + pktgen.HDRS_LEN + 32),
-                "pcie_d2h_bytes_per_rank": n * (pktgen.HDRS_LEN + pktgen.TCP_MSS),
-                "kernel": xsum.last_kernel(),
-                "note": "tas_shm, frames and descriptors in pinned host memory; payload read and frame "
-                        "written over PCIe in one pass"}
+        h2d, d2h = n * (pktgen.TCP_MSS + pktgen.HDRS_LEN + 32), n * (pktgen.HDRS_LEN + pktgen.TCP_MSS)
+        res = {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s (algorithmic, as tx_segment)",
+               "ms_per_batch": tm / reps * 1e3, "segments_per_s": sum_over_ranks(n * reps, ws) / tm,
+               "pcie_h2d_bytes_per_rank": h2d, "pcie_d2h_bytes_per_rank": d2h,
+               "kernel": kernel,
+               "note": "tas_shm, frames and descriptors in pinned host memory; payload read and frame "
+                       "written over PCIe in one pass"}
+    finally:
+        for pb in pins:
+            pb.free()
+    if rank == 0:
+        # is the link the bound?  The same bytes each way moved by a plain
+        # streaming copy between two pinned host buffers
+        res["link_ceiling"] = host_link_ceiling(max(h2d, d2h))
+        lc = res["link_ceiling"]
+        res["link_ceiling"]["build_frac_of_copy"] = round(lc["us"] / (res["ms_per_batch"] * 1e3), 4)
+    return res
+
+
+def host_link_ceiling(nbytes: int, copies: int = 20) -> dict:
+    """The GPU's concurrent read-from and write-to host rate, measured live:
+    the grid-stride copy kernel (tasx_ab_stream_copy, the A/B build) from one
+    pinned host buffer to another, `nbytes` each way -- what the TX build from
+    host memory moves (payloads and headers in, frames out), with none of its
+    gather.  Also the read-only and write-only halves (host -> HBM, HBM ->
+    host) by the same kernel."""
+    nbytes = nbytes // 16 * 16
+    ab = xsum._load(xsum.AB_LIB_PATH)
+    st = torch.cuda.current_stream().cuda_stream
+    pins = []
+    try:
+        a = xsum.PinnedBuffer(nbytes)
+        pins.append(a)
+        b = xsum.PinnedBuffer(nbytes)
+        pins.append(b)
+        a.array[:] = 1
+        d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+
+        def timed(src, dst):
+            for _ in range(3):
+                ab.tasx_ab_stream_copy(src, dst, nbytes, st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(copies):
+                rc = ab.tasx_ab_stream_copy(src, dst, nbytes, st)
+                if rc:
+                    raise xsum.TasxError(rc, "tasx_ab_stream_copy")
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) * 1e3 / copies
+        us = timed(a.dev_addr, b.dev_addr)
+        us_rd = timed(a.dev_addr, d.data_ptr())
+        us_wr = timed(d.data_ptr(), b.dev_addr)
+        del d
+        return {"bytes_each_way": nbytes, "us": round(us, 1), "GBps_each_way": round(nbytes / us / 1e3, 1),
+                "read_only_GBps": round(nbytes / us_rd / 1e3, 1), "write_only_GBps": round(nbytes / us_wr / 1e3, 1),
+                "how": "stream_copy_kernel (libtasx_ab.so) between two pinned host buffers (and host -> HBM, "
+                       "HBM -> host), HIP events around 20 copies"}
     finally:
         for pb in pins:
             pb.free()
