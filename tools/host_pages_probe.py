@@ -131,6 +131,21 @@ def main():
             same = None if ref is None else bool(np.array_equal(got, ref))
             ref = got if ref is None else ref
             us = events_us(build, a.reps)
+            # the same launches by the host's clock (what e2e.tx_segment_host
+            # reports), then by the host's clock with the device synchronized
+            # through the stream only
+            import time
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                build()
+            torch.cuda.synchronize()
+            wall_us = (time.perf_counter() - t0) * 1e6 / a.reps
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                build()
+            torch.cuda.current_stream().synchronize()
+            wall_stream_us = (time.perf_counter() - t0) * 1e6 / a.reps
             h2d = n * (pktgen.TCP_MSS + pktgen.HDRS_LEN + 32)
             cb = h2d // 16 * 16
             c1 = HostBuf(cb, kind)
@@ -140,6 +155,7 @@ def main():
             c1.array[:] = 1
             cus = events_us(lambda: ab.tasx_ab_stream_copy(c1.dev_addr, c2.dev_addr, cb, st), a.reps)
             print(json.dumps({"kind": kind, "anon_huge_kib": anon_huge_kib(), "build_us": round(us, 1),
+                              "build_wall_us": round(wall_us, 1), "build_wall_stream_us": round(wall_stream_us, 1),
                               "segments_per_s": round(n / us * 1e6), "copy_us": round(cus, 1),
                               "copy_GBps_each_way": round(cb / cus / 1e3, 1),
                               "build_frac_of_copy": round(cus / us, 3), "frames_match_hostmalloc": same,
