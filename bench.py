@@ -1030,12 +1030,33 @@ def txseg_host_leg(ws: int, rank: int, reps: int) -> dict:
         e1.record()
         torch.cuda.synchronize()
         kern_us = e0.elapsed_time(e1) * 1e3 / reps
+        # its access pattern alone over the same host buffers (as
+        # txseg_pattern_ceiling: the loads and stores, no realignment; last,
+        # since it stores unrealigned bytes into the frames)
+        ab = xsum._load(xsum.AB_LIB_PATH)
+        s = torch.cuda.current_stream().cuda_stream
+
+        def pat():
+            rc = ab.tasx_ab_tx_segment_form(40, hs.dev_addr, shm_len, hf.dev_addr, hd.dev_addr, n, IP_OFF, L4_OFF,
+                                            out.data_ptr(), s)
+            if rc:
+                raise xsum.TasxError(rc, "tasx_ab_tx_segment_form(40)")
+        pat()
+        e0.record()
+        for _ in range(reps):
+            pat()
+        e1.record()
+        torch.cuda.synchronize()
+        pat_us = e0.elapsed_time(e1) * 1e3 / reps
         hdr = pktgen.HDRS_LEN - pktgen.ETH_LEN - pktgen.IP_LEN
         alg = n * (2 * pktgen.TCP_MSS + pktgen.IP_LEN + hdr + 4)
         h2d, d2h = n * (pktgen.TCP_MSS + pktgen.HDRS_LEN + 32), n * (pktgen.HDRS_LEN + pktgen.TCP_MSS)
         res = {"value": sum_over_ranks(alg * reps, ws) / tm / GIB, "unit": "GiB/s (algorithmic, as tx_segment)",
                "ms_per_batch": tm / reps * 1e3, "segments_per_s": sum_over_ranks(n * reps, ws) / tm,
                "kernel_us_events": round(kern_us, 1),
+               "pattern_ceiling": {"us": round(pat_us, 1), "frac": round(pat_us / kern_us, 4),
+                                   "kernel": "tx_segment_lds_kernel<pattern> (libtasx_ab.so) over the same host "
+                                             "buffers: the product's loads and stores, no realignment"},
                "pcie_h2d_bytes_per_rank": h2d, "pcie_d2h_bytes_per_rank": d2h,
                "kernel": kernel,
                "note": "tas_shm, frames and descriptors in pinned host memory; payload read and frame "
