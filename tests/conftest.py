@@ -1,8 +1,16 @@
+import os
 import sys
 from pathlib import Path
 
-import numpy as np
-import pytest
+# The HIP runtime's error log (level 1: errors only), set before anything
+# loads the runtime: a GPU memory fault is then logged with its address and
+# reason where the runtime sees it.  Round 6's three sightings of an illegal
+# address in test_txseg.py (profiles/r06/INDEX.md) reached the test only as
+# hipErrorIllegalAddress at a later copy, with nothing to attribute them by.
+os.environ.setdefault("AMD_LOG_LEVEL", "1")
+
+import numpy as np  # noqa: E402
+import pytest  # noqa: E402
 
 ROOT = Path(__file__).resolve().parent.parent
 GOLDEN = ROOT / "tests" / "golden"
