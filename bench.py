@@ -1093,16 +1093,19 @@ def host_link_ceiling(nbytes: int, copies: int = 20) -> dict:
         a.array[:] = 1
         d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
 
+        def copy(src, dst):
+            rc = ab.tasx_ab_stream_copy(src, dst, nbytes, st)
+            if rc:
+                raise xsum.TasxError(rc, "tasx_ab_stream_copy")
+
         def timed(src, dst):
             for _ in range(3):
-                ab.tasx_ab_stream_copy(src, dst, nbytes, st)
+                copy(src, dst)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize()
             e0.record()
             for _ in range(copies):
-                rc = ab.tasx_ab_stream_copy(src, dst, nbytes, st)
-                if rc:
-                    raise xsum.TasxError(rc, "tasx_ab_stream_copy")
+                copy(src, dst)
             e1.record()
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) * 1e3 / copies
