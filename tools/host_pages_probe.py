@@ -153,7 +153,11 @@ def main():
             c2 = HostBuf(cb, kind)
             bufs.append(c2)
             c1.array[:] = 1
-            cus = events_us(lambda: ab.tasx_ab_stream_copy(c1.dev_addr, c2.dev_addr, cb, st), a.reps)
+            def copy():
+                rc = ab.tasx_ab_stream_copy(c1.dev_addr, c2.dev_addr, cb, st)
+                if rc:
+                    raise xsum.TasxError(rc, "tasx_ab_stream_copy")
+            cus = events_us(copy, a.reps)
             print(json.dumps({"kind": kind, "anon_huge_kib": anon_huge_kib(), "build_us": round(us, 1),
                               "build_wall_us": round(wall_us, 1), "build_wall_stream_us": round(wall_stream_us, 1),
                               "segments_per_s": round(n / us * 1e6), "copy_us": round(cus, 1),
