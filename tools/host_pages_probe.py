@@ -18,6 +18,7 @@ import ctypes
 import json
 import mmap
 import sys
+import time
 from pathlib import Path
 
 import numpy as np
@@ -134,7 +135,6 @@ def main():
             # the same launches by the host's clock (what e2e.tx_segment_host
             # reports), then by the host's clock with the device synchronized
             # through the stream only
-            import time
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.reps):
@@ -153,6 +153,7 @@ def main():
             c2 = HostBuf(cb, kind)
             bufs.append(c2)
             c1.array[:] = 1
+
             def copy():
                 rc = ab.tasx_ab_stream_copy(c1.dev_addr, c2.dev_addr, cb, st)
                 if rc:
