@@ -5,7 +5,8 @@ DPDK's mbuf pools live in hugepages, while the bench's `e2e.tx_segment_host`
 leg uses hipHostMalloc memory.  For each kind -- hipHostMalloc, plain 4 KiB
 pages pinned by hipHostRegister, transparent huge pages (madvise
 MADV_HUGEPAGE on a 2 MiB-aligned anonymous mapping) pinned by hipHostRegister
--- it times the bench's 64K-segment build (same segments and frames) and the
+-- it times the bench's 64K-segment build (same segments and frames; by HIP
+events and by the host's clock) and the
 plain streaming copy of the same bytes between two buffers of that kind, and
 checks the frames built against the hipHostMalloc run's.
 
