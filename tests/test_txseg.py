@@ -312,6 +312,68 @@ def test_gpu_txseg_host_memory(oracle, where):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pages", ["huge", "4k"])
+def test_gpu_txseg_registered_pages(oracle, pages):
+    """The TX build over host memory as TAS allocates it: `tas_shm` is
+    hugepage-backed by default (fp_hugepages, /root/reference/tas/config.c:591,
+    tas/shm.c:51-64) and DPDK's mbuf pool lives in hugepages; here anonymous
+    memory with transparent huge pages asked for (MADV_HUGEPAGE on 2 MiB
+    boundaries; plain pages where the host disables THP) or refused, pinned by
+    tasx_host_register, with the frames at an odd 2 MiB-page offset."""
+    import ctypes
+    import mmap
+    from tas_amd import xsum
+    huge = 2 << 20
+    n = 4096
+    pay = np.where(np.arange(n) % 5 == 0, (np.arange(n) * 29) % 1449, pktgen.TCP_MSS)
+    shm, fr, segs, sl = pktgen.tx_segments(n, payload=pay, tx_len=16384, nflows=512, odd=True, seed=0x70A,
+                                           room=pktgen.MBUF_ROOM)
+    exp_fr = fr.copy()
+    exp = oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    lib = xsum.lib()
+    maps, regs = [], []
+
+    def region(nbytes, shift=0):
+        size = (nbytes + shift + huge - 1) // huge * huge
+        mm = mmap.mmap(-1, size + huge, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        maps.append(mm)
+        base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+        off = (-base) % huge
+        mm.madvise(mmap.MADV_HUGEPAGE if pages == "huge" else mmap.MADV_NOHUGEPAGE, off, size)
+        arr = np.frombuffer(mm, dtype=np.uint8, count=size, offset=off)
+        arr[:] = 0
+        assert lib.tasx_host_register(ctypes.c_void_p(base + off), ctypes.c_size_t(size)) == 0
+        regs.append(base + off)
+        dev = lib.tasx_host_device_pointer(ctypes.c_void_p(base + off))
+        assert dev
+        return arr[shift:shift + nbytes], dev + shift
+
+    try:
+        hs, ds = region(sl)
+        hs[:] = shm[:sl]
+        hf, df = region(fr.size, shift=3 * 4096 + 16 * 7)  # frames 16-byte aligned, off any page start
+        hf[:] = fr
+        hd, dd = region(segs.nbytes)
+        hd[:] = segs.view(np.uint8)
+        out = xsum.tx_segment_batch(ds, df, dd, n, shm_len=sl)
+        got = out.cpu().numpy().view(np.uint32)
+        assert xsum.last_kernel() == "tx_segment_lds_kernel"
+        np.testing.assert_array_equal(got, exp)
+        np.testing.assert_array_equal(hf.copy(), exp_fr)
+    finally:
+        import torch
+        torch.cuda.synchronize()
+        for a in regs:
+            assert lib.tasx_host_unregister(ctypes.c_void_p(a)) == 0
+        hs = hf = hd = None
+        for mm in maps:
+            try:
+                mm.close()
+            except BufferError:  # a view still held (by a failure's traceback): the process frees it
+                pass
+
+
+@pytest.mark.gpu
 def test_gpu_txseg_errors():
     import torch
     from tas_amd import xsum
