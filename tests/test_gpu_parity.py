@@ -880,13 +880,28 @@ def test_async_flush_pipeline(oracle, zero_copy):
         xsum.ctx_destroy(ctx)
 
 
-def test_zero_copy_pageable_region(oracle):
-    """hipHostRegister of ordinary (numpy) memory as the frame region."""
+@pytest.mark.parametrize("pages", ["4k", "huge"])
+def test_zero_copy_pageable_region(oracle, pages):
+    """hipHostRegister of ordinary (numpy) memory as the frame region; `huge`:
+    anonymous memory on a 2 MiB transparent huge page (MADV_HUGEPAGE), as a
+    DPDK hugepage mempool's mbufs would be."""
+    import ctypes
+    import mmap
     xsum.ctx_init(4, 0, 1 << 20)
+    mm = None
     try:
         n = 64
-        raw = np.zeros(n * 2048 + 8192, np.uint8)
-        start = (-raw.ctypes.data) % 4096
+        if pages == "huge":
+            huge = 2 << 20
+            mm = mmap.mmap(-1, 2 * huge, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+            base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+            mm.madvise(mmap.MADV_HUGEPAGE, (-base) % huge, huge)
+            raw = np.frombuffer(mm, dtype=np.uint8, count=huge, offset=(-base) % huge)
+            raw[:] = 0
+            start = 0
+        else:
+            raw = np.zeros(n * 2048 + 8192, np.uint8)
+            start = (-raw.ctypes.data) % 4096
         region = raw[start:start + n * 2048]
         region[:] = pktgen.tcp4_frames(n, payload=1448, stride=2048, seed=63)
         ref = region.copy()
@@ -898,7 +913,13 @@ def test_zero_copy_pageable_region(oracle):
         np.testing.assert_array_equal(region, ref)
         assert xsum.ctx_stats(4)[0] == 1
     finally:
-        xsum.ctx_destroy(4)
+        xsum.ctx_destroy(4)  # unregisters the region
+        raw = region = None
+        if mm is not None:
+            try:
+                mm.close()
+            except BufferError:  # a view still held (by a failure's traceback): the process frees it
+                pass
 
 
 def test_device_batch_on_pinned_host_memory(oracle):

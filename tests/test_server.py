@@ -7,6 +7,7 @@ tcp_checksums (fast_flows.c:1058-1069) over the same frames.
 
 Run on the MI355X box:  python -m pytest tests/test_server.py -m gpu -x -q
 """
+import ctypes
 import errno
 import threading
 import time
@@ -189,23 +190,35 @@ def test_server_reused_mbufs_and_large_flush(oracle):
         cx.close()
 
 
-@pytest.mark.parametrize("mem", ["host_alloc", "registered"])
+@pytest.mark.parametrize("mem", ["host_alloc", "registered", "registered_huge"])
 def test_server_refilled_mbufs_every_flush(oracle, mem):
     """TAS reuses an mbuf as soon as its frame has left: 300 flushes of 32
     frames through the SAME 32 mbufs, new headers and payload every time, in
     pinned memory from tasx_host_alloc and in plain pages pinned by
-    tasx_ctx_register_frames (hipHostRegister, as a DPDK mempool would be).
-    The ring's workgroups come back to the same mbufs every few flushes: a
-    frame line cached in an XCD's L2 by an earlier batch must never be summed."""
+    tasx_ctx_register_frames (hipHostRegister, as a DPDK mempool would be;
+    `registered_huge`: a 2 MiB transparent huge page, as DPDK's hugepage
+    mempool).  The ring's workgroups come back to the same mbufs every few
+    flushes: a frame line cached in an XCD's L2 by an earlier batch must never
+    be summed."""
+    import mmap
     xsum.server_start(0)
     cx = _Ctxs([6])
-    raw = None
+    raw = mm = None
     try:
         n, rounds, nbytes = 32, 300, 32 * 2048 + 4096
         if mem == "host_alloc":
             pin = xsum.PinnedBuffer(nbytes)
             cx.pins.append(pin)
             arr, addr = pin.array, pin.addr
+        elif mem == "registered_huge":
+            huge = 2 << 20
+            mm = mmap.mmap(-1, 2 * huge, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+            base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+            off = (-base) % huge
+            mm.madvise(mmap.MADV_HUGEPAGE, off, huge)
+            raw = np.frombuffer(mm, dtype=np.uint8, count=huge, offset=off)
+            raw[:] = 0
+            arr, addr = raw[:nbytes], base + off
         else:
             raw = np.zeros(nbytes + 4096, np.uint8)
             off = (-raw.ctypes.data) % 4096
@@ -229,6 +242,12 @@ def test_server_refilled_mbufs_every_flush(oracle, mem):
         cx.close()
         _stop_if_running()
         del raw  # unregistered by the context's release (at the server's stop at the latest)
+        arr = None
+        if mm is not None:
+            try:
+                mm.close()
+            except BufferError:  # a view still held (by a failure's traceback): the process frees it
+                pass
 
 
 def test_server_ring_wrap_and_tag_wrap(oracle):
