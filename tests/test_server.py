@@ -513,7 +513,8 @@ def test_server_stop_is_bounded_and_restarts(oracle):
         _stop_if_running()
 
 
-@pytest.mark.parametrize("odd,shm_mem", [(False, "host_alloc"), (True, "host_alloc"), (True, "registered")])
+@pytest.mark.parametrize("odd,shm_mem", [(False, "host_alloc"), (True, "host_alloc"), (True, "registered"),
+                                         (True, "registered_huge")])
 def test_server_tx_segments(oracle, odd, shm_mem):
     """The fused TX segment build through the server (tasx_server_tx_segments,
     SURVEY 8f rows 1 + 2 at TAS's batch size): payloads gathered from the
@@ -533,8 +534,10 @@ def test_server_tx_segments(oracle, odd, shm_mem):
     segs["payload"][17] = 4097                     # > tx_len: dma_read would assert; left alone
     exp_fr = fr.copy()
     oracle.tx_segment_batch(shm, sl, exp_fr, segs)
+    import mmap
     xsum.server_start(0)
     cx = _Ctxs([14])
+    mm = raw_shm = shm_arr = None
     try:
         hf = xsum.PinnedBuffer(fr.size + 4096)
         cx.pins.append(hf)
@@ -542,6 +545,16 @@ def test_server_tx_segments(oracle, odd, shm_mem):
             hs = xsum.PinnedBuffer(sl + 64)
             cx.pins.append(hs)
             shm_arr, shm_addr = hs.array, hs.addr
+        elif shm_mem == "registered_huge":  # a 2 MiB transparent huge page: TAS's default hugepage tas_shm
+            huge = 2 << 20
+            assert sl + 64 <= huge
+            mm = mmap.mmap(-1, 2 * huge, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+            base = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+            o = (-base) % huge
+            mm.madvise(mmap.MADV_HUGEPAGE, o, huge)
+            raw_shm = np.frombuffer(mm, dtype=np.uint8, count=huge, offset=o)
+            raw_shm[:] = 0
+            shm_arr, shm_addr = raw_shm[:sl + 64], base + o
         else:  # plain pages, pinned by tasx_ctx_register_shm (hipHostRegister), as TAS's tas_shm would be
             raw_shm = np.zeros(sl + 8192, np.uint8)
             o = (-raw_shm.ctypes.data) % 4096
@@ -578,6 +591,12 @@ def test_server_tx_segments(oracle, odd, shm_mem):
     finally:
         cx.close()
         _stop_if_running()
+        raw_shm = shm_arr = None  # unregistered by the context's release
+        if mm is not None:
+            try:
+                mm.close()
+            except BufferError:  # a view still held (by a failure's traceback): the process frees it
+                pass
 
 
 def test_server_beside_feeder_and_device_batches(oracle):
