@@ -60,8 +60,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_aggregation():
-    world = 2
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_world_aggregation(world):
+    """bench.py's control plane at 2 ranks and at the driver's 8 (one process
+    per GPU there): byte-balanced shards that tile the batch, the whole-job sum
+    and the max over ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,10 +77,11 @@ def test_gloo_world2_aggregation():
         assert p.exitcode == 0
     lens = pktgen.mixed_lengths(4096, seed=7)
     total = float(lens.astype(np.int64).sum())
-    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 4096
+    assert res[0][1] == 0 and res[-1][2] == 4096
+    assert all(res[r][2] == res[r + 1][1] for r in range(world - 1))
     for _, _, _, tot, mx in res:
         assert tot == total
-        assert mx == 3.0
+        assert mx == world * 1.5
 
 
 def test_bench_cli_defaults():
