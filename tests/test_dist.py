@@ -101,16 +101,40 @@ def _bench(*args, timeout=180):
                           timeout=timeout, env=env, cwd=str(ROOT))
 
 
-def test_bench_spawns_n_ranks_itself():
-    """`bench.py --gpus 2` with no launcher starts 2 rank processes of its own
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_spawns_n_ranks_itself(n):
+    """`bench.py --gpus N` with no launcher starts N rank processes of its own
     (here with the GPU-free control self-test: gloo barrier, MAX / SUM /
-    gather over ranks); rank 0 prints the per-rank aggregate."""
+    gather over ranks); rank 0 prints the per-rank aggregate.  N = 8 is the
+    driver's scaling run."""
     import json
-    r = _bench("--gpus", "2", "--control-selftest")
+    r = _bench("--gpus", str(n), "--control-selftest")
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["n_gpus"] == 2 and line["per_rank_value"] == [1.0, 2.0]
-    assert line["sum"] == 3.0 and line["max"] == 2.0 and line["ranks"] == ["cpu0", "cpu1"]
+    assert line["n_gpus"] == n and line["per_rank_value"] == [float(k + 1) for k in range(n)]
+    assert line["sum"] == n * (n + 1) / 2 and line["max"] == float(n)
+    assert line["ranks"] == [f"cpu{k}" for k in range(n)]
+
+
+def test_bench_under_the_drivers_launcher_8_ranks():
+    """The driver's own N > 1 command shape: torch.distributed.run with 8
+    processes on one node, each rank reading RANK / WORLD_SIZE / MASTER_* from
+    the environment (the GPU-free control self-test)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+                        "--gpus", "8", "--control-selftest"], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and line["per_rank_value"] == [float(k + 1) for k in range(8)]
+    assert line["sum"] == 36.0 and line["max"] == 8.0
 
 
 def test_bench_refuses_more_gpus_than_visible():
