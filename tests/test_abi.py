@@ -180,3 +180,11 @@ def test_both_builds_coexist_in_one_process(L):
         assert ab.tasx_ab_stream_read(None, 1024, 0, None, None) == -errno.EINVAL
     assert b"variant -1" in L.tasx_last_error()
     assert not hasattr(L, "tasx_ab_stream_read")
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: a missing build is an error naming the build step, not
+    a silent switch to another path."""
+    from tas_amd import xsum
+    with pytest.raises(RuntimeError, match="not built"):
+        xsum._load(tmp_path / "libtasx.so")
